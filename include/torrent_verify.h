@@ -1,0 +1,136 @@
+/*
+ * torrent_verify.h -- C ABI of the MI355X piece-verification engine (libtorrent_verify.so).
+ *
+ * The reference (rclarey/torrent, TypeScript for Deno) has no verify function and no FFI:
+ * its only per-piece SHA-1 is `crypto.subtle.digest("SHA-1", content)` inside
+ * tools/make_torrent.ts:28-31.  This ABI is what a Deno `Deno.dlopen` binding of the new
+ * verify path (ts/verify.ts) binds.  Each entry point names the reference
+ * interface whose data it consumes or replaces.
+ *
+ * Conventions
+ *   - Only fixed-width integers and plain pointers cross the boundary.
+ *   - Every function returns TV_OK (0) or a negative TV_ERR_*; the message is available from
+ *     tv_last_error().  (The TS/Python host turns a negative status into a thrown Error, like
+ *     piece.ts:21-65; unreadable data is NOT an error: it yields a 0 bit, like Storage.get
+ *     returning null, storage.ts:50-65.)
+ *   - One tv_ctx drives one GPU (one process or host thread per GPU).  Calls on one ctx are
+ *     serialised by an internal mutex; different ctxs are independent.
+ *   - The caller owns every host pointer and keeps it valid for the duration of the call.
+ *     The library owns its HIP streams, events, pinned staging buffers and device memory.
+ *   - Piece indices are GLOBAL torrent piece indices; a ctx holds the shard
+ *     [shard_first, shard_first + shard_count) resident in HBM.
+ *   - Bitfields are MSB-first, piece i -> byte i>>3, mask 0x80>>(i&7), spare bits 0
+ *     (reference torrent.ts:53,60 and :147-149).
+ */
+#ifndef TORRENT_VERIFY_H
+#define TORRENT_VERIFY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TV_ABI_VERSION 1
+
+#define TV_OK 0
+#define TV_ERR_ARG (-1)     /* invalid argument / geometry */
+#define TV_ERR_HIP (-2)     /* HIP runtime failure (message has the hipError string) */
+#define TV_ERR_STATE (-3)   /* call out of order (e.g. verify before set_layout) */
+#define TV_ERR_NOMEM (-4)   /* device or pinned host allocation failed */
+
+typedef struct tv_ctx tv_ctx;
+
+/* ABI version of the loaded library (== TV_ABI_VERSION). */
+int tv_abi_version(void);
+
+/* Number of visible HIP devices. */
+int tv_device_count(int *count);
+
+/* Create a context bound to HIP device `device`. */
+int tv_create(tv_ctx **out, int device);
+
+/* Release every resource of the context.  NULL is a no-op. */
+void tv_destroy(tv_ctx *ctx);
+
+/* Copy the last error message of `ctx` (or of the calling thread when ctx == NULL) into buf.
+ * Returns the full message length. */
+int tv_last_error(const tv_ctx *ctx, char *buf, size_t n);
+
+/*
+ * Geometry of the torrent and of this ctx's shard; allocates the resident payload.
+ *   total_length : InfoDict.length (metainfo.ts:21,40 / :125 sum of file lengths)
+ *   piece_length : InfoDict.pieceLength (metainfo.ts:14)
+ *   n_pieces     : InfoDict.pieces.length, the DIGEST count (metainfo.ts:16,111);
+ *                  piece i has length piece.ts:16-19 and linear offset i*piece_length
+ *                  (torrent.ts:165,186)
+ *   shard_first, shard_count : pieces resident on this device; shard_first % 8 == 0 so the
+ *                  bitfield slice is whole bytes
+ * Replaces: the per-piece Storage.get(i*pieceLength, pieceLength(i)) walk (storage.ts:50-65).
+ */
+int tv_set_layout(tv_ctx *ctx, uint64_t total_length, uint64_t piece_length, uint64_t n_pieces,
+                  uint64_t shard_first, uint64_t shard_count);
+
+/*
+ * Expected digests: the raw `info.pieces` byte string (pieces_len bytes; NOT 20*n_pieces when
+ * the string is ragged).  Slice i is bytes [20i, 20i+20) as partition(info.pieces, 20)
+ * makes it (metainfo.ts:111, _bytes.ts:92-99); a slice shorter than 20 bytes never matches.
+ */
+int tv_set_digests(tv_ctx *ctx, const uint8_t *pieces, uint64_t pieces_len);
+
+/*
+ * Copy `len` payload bytes at LINEAR torrent offset `linear_offset` (the concatenation of the
+ * files in info.files order, storage.ts:89-137) into the resident payload.  Bytes outside the
+ * shard are ignored.  The copy goes through the library's pinned staging ring and is complete
+ * when the call returns.  Replaces: fsStorage.get reads feeding Storage.get (storage.ts:150-172).
+ */
+int tv_stage(tv_ctx *ctx, uint64_t linear_offset, const uint8_t *src, uint64_t len);
+
+/* Fill the resident shard with the synthetic payload of `seed` (benchmarks / GPU tests):
+ * byte at linear offset o = byte (o & 7) of splitmix64(seed, o >> 3), little-endian. */
+int tv_fill_synthetic(tv_ctx *ctx, uint64_t seed);
+
+/*
+ * Verify every resident piece of the shard (HBM-resident path).
+ *   avail_bits : optional (NULL = all readable) shard-relative MSB-first bitfield, ceil(shard_count/8)
+ *                bytes; a clear bit forces 0 (Storage.get -> null: missing / short file).
+ *   bitfield_out : ceil(shard_count/8) bytes, shard-relative; bit j = piece shard_first + j.
+ * Piece i's bit is 1 iff its bytes are readable AND SHA-1(bytes) == info.pieces[i].
+ */
+int tv_verify(tv_ctx *ctx, const uint8_t *avail_bits, uint8_t *bitfield_out);
+
+/*
+ * Verify the shard from a HOST buffer (end-to-end resume check): `src` holds the
+ * shard's linear bytes [shard_first*piece_length, ...) (src_len bytes; pieces extending past
+ * src_len are unreadable).  Data streams host -> pinned ring -> HBM over PCIe with copy/compute
+ * overlap; no resident payload is needed.
+ */
+int tv_verify_host(tv_ctx *ctx, const uint8_t *src, uint64_t src_len, const uint8_t *avail_bits,
+                   uint8_t *bitfield_out);
+
+/* Creation mode (make_torrent.ts:28-31, :147-173): 20-byte SHA-1 of every resident piece of the
+ * shard, written to digests_out (20*shard_count bytes), in piece order. */
+int tv_hash(tv_ctx *ctx, uint8_t *digests_out);
+
+/* Options (tv_set_option keys). */
+#define TV_OPT_KERNEL 1      /* 0 = auto, 1 = lane kernel, 2 = split (schedule-offload) kernel */
+#define TV_OPT_STRIDE_PAD 2  /* bytes of padding between resident pieces (default 256) */
+#define TV_OPT_STREAM_CHUNK 3 /* tv_verify_host: bytes of each piece per streamed column chunk */
+int tv_set_option(tv_ctx *ctx, int key, int64_t value);
+int tv_get_option(tv_ctx *ctx, int key, int64_t *value);
+
+/* Timing of the last tv_verify / tv_hash / tv_verify_host call, from HIP events recorded on the
+ * library's compute stream: kernel_ms = the verify kernel(s) only; total_ms = whole call. */
+int tv_last_timing(tv_ctx *ctx, double *kernel_ms, double *total_ms);
+
+/* Kernel chosen for the last call (1 lane, 2 split) and launches it used. */
+int tv_last_kernel(tv_ctx *ctx, int *kernel, int *launches);
+
+/* Block until all work queued by the ctx is complete. */
+int tv_synchronize(tv_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TORRENT_VERIFY_H */

@@ -1,0 +1,163 @@
+"""GPU parity: the HIP path (through the C ABI) vs the CPU oracle on the same seeded inputs.
+
+Bar: bit-exact digests and bitfields.  Oracle = oracle/sha1_oracle.c (pinned against the
+reference's test_data digests in tests/test_oracle.py).
+"""
+import hashlib
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+KERNELS = [1, 2]  # lane, split
+
+
+def _ctx(native, kernel=0):
+    c = native.Context(0)
+    c.set_option(native.TV_OPT_KERNEL, kernel)
+    return c
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_hash_lengths_all_tail_cases(native, oracle, kernel):
+    """One piece per length: every len % 64 residue near the padding edges, 0..300 bytes, and
+    multi-block pieces.  Digest must equal hashlib / oracle."""
+    lengths = list(range(1, 140)) + [183, 191, 192, 255, 256, 257, 1000, 4095, 4096, 4097, 65536 + 55]
+    with _ctx(native, kernel) as ctx:
+        for n in lengths:
+            data = oracle.synth_fill(n + 1, 0, n)
+            ctx.set_layout(n, max(n, 1), 1)
+            ctx.stage(0, data)
+            got = ctx.hash()
+            assert got == hashlib.sha1(bytes(data)).digest(), n
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("L,P,last", [(4096, 300, 4096), (4096, 300, 1), (16384, 129, 9000),
+                                      (65536, 64, 65536 - 9), (1 << 20, 70, 123457), (64, 1000, 55)])
+def test_verify_matches_oracle(native, oracle, kernel, L, P, last):
+    total = L * (P - 1) + last
+    payload = oracle.synth_fill(L + P, 0, total)
+    pieces = bytearray(oracle.hash_pieces(payload, total, L, P))
+    rng = random.Random(L * 7 + P)
+    # corrupt ~3% of pieces: payload bit flips and digest bit flips, always incl. first and last
+    bad = sorted(set([0, P - 1] + rng.sample(range(P), max(1, P // 33))))
+    for i in bad:
+        if rng.random() < 0.5:
+            n = last if i == P - 1 else L
+            payload[i * L + rng.randrange(n)] ^= 1 << rng.randrange(8)
+        else:
+            pieces[20 * i + rng.randrange(20)] ^= 1 << rng.randrange(8)
+    expect = oracle.verify_linear(payload, total, L, bytes(pieces))
+    with _ctx(native, kernel) as ctx:
+        ctx.set_layout(total, L, P)
+        ctx.set_digests(bytes(pieces))
+        ctx.stage(0, payload)
+        got = ctx.verify()
+        assert got == expect
+        # hash mode agrees with the oracle on the corrupted payload
+        assert ctx.hash() == oracle.hash_pieces(payload, total, L, P)
+    for i in bad:
+        assert not (got[i >> 3] >> (7 - (i & 7))) & 1
+
+
+def test_kernels_agree_and_avail_mask(native, oracle):
+    L, P = 8192, 515
+    total = L * (P - 1) + 77
+    payload = oracle.synth_fill(99, 0, total)
+    pieces = oracle.hash_pieces(payload, total, L, P)
+    rng = random.Random(3)
+    avail = bytearray(rng.randrange(256) for _ in range((P + 7) // 8))
+    expect = oracle.verify_linear(payload, total, L, pieces, bytes(avail))
+    outs = []
+    for k in KERNELS:
+        with _ctx(native, k) as ctx:
+            ctx.set_layout(total, L, P)
+            ctx.set_digests(pieces)
+            ctx.stage(0, payload)
+            outs.append(ctx.verify(bytes(avail)))
+    assert outs[0] == outs[1] == expect
+
+
+def test_ragged_digest_string_and_extra_pieces(native, oracle):
+    """pieces.byteLength % 20 != 0 -> the short final slice never matches (_bytes.ts:94-96);
+    more digests than ceil(length/L) -> the extra pieces are unreadable (bit 0)."""
+    L = 4096
+    total = 10 * L
+    payload = oracle.synth_fill(5, 0, total)
+    good = oracle.hash_pieces(payload, total, L, 10)
+    # ragged: 9 full digests + 7 bytes of the 10th
+    ragged = good[:9 * 20 + 7]
+    with _ctx(native) as ctx:
+        ctx.set_layout(total, L, 10)
+        ctx.set_digests(ragged)
+        ctx.stage(0, payload)
+        got = ctx.verify()
+    assert got == oracle.verify_linear(payload, total, L, ragged) == bytes([0xFF, 0x80])
+    # 12 digests for 10 pieces of data: pieces 10, 11 unreadable; piece 11 is the "last" piece
+    extra = good + hashlib.sha1(b"x").digest() * 2
+    with _ctx(native) as ctx:
+        ctx.set_layout(total, L, 12)
+        ctx.set_digests(extra)
+        ctx.stage(0, payload)
+        got = ctx.verify()
+    assert got == oracle.verify_linear(payload, total, L, extra) == bytes([0xFF, 0xC0])
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_shards_concatenate(native, oracle, kernel):
+    """Sharded verification (the multi-GPU decomposition, run here shard by shard on one GPU)
+    concatenates to the single-shard bitfield."""
+    from torrent_amd.verify import shard_ranges
+    L, P = 2048, 1003
+    total = L * (P - 1) + 5
+    payload = oracle.synth_fill(17, 0, total)
+    pieces = bytearray(oracle.hash_pieces(payload, total, L, P))
+    for i in range(0, P, 37):
+        pieces[20 * i] ^= 0xFF
+    expect = oracle.verify_linear(payload, total, L, bytes(pieces))
+    out = bytearray((P + 7) // 8)
+    for first, count in shard_ranges(P, 8):
+        with _ctx(native, kernel) as ctx:
+            ctx.set_layout(total, L, P, first, count)
+            ctx.set_digests(bytes(pieces))
+            ctx.stage(0, payload)  # bytes outside the shard are ignored
+            sl = ctx.verify()
+        out[first // 8:first // 8 + len(sl)] = sl
+    assert bytes(out) == expect
+
+
+@pytest.mark.parametrize("chunk", [0, 64, 4096, 65536])
+def test_stream_from_host_matches(native, oracle, chunk):
+    L, P = 65536, 97
+    total = L * (P - 1) + 4321
+    payload = oracle.synth_fill(23, 0, total)
+    pieces = bytearray(oracle.hash_pieces(payload, total, L, P))
+    payload[3 * L + 100] ^= 0x10
+    pieces[20 * 50 + 3] ^= 0x01
+    expect = oracle.verify_linear(payload, total, L, bytes(pieces))
+    with _ctx(native) as ctx:
+        ctx.set_option(native.TV_OPT_STREAM_CHUNK, chunk)
+        ctx.set_layout(total, L, P)
+        ctx.set_digests(bytes(pieces))
+        assert ctx.verify_host(payload) == expect
+        # truncated source: pieces whose bytes extend past the end are unreadable
+        cut = 40 * L + 5
+        avail = bytearray((P + 7) // 8)
+        for i in range(P):
+            n = 4321 if i == P - 1 else L
+            if i * L + n <= cut:
+                avail[i >> 3] |= 0x80 >> (i & 7)
+        assert ctx.verify_host(memoryview(payload)[:cut]) == oracle.verify_linear(
+            payload, total, L, bytes(pieces), bytes(avail))
+
+
+def test_fill_synthetic_matches_oracle(native, oracle):
+    L, P = 4096, 40
+    total = L * P
+    with _ctx(native) as ctx:
+        ctx.set_layout(total, L, P, 8, 16)
+        ctx.fill_synthetic(77)
+        got = ctx.hash()
+    assert got == oracle.synth_piece_digests(77, total, L, P, 8, 16)

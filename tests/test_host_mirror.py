@@ -1,0 +1,227 @@
+"""Host-side mirror of the reference interfaces (CPU only): metainfo.ts, piece.ts, storage.ts.
+
+Ports of the reference's own test cases (metainfo_test.ts, storage_test.ts) plus the
+file-to-piece mapping quirks the device offset table relies on.
+"""
+import os
+
+import pytest
+
+from torrent_amd.bencode import bdecode as _bdecode, bencode as _bencode
+from torrent_amd.metainfo import encode_metainfo, make_info, parse_metainfo, partition, FileInfo
+from torrent_amd.piece import (BLOCK_SIZE, PieceMsg, RequestMsg, piece_length, validate_received_block,
+                               validate_requested_block)
+from torrent_amd.storage import FsStorage, MemoryStorage, Storage
+from torrent_amd.verify import shard_ranges
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _load(name):
+    with open(os.path.join(GOLDEN, name), "rb") as f:
+        return f.read()
+
+
+# ---- metainfo_test.ts ------------------------------------------------------------------
+
+def test_parse_single_file():  # metainfo_test.ts:11-30
+    m = parse_metainfo(_load("singlefile.torrent"))
+    assert m is not None
+    assert m.comment == "comment" and m.announce == "http://example.com/announce"
+    assert m.encoding == "UTF-8"
+    assert m.created_by == "https://github.com/rclarey/torrent/blob/master/tools/make_torrent.ts"
+    assert m.creation_date == 1602023427
+    i = m.info
+    assert (i.piece_length, i.name, i.length, len(i.pieces), i.private) == (262144, "singlefile.txt", 447135744, 1706, 0)
+    assert all(len(p) == 20 for p in i.pieces) and b"".join(i.pieces) == i.pieces_raw
+
+
+def test_parse_multi_file():  # metainfo_test.ts:32-59
+    m = parse_metainfo(_load("multifile.torrent"))
+    i = m.info
+    assert m.creation_date == 1599690859
+    assert (i.piece_length, i.name, len(i.pieces), i.private, len(i.files)) == (524288, "multifile", 1855, 0, 2)
+    assert i.files[0].length == 447135744 and "/".join(i.files[0].path) == "file1.txt"
+    assert i.files[1].length == 525148160 and "/".join(i.files[1].path) == "dir/file2.txt"
+    assert i.length == 447135744 + 525148160  # metainfo.ts:125
+
+
+def test_parse_minimal_extra_missing():  # metainfo_test.ts:61-111
+    m = parse_metainfo(_load("minimal.torrent"))
+    assert m is not None and m.info.private == 0 and m.comment is None and m.created_by is None
+    assert parse_metainfo(_load("extra.torrent")) is not None
+    assert parse_metainfo(_load("missing.torrent")) is None
+    assert parse_metainfo(b"not bencode") is None
+
+
+def test_bencode_roundtrip_and_insertion_order():
+    d = {"b": 1, "a": [b"x", "y", {"z": -3}], "skip": None}
+    enc = _bencode(d)
+    assert enc == b"d1:bi1e1:al1:x1:yd1:zi-3eeee"  # insertion order, None skipped (bencode.ts:56-64)
+    dec = _bdecode(enc)
+    assert dec["b"] == 1 and bytes(dec["a"][0]) == b"x" and dec["a"][2]["z"] == -3
+    with pytest.raises(ValueError):
+        _bdecode(b"i12")
+
+
+def test_encode_metainfo_roundtrip():
+    info = make_info(1 << 20, bytes(range(40)), "x", files=[FileInfo(5, ["a"]), FileInfo(7, ["d", "b"])])
+    m = parse_metainfo(encode_metainfo(info))
+    assert m.info.piece_length == 1 << 20 and m.info.length == 12 and m.info.pieces_raw == bytes(range(40))
+    assert [f.path for f in m.info.files] == [["a"], ["d", "b"]]
+
+
+def test_partition_ragged():  # _bytes.ts:92-99
+    assert [len(x) for x in partition(bytes(47), 20)] == [20, 20, 7]
+    assert partition(b"", 20) == []
+
+
+# ---- piece.ts -----------------------------------------------------------------------------
+
+def test_piece_length_rule():
+    info = make_info(4096, bytes(20 * 10), "x", length=9 * 4096 + 5)
+    assert piece_length(9, info) == 5 and piece_length(8, info) == 4096
+    info2 = make_info(4096, bytes(20 * 10), "x", length=10 * 4096)
+    assert piece_length(9, info2) == 4096
+
+
+def test_validate_blocks():
+    info = make_info(2 * BLOCK_SIZE, bytes(20 * 3), "x", length=2 * 2 * BLOCK_SIZE + 100)
+    validate_requested_block(info, RequestMsg(0, 0, BLOCK_SIZE))
+    with pytest.raises(ValueError, match="invalid piece index"):
+        validate_requested_block(info, RequestMsg(3, 0, 1))
+    with pytest.raises(ValueError, match="invalid block length"):
+        validate_requested_block(info, RequestMsg(2, 0, 101))
+    validate_received_block(info, PieceMsg(2, 0, bytes(100)))
+    with pytest.raises(ValueError, match="invalid block offset"):
+        validate_received_block(info, PieceMsg(0, 5, bytes(BLOCK_SIZE)))
+    with pytest.raises(ValueError, match="invalid last block length"):
+        validate_received_block(info, PieceMsg(2, 0, bytes(99)))
+    with pytest.raises(ValueError, match="invalid block length"):
+        validate_received_block(info, PieceMsg(0, 0, bytes(7)))
+
+
+# ---- storage_test.ts -------------------------------------------------------------------------
+
+BASE_MULTI = make_info(32 * 1024, bytes(20), "__test", files=[FileInfo(16 * 1024 + 10, ["__test1.txt"]),
+                                                              FileInfo(16 * 1024 - 11, ["__test2.txt"])])
+
+
+class Recorder:
+    def __init__(self, results):
+        self.calls = []
+        self.results = list(results)
+
+    def get(self, path, offset, length):
+        self.calls.append((list(path), offset, length))
+        return self.results.pop(0)
+
+    def set(self, path, offset, data):
+        self.calls.append((list(path), offset, bytes(data)))
+        return True
+
+    def exists(self, path):
+        return True
+
+
+def test_storage_get_across_files():  # storage_test.ts:180-204
+    vals = os.urandom(16 * 1024 - 1)
+    rec = Recorder([vals[:10], vals[10:]])
+    st = Storage(rec, BASE_MULTI, os.getcwd())
+    assert st.get(16 * 1024, 16 * 1024 - 1) == vals
+    assert rec.calls == [(["__test1.txt"], 16 * 1024, 10), (["__test2.txt"], 0, 16 * 1024 - 11)]
+
+
+def test_storage_get_inside_one_file():  # storage_test.ts:161-178
+    vals = os.urandom(16 * 1024)
+    rec = Recorder([vals])
+    st = Storage(rec, BASE_MULTI, os.getcwd())
+    assert st.get(0, 16 * 1024) == vals
+    assert rec.calls == [(["__test1.txt"], 0, 16 * 1024)]
+
+
+def test_storage_fails_if_method_fails():  # storage_test.ts:206-228
+    st = Storage(Recorder([None]), BASE_MULTI, os.getcwd())
+    assert st.get(0, 10) is None
+
+    class Boom(Recorder):
+        def get(self, *a):
+            raise RuntimeError("x")
+    assert Storage(Boom([]), BASE_MULTI, os.getcwd()).get(0, 10) is None
+
+
+def test_storage_set_across_files_and_dedupe():  # storage_test.ts:313-335, storage.ts:67-87
+    rec = Recorder([])
+    st = Storage(rec, BASE_MULTI, os.getcwd())
+    data = os.urandom(16 * 1024 - 1)
+    assert st.set(16 * 1024, data)
+    assert rec.calls == [(["__test1.txt"], 16 * 1024, data[:10]), (["__test2.txt"], 0, data[10:])]
+    assert st.set(16 * 1024, data) and len(rec.calls) == 2  # same block: not written again
+
+
+def test_segments_quirks():
+    # zero-length segment at an exact boundary (storage.ts:109-110); past the end -> None (:136)
+    info = make_info(8, bytes(20), "t", files=[FileInfo(8, ["a"]), FileInfo(0, ["z"]), FileInfo(8, ["b"])])
+    st = Storage(MemoryStorage(), info, os.getcwd())
+    assert st.segments(8, 8) == [(["a"], 8, 0, 0), (["z"], 0, 0, 0), (["b"], 0, 8, 0)]
+    assert st.segments(12, 8) is None
+    single = make_info(8, bytes(20), "s.bin", length=8)
+    assert Storage(MemoryStorage(), single, os.path.join(os.getcwd(), "dl")).segments(3, 4) == [(["dl", "s.bin"], 3, 4, 0)]
+
+
+def test_fs_storage(tmp_path):  # storage_test.ts:41-62
+    p = tmp_path / "__test.txt"
+    p.write_bytes(bytes([1, 2, 3, 4, 5, 6, 7, 8]))
+    fs = FsStorage()
+    assert list(fs.get([str(p)], 2, 4)) == [3, 4, 5, 6]
+    assert fs.get([str(p)], 7, 4) is None                 # reading fails (EOF)
+    missing = tmp_path / "nope.txt"
+    assert fs.get([str(missing)], 2, 4) is None           # doesn't exist ...
+    assert missing.exists()                               # ... but is created (OPEN_OPTIONS create: true)
+    assert fs.set([str(tmp_path / "d" / "x.bin")], 3, b"abc") and (tmp_path / "d" / "x.bin").read_bytes() == b"\0\0\0abc"
+    assert fs.exists([str(p)]) and not fs.exists([str(tmp_path / "zz")])
+
+
+def test_layout_segments_agree_with_storage(oracle):
+    """The seeded multi-file layouts: Storage.get over a MemoryStorage of the on-disk files
+    returns exactly the layout's expected piece bytes (including missing / short files)."""
+    from tests.layouts import LAYOUTS, build_layout
+    for spec in LAYOUTS:
+        if spec.get("big"):
+            continue
+        lay = build_layout(spec)
+        info = lay["info"]
+        st = Storage(MemoryStorage(lay["disk_files"]()), info, os.getcwd())
+        for i in range(lay["n_pieces"]):
+            got = st.get(i * info.piece_length, piece_length(i, info))
+            exp = lay["read_piece"](i)
+            assert (got is None) == (exp is None), (spec["name"], i)
+            if got is not None:
+                assert bytes(got) == exp
+
+
+def test_golden_layout_bitfields_match_oracle(oracle):
+    """The committed expected bitfields (hashlib) equal the oracle on the regenerated layouts."""
+    import hashlib
+    import json
+    from tests.layouts import build_layout, by_name
+    for rec in json.load(open(os.path.join(GOLDEN, "layouts.json"))):
+        if rec["name"] == "cfg3":
+            continue  # 2.6 GB: covered by the GPU test
+        lay = build_layout(by_name(rec["name"]))
+        assert hashlib.sha1(lay["pieces_raw"]).hexdigest() == rec["pieces_sha1"]
+        bf = oracle.verify_linear(lay["payload"], lay["total_length"], lay["info"].piece_length,
+                                  lay["pieces_raw"], lay["avail"])
+        assert bf.hex() == rec["expected_bitfield"], rec["name"]
+
+
+def test_shard_ranges_byte_aligned():
+    for P in [0, 1, 7, 8, 9, 1706, 51200, 16384]:
+        for n in [1, 2, 3, 4, 8]:
+            rs = shard_ranges(P, n)
+            assert len(rs) == n
+            assert sum(c for _, c in rs) == P
+            pos = 0
+            for f, c in rs:
+                assert f == pos and (f % 8 == 0 or c == 0)
+                pos += c

@@ -1,0 +1,57 @@
+"""Build libtorrent_verify.so in-tree (hipcc, gfx950) -- the only native product artifact.
+
+    python -m torrent_amd._build            # regenerate the asm header, compile the .so
+
+The generated header torrent_amd/csrc/sha1_asm.h is produced by tools/gen_sha1_asm.py, which
+first checks its instruction streams against hashlib in an emulator.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "libtorrent_verify.so")
+SOURCES = ["tv_kernels.hip", "tv_api.hip"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("TV_OFFLOAD_ARCH", "gfx950")
+
+
+def _newer(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    gen = os.path.join(ROOT, "tools", "gen_sha1_asm.py")
+    header = os.path.join(CSRC, "sha1_asm.h")
+    if force or _newer(header, [gen]):
+        subprocess.check_call([sys.executable, gen, "--out", header])
+    srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    deps = srcs + [header, os.path.join(CSRC, "tv_internal.h"),
+                   os.path.join(ROOT, "include", "torrent_verify.h")]
+    if not (force or _newer(LIB, deps)):
+        return LIB
+    objs = []
+    for s in srcs:
+        o = os.path.join(CSRC, os.path.basename(s) + ".o")
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+               "-I", os.path.join(ROOT, "include"), "-c", s, "-o", o]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd)
+        objs.append(o)
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

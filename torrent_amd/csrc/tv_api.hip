@@ -1,0 +1,670 @@
+// tv_api.hip -- C ABI of libtorrent_verify.so (declared in include/torrent_verify.h).
+//
+// Owns, per context (= per GPU): the compute and copy HIP streams, timing events, a ring of
+// pinned host staging buffers, and the device allocations (resident payload with padded piece
+// stride, digests, availability / output bitfields, chaining state for streamed runs).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/torrent_verify.h"
+#include "tv_internal.h"
+
+namespace {
+
+thread_local std::string g_thread_error;
+
+constexpr uint64_t kSlack = 256;               // bytes past the last resident piece (tail over-read)
+constexpr int kRingSlots = 3;                  // pinned staging buffers
+constexpr size_t kRingSlotBytes = 64ull << 20;
+
+}  // namespace
+
+struct tv_ctx {
+    int device = 0;
+    std::mutex mu;
+    std::string err;
+
+    hipStream_t stream = nullptr;       // kernels
+    hipStream_t copy_stream = nullptr;  // H2D staging
+    hipEvent_t ev_call0 = nullptr, ev_k0 = nullptr, ev_k1 = nullptr, ev_call1 = nullptr;
+
+    // geometry
+    bool has_layout = false;
+    uint64_t total = 0, L = 0, P = 0, first = 0, count = 0;
+    uint64_t stride = 0;
+    // options
+    int kernel_opt = TV_KERNEL_AUTO;
+    uint64_t pad = 256;
+    uint64_t stream_chunk = 0;  // 0 = automatic
+
+    // device memory
+    uint8_t* d_payload = nullptr;
+    uint32_t* d_digests = nullptr;    // [5][count]
+    uint64_t* d_avail = nullptr;      // bit words, sized to whole 256-piece groups
+    uint64_t* d_out = nullptr;
+    uint32_t* d_state = nullptr;      // [5][count]
+    uint32_t* d_hash = nullptr;       // [5][count]
+    uint8_t* d_chunk[2] = {nullptr, nullptr};
+    uint64_t chunk_bytes = 0;
+    size_t bit_words = 0;
+
+    bool digests_set = false;
+    std::vector<uint8_t> digest_ok;   // shard-relative MSB-first bits: digest slice is 20 bytes
+
+    // pinned staging ring
+    uint8_t* ring[kRingSlots] = {nullptr, nullptr, nullptr};
+    hipEvent_t ring_ev[kRingSlots] = {nullptr, nullptr, nullptr};
+    int ring_next = 0;
+    uint8_t* h_bits = nullptr;        // pinned bitfield bounce buffer
+    size_t h_bits_cap = 0;
+
+    // last call
+    float kernel_ms = 0.f, total_ms = 0.f;
+    int last_kernel = 0, last_launches = 0;
+};
+
+namespace {
+
+int fail(tv_ctx* c, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    g_thread_error = buf;
+    return code;
+}
+
+#define TV_HIP(c, call)                                                                         \
+    do {                                                                                        \
+        hipError_t e_ = (call);                                                                 \
+        if (e_ != hipSuccess)                                                                   \
+            return fail((c), e_ == hipErrorOutOfMemory ? TV_ERR_NOMEM : TV_ERR_HIP, "%s: %s (%s:%d)", #call, \
+                        hipGetErrorString(e_), __FILE__, __LINE__);                             \
+    } while (0)
+
+uint64_t piece_len(const tv_ctx* c, uint64_t i) {  // piece.ts:16-19
+    if (i == c->P - 1 && c->total % c->L) return c->total % c->L;
+    return c->L;
+}
+
+inline void set_bit(uint8_t* bf, uint64_t i) { bf[i >> 3] |= (uint8_t)(0x80u >> (i & 7)); }
+inline bool get_bit(const uint8_t* bf, uint64_t i) { return (bf[i >> 3] >> (7 - (i & 7))) & 1; }
+
+void free_device(tv_ctx* c) {
+    (void)hipFree(c->d_payload); c->d_payload = nullptr;
+    (void)hipFree(c->d_digests); c->d_digests = nullptr;
+    (void)hipFree(c->d_avail); c->d_avail = nullptr;
+    (void)hipFree(c->d_out); c->d_out = nullptr;
+    (void)hipFree(c->d_state); c->d_state = nullptr;
+    (void)hipFree(c->d_hash); c->d_hash = nullptr;
+    for (auto& p : c->d_chunk) { (void)hipFree(p); p = nullptr; }
+    c->chunk_bytes = 0;
+}
+
+int ensure_ring(tv_ctx* c) {
+    for (int s = 0; s < kRingSlots; s++) {
+        if (!c->ring[s]) TV_HIP(c, hipHostMalloc((void**)&c->ring[s], kRingSlotBytes, hipHostMallocDefault));
+        if (!c->ring_ev[s]) TV_HIP(c, hipEventCreateWithFlags(&c->ring_ev[s], hipEventDisableTiming));
+    }
+    return TV_OK;
+}
+
+int ensure_hbits(tv_ctx* c, size_t bytes) {
+    if (c->h_bits_cap >= bytes) return TV_OK;
+    if (c->h_bits) (void)hipHostFree(c->h_bits);
+    c->h_bits = nullptr;
+    c->h_bits_cap = 0;
+    TV_HIP(c, hipHostMalloc((void**)&c->h_bits, bytes, hipHostMallocDefault));
+    c->h_bits_cap = bytes;
+    return TV_OK;
+}
+
+// Take the next pinned ring slot (waiting for its previous copy to finish).
+int take_slot(tv_ctx* c, int* slot) {
+    int rc = ensure_ring(c);
+    if (rc) return rc;
+    int s = c->ring_next;
+    c->ring_next = (s + 1) % kRingSlots;
+    TV_HIP(c, hipEventSynchronize(c->ring_ev[s]));
+    *slot = s;
+    return TV_OK;
+}
+
+// Effective availability of every shard piece: caller bit & digest slice complete & bytes
+// inside the torrent (piece.ts:16-19 length at offset i*L must end <= total).
+int upload_avail(tv_ctx* c, const uint8_t* avail_bits) {
+    const size_t nbytes = c->bit_words * 8;
+    std::vector<uint8_t> bits(nbytes, 0);
+    for (uint64_t j = 0; j < c->count; j++) {
+        const uint64_t i = c->first + j;
+        bool ok = get_bit(c->digest_ok.data(), j);
+        ok = ok && (i * c->L + piece_len(c, i) <= c->total);
+        ok = ok && (!avail_bits || get_bit(avail_bits, j));
+        if (ok) set_bit(bits.data(), j);
+    }
+    TV_HIP(c, hipMemcpyAsync(c->d_avail, bits.data(), nbytes, hipMemcpyHostToDevice, c->stream));
+    TV_HIP(c, hipStreamSynchronize(c->stream));
+    return TV_OK;
+}
+
+int choose_kernel(const tv_ctx* c) {
+    if (c->kernel_opt == TV_KERNEL_LANE || c->kernel_opt == TV_KERNEL_SPLIT) return c->kernel_opt;
+    // Split (schedule offload) while the split workgroups fit co-resident: 4 x 40 KiB LDS per
+    // CU x 256 CUs x 64 pieces.  Above that the lane kernel fills >= 1 wave per SIMD on its own.
+    return c->count <= 65536 ? TV_KERNEL_SPLIT : TV_KERNEL_LANE;
+}
+
+TvPieces resident_launch(const tv_ctx* c) {
+    TvPieces p{};
+    p.data = c->d_payload;
+    p.stride = c->stride;
+    p.data_off = 0;
+    p.L = c->L;
+    p.n = (uint32_t)c->count;
+    const uint64_t last = c->P - 1;
+    p.last_idx = (last >= c->first && last < c->first + c->count) ? (uint32_t)(last - c->first) : 0xFFFFFFFFu;
+    p.last_len = piece_len(c, last);
+    p.blk_begin = 0;
+    p.blk_end = UINT64_MAX;
+    p.finalize = 1;
+    p.state = c->d_state;
+    p.digests = c->d_digests;
+    p.avail64 = c->d_avail;
+    p.out64 = c->d_out;
+    p.out_digests = c->d_hash;
+    return p;
+}
+
+int require_layout(tv_ctx* c, bool need_digests) {
+    if (!c->has_layout) return fail(c, TV_ERR_STATE, "tv_set_layout has not been called");
+    if (need_digests && !c->digests_set) return fail(c, TV_ERR_STATE, "tv_set_digests has not been called");
+    return TV_OK;
+}
+
+int read_bits(tv_ctx* c, uint8_t* out) {
+    const size_t nbytes = (c->count + 7) / 8;
+    int rc = ensure_hbits(c, c->bit_words * 8);
+    if (rc) return rc;
+    TV_HIP(c, hipMemcpyAsync(c->h_bits, c->d_out, c->bit_words * 8, hipMemcpyDeviceToHost, c->stream));
+    TV_HIP(c, hipEventRecord(c->ev_call1, c->stream));
+    TV_HIP(c, hipEventSynchronize(c->ev_call1));
+    memcpy(out, c->h_bits, nbytes);
+    if (c->count % 8) out[nbytes - 1] &= (uint8_t)(0xFF00u >> (c->count % 8));  // spare bits 0
+    return TV_OK;
+}
+
+int finish_timing(tv_ctx* c) {
+    TV_HIP(c, hipEventElapsedTime(&c->kernel_ms, c->ev_k0, c->ev_k1));
+    TV_HIP(c, hipEventElapsedTime(&c->total_ms, c->ev_call0, c->ev_call1));
+    return TV_OK;
+}
+
+// Stage one contiguous range of LINEAR bytes that lies inside a single piece or covers whole
+// pieces; src is host memory.  Rows of whole pieces use one 2D copy (src pitch L, dst pitch stride).
+int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n) {
+    while (n) {
+        const uint64_t i = pos / c->L, within = pos % c->L;
+        const uint64_t plen = piece_len(c, i);
+        uint8_t* dst = c->d_payload + (i - c->first) * c->stride + within;
+        int slot;
+        int rc = take_slot(c, &slot);
+        if (rc) return rc;
+        uint64_t bytes;
+        if (within == 0 && plen == c->L && n >= c->L && c->L <= kRingSlotBytes) {
+            // k whole pieces (none of them the short last piece)
+            uint64_t k = std::min<uint64_t>(n / c->L, kRingSlotBytes / c->L);
+            const uint64_t last_full = (c->total % c->L) ? c->P - 1 : c->P;  // first index that is not full
+            k = std::min<uint64_t>(k, (last_full > i) ? last_full - i : 1);
+            bytes = k * c->L;
+            memcpy(c->ring[slot], src, bytes);
+            TV_HIP(c, hipMemcpy2DAsync(dst, c->stride, c->ring[slot], c->L, c->L, k, hipMemcpyHostToDevice,
+                                       c->copy_stream));
+        } else {
+            bytes = std::min<uint64_t>({n, plen > within ? plen - within : 0, (uint64_t)kRingSlotBytes});
+            if (bytes == 0) return fail(c, TV_ERR_ARG, "stage offset %llu is past piece %llu", (unsigned long long)pos,
+                                        (unsigned long long)i);
+            memcpy(c->ring[slot], src, bytes);
+            TV_HIP(c, hipMemcpyAsync(dst, c->ring[slot], bytes, hipMemcpyHostToDevice, c->copy_stream));
+        }
+        TV_HIP(c, hipEventRecord(c->ring_ev[slot], c->copy_stream));
+        pos += bytes;
+        src += bytes;
+        n -= bytes;
+    }
+    return TV_OK;
+}
+
+}  // namespace
+
+// ============================================================================================
+extern "C" {
+
+int tv_abi_version(void) { return TV_ABI_VERSION; }
+
+int tv_device_count(int* count) {
+    if (!count) return fail(nullptr, TV_ERR_ARG, "count is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e == hipErrorNoDevice) n = 0;
+    else if (e != hipSuccess) return fail(nullptr, TV_ERR_HIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    *count = n;
+    return TV_OK;
+}
+
+int tv_create(tv_ctx** out, int device) {
+    if (!out) return fail(nullptr, TV_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    int rc = tv_device_count(&n);
+    if (rc) return rc;
+    if (device < 0 || device >= n) return fail(nullptr, TV_ERR_ARG, "device %d out of range (%d devices)", device, n);
+    tv_ctx* c = new tv_ctx();
+    c->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev_call0);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev_k0);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev_k1);
+    if (e == hipSuccess) e = hipEventCreate(&c->ev_call1);
+    if (e != hipSuccess) {
+        fail(nullptr, TV_ERR_HIP, "tv_create: %s", hipGetErrorString(e));
+        tv_destroy(c);
+        return TV_ERR_HIP;
+    }
+    *out = c;
+    return TV_OK;
+}
+
+void tv_destroy(tv_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+    free_device(c);
+    for (int s = 0; s < kRingSlots; s++) {
+        if (c->ring[s]) (void)hipHostFree(c->ring[s]);
+        if (c->ring_ev[s]) (void)hipEventDestroy(c->ring_ev[s]);
+    }
+    if (c->h_bits) (void)hipHostFree(c->h_bits);
+    for (hipEvent_t ev : {c->ev_call0, c->ev_k0, c->ev_k1, c->ev_call1})
+        if (ev) (void)hipEventDestroy(ev);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+    delete c;
+}
+
+int tv_last_error(const tv_ctx* c, char* buf, size_t n) {
+    const std::string& s = c ? c->err : g_thread_error;
+    if (buf && n) {
+        size_t k = std::min(n - 1, s.size());
+        memcpy(buf, s.data(), k);
+        buf[k] = 0;
+    }
+    return (int)s.size();
+}
+
+int tv_set_option(tv_ctx* c, int key, int64_t value) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    switch (key) {
+        case TV_OPT_KERNEL:
+            if (value < 0 || value > 2) return fail(c, TV_ERR_ARG, "TV_OPT_KERNEL must be 0, 1 or 2");
+            c->kernel_opt = (int)value;
+            return TV_OK;
+        case TV_OPT_STRIDE_PAD:
+            if (value < 64 || value % 64) return fail(c, TV_ERR_ARG, "TV_OPT_STRIDE_PAD must be a multiple of 64, >= 64");
+            if (c->has_layout) return fail(c, TV_ERR_STATE, "TV_OPT_STRIDE_PAD must be set before tv_set_layout");
+            c->pad = (uint64_t)value;
+            return TV_OK;
+        case TV_OPT_STREAM_CHUNK:
+            if (value < 0 || value % 64) return fail(c, TV_ERR_ARG, "TV_OPT_STREAM_CHUNK must be a multiple of 64");
+            c->stream_chunk = (uint64_t)value;
+            return TV_OK;
+    }
+    return fail(c, TV_ERR_ARG, "unknown option %d", key);
+}
+
+int tv_get_option(tv_ctx* c, int key, int64_t* value) {
+    if (!c || !value) return fail(c, TV_ERR_ARG, "NULL argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    switch (key) {
+        case TV_OPT_KERNEL: *value = c->kernel_opt; return TV_OK;
+        case TV_OPT_STRIDE_PAD: *value = (int64_t)c->pad; return TV_OK;
+        case TV_OPT_STREAM_CHUNK: *value = (int64_t)c->stream_chunk; return TV_OK;
+    }
+    return fail(c, TV_ERR_ARG, "unknown option %d", key);
+}
+
+int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint64_t n_pieces,
+                  uint64_t shard_first, uint64_t shard_count) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (piece_length == 0) return fail(c, TV_ERR_ARG, "piece_length must be > 0");
+    if (shard_first > n_pieces || shard_count > n_pieces - shard_first)
+        return fail(c, TV_ERR_ARG, "shard [%llu, +%llu) outside %llu pieces", (unsigned long long)shard_first,
+                    (unsigned long long)shard_count, (unsigned long long)n_pieces);
+    if (shard_first % 8) return fail(c, TV_ERR_ARG, "shard_first must be a multiple of 8 (whole bitfield bytes)");
+    if (shard_count >= 0xFFFFFFFFull) return fail(c, TV_ERR_ARG, "shard_count too large");
+    if (piece_length > (1ull << 40)) return fail(c, TV_ERR_ARG, "piece_length too large");
+    TV_HIP(c, hipSetDevice(c->device));
+    TV_HIP(c, hipStreamSynchronize(c->stream));
+    TV_HIP(c, hipStreamSynchronize(c->copy_stream));
+    free_device(c);
+    c->has_layout = false;
+    c->digests_set = false;
+    c->total = total_length;
+    c->L = piece_length;
+    c->P = n_pieces;
+    c->first = shard_first;
+    c->count = shard_count;
+    c->stride = ((piece_length + 63) / 64) * 64 + c->pad;
+    c->bit_words = ((shard_count + 255) / 256) * 4;
+    c->digest_ok.assign((shard_count + 7) / 8 + 8, 0);
+    if (shard_count) {
+        TV_HIP(c, hipMalloc((void**)&c->d_payload, shard_count * c->stride + kSlack));
+        TV_HIP(c, hipMalloc((void**)&c->d_digests, 5 * shard_count * sizeof(uint32_t)));
+        TV_HIP(c, hipMalloc((void**)&c->d_state, 5 * shard_count * sizeof(uint32_t)));
+        TV_HIP(c, hipMalloc((void**)&c->d_hash, 5 * shard_count * sizeof(uint32_t)));
+        TV_HIP(c, hipMalloc((void**)&c->d_avail, c->bit_words * 8));
+        TV_HIP(c, hipMalloc((void**)&c->d_out, c->bit_words * 8));
+        TV_HIP(c, hipMemsetAsync(c->d_payload + shard_count * c->stride, 0, kSlack, c->stream));
+        TV_HIP(c, hipStreamSynchronize(c->stream));
+    }
+    c->has_layout = true;
+    return TV_OK;
+}
+
+int tv_set_digests(tv_ctx* c, const uint8_t* pieces, uint64_t pieces_len) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = require_layout(c, false);
+    if (rc) return rc;
+    if (!pieces && pieces_len) return fail(c, TV_ERR_ARG, "pieces is NULL");
+    // partition(info.pieces, 20) (metainfo.ts:111, _bytes.ts:92-99): slice i = [20i, 20i+20)
+    std::vector<uint32_t> soa(5 * c->count, 0);
+    std::fill(c->digest_ok.begin(), c->digest_ok.end(), 0);
+    for (uint64_t j = 0; j < c->count; j++) {
+        const uint64_t i = c->first + j;
+        if (20 * i + 20 > pieces_len) continue;  // short or missing slice: never equal
+        const uint8_t* d = pieces + 20 * i;
+        for (int k = 0; k < 5; k++)
+            soa[(uint64_t)k * c->count + j] = ((uint32_t)d[4 * k] << 24) | ((uint32_t)d[4 * k + 1] << 16) |
+                                              ((uint32_t)d[4 * k + 2] << 8) | (uint32_t)d[4 * k + 3];
+        set_bit(c->digest_ok.data(), j);
+    }
+    if (c->count) {
+        TV_HIP(c, hipSetDevice(c->device));
+        TV_HIP(c, hipMemcpyAsync(c->d_digests, soa.data(), soa.size() * 4, hipMemcpyHostToDevice, c->stream));
+        TV_HIP(c, hipStreamSynchronize(c->stream));
+    }
+    c->digests_set = true;
+    return TV_OK;
+}
+
+int tv_stage(tv_ctx* c, uint64_t linear_offset, const uint8_t* src, uint64_t len) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = require_layout(c, false);
+    if (rc) return rc;
+    if (!src && len) return fail(c, TV_ERR_ARG, "src is NULL");
+    if (c->count == 0 || len == 0) return TV_OK;
+    TV_HIP(c, hipSetDevice(c->device));
+    // clip to the shard's linear range
+    const uint64_t lo = c->first * c->L;
+    const uint64_t last = c->first + c->count - 1;
+    const uint64_t hi = last * c->L + piece_len(c, last);
+    uint64_t a = std::max(linear_offset, lo), b = std::min(linear_offset + len, hi);
+    if (linear_offset + len < linear_offset) return fail(c, TV_ERR_ARG, "offset + len overflows");
+    if (a >= b) return TV_OK;
+    // piece by piece segments (a piece may be shorter than L only at the end of the torrent)
+    uint64_t pos = a;
+    while (pos < b) {
+        const uint64_t i = pos / c->L, within = pos % c->L;
+        const uint64_t plen = piece_len(c, i);
+        if (within >= plen) {  // inside a short last piece's missing tail: nothing to store
+            pos = (i + 1) * c->L;
+            continue;
+        }
+        uint64_t n;
+        if (within == 0 && plen == c->L) {
+            n = ((b - pos) / c->L) * c->L;  // whole pieces
+            if (n == 0) n = b - pos;
+        } else {
+            n = std::min(b - pos, plen - within);
+        }
+        rc = stage_copy(c, pos, src + (pos - linear_offset), n);
+        if (rc) return rc;
+        pos += n;
+    }
+    TV_HIP(c, hipStreamSynchronize(c->copy_stream));
+    return TV_OK;
+}
+
+int tv_fill_synthetic(tv_ctx* c, uint64_t seed) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = require_layout(c, false);
+    if (rc) return rc;
+    if (!c->count) return TV_OK;
+    TV_HIP(c, hipSetDevice(c->device));
+    TV_HIP(c, tv_launch_fill(c->d_payload, c->stride, c->first, (uint32_t)c->count, c->L, seed, c->stream));
+    TV_HIP(c, hipStreamSynchronize(c->stream));
+    return TV_OK;
+}
+
+int tv_verify(tv_ctx* c, const uint8_t* avail_bits, uint8_t* bitfield_out) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = require_layout(c, true);
+    if (rc) return rc;
+    if (!bitfield_out && c->count) return fail(c, TV_ERR_ARG, "bitfield_out is NULL");
+    if (!c->count) return TV_OK;
+    TV_HIP(c, hipSetDevice(c->device));
+    TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
+    rc = upload_avail(c, avail_bits);
+    if (rc) return rc;
+    const int kernel = choose_kernel(c);
+    TvPieces p = resident_launch(c);
+    TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
+    TV_HIP(c, tv_launch_verify(p, kernel, false, c->stream));
+    TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
+    rc = read_bits(c, bitfield_out);
+    if (rc) return rc;
+    c->last_kernel = kernel;
+    c->last_launches = 1;
+    return finish_timing(c);
+}
+
+int tv_hash(tv_ctx* c, uint8_t* digests_out) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = require_layout(c, false);
+    if (rc) return rc;
+    if (!digests_out && c->count) return fail(c, TV_ERR_ARG, "digests_out is NULL");
+    if (!c->count) return TV_OK;
+    TV_HIP(c, hipSetDevice(c->device));
+    TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
+    const int kernel = choose_kernel(c);
+    TvPieces p = resident_launch(c);
+    p.avail64 = nullptr;
+    TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
+    TV_HIP(c, tv_launch_verify(p, kernel, true, c->stream));
+    TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
+    std::vector<uint32_t> soa(5 * c->count);
+    TV_HIP(c, hipMemcpyAsync(soa.data(), c->d_hash, soa.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    TV_HIP(c, hipEventRecord(c->ev_call1, c->stream));
+    TV_HIP(c, hipEventSynchronize(c->ev_call1));
+    for (uint64_t j = 0; j < c->count; j++)
+        for (int k = 0; k < 5; k++) {
+            const uint32_t v = soa[(uint64_t)k * c->count + j];
+            uint8_t* d = digests_out + 20 * j + 4 * k;
+            d[0] = (uint8_t)(v >> 24); d[1] = (uint8_t)(v >> 16); d[2] = (uint8_t)(v >> 8); d[3] = (uint8_t)v;
+        }
+    c->last_kernel = kernel;
+    c->last_launches = 1;
+    return finish_timing(c);
+}
+
+// End-to-end verification from host memory: column-chunked streaming.  Column c carries bytes
+// [c*C, (c+1)*C) of every shard piece; it is copied (one 2D DMA, src pitch L) into one of two
+// device chunk buffers while the kernel hashes the previous column.  Chaining values persist in
+// d_state between columns; the last column finalises (padding block, compare).
+int tv_verify_host(tv_ctx* c, const uint8_t* src, uint64_t src_len, const uint8_t* avail_bits,
+                   uint8_t* bitfield_out) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = require_layout(c, true);
+    if (rc) return rc;
+    if (!bitfield_out && c->count) return fail(c, TV_ERR_ARG, "bitfield_out is NULL");
+    if (!src && src_len) return fail(c, TV_ERR_ARG, "src is NULL");
+    if (!c->count) return TV_OK;
+    TV_HIP(c, hipSetDevice(c->device));
+
+    // pieces whose bytes extend past src_len are unreadable
+    std::vector<uint8_t> av((c->count + 7) / 8 + 8, 0);
+    for (uint64_t j = 0; j < c->count; j++) {
+        const uint64_t i = c->first + j;
+        const uint64_t end = (j * c->L) + piece_len(c, i);
+        if (end <= src_len && (!avail_bits || get_bit(avail_bits, j))) set_bit(av.data(), j);
+    }
+    TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
+    rc = upload_avail(c, av.data());
+    if (rc) return rc;
+
+    const uint64_t n = c->count;
+    uint64_t C = c->stream_chunk;
+    if (!C) {  // ~512 MiB columns, 64 KiB .. L
+        C = 64ull << 10;
+        while (C * 2 <= c->L && C * 2 * n <= (512ull << 20)) C *= 2;
+    }
+    C = std::max<uint64_t>(64, std::min<uint64_t>((C / 64) * 64, ((c->L + 63) / 64) * 64));
+    const uint64_t row = C + 256;  // device row pitch (tail over-read slack)
+    if (c->chunk_bytes < row * n + kSlack) {
+        for (auto& p : c->d_chunk) { (void)hipFree(p); p = nullptr; }
+        c->chunk_bytes = 0;
+        for (auto& p : c->d_chunk) TV_HIP(c, hipMalloc((void**)&p, row * n + kSlack));
+        c->chunk_bytes = row * n + kSlack;
+    }
+    hipPointerAttribute_t attr{};
+    bool pinned = hipPointerGetAttributes(&attr, src) == hipSuccess && attr.type == hipMemoryTypeHost;
+    (void)hipGetLastError();
+
+    const uint64_t ncol = (c->L + C - 1) / C;
+    const int kernel = choose_kernel(c);
+    TvPieces p = resident_launch(c);
+    p.stride = row;
+    hipEvent_t col_ev[2];
+    TV_HIP(c, hipEventCreateWithFlags(&col_ev[0], hipEventDisableTiming));
+    TV_HIP(c, hipEventCreateWithFlags(&col_ev[1], hipEventDisableTiming));
+    hipEvent_t done_ev[2];
+    TV_HIP(c, hipEventCreateWithFlags(&done_ev[0], hipEventDisableTiming));
+    TV_HIP(c, hipEventCreateWithFlags(&done_ev[1], hipEventDisableTiming));
+    TV_HIP(c, hipEventRecord(done_ev[0], c->stream));
+    TV_HIP(c, hipEventRecord(done_ev[1], c->stream));
+    bool k0_recorded = false;
+    for (uint64_t col = 0; col < ncol; col++) {
+        const int buf = (int)(col & 1);
+        const uint64_t off = col * C;
+        const uint64_t width = std::min(C, c->L - off);
+        // the copy into buf must wait until the kernel that last read buf is done
+        TV_HIP(c, hipStreamWaitEvent(c->copy_stream, done_ev[buf], 0));
+        // rows whose piece holds all `width` bytes inside src: 2D copy; the others one by one
+        uint64_t full_rows = 0;
+        while (full_rows < n && full_rows * c->L + off + width <= src_len &&
+               (c->first + full_rows != c->P - 1 || piece_len(c, c->P - 1) >= off + width))
+            full_rows++;
+        if (pinned) {
+            if (full_rows)
+                TV_HIP(c, hipMemcpy2DAsync(c->d_chunk[buf], row, src + off, c->L, width, full_rows,
+                                           hipMemcpyHostToDevice, c->copy_stream));
+        } else {
+            // pageable source: gather rows through the pinned ring
+            uint64_t r = 0;
+            while (r < full_rows) {
+                int slot;
+                rc = take_slot(c, &slot);
+                if (rc) return rc;
+                const uint64_t k = std::min<uint64_t>(full_rows - r, std::max<uint64_t>(1, kRingSlotBytes / width));
+                for (uint64_t q = 0; q < k; q++) memcpy(c->ring[slot] + q * width, src + (r + q) * c->L + off, width);
+                TV_HIP(c, hipMemcpy2DAsync(c->d_chunk[buf] + r * row, row, c->ring[slot], width, width, k,
+                                           hipMemcpyHostToDevice, c->copy_stream));
+                TV_HIP(c, hipEventRecord(c->ring_ev[slot], c->copy_stream));
+                r += k;
+            }
+        }
+        for (uint64_t r = full_rows; r < n; r++) {  // short / truncated rows
+            const uint64_t start = r * c->L + off;
+            const uint64_t plen = piece_len(c, c->first + r);
+            uint64_t have = 0;
+            if (start < src_len && off < plen) have = std::min({width, src_len - start, plen - off});
+            if (!have) continue;
+            int slot;
+            rc = take_slot(c, &slot);
+            if (rc) return rc;
+            memcpy(c->ring[slot], src + start, have);
+            TV_HIP(c, hipMemcpyAsync(c->d_chunk[buf] + r * row, c->ring[slot], have, hipMemcpyHostToDevice, c->copy_stream));
+            TV_HIP(c, hipEventRecord(c->ring_ev[slot], c->copy_stream));
+        }
+        TV_HIP(c, hipEventRecord(col_ev[buf], c->copy_stream));
+        TV_HIP(c, hipStreamWaitEvent(c->stream, col_ev[buf], 0));
+        if (!k0_recorded) {
+            TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
+            k0_recorded = true;
+        }
+        p.data = c->d_chunk[buf];
+        p.data_off = off;
+        p.blk_begin = off / 64;
+        const bool last_col = col + 1 == ncol;
+        p.blk_end = last_col ? UINT64_MAX : (off + C) / 64;
+        p.finalize = last_col ? 1 : 0;
+        TV_HIP(c, tv_launch_verify(p, kernel, false, c->stream));
+        TV_HIP(c, hipEventRecord(done_ev[buf], c->stream));
+    }
+    TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
+    rc = read_bits(c, bitfield_out);
+    for (int k = 0; k < 2; k++) {
+        (void)hipEventDestroy(col_ev[k]);
+        (void)hipEventDestroy(done_ev[k]);
+    }
+    if (rc) return rc;
+    c->last_kernel = kernel;
+    c->last_launches = (int)ncol;
+    return finish_timing(c);
+}
+
+int tv_last_timing(tv_ctx* c, double* kernel_ms, double* total_ms) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (kernel_ms) *kernel_ms = c->kernel_ms;
+    if (total_ms) *total_ms = c->total_ms;
+    return TV_OK;
+}
+
+int tv_last_kernel(tv_ctx* c, int* kernel, int* launches) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (kernel) *kernel = c->last_kernel;
+    if (launches) *launches = c->last_launches;
+    return TV_OK;
+}
+
+int tv_synchronize(tv_ctx* c) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    TV_HIP(c, hipSetDevice(c->device));
+    TV_HIP(c, hipStreamSynchronize(c->copy_stream));
+    TV_HIP(c, hipStreamSynchronize(c->stream));
+    return TV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,33 @@
+// tv_internal.h -- shared between the kernels (tv_kernels.hip) and the C ABI (tv_api.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define TV_KERNEL_AUTO 0
+#define TV_KERNEL_LANE 1
+#define TV_KERNEL_SPLIT 2
+
+// One launch over a contiguous run of n pieces.  Piece j's byte k (piece-relative) is at
+// data + j*stride + k - data_off.  Blocks [blk_begin, min(blk_end, nb_j)) are processed.
+struct TvPieces {
+    const uint8_t* data;
+    uint64_t stride;
+    uint64_t data_off;
+    uint64_t L;              // piece length of every piece except last_idx
+    uint64_t last_len;       // length of piece last_idx
+    uint64_t blk_begin;
+    uint64_t blk_end;        // UINT64_MAX = through the end of every piece
+    uint32_t n;
+    uint32_t last_idx;       // launch-local index of the torrent's last piece, 0xFFFFFFFF if absent
+    uint32_t finalize;       // 1: compare / emit digests; 0: store chaining values to `state`
+    uint32_t pad_;
+    uint32_t* state;         // [5][n] chaining values (read when blk_begin > 0, written when !finalize)
+    const uint32_t* digests; // [5][n] expected digest words (big-endian values)
+    const uint64_t* avail64; // per 64 pieces, MSB-first bitfield bytes; may be null
+    uint64_t* out64;         // per 64 pieces, MSB-first bitfield bytes (sized to whole 256-piece groups)
+    uint32_t* out_digests;   // hash mode: [5][n]
+};
+
+hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_t s);
+hipError_t tv_launch_fill(uint8_t* payload, uint64_t stride, uint64_t first, uint32_t n, uint64_t L,
+                          uint64_t seed, hipStream_t s);

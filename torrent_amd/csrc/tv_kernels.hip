@@ -1,0 +1,368 @@
+// tv_kernels.hip -- gfx950 SHA-1 piece-verification kernels.
+//
+// Reference semantics (rclarey/torrent): piece i = bytes [i*L, i*L + len_i) of the linear
+// torrent space (torrent.ts:165,186); len_i per piece.ts:16-19; digest = SHA-1 as in
+// crypto.subtle.digest("SHA-1", content) (tools/make_torrent.ts:28-31); have-bit i set iff
+// the digest equals info.pieces[i] (metainfo.ts:111) and the bytes were readable
+// (Storage.get non-null, storage.ts:50-65), MSB-first (torrent.ts:147-149).
+//
+// Parallelism is one LANE per piece (SHA-1 is serial inside a piece).  Two kernels:
+//   lane  : each lane loads its own 64-byte blocks (register prefetch, 2 blocks ahead) and runs
+//           the full compression (schedule + rounds) as one generated asm block (613 VALU/block).
+//   split : schedule offload.  A workgroup is 2 waves for 64 pieces: the helper wave loads the
+//           blocks and computes W[0..79] into an LDS double buffer; the rounds wave runs only
+//           the 80 rounds from LDS (400 VALU + 20 ds_read_b128 per block).  When there are
+//           fewer pieces than SIMDs x 2 waves, the per-lane serial issue rate is the bound, and
+//           this cuts the serial stream from ~613 to ~420 instructions per block.
+//
+// HBM layout: resident piece j (shard-local) starts at payload + j*stride, stride = L + pad
+// (pad breaks the power-of-two stride that would put all 64 lanes of a wave on one channel).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sha1_asm.h"
+#include "tv_internal.h"
+
+#define TV_K0 0x5A827999u
+#define TV_K1 0x6ED9EBA1u
+#define TV_K2 0x8F1BBCDCu
+#define TV_K3 0xCA62C1D6u
+
+namespace {
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return __builtin_rotateleft32(x, n); }
+
+__device__ __forceinline__ void sha1_iv(uint32_t h[5]) {
+    h[0] = 0x67452301u; h[1] = 0xEFCDAB89u; h[2] = 0x98BADCFEu; h[3] = 0x10325476u; h[4] = 0xC3D2E1F0u;
+}
+
+// Per-wave uniform geometry.  Every piece of a launch has length L except the global last
+// piece (launch-local index last_idx), which is always the final piece of the launch.
+struct WaveGeom {
+    uint64_t nfull_min;  // min over the wave's lanes of len/64: blocks [.., nfull_min) are raw data for every lane
+    uint64_t nb_max;     // max over lanes of the padded block count ceil((len+9)/64)
+};
+
+__device__ __forceinline__ uint64_t nblocks(uint64_t len) { return (len + 8) / 64 + 1; }
+
+__device__ __forceinline__ WaveGeom wave_geom(const TvPieces& p, uint32_t j0) {
+    WaveGeom g;
+    const bool has_last = p.last_idx != 0xFFFFFFFFu && (p.last_idx >> 6) == (j0 >> 6);
+    const bool only_last = has_last && p.last_idx == j0;
+    g.nfull_min = (has_last ? p.last_len : p.L) / 64;
+    g.nb_max = nblocks(only_last ? p.last_len : p.L);
+    return g;
+}
+
+// Build the 16 big-endian message words of block b of a piece of length len whose byte 0 is
+// at `piece` (slow path: data tail, 0x80 terminator, zero fill, bit length).  Reads at most
+// 64 bytes from piece + 64*b; the buffers carry >= 64 bytes of slack past every piece.
+__device__ __forceinline__ void build_tail_block(const uint8_t* piece, uint64_t len, uint64_t b,
+                                                 uint32_t w[16]) {
+    const int64_t rem = (int64_t)len - (int64_t)(b * 64);
+    uint4 raw[4];
+    if (rem > 0) {
+        const uint4* src = reinterpret_cast<const uint4*>(piece + b * 64);
+#pragma unroll
+        for (int i = 0; i < 4; i++) raw[i] = src[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++) raw[i] = make_uint4(0, 0, 0, 0);
+    }
+    const uint32_t* rw = reinterpret_cast<const uint32_t*>(raw);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int64_t v = rem - 4 * k;  // valid data bytes in word k (may be <0 or >=4)
+        uint32_t x = bswap32(rw[k]);
+        if (v < 4) {
+            if (v < 0) {
+                x = 0;
+            } else {
+                const uint32_t keep = v == 0 ? 0u : (0xFFFFFFFFu << (32 - 8 * (int)v));
+                x = (x & keep) | (0x80u << (24 - 8 * (int)v));
+            }
+        }
+        w[k] = x;
+    }
+    if (b == nblocks(len) - 1) {
+        const uint64_t bits = len * 8;
+        w[14] = (uint32_t)(bits >> 32);
+        w[15] = (uint32_t)bits;
+    }
+}
+
+__device__ __forceinline__ void load_block(const uint8_t* piece, uint64_t b, uint4 (&r)[4]) {
+    const uint4* src = reinterpret_cast<const uint4*>(piece + b * 64);
+#pragma unroll
+    for (int i = 0; i < 4; i++) r[i] = src[i];
+}
+
+__device__ __forceinline__ void bswap_block(const uint4 (&r)[4], uint32_t w[16]) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        w[4 * i + 0] = bswap32(r[i].x);
+        w[4 * i + 1] = bswap32(r[i].y);
+        w[4 * i + 2] = bswap32(r[i].z);
+        w[4 * i + 3] = bswap32(r[i].w);
+    }
+}
+
+__device__ __forceinline__ void compress_full(uint32_t h[5], uint32_t w[16]) {
+    uint32_t r[5];
+    tv_sha1_full(h, r, w, TV_K0, TV_K1, TV_K2, TV_K3);
+#pragma unroll
+    for (int i = 0; i < 5; i++) h[i] += r[i];
+}
+
+// Lane-local piece length.
+__device__ __forceinline__ uint64_t lane_len(const TvPieces& p, uint32_t jj) {
+    return jj == p.last_idx ? p.last_len : p.L;
+}
+
+// Final step shared by both kernels: compare (verify) or store (hash) the digest, or keep the
+// chaining value for the next launch of a streamed run.
+template <bool HASH>
+__device__ __forceinline__ void finish(const TvPieces& p, uint32_t j, uint32_t jj, uint32_t j0,
+                                       const uint32_t h[5]) {
+    if (!p.finalize) {
+        if (j < p.n) {
+#pragma unroll
+            for (int k = 0; k < 5; k++) p.state[(uint64_t)k * p.n + j] = h[k];
+        }
+        return;
+    }
+    if (HASH) {
+        if (j < p.n) {
+#pragma unroll
+            for (int k = 0; k < 5; k++) p.out_digests[(uint64_t)k * p.n + j] = h[k];
+        }
+        return;
+    }
+    bool ok = j < p.n;
+#pragma unroll
+    for (int k = 0; k < 5; k++) ok = ok && (h[k] == p.digests[(uint64_t)k * p.n + jj]);
+    const uint64_t mask = __ballot(ok);
+    if ((threadIdx.x & 63) == 0) {
+        // ballot bit l = piece j0+l  ->  MSB-first bytes: byte m holds pieces j0+8m .. j0+8m+7
+        uint64_t bits = __builtin_bswap64(__builtin_bitreverse64(mask));
+        if (p.avail64) bits &= p.avail64[j0 >> 6];
+        p.out64[j0 >> 6] = bits;
+    }
+}
+
+__device__ __forceinline__ void start_state(const TvPieces& p, uint32_t jj, uint32_t h[5]) {
+    if (p.blk_begin == 0) {
+        sha1_iv(h);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 5; k++) h[k] = p.state[(uint64_t)k * p.n + jj];
+    }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// lane kernel: one lane per piece, full compression per lane.
+// ------------------------------------------------------------------------------------------
+template <bool HASH>
+__global__ __launch_bounds__(256) void tv_lane_kernel(TvPieces p) {
+    const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t jj = j < p.n ? j : p.n - 1;
+    const uint32_t j0 = blockIdx.x * 256u + (threadIdx.x & ~63u);
+    if (j0 >= p.n) return;  // wave-uniform: no piece in this wave
+    const WaveGeom g = wave_geom(p, j0);
+    const uint64_t len = lane_len(p, jj);
+    const uint64_t nb = nblocks(len);
+    const uint8_t* piece = p.data + (uint64_t)jj * p.stride - p.data_off;
+
+    uint32_t h[5];
+    start_state(p, jj, h);
+
+    uint64_t b = p.blk_begin;
+    const uint64_t fast_end = g.nfull_min < p.blk_end ? g.nfull_min : p.blk_end;
+    const uint64_t end = g.nb_max < p.blk_end ? g.nb_max : p.blk_end;
+    uint32_t w[16];
+
+    if (b < fast_end) {
+        uint4 A[4], B[4];
+        load_block(piece, b, A);
+        if (b + 1 < fast_end) load_block(piece, b + 1, B);
+        for (;;) {
+            bswap_block(A, w);
+            if (b + 2 < fast_end) load_block(piece, b + 2, A);
+            compress_full(h, w);
+            if (++b >= fast_end) break;
+            bswap_block(B, w);
+            if (b + 2 < fast_end) load_block(piece, b + 2, B);
+            compress_full(h, w);
+            if (++b >= fast_end) break;
+        }
+    }
+    for (; b < end; b++) {
+        build_tail_block(piece, len, b, w);
+        uint32_t r[5];
+        tv_sha1_full(h, r, w, TV_K0, TV_K1, TV_K2, TV_K3);
+        if (b < nb) {
+#pragma unroll
+            for (int i = 0; i < 5; i++) h[i] += r[i];
+        }
+    }
+    finish<HASH>(p, j, jj, j0, h);
+}
+
+// ------------------------------------------------------------------------------------------
+// split kernel: wave 0 = rounds (80 rounds per block from LDS), wave 1 = helper (loads +
+// message schedule into a 2 x 20 KiB LDS ring).  One barrier per block.
+// ------------------------------------------------------------------------------------------
+namespace {
+
+constexpr int kRingWords = 80 * 64;  // one buffer: [20 quads][64 lanes][4 words]
+
+// Helper: W[0..79] of one block into LDS buffer `buf` as [t/4][lane][4].
+__device__ __forceinline__ void schedule_to_lds(uint32_t w[16], uint4* buf, uint32_t lane) {
+#pragma unroll
+    for (int q = 0; q < 20; q++) {
+        if (q >= 4) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int t = 4 * q + i;
+                w[t & 15] = rotl(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
+            }
+        }
+        const int t = 4 * q;
+        buf[q * 64 + lane] = make_uint4(w[t & 15], w[(t + 1) & 15], w[(t + 2) & 15], w[(t + 3) & 15]);
+    }
+}
+
+__device__ __forceinline__ void lds_barrier() {
+    // LDS writes of this wave complete, then the workgroup barrier.  Deliberately NOT
+    // __syncthreads(): the helper's global prefetch loads must stay in flight across it.
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+}  // namespace
+
+template <bool HASH>
+__global__ __launch_bounds__(128) void tv_split_kernel(TvPieces p) {
+    __shared__ __attribute__((aligned(16))) uint4 ring[2 * kRingWords / 4];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t j0 = blockIdx.x * 64u;
+    const uint32_t j = j0 + lane;
+    const uint32_t jj = j < p.n ? j : p.n - 1;
+    const WaveGeom g = wave_geom(p, j0);
+    const uint64_t len = lane_len(p, jj);
+    const uint64_t nb = nblocks(len);
+    const uint8_t* piece = p.data + (uint64_t)jj * p.stride - p.data_off;
+
+    const uint64_t b0 = p.blk_begin;
+    const uint64_t fast_end = g.nfull_min < p.blk_end ? g.nfull_min : p.blk_end;
+    const uint64_t end = g.nb_max < p.blk_end ? g.nb_max : p.blk_end;
+
+    if (wave != 0) {
+        // ---------------- helper wave ----------------
+        uint32_t w[16];
+        uint4 A[4], B[4];
+        auto stage = [&](uint64_t b, uint4 (&raw)[4]) {
+            uint4* buf = ring + ((b - b0) & 1) * (kRingWords / 4);
+            if (b < fast_end) {
+                bswap_block(raw, w);
+                if (b + 2 < fast_end) load_block(piece, b + 2, raw);
+            } else {
+                build_tail_block(piece, len, b, w);
+            }
+            schedule_to_lds(w, buf, lane);
+        };
+        if (b0 < end) {
+            if (b0 < fast_end) load_block(piece, b0, A);
+            if (b0 + 1 < fast_end) load_block(piece, b0 + 1, B);
+            stage(b0, A);
+        }
+        lds_barrier();
+        for (uint64_t b = b0; b < end;) {
+            if (b + 1 < end) stage(b + 1, B);
+            lds_barrier();
+            if (++b >= end) break;
+            if (b + 1 < end) stage(b + 1, A);
+            lds_barrier();
+            ++b;
+        }
+        return;
+    }
+
+    // ---------------- rounds wave ----------------
+    uint32_t h[5];
+    start_state(p, jj, h);
+    const uint32_t ring_base = (uint32_t)(uintptr_t)(void*)ring + lane * 16u;
+    const uint64_t nb_min = g.nfull_min + 1;  // every lane has >= nfull_min + 1 blocks
+    lds_barrier();
+    for (uint64_t b = b0; b < end; b++) {
+        uint32_t r[5];
+        tv_sha1_lds(h, r, ring_base + (uint32_t)((b - b0) & 1) * (kRingWords * 4), TV_K0, TV_K1, TV_K2, TV_K3);
+        if (b < nb_min || b < nb) {
+#pragma unroll
+            for (int i = 0; i < 5; i++) h[i] += r[i];
+        }
+        lds_barrier();
+    }
+    finish<HASH>(p, j, jj, j0, h);
+}
+
+// ------------------------------------------------------------------------------------------
+// synthetic payload fill: byte at linear offset o = byte (o & 7) of splitmix64(seed, o >> 3).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t seed, uint64_t idx) {
+    uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// L % 8 == 0: whole 8-byte words.  Piece j of the launch = global piece first + j.
+__global__ __launch_bounds__(256) void tv_fill_words_kernel(uint8_t* payload, uint64_t stride, uint64_t first,
+                                                            uint32_t n, uint64_t L, uint64_t seed) {
+    const uint64_t wpp = L / 8;
+    const uint64_t total = wpp * n;
+    for (uint64_t g = blockIdx.x * 256ull + threadIdx.x; g < total; g += (uint64_t)gridDim.x * 256ull) {
+        const uint64_t j = g / wpp, k = g - j * wpp;
+        const uint64_t o = (first + j) * L + 8 * k;
+        *reinterpret_cast<uint64_t*>(payload + j * stride + 8 * k) = splitmix64(seed, o >> 3);
+    }
+}
+
+__global__ __launch_bounds__(256) void tv_fill_bytes_kernel(uint8_t* payload, uint64_t stride, uint64_t first,
+                                                            uint32_t n, uint64_t L, uint64_t seed) {
+    const uint64_t total = L * n;
+    for (uint64_t g = blockIdx.x * 256ull + threadIdx.x; g < total; g += (uint64_t)gridDim.x * 256ull) {
+        const uint64_t j = g / L, k = g - j * L;
+        const uint64_t o = (first + j) * L + k;
+        payload[j * stride + k] = (uint8_t)(splitmix64(seed, o >> 3) >> (8 * (o & 7)));
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// host-side launchers (called by tv_api.hip)
+// ------------------------------------------------------------------------------------------
+hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_t s) {
+    if (p.n == 0) return hipSuccess;
+    if (kernel == TV_KERNEL_SPLIT) {
+        const unsigned grid = (p.n + 63) / 64;
+        if (hash) hipLaunchKernelGGL(tv_split_kernel<true>, dim3(grid), dim3(128), 0, s, p);
+        else hipLaunchKernelGGL(tv_split_kernel<false>, dim3(grid), dim3(128), 0, s, p);
+    } else {
+        const unsigned grid = (p.n + 255) / 256;
+        if (hash) hipLaunchKernelGGL(tv_lane_kernel<true>, dim3(grid), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL(tv_lane_kernel<false>, dim3(grid), dim3(256), 0, s, p);
+    }
+    return hipGetLastError();
+}
+
+hipError_t tv_launch_fill(uint8_t* payload, uint64_t stride, uint64_t first, uint32_t n, uint64_t L,
+                          uint64_t seed, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const unsigned grid = 256 * 32;
+    if (L % 8 == 0) hipLaunchKernelGGL(tv_fill_words_kernel, dim3(grid), dim3(256), 0, s, payload, stride, first, n, L, seed);
+    else hipLaunchKernelGGL(tv_fill_bytes_kernel, dim3(grid), dim3(256), 0, s, payload, stride, first, n, L, seed);
+    return hipGetLastError();
+}

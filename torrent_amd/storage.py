@@ -1,0 +1,185 @@
+"""Storage plugin API and the file-to-piece mapping, mirroring reference storage.ts.
+
+* StorageMethod {get, set, exists} is the reference's only plugin API (storage.ts:16-26).
+* Storage maps the linear torrent byte space to files (storage.ts:41-137).
+  `segments(offset, length)` is `findAndDo`'s walk (storage.ts:89-137) returned as data:
+  ordered (path, file_offset, n_bytes, slice_start) tuples.  It keeps the reference's
+  quirks: single-file paths are [*dir, name] (:99-101); multi-file paths are
+  [*dir, *file.path] WITHOUT info.name (:114); `fileEnd >= offset` emits a zero-length
+  segment at an exact file boundary (:109-110); a range past the last file fails (:136).
+* Any action failure or exception makes get() return None and set() return False
+  (storage.ts:130-136, 163-171).
+* fs_storage opens with read/write/create like OPEN_OPTIONS (storage.ts:28-32), so get() on
+  a missing file creates it empty and then fails the read -> None (storage_test.ts:59-62).
+
+The same segment walk produces the device offset table for multi-file torrents: the GPU
+path stages each segment at its linear offset, so pieces spanning file boundaries are
+contiguous in HBM (see verify.py).
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable, List, Optional, Protocol, Tuple
+
+from .piece import BLOCK_SIZE
+
+Segment = Tuple[List[str], int, int, int]  # (path, file_offset, n_bytes, slice_start)
+
+
+class StorageMethod(Protocol):
+    def get(self, path: List[str], offset: int, length: int) -> Optional[bytes]: ...
+
+    def set(self, path: List[str], offset: int, data: bytes) -> bool: ...
+
+    def exists(self, path: List[str]) -> bool: ...
+
+
+def _split_dir(dir_path: str) -> List[str]:
+    # storage.ts:45-48: relative(Deno.cwd(), dirPath).split(SEP), leading "" dropped
+    rel = os.path.relpath(dir_path, os.getcwd())
+    parts = rel.split(os.sep)
+    if rel == ".":
+        parts = [""]
+    if parts and parts[0] == "":
+        parts = parts[1:]
+    return parts
+
+
+class Storage:
+    """storage.ts:34-138."""
+
+    def __init__(self, method: StorageMethod, info, dir_path: str):
+        self.method = method
+        self.info = info
+        self.dir_path = _split_dir(dir_path)
+        self._written: dict = {}
+
+    # -- mapping ---------------------------------------------------------------------
+    def segments(self, offset: int, length: int) -> Optional[List[Segment]]:
+        """findAndDo's walk (storage.ts:89-137) without the action.  None = unmappable."""
+        if self.info.files is None:
+            return [([*self.dir_path, self.info.name], offset, length, 0)]
+        out: List[Segment] = []
+        i = 0
+        file_start = 0
+        for f in self.info.files:
+            file_end = file_start + f.length
+            if file_end >= offset:
+                n_bytes = min(file_end - offset - i, length - i)
+                file_offset = max(0, offset - file_start)
+                out.append(([*self.dir_path, *f.path], file_offset, n_bytes, i))
+                i += n_bytes
+                if i == length:
+                    return out
+            file_start = file_end
+        return None
+
+    def _find_and_do(self, offset: int, buf: bytearray | memoryview,
+                     action: Callable[[List[str], int, memoryview], bool]) -> bool:
+        try:
+            segs = self.segments(offset, len(buf))
+            if segs is None:
+                return False
+            mv = memoryview(buf)
+            for path, foff, n, start in segs:
+                if not action(path, foff, mv[start:start + n]):
+                    return False
+            return True
+        except Exception:
+            return False
+
+    # -- reference API -----------------------------------------------------------------
+    def get(self, offset: int, length: int) -> Optional[bytearray]:
+        """storage.ts:50-65."""
+        out = bytearray(length)
+
+        def act(path, foff, sl):
+            got = self.method.get(path, foff, len(sl))
+            if got is not None:
+                sl[:] = got
+            return got is not None
+
+        return out if self._find_and_do(offset, out, act) else None
+
+    def set(self, offset: int, data: bytes) -> bool:
+        """storage.ts:67-87 (blocks deduplicated by offset / BLOCK_SIZE)."""
+        index = offset / BLOCK_SIZE
+        if self._written.get(index):
+            return True
+        ok = self._find_and_do(offset, bytearray(data),
+                               lambda path, foff, sl: self.method.set(path, foff, bytes(sl)))
+        if ok:
+            self._written[index] = True
+        return ok
+
+
+class FsStorage:
+    """fsStorage (storage.ts:149-206)."""
+
+    def get(self, path: List[str], offset: int, length: int) -> Optional[bytes]:
+        p = os.path.join(*path)
+        try:
+            fd = os.open(p, os.O_RDWR | os.O_CREAT, 0o644)
+        except OSError:
+            return None
+        try:
+            data = os.pread(fd, length, offset) if length else b""
+            if len(data) != length:  # readN: UnexpectedEof (_bytes.ts:13-17)
+                return None
+            return data
+        except OSError:
+            return None
+        finally:
+            os.close(fd)
+
+    def set(self, path: List[str], offset: int, data: bytes) -> bool:
+        p = os.path.join(*path)
+        try:
+            try:
+                fd = os.open(p, os.O_RDWR | os.O_CREAT, 0o644)
+            except FileNotFoundError:
+                os.makedirs(os.path.dirname(p) or ".", exist_ok=True)
+                fd = os.open(p, os.O_RDWR | os.O_CREAT, 0o644)
+            try:
+                view = memoryview(data)
+                while view:
+                    n = os.pwrite(fd, view, offset)
+                    view = view[n:]
+                    offset += n
+            finally:
+                os.close(fd)
+            return True
+        except OSError:
+            return False
+
+    def exists(self, path: List[str]) -> bool:
+        return os.path.exists(os.path.join(*path))
+
+
+fs_storage = FsStorage()
+
+
+class MemoryStorage:
+    """An in-memory StorageMethod (tests / synthetic torrents): path tuple -> bytearray.
+    Missing path or a read past the end -> None, like fsStorage's EOF."""
+
+    def __init__(self, files: Optional[dict] = None):
+        self.files = {tuple(k): bytearray(v) for k, v in (files or {}).items()}
+
+    def get(self, path, offset, length):
+        f = self.files.get(tuple(path))
+        if f is None:
+            return None if length else b""
+        if offset + length > len(f):
+            return None
+        return bytes(f[offset:offset + length])
+
+    def set(self, path, offset, data):
+        f = self.files.setdefault(tuple(path), bytearray())
+        if len(f) < offset + len(data):
+            f.extend(b"\0" * (offset + len(data) - len(f)))
+        f[offset:offset + len(data)] = data
+        return True
+
+    def exists(self, path):
+        return tuple(path) in self.files

@@ -1,0 +1,215 @@
+"""Piece verification on MI355X -- the host-side mirror of the new `verify.ts` module.
+
+The reference (rclarey/torrent) has no verify function.  This module adds it
+by composing the reference's own pieces, exactly as SURVEY.md 3(D) states:
+
+    for i < P = info.pieces.length (metainfo.ts:16):
+        off_i = i * pieceLength                                   (torrent.ts:165)
+        len_i = pieceLength(i, info)                              (piece.ts:16-19)
+        bytes = storage.get(off_i, len_i)   # null => bit 0       (storage.ts:50-65)
+        bit i = SHA-1(bytes) == info.pieces[i]                    (make_torrent.ts:28-31)
+    bitfield: ceil(P/8) bytes, byte i>>3 |= 0x80 >> (i % 8)       (torrent.ts:53,60,147-149)
+
+The SHA-1 work runs in libtorrent_verify.so (HIP, gfx950): the bytes are staged into HBM and
+one kernel verifies every piece (one lane per piece).  There is no CPU fallback: without the
+library or a GPU these functions raise.
+
+Public API (names follow the reference's camelCase surface, snake_cased):
+    verify_pieces(info, storage, devices=None) -> bytearray         (verifyPieces)
+    verify_piece(info, index, data) -> bool                         (verifyPiece)
+    verify_payload(info, payload, devices=None, resident=True) -> bytearray
+    hash_pieces(payload, piece_length, devices=None) -> bytes       (creation mode, make_torrent.ts)
+and asyncio wrappers verify_pieces_async / verify_piece_async (the reference API is Promise-based).
+"""
+from __future__ import annotations
+
+import asyncio
+import threading
+from concurrent.futures import ThreadPoolExecutor
+from typing import List, Optional, Sequence
+
+from . import _native
+from .metainfo import InfoDict
+from .piece import piece_length
+
+# pieces gathered per tv_stage call when reading through a Storage
+_STAGE_BATCH_BYTES = 256 << 20
+
+
+def shard_ranges(n_pieces: int, n_shards: int) -> List[tuple]:
+    """Contiguous piece ranges, each starting at a multiple of 8 pieces so every shard's
+    bitfield slice is whole bytes.  Returns [(first, count), ...]."""
+    n_shards = max(1, n_shards)
+    per = -(-n_pieces // n_shards)
+    per = -(-per // 8) * 8
+    out = []
+    first = 0
+    for _ in range(n_shards):
+        count = max(0, min(per, n_pieces - first))
+        out.append((first, count))
+        first += count
+    return out
+
+
+def _set_bit(bf: bytearray, i: int) -> None:
+    bf[i >> 3] |= 0x80 >> (i & 7)
+
+
+def _concat(slices: Sequence[bytes], ranges: Sequence[tuple], n_pieces: int) -> bytearray:
+    out = bytearray((n_pieces + 7) // 8)
+    for (first, count), sl in zip(ranges, slices):
+        if count:
+            out[first // 8:first // 8 + len(sl)] = sl
+    return out
+
+
+_ctx_cache: dict = {}
+_ctx_lock = threading.Lock()
+
+
+def _context(device: int) -> _native.Context:
+    """One cached context per device per process (device memory is reused across calls)."""
+    with _ctx_lock:
+        c = _ctx_cache.get(device)
+        if c is None:
+            c = _native.Context(device)
+            _ctx_cache[device] = c
+        return c
+
+
+def _devices(devices) -> List[int]:
+    if devices is None:
+        return [0]
+    if isinstance(devices, int):
+        return list(range(devices))
+    return list(devices)
+
+
+def _run_shards(devs: List[int], n_pieces: int, fn):
+    ranges = shard_ranges(n_pieces, len(devs))
+    if len(devs) == 1:
+        return ranges, [fn(devs[0], *ranges[0])]
+    with ThreadPoolExecutor(len(devs)) as ex:  # ctypes releases the GIL inside each call
+        futs = [ex.submit(fn, d, f, c) for d, (f, c) in zip(devs, ranges)]
+        return ranges, [f.result() for f in futs]
+
+
+def verify_pieces(info: InfoDict, storage, devices=None) -> bytearray:
+    """verifyPieces(info, storage): have-bitfield of every piece read through `storage`
+    (a torrent_amd.storage.Storage, i.e. the reference's Storage over any StorageMethod)."""
+    P, L = info.n_pieces, info.piece_length
+
+    def shard(dev: int, first: int, count: int) -> bytes:
+        ctx = _context(dev)
+        ctx.set_layout(info.length, L, P, first, count)
+        ctx.set_digests(info.pieces_raw)
+        avail = bytearray((count + 7) // 8)
+        per_batch = max(1, _STAGE_BATCH_BYTES // max(1, L))
+        j = 0
+        while j < count:
+            k = min(per_batch, count - j)
+            buf = bytearray(k * L)
+            hi = 0
+            for q in range(k):
+                i = first + j + q
+                n = piece_length(i, info)
+                data = storage.get(i * L, n)  # storage.ts:50-65; None => unreadable => bit 0
+                if data is None:
+                    continue
+                buf[q * L:q * L + n] = data
+                hi = q * L + n
+                _set_bit(avail, j + q)
+            if hi:
+                ctx.stage((first + j) * L, memoryview(buf)[:hi])
+            j += k
+        return ctx.verify(avail)
+
+    if P == 0:
+        return bytearray()
+    ranges, slices = _run_shards(_devices(devices), P, shard)
+    return _concat(slices, ranges, P)
+
+
+def verify_payload(info: InfoDict, payload, devices=None, resident: bool = True,
+                   avail: Optional[bytes] = None) -> bytearray:
+    """Verify a linear payload already in host memory (the concatenation of info.files in
+    order).  resident=True stages it into HBM and verifies there; resident=False streams it
+    column by column over PCIe (tv_verify_host, the end-to-end resume-check path)."""
+    P, L = info.n_pieces, info.piece_length
+    mv = memoryview(payload).cast("B")
+
+    def shard(dev: int, first: int, count: int) -> bytes:
+        ctx = _context(dev)
+        ctx.set_layout(info.length, L, P, first, count)
+        ctx.set_digests(info.pieces_raw)
+        av = None
+        if avail is not None:
+            av = bytearray((count + 7) // 8)
+            for j in range(count):
+                i = first + j
+                if (avail[i >> 3] >> (7 - (i & 7))) & 1:
+                    _set_bit(av, j)
+        lo = min(first * L, len(mv))
+        hi = min((first + count) * L, len(mv))
+        if resident:
+            if hi > lo:
+                ctx.stage(lo, mv[lo:hi])
+            # pieces whose bytes are not all present are unreadable
+            have = bytearray((count + 7) // 8)
+            for j in range(count):
+                i = first + j
+                if i * L + piece_length(i, info) <= len(mv):
+                    _set_bit(have, j)
+            if av is not None:
+                have = bytearray(a & b for a, b in zip(have, av))
+            return ctx.verify(have)
+        return ctx.verify_host(mv[lo:hi] if hi > lo else b"", av)
+
+    if P == 0:
+        return bytearray()
+    ranges, slices = _run_shards(_devices(devices), P, shard)
+    return _concat(slices, ranges, P)
+
+
+def verify_piece(info: InfoDict, index: int, data) -> bool:
+    """verifyPiece(info, index, bytes): SHA-1(bytes) == info.pieces[index] for a piece of the
+    right length (piece.ts:16-19).  Raises ValueError for an index out of range (piece.ts:22)."""
+    if index < 0 or index >= info.n_pieces:
+        raise ValueError(f"verify_piece: invalid piece index {index}")
+    n = memoryview(data).nbytes
+    if n != piece_length(index, info) or len(info.pieces[index]) != 20 or n == 0:
+        return False
+    ctx = _context(0)
+    ctx.set_layout(n, n, 1, 0, 1)
+    ctx.set_digests(bytes(info.pieces[index]))
+    ctx.stage(0, data)
+    return bool(ctx.verify()[0] & 0x80)
+
+
+def hash_pieces(payload, piece_length_: int, devices=None) -> bytes:
+    """Creation mode: the `pieces` byte string for a linear payload (make_torrent.ts:147-173;
+    multi-file payloads are the files concatenated in order, make_torrent.ts:62-113)."""
+    mv = memoryview(payload).cast("B")
+    total = len(mv)
+    P = -(-total // piece_length_) if total else 0
+
+    def shard(dev: int, first: int, count: int) -> bytes:
+        ctx = _context(dev)
+        ctx.set_layout(total, piece_length_, P, first, count)
+        lo, hi = first * piece_length_, min(total, (first + count) * piece_length_)
+        if hi > lo:
+            ctx.stage(lo, mv[lo:hi])
+        return ctx.hash()
+
+    if P == 0:
+        return b""
+    _, slices = _run_shards(_devices(devices), P, shard)
+    return b"".join(slices)
+
+
+async def verify_pieces_async(info: InfoDict, storage, devices=None) -> bytearray:
+    return await asyncio.to_thread(verify_pieces, info, storage, devices)
+
+
+async def verify_piece_async(info: InfoDict, index: int, data) -> bool:
+    return await asyncio.to_thread(verify_piece, info, index, data)
