@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""Benchmark: verified GB/s of SHA-1 piece verification, HBM-resident (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg2|suppl|cfg4]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (default cfg2 = BASELINE.json configs[1]): a synthetic single-file torrent, 16 GiB per
+GPU, 1 MiB pieces (16,384 pieces per GPU).  Weak scaling: the torrent has N x 16,384 pieces and
+rank r verifies the contiguous shard [r*16384, (r+1)*16384) of it (shard start a multiple of 8 so
+its bitfield slice is whole bytes; no data-path collective exists).  The payload is generated in
+HBM by the device fill kernel (counter PRNG, the oracle's definition); expected digests are the
+GPU's own creation-mode digests, with 1 % of them corrupted so the expected bitfield is known, and
+a sample of them is checked against the CPU oracle.
+
+One step = one tv_verify of the rank's whole resident shard (upload availability bits, the verify
+kernel, bitfield download).  W untimed steps, then exactly K steps between a barrier +
+device synchronize on both sides; the time is the max over ranks.  value = total payload bytes
+of all ranks x K / time.
+
+The roofline object is for the verify kernel: algorithmic bytes per launch (the shard's payload
+bytes, SURVEY.md 8d: one byte read per payload byte) / the average kernel duration from HIP events
+recorded on the library's compute stream around each launch.  The cpu_baseline leg (rank 0, N=1)
+times the CPU oracle (a port of the reference's per-piece SHA-1 path) on a bounded sample of the
+same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from torrent_amd import _native  # noqa: E402  (load the HIP library before torch)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+WORKLOADS = {
+    # name: (piece_length, pieces per GPU, description)
+    "cfg2": (1 << 20, 16384, "cfg2: 16 GiB synthetic single-file torrent per GPU, 1 MiB pieces (16384 pieces), HBM-resident"),
+    "suppl": (256 << 10, 65536, "suppl: 16 GiB per GPU, 256 KiB pieces (65536 pieces), HBM-resident"),
+    "cfg4": (4 << 20, 51200, "cfg4: 200 GiB single-file torrent, 4 MiB pieces (51200 pieces per GPU at N=1), HBM-resident"),
+    "p262k": (64 << 10, 262144, "p262k: 16 GiB per GPU, 64 KiB pieces (262144 pieces), HBM-resident (VALU-saturating)"),
+}
+SEED = 2
+
+
+def _dist():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method="env://")
+        return dist, rank, ws, local
+    return None, 0, 1, 0
+
+
+def _barrier(dist):
+    if dist is not None:
+        dist.barrier()
+
+
+def _max(dist, x: float) -> float:
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _sum(dist, x: float) -> float:
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def _device_sync(ctx, local: int) -> None:
+    ctx.synchronize()
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize(local)
+    except Exception:
+        pass
+
+
+def cpu_baseline(L: int, total: int, P: int, first: int, gpu_digests: bytes, target_s: float = 10.0):
+    """Time the CPU oracle (C port of the per-piece SHA-1 path) on a bounded sample: the first
+    `n` pieces of this shard, generated once (not timed), hashed repeatedly for ~target_s.
+    Also checks the sample's digests against the GPU's (parity inside the bench)."""
+    from oracle import oracle as O
+    n = max(1, min(256, (256 << 20) // L))
+    cores = min(16, len(os.sched_getaffinity(0)))
+    buf = O.synth_fill(SEED, first * L, n * L)
+    # digests of the sample (piece-relative: a sub-torrent of n pieces of length L)
+    d = O.hash_pieces(buf, n * L, L, n, 0, n, threads=cores)
+    parity_ok = d == gpu_digests[: 20 * n]
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        O.hash_pieces(buf, n * L, L, n, 0, n, threads=cores)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= target_s:
+            break
+    gbps = reps * n * L / el / 1e9
+    return {"value": round(gbps, 3), "unit": "GB/s", "cores": cores, "kind": "port",
+            "sample": f"{n} pieces x {L >> 10} KiB of the same synthetic payload hashed {reps} times "
+                      f"({el:.1f} s) by oracle/sha1_oracle.c (scalar C SHA-1, one piece per task)",
+            "parity_vs_gpu": parity_ok}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
+    ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 lane, 2 split")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    a = ap.parse_args()
+
+    dist, rank, ws, local = _dist()
+    L, per_gpu, desc = WORKLOADS[a.workload]
+    P = per_gpu * ws
+    total = L * P
+    first = rank * per_gpu
+
+    ctx = _native.Context(local)
+    ctx.set_option(_native.TV_OPT_KERNEL, a.kernel)
+    ctx.set_layout(total, L, P, first, per_gpu)
+    ctx.fill_synthetic(SEED)
+    shard_digests = ctx.hash()                     # creation mode on the resident shard
+    # 1 % corrupted digests (every 100th piece, plus the shard's last) -> known expected bitfield
+    bad = set(range(0, per_gpu, 100)) | {per_gpu - 1}
+    dig = bytearray(shard_digests)
+    for j in bad:
+        dig[20 * j + 7] ^= 0x10
+    pieces = bytearray(20 * P)
+    pieces[20 * first:20 * (first + per_gpu)] = dig
+    ctx.set_digests(bytes(pieces))
+    expect = bytearray(b"\xff" * ((per_gpu + 7) // 8))
+    if per_gpu % 8:
+        expect[-1] = (0xFF00 >> (per_gpu % 8)) & 0xFF
+    for j in bad:
+        expect[j >> 3] &= ~(0x80 >> (j & 7)) & 0xFF
+
+    for _ in range(a.warmup):
+        bf = ctx.verify()
+    _device_sync(ctx, local)
+    _barrier(dist)
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        bf = ctx.verify()
+        kernel_ms.append(ctx.last_timing()[0])
+    _device_sync(ctx, local)
+    t1 = time.perf_counter()
+    _barrier(dist)
+    elapsed = _max(dist, t1 - t0)
+    correct = bf == bytes(expect)
+    all_correct = _sum(dist, 1.0 if correct else 0.0) == ws
+    kernel, _ = ctx.last_kernel()
+    avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
+    worst_kernel_ms = _max(dist, avg_kernel_ms)
+
+    bytes_per_gpu = L * per_gpu
+    value = bytes_per_gpu * ws * a.steps / elapsed / 1e9
+    achieved = bytes_per_gpu / (avg_kernel_ms / 1e3) / 1e9
+
+    if rank == 0:
+        traffic = None
+        tpath = os.path.join(ROOT, "profiles", f"traffic_{a.workload}.json")
+        if os.path.exists(tpath):
+            try:
+                traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out = {
+            "metric": "verified GB/s (SHA-1 pieces, HBM-resident)",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": ws,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed * 1e3 / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (device counter-PRNG payload; 1% corrupted digests)",
+            "config": {"workload": desc, "piece_length": L, "pieces_per_gpu": per_gpu,
+                       "total_pieces": P, "bytes_per_gpu": bytes_per_gpu,
+                       "kernel": {1: "lane", 2: "split"}.get(kernel, str(kernel)),
+                       "parallelism": f"piece shards x{ws}, no collective"},
+            "bitfield_exact": all_correct,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                         "kernel_ms_avg": round(avg_kernel_ms, 3), "kernel_ms_max_over_ranks": round(worst_kernel_ms, 3)},
+        }
+        if ws == 1 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(L, total, P, first, shard_digests, a.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0 if all_correct else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

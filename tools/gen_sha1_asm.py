@@ -37,10 +37,17 @@ import sys
 K = [0x5A827999, 0x6ED9EBA1, 0x8F1BBCDC, 0xCA62C1D6]
 M32 = 0xFFFFFFFF
 
-# physical VGPRs used by SHA1_LDS for its W ring (4 quads, 16-aligned is not required,
-# quad-aligned is).  The kernel's VGPR count is therefore >= RING_BASE + 16.
+# physical VGPRs used by SHA1_LDS for its K+W ring (quad-aligned; a 128-bit asm operand cannot
+# be split in AMDGPU asm).  The kernel's VGPR count is therefore >= RING_BASE + 4*RING_QUADS.
 RING_BASE = 64
-RING_QUADS = 4
+RING_QUADS = 8
+READ_AHEAD = 6      # quads in flight ahead of the one being consumed
+WAIT_EVERY = 2      # one s_waitcnt per 2 quads (8 rounds)
+# physical VGPRs of the helper (schedule) block: 16-word W window, xor3 temp, 3 output quads
+HW_BASE = 80
+HT = 96
+HOUT_BASE = 100
+HOUT_QUADS = 3
 
 
 def f_kind(t: int) -> str:
@@ -110,25 +117,25 @@ def ring_reg(q: int, j: int) -> str:
 
 
 def gen_lds():
-    """SHA1_LDS instruction list. Operands: r0-4 (out), t0-1 (tmp), h0-4 (in), addr (vgpr in),
-    k0-3 (sgpr in).  Reads quad g (W[4g..4g+3]) from addr + g*1024."""
+    """SHA1_LDS instruction list. Operands: r0-4 (out), t0-1 (tmp), h0-4 (in), addr (vgpr in).
+    Quad g (K+W[4g..4g+3], K pre-added by the helper) is read from addr + g*1024."""
     ins = [("s_waitcnt_lgkm", 0)]
-    ahead = RING_QUADS - 1
     issued = -1
-    for g in range(min(ahead, 20)):
+    for g in range(min(READ_AHEAD, 20)):
         ins.append(("ds_read_b128", g, g * 1024))
         issued = g
     R = Regs()
     for t in range(80):
         g = t // 4
-        if t % 4 == 0:
-            ins.append(("s_waitcnt_lgkm", issued - g))
+        if t % 4 == 0 and g % WAIT_EVERY == 0:
+            need = min(g + WAIT_EVERY - 1, 19)          # quads consumed before the next wait
+            ins.append(("s_waitcnt_lgkm", max(0, issued - need)))
         A, B, C, D, E = roles(t)
         e_src = R.rd(E)
-        ins.append(("v_add3_u32", R.wr(E), e_src, f"k{t // 20}", ring_reg(g, t % 4)))
-        if t % 4 == 3 and g + ahead < 20:
-            ins.append(("ds_read_b128", g + ahead, (g + ahead) * 1024))
-            issued = g + ahead
+        ins.append(("v_add_u32", R.wr(E), ring_reg(g, t % 4), e_src))
+        if t % 4 == 3 and g + READ_AHEAD < 20:
+            ins.append(("ds_read_b128", g + READ_AHEAD, (g + READ_AHEAD) * 1024))
+            issued = g + READ_AHEAD
         ins.append(("v_alignbit_b32", "t0", R.rd(A), R.rd(A), 27))
         ins.append(_fop(t, "t1", R.rd(B), R.rd(C), R.rd(D)))
         b_src = R.rd(B)
@@ -136,6 +143,88 @@ def gen_lds():
         ins.append(("v_add3_u32", R.rd(E), R.rd(E), "t0", "t1"))
     assert R.cur == [f"r{i}" for i in range(5)]
     return ins
+
+
+def hw(t: int) -> str:
+    return f"v{HW_BASE + (t & 15)}"
+
+
+def gen_helper(src=None, off_base: int = 0):
+    """Helper (schedule) block: src = 16 registers holding the block's words as loaded
+    (little-endian; default operands raw0-15), sel (sgpr 0x00010203), addr (vgpr, LDS byte address
+    of this lane in ring buffer 0), k0-3 (sgpr).  Writes K+W[t] for t = 0..79 to LDS at
+    addr + off_base + (t/4)*1024 as [t/4][lane][4] (one ds_write_b128 per quad)."""
+    if src is None:
+        src = [f"raw{i}" for i in range(16)]
+    ins = []
+    for i in range(16):
+        ins.append(("v_perm_b32", hw(i), 0, src[i], "sel"))
+    for q in range(20):
+        if q >= 4:
+            for i in range(4):
+                t = 4 * q + i
+                ins.append(("v_bitop3_b32", f"v{HT}", hw(t - 3), hw(t - 8), hw(t - 14), 0x96))
+                ins.append(("v_xor_b32", hw(t), f"v{HT}", hw(t)))
+                ins.append(("v_alignbit_b32", hw(t), hw(t), hw(t), 31))
+        o = HOUT_BASE + 4 * (q % HOUT_QUADS)
+        for j in range(4):
+            ins.append(("v_add_u32", f"v{o + j}", f"k{q // 5}", hw(4 * q + j)))
+        ins.append(("ds_write_b128", o, off_base + q * 1024))
+    return ins
+
+
+P0_BASE, P1_BASE, VL = 112, 128, 144   # prefetch buffers (2 blocks) and the running load pointer
+RING_BYTES = 80 * 64 * 4               # one K+W buffer
+
+
+def helper_loop_text() -> str:
+    """The helper wave's steady state as ONE asm statement (text, not emulated: its body is
+    gen_helper, which the emulator checks).  For each raw block: wait for its prefetched words,
+    byte-swap them, issue the loads 2 blocks ahead into the freed registers, expand the schedule,
+    write K+W to LDS, barrier.  Loads land in physical registers the compiler never sees, so no
+    compiler copy can touch an in-flight register and no compiler wait drains the prefetch."""
+    L = []
+
+    def loads(base):
+        for q in range(4):
+            L.append(f"global_load_dwordx4 v[{base + 4 * q}:{base + 4 * q + 3}], v[{VL}:{VL + 1}], off offset:{16 * q}")
+
+    def advance():
+        L.append("s_cmp_gt_u32 %[adv], 0")
+        L.append("s_cselect_b64 %[inc], 64, 0")
+        L.append("s_subb_u32 %[adv], %[adv], 0")
+        L.append(f"v_lshl_add_u64 v[{VL}:{VL + 1}], v[{VL}:{VL + 1}], 0, %[inc]")
+
+    def step(pbase, off_base):
+        L.append("s_waitcnt vmcnt(4)")
+        body = gen_helper([f"v{pbase + i}" for i in range(16)], off_base)
+        perms, rest = body[:16], body[16:]
+        L.extend(_emit_lines(perms))
+        loads(pbase)        # the perms have read pbase: refill it with the block 2 ahead
+        advance()
+        L.extend(_emit_lines(rest))
+        L.append("s_waitcnt lgkmcnt(0)")
+        L.append("s_barrier")
+
+    L.append("s_sub_u32 %[adv], %[nraw], 1")
+    L.append(f"v_mov_b64 v[{VL}:{VL + 1}], %[va]")
+    loads(P0_BASE)
+    advance()
+    loads(P1_BASE)
+    advance()
+    L.append("s_mov_b32 %[cnt], %[nraw]")
+    L.append("L_hloop_%=:")
+    step(P0_BASE, 0)
+    L.append("s_sub_u32 %[cnt], %[cnt], 1")
+    L.append("s_cmp_eq_u32 %[cnt], 0")
+    L.append("s_cbranch_scc1 L_hdone_%=")
+    step(P1_BASE, RING_BYTES)
+    L.append("s_sub_u32 %[cnt], %[cnt], 1")
+    L.append("s_cmp_lg_u32 %[cnt], 0")
+    L.append("s_cbranch_scc1 L_hloop_%=")
+    L.append("L_hdone_%=:")
+    L.append("s_waitcnt vmcnt(0)")
+    return "\n".join(f'    "{l}\\n"' for l in L)
 
 
 # ---------------------------------------------------------------- emulator -------------
@@ -166,6 +255,16 @@ def emulate(ins, regs: dict, lds: dict | None = None, addr: int = 0):
             regs[op[1]] = r
         elif o == "v_xor_b32":
             regs[op[1]] = v(op[2]) ^ v(op[3])
+        elif o == "v_add_u32":
+            regs[op[1]] = (v(op[2]) + v(op[3])) & M32
+        elif o == "v_perm_b32":
+            assert op[2] == 0 and regs[op[4]] == 0x00010203
+            x = v(op[3])
+            regs[op[1]] = int.from_bytes(x.to_bytes(4, "little"), "big")
+        elif o == "ds_write_b128":
+            base, off = op[1], op[2]
+            for j in range(4):
+                lds[addr + off + 4 * j] = regs[f"v{base + j}"]
         elif o == "ds_read_b128":
             q, off = op[1], op[2]
             for j in range(4):
@@ -205,11 +304,16 @@ def _check_block(block: bytes, h):
     emulate(gen_full(), regs)
     got = [(h[i] + regs[f"r{i}"]) & M32 for i in range(5)]
     assert got == exp, "SHA1_FULL mismatch"
-    # LDS
-    regs = dict(base)
+    # HELPER: raw little-endian words -> K+W[0..79] in LDS
+    regs = {"sel": 0x00010203}
+    regs.update({f"k{i}": K[i] for i in range(4)})
+    regs.update({f"raw{i}": int.from_bytes(block[4 * i:4 * i + 4], "little") for i in range(16)})
     lds = {}
+    emulate(gen_helper(), regs, lds, 0)
     for t in range(80):
-        lds[1024 * (t // 4) + 4 * (t % 4)] = ww[t]
+        assert lds[1024 * (t // 4) + 4 * (t % 4)] == (ww[t] + K[t // 20]) & M32, "SHA1_HELPER mismatch"
+    # LDS rounds consume the helper's output
+    regs = dict(base)
     emulate(gen_lds(), regs, lds, 0)
     got = [(h[i] + regs[f"r{i}"]) & M32 for i in range(5)]
     assert got == exp, "SHA1_LDS mismatch"
@@ -241,7 +345,7 @@ def _opnd(x, full: bool):
     return f"%[{x}]"
 
 
-def emit(ins, full: bool) -> str:
+def _emit_lines(ins, full: bool = False):
     lines = []
     for op in ins:
         o = op[0]
@@ -256,11 +360,19 @@ def emit(ins, full: bool) -> str:
                          f"{_opnd(op[4], full)} bitop3:0x{op[5]:02x}")
         elif o == "v_alignbit_b32":
             lines.append(f"v_alignbit_b32 {_opnd(op[1], full)}, {_opnd(op[2], full)}, {_opnd(op[3], full)}, {op[4]}")
-        elif o == "v_xor_b32":
-            lines.append(f"v_xor_b32 {_opnd(op[1], full)}, {_opnd(op[2], full)}, {_opnd(op[3], full)}")
+        elif o in ("v_xor_b32", "v_add_u32"):
+            lines.append(f"{o} {_opnd(op[1], full)}, {_opnd(op[2], full)}, {_opnd(op[3], full)}")
+        elif o == "v_perm_b32":
+            lines.append(f"v_perm_b32 {_opnd(op[1], full)}, 0, {_opnd(op[3], full)}, {_opnd(op[4], full)}")
+        elif o == "ds_write_b128":
+            lines.append(f"ds_write_b128 %[addr], v[{op[1]}:{op[1] + 3}] offset:{op[2]}")
         else:
             lines.append(f"{o} " + ", ".join(_opnd(x, full) for x in op[1:]))
-    return "\n".join(f'    "{l}\\n"' for l in lines)
+    return lines
+
+
+def emit(ins, full: bool) -> str:
+    return "\n".join(f'    "{l}\\n"' for l in _emit_lines(ins, full))
 
 
 HEADER = """// GENERATED by tools/gen_sha1_asm.py -- do not edit.  Regenerate with:
@@ -278,7 +390,9 @@ HEADER = """// GENERATED by tools/gen_sha1_asm.py -- do not edit.  Regenerate wi
 __device__ __forceinline__ void tv_sha1_full(const uint32_t h[5], uint32_t r[5], uint32_t w[16],
                                              uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {{
     uint32_t t0, t1, t2;
-    asm(
+    // volatile + "memory": the compiler may not move the caller's prefetch loads across the block
+    // (otherwise it sinks them next to their use and the load latency is exposed every block).
+    asm volatile(
 {full}
     : [r0] "=&v"(r[0]), [r1] "=&v"(r[1]), [r2] "=&v"(r[2]), [r3] "=&v"(r[3]), [r4] "=&v"(r[4]),
       [w0] "+v"(w[0]), [w1] "+v"(w[1]), [w2] "+v"(w[2]), [w3] "+v"(w[3]),
@@ -287,29 +401,65 @@ __device__ __forceinline__ void tv_sha1_full(const uint32_t h[5], uint32_t r[5],
       [w12] "+v"(w[12]), [w13] "+v"(w[13]), [w14] "+v"(w[14]), [w15] "+v"(w[15]),
       [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2)
     : [h0] "v"(h[0]), [h1] "v"(h[1]), [h2] "v"(h[2]), [h3] "v"(h[3]), [h4] "v"(h[4]),
-      [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3));
+      [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
+    : "memory");
 }}
 
-// The 80 rounds of one compression with W[0..79] read from LDS at byte address `addr`
-// (+ g*1024 for quad g).  Waits for all of its own LDS reads before returning.
-__device__ __forceinline__ void tv_sha1_lds(const uint32_t h[5], uint32_t r[5], uint32_t addr,
-                                            uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {{
+// The 80 rounds of one compression with K+W[0..79] read from LDS at byte address `addr`
+// (+ g*1024 for quad g), as written by tv_sha1_schedule_lds.  Waits for all of its own LDS reads
+// before returning.
+__device__ __forceinline__ void tv_sha1_lds(const uint32_t h[5], uint32_t r[5], uint32_t addr) {{
     uint32_t t0, t1;
     asm volatile(
 {lds}
     : [r0] "=&v"(r[0]), [r1] "=&v"(r[1]), [r2] "=&v"(r[2]), [r3] "=&v"(r[3]), [r4] "=&v"(r[4]),
       [t0] "=&v"(t0), [t1] "=&v"(t1)
-    : [h0] "v"(h[0]), [h1] "v"(h[1]), [h2] "v"(h[2]), [h3] "v"(h[3]), [h4] "v"(h[4]),
-      [addr] "v"(addr), [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
-    : {clobbers}, "memory");
+    : [h0] "v"(h[0]), [h1] "v"(h[1]), [h2] "v"(h[2]), [h3] "v"(h[3]), [h4] "v"(h[4]), [addr] "v"(addr)
+    : {ring_clobbers}, "memory");
+}}
+
+// The split kernel's helper wave over its nraw (>= 1) raw blocks: va = address of the first
+// block of this lane's piece, addr = LDS byte address of this lane in ring buffer 0.  One
+// workgroup barrier per block (matching the rounds wave).  Returns with no load in flight.
+__device__ __forceinline__ void tv_sha1_helper_loop(const void* va, uint32_t nraw, uint32_t addr,
+                                                    uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {{
+    uint32_t cnt, adv;
+    uint64_t inc;
+    asm volatile(
+{helper_loop}
+    : [cnt] "=&s"(cnt), [adv] "=&s"(adv), [inc] "=&s"(inc)
+    : [va] "v"(va), [nraw] "s"(nraw), [addr] "v"(addr), [sel] "s"(0x00010203u),
+      [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
+    : {loop_clobbers}, "scc", "memory");
+}}
+
+// Message schedule of one block for the split kernel's helper wave: raw[16] are the block's words
+// as loaded (little-endian); writes K+W[0..79] to LDS at `addr` (+ q*1024 for quad q).  The LDS
+// writes are left in flight (the caller's barrier waits lgkmcnt(0)).
+__device__ __forceinline__ void tv_sha1_schedule_lds(const uint32_t raw[16], uint32_t addr,
+                                                     uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {{
+    asm volatile(
+{helper}
+    :
+    : [raw0] "v"(raw[0]), [raw1] "v"(raw[1]), [raw2] "v"(raw[2]), [raw3] "v"(raw[3]),
+      [raw4] "v"(raw[4]), [raw5] "v"(raw[5]), [raw6] "v"(raw[6]), [raw7] "v"(raw[7]),
+      [raw8] "v"(raw[8]), [raw9] "v"(raw[9]), [raw10] "v"(raw[10]), [raw11] "v"(raw[11]),
+      [raw12] "v"(raw[12]), [raw13] "v"(raw[13]), [raw14] "v"(raw[14]), [raw15] "v"(raw[15]),
+      [addr] "v"(addr), [sel] "s"(0x00010203u), [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
+    : {helper_clobbers}, "memory");
 }}
 """
 
 
 def render() -> str:
-    clob = ", ".join(f'"v{RING_BASE + i}"' for i in range(4 * RING_QUADS))
+    ring = ", ".join(f'"v{RING_BASE + i}"' for i in range(4 * RING_QUADS))
+    hregs = list(range(HW_BASE, HW_BASE + 16)) + [HT] + list(range(HOUT_BASE, HOUT_BASE + 4 * HOUT_QUADS))
+    helper = ", ".join(f'"v{i}"' for i in hregs)
+    loop = ", ".join(f'"v{i}"' for i in hregs + list(range(P0_BASE, VL + 2)))
     return HEADER.format(ring_base=RING_BASE, ring_quads=RING_QUADS, full=emit(gen_full(), True),
-                         lds=emit(gen_lds(), False), clobbers=clob)
+                         lds=emit(gen_lds(), False), helper=emit(gen_helper(), False),
+                         helper_loop=helper_loop_text(), ring_clobbers=ring, helper_clobbers=helper,
+                         loop_clobbers=loop)
 
 
 def main():
@@ -324,9 +474,8 @@ def main():
     txt = render()
     with open(a.out, "w") as f:
         f.write(txt)
-    full = gen_full()
-    lds = gen_lds()
-    print(f"wrote {a.out}: FULL {len(full)} instr, LDS {len(lds)} instr")
+    print(f"wrote {a.out}: FULL {len(gen_full())} instr, LDS {len(gen_lds())} instr, "
+          f"HELPER {len(gen_helper())} instr")
 
 
 if __name__ == "__main__":

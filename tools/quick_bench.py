@@ -24,6 +24,8 @@ def run(total, L, kernels=(1, 2), reps=3, pad=None):
     ctx.close()
 
 if __name__ == "__main__":
-    run(16 << 30, 1 << 20)
-    run(16 << 30, 256 << 10)
-    run(4 << 30, 1 << 20)
+    run(16 << 30, 1 << 20)           # cfg2: 16384 pieces
+    run(16 << 30, 256 << 10)         # 65536 pieces
+    run(16 << 30, 128 << 10, (1,))   # 131072 pieces (lane)
+    run(16 << 30, 64 << 10, (1,))    # 262144 pieces (lane)
+    run(50 << 30, 4 << 20)           # cfg4 on one GPU: 12800 pieces x 4 MiB (quarter of cfg4)

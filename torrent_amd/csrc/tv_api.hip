@@ -355,7 +355,7 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
                     (unsigned long long)shard_count, (unsigned long long)n_pieces);
     if (shard_first % 8) return fail(c, TV_ERR_ARG, "shard_first must be a multiple of 8 (whole bitfield bytes)");
     if (shard_count >= 0xFFFFFFFFull) return fail(c, TV_ERR_ARG, "shard_count too large");
-    if (piece_length > (1ull << 40)) return fail(c, TV_ERR_ARG, "piece_length too large");
+    if (piece_length > (1ull << 36)) return fail(c, TV_ERR_ARG, "piece_length must be <= 64 GiB");
     TV_HIP(c, hipSetDevice(c->device));
     TV_HIP(c, hipStreamSynchronize(c->stream));
     TV_HIP(c, hipStreamSynchronize(c->copy_stream));
@@ -556,7 +556,10 @@ int tv_verify_host(tv_ctx* c, const uint8_t* src, uint64_t src_len, const uint8_
         c->chunk_bytes = row * n + kSlack;
     }
     hipPointerAttribute_t attr{};
-    bool pinned = hipPointerGetAttributes(&attr, src) == hipSuccess && attr.type == hipMemoryTypeHost;
+    // DMA straight from the caller's buffer only when it is page-locked (hipHostMalloc or
+    // hipHostRegister): such memory has a device mapping.  Pageable memory goes through the ring.
+    bool pinned = hipPointerGetAttributes(&attr, src) == hipSuccess && attr.type == hipMemoryTypeHost &&
+                  attr.devicePointer != nullptr;
     (void)hipGetLastError();
 
     const uint64_t ncol = (c->L + C - 1) / C;

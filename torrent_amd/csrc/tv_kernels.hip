@@ -10,10 +10,12 @@
 //   lane  : each lane loads its own 64-byte blocks (register prefetch, 2 blocks ahead) and runs
 //           the full compression (schedule + rounds) as one generated asm block (613 VALU/block).
 //   split : schedule offload.  A workgroup is 2 waves for 64 pieces: the helper wave loads the
-//           blocks and computes W[0..79] into an LDS double buffer; the rounds wave runs only
-//           the 80 rounds from LDS (400 VALU + 20 ds_read_b128 per block).  When there are
-//           fewer pieces than SIMDs x 2 waves, the per-lane serial issue rate is the bound, and
-//           this cuts the serial stream from ~613 to ~420 instructions per block.
+//           blocks and writes K+W[0..79] into an LDS double buffer (generated asm: v_perm bswap,
+//           v_bitop3 xor3, ds_write_b128); the rounds wave runs only the 80 rounds from LDS
+//           (400 VALU + 20 ds_read_b128 + 10 waits per block).  A lone wave issues one VALU per
+//           ~4.5 cycles whether or not it is dependent (tools/ubench_valu.hip), so with fewer
+//           pieces than SIMDs the per-lane instruction count IS the bound; this cuts the serial
+//           stream from ~630 to ~445 instructions per block.
 //
 // HBM layout: resident piece j (shard-local) starts at payload + j*stride, stride = L + pad
 // (pad breaks the power-of-two stride that would put all 64 lanes of a wave on one channel).
@@ -31,27 +33,40 @@
 namespace {
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
-__device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return __builtin_rotateleft32(x, n); }
 
 __device__ __forceinline__ void sha1_iv(uint32_t h[5]) {
     h[0] = 0x67452301u; h[1] = 0xEFCDAB89u; h[2] = 0x98BADCFEu; h[3] = 0x10325476u; h[4] = 0xC3D2E1F0u;
 }
 
 // Per-wave uniform geometry.  Every piece of a launch has length L except the global last
-// piece (launch-local index last_idx), which is always the final piece of the launch.
+// piece (launch-local index last_idx), which is always the final piece of the launch.  All
+// values are made provably wave-uniform (readfirstlane) so loop control stays scalar and the
+// prefetch loads are never predicated (a predicated load forces a vmcnt(0) + copy at the join).
 struct WaveGeom {
-    uint64_t nfull_min;  // min over the wave's lanes of len/64: blocks [.., nfull_min) are raw data for every lane
-    uint64_t nb_max;     // max over lanes of the padded block count ceil((len+9)/64)
+    uint32_t fast_begin;  // first block of this launch
+    uint32_t fast_end;    // blocks [fast_begin, fast_end) are raw data for EVERY lane of the wave
+    uint32_t end;         // blocks [.., end) are processed (max over lanes, clipped to blk_end)
+    uint32_t nb_min;      // every lane has at least nb_min blocks (no masking below it)
 };
 
 __device__ __forceinline__ uint64_t nblocks(uint64_t len) { return (len + 8) / 64 + 1; }
 
+__device__ __forceinline__ uint32_t uni(uint64_t x) {
+    return __builtin_amdgcn_readfirstlane((uint32_t)x);
+}
+
+// j0 must be wave-uniform (first piece of the wave).
 __device__ __forceinline__ WaveGeom wave_geom(const TvPieces& p, uint32_t j0) {
-    WaveGeom g;
     const bool has_last = p.last_idx != 0xFFFFFFFFu && (p.last_idx >> 6) == (j0 >> 6);
     const bool only_last = has_last && p.last_idx == j0;
-    g.nfull_min = (has_last ? p.last_len : p.L) / 64;
-    g.nb_max = nblocks(only_last ? p.last_len : p.L);
+    const uint64_t nfull_min = (has_last ? p.last_len : p.L) / 64;
+    const uint64_t nb_max = nblocks(only_last ? p.last_len : p.L);
+    const uint64_t nb_min = nblocks(has_last ? p.last_len : p.L);
+    WaveGeom g;
+    g.fast_begin = uni(p.blk_begin);
+    g.fast_end = uni(nfull_min < p.blk_end ? nfull_min : p.blk_end);
+    g.end = uni(nb_max < p.blk_end ? nb_max : p.blk_end);
+    g.nb_min = uni(nb_min);
     return g;
 }
 
@@ -92,8 +107,8 @@ __device__ __forceinline__ void build_tail_block(const uint8_t* piece, uint64_t 
     }
 }
 
-__device__ __forceinline__ void load_block(const uint8_t* piece, uint64_t b, uint4 (&r)[4]) {
-    const uint4* src = reinterpret_cast<const uint4*>(piece + b * 64);
+__device__ __forceinline__ void load_block(const uint8_t* piece, uint32_t b, uint4 (&r)[4]) {
+    const uint4* src = reinterpret_cast<const uint4*>(piece + (uint64_t)b * 64);
 #pragma unroll
     for (int i = 0; i < 4; i++) r[i] = src[i];
 }
@@ -141,7 +156,7 @@ __device__ __forceinline__ void finish(const TvPieces& p, uint32_t j, uint32_t j
     }
     bool ok = j < p.n;
 #pragma unroll
-    for (int k = 0; k < 5; k++) ok = ok && (h[k] == p.digests[(uint64_t)k * p.n + jj]);
+    for (int k = 0; k < 5; k++) ok &= (h[k] == p.digests[(uint64_t)k * p.n + jj]);
     const uint64_t mask = __ballot(ok);
     if ((threadIdx.x & 63) == 0) {
         // ballot bit l = piece j0+l  ->  MSB-first bytes: byte m holds pieces j0+8m .. j0+8m+7
@@ -167,39 +182,40 @@ __device__ __forceinline__ void start_state(const TvPieces& p, uint32_t jj, uint
 // ------------------------------------------------------------------------------------------
 template <bool HASH>
 __global__ __launch_bounds__(256) void tv_lane_kernel(TvPieces p) {
-    const uint32_t j = blockIdx.x * 256u + threadIdx.x;
-    const uint32_t jj = j < p.n ? j : p.n - 1;
-    const uint32_t j0 = blockIdx.x * 256u + (threadIdx.x & ~63u);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t j0 = blockIdx.x * 256u + wave * 64u;
     if (j0 >= p.n) return;  // wave-uniform: no piece in this wave
+    const uint32_t j = j0 + (threadIdx.x & 63u);
+    const uint32_t jj = j < p.n ? j : p.n - 1;
     const WaveGeom g = wave_geom(p, j0);
     const uint64_t len = lane_len(p, jj);
-    const uint64_t nb = nblocks(len);
+    const uint32_t nb = (uint32_t)nblocks(len);
     const uint8_t* piece = p.data + (uint64_t)jj * p.stride - p.data_off;
 
     uint32_t h[5];
     start_state(p, jj, h);
 
-    uint64_t b = p.blk_begin;
-    const uint64_t fast_end = g.nfull_min < p.blk_end ? g.nfull_min : p.blk_end;
-    const uint64_t end = g.nb_max < p.blk_end ? g.nb_max : p.blk_end;
+    uint32_t b = g.fast_begin;
     uint32_t w[16];
-
-    if (b < fast_end) {
+    if (b < g.fast_end) {
+        // Two register blocks in flight.  Loads are unconditional (the block index is clamped to
+        // the last raw block), so they are never predicated and stay in flight across a block.
+        const uint32_t last = g.fast_end - 1;
         uint4 A[4], B[4];
         load_block(piece, b, A);
-        if (b + 1 < fast_end) load_block(piece, b + 1, B);
+        load_block(piece, b + 1 < last ? b + 1 : last, B);
         for (;;) {
             bswap_block(A, w);
-            if (b + 2 < fast_end) load_block(piece, b + 2, A);
+            load_block(piece, b + 2 < last ? b + 2 : last, A);
             compress_full(h, w);
-            if (++b >= fast_end) break;
+            if (++b >= g.fast_end) break;
             bswap_block(B, w);
-            if (b + 2 < fast_end) load_block(piece, b + 2, B);
+            load_block(piece, b + 2 < last ? b + 2 : last, B);
             compress_full(h, w);
-            if (++b >= fast_end) break;
+            if (++b >= g.fast_end) break;
         }
     }
-    for (; b < end; b++) {
+    for (; b < g.end; b++) {
         build_tail_block(piece, len, b, w);
         uint32_t r[5];
         tv_sha1_full(h, r, w, TV_K0, TV_K1, TV_K2, TV_K3);
@@ -219,22 +235,6 @@ namespace {
 
 constexpr int kRingWords = 80 * 64;  // one buffer: [20 quads][64 lanes][4 words]
 
-// Helper: W[0..79] of one block into LDS buffer `buf` as [t/4][lane][4].
-__device__ __forceinline__ void schedule_to_lds(uint32_t w[16], uint4* buf, uint32_t lane) {
-#pragma unroll
-    for (int q = 0; q < 20; q++) {
-        if (q >= 4) {
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const int t = 4 * q + i;
-                w[t & 15] = rotl(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
-            }
-        }
-        const int t = 4 * q;
-        buf[q * 64 + lane] = make_uint4(w[t & 15], w[(t + 1) & 15], w[(t + 2) & 15], w[(t + 3) & 15]);
-    }
-}
-
 __device__ __forceinline__ void lds_barrier() {
     // LDS writes of this wave complete, then the workgroup barrier.  Deliberately NOT
     // __syncthreads(): the helper's global prefetch loads must stay in flight across it.
@@ -253,40 +253,28 @@ __global__ __launch_bounds__(128) void tv_split_kernel(TvPieces p) {
     const uint32_t jj = j < p.n ? j : p.n - 1;
     const WaveGeom g = wave_geom(p, j0);
     const uint64_t len = lane_len(p, jj);
-    const uint64_t nb = nblocks(len);
+    const uint32_t nb = (uint32_t)nblocks(len);
     const uint8_t* piece = p.data + (uint64_t)jj * p.stride - p.data_off;
-
-    const uint64_t b0 = p.blk_begin;
-    const uint64_t fast_end = g.nfull_min < p.blk_end ? g.nfull_min : p.blk_end;
-    const uint64_t end = g.nb_max < p.blk_end ? g.nb_max : p.blk_end;
+    const uint32_t b0 = g.fast_begin, end = g.end, fast_end = g.fast_end;
 
     if (wave != 0) {
         // ---------------- helper wave ----------------
-        uint32_t w[16];
-        uint4 A[4], B[4];
-        auto stage = [&](uint64_t b, uint4 (&raw)[4]) {
-            uint4* buf = ring + ((b - b0) & 1) * (kRingWords / 4);
-            if (b < fast_end) {
-                bswap_block(raw, w);
-                if (b + 2 < fast_end) load_block(piece, b + 2, raw);
-            } else {
-                build_tail_block(piece, len, b, w);
-            }
-            schedule_to_lds(w, buf, lane);
-        };
-        if (b0 < end) {
-            if (b0 < fast_end) load_block(piece, b0, A);
-            if (b0 + 1 < fast_end) load_block(piece, b0 + 1, B);
-            stage(b0, A);
+        // Raw blocks [b0, fast_end): one asm loop (loads 2 blocks ahead into registers the compiler
+        // never allocates, schedule, K+W -> LDS, barrier per block).  Then the 1-2 padded tail blocks
+        // (and one spare block past `end` that the rounds wave never reads) in C++.
+        const uint32_t lds_lane = (uint32_t)(uintptr_t)(void*)ring + lane * 16u;
+        uint32_t b = b0;
+        if (fast_end > b0) {
+            tv_sha1_helper_loop(piece + (uint64_t)b0 * 64, fast_end - b0, lds_lane, TV_K0, TV_K1, TV_K2, TV_K3);
+            b = fast_end;
         }
-        lds_barrier();
-        for (uint64_t b = b0; b < end;) {
-            if (b + 1 < end) stage(b + 1, B);
+        for (; b <= end; b++) {
+            uint32_t w[16];
+            build_tail_block(piece, len, b, w);
+#pragma unroll
+            for (int i = 0; i < 16; i++) w[i] = bswap32(w[i]);  // the schedule block byte-swaps
+            tv_sha1_schedule_lds(w, lds_lane + ((b - b0) & 1u) * (kRingWords * 4u), TV_K0, TV_K1, TV_K2, TV_K3);
             lds_barrier();
-            if (++b >= end) break;
-            if (b + 1 < end) stage(b + 1, A);
-            lds_barrier();
-            ++b;
         }
         return;
     }
@@ -295,11 +283,11 @@ __global__ __launch_bounds__(128) void tv_split_kernel(TvPieces p) {
     uint32_t h[5];
     start_state(p, jj, h);
     const uint32_t ring_base = (uint32_t)(uintptr_t)(void*)ring + lane * 16u;
-    const uint64_t nb_min = g.nfull_min + 1;  // every lane has >= nfull_min + 1 blocks
+    const uint32_t nb_min = g.nb_min;
     lds_barrier();
-    for (uint64_t b = b0; b < end; b++) {
+    for (uint32_t b = b0; b < end; b++) {
         uint32_t r[5];
-        tv_sha1_lds(h, r, ring_base + (uint32_t)((b - b0) & 1) * (kRingWords * 4), TV_K0, TV_K1, TV_K2, TV_K3);
+        tv_sha1_lds(h, r, ring_base + ((b - b0) & 1u) * (kRingWords * 4u));
         if (b < nb_min || b < nb) {
 #pragma unroll
             for (int i = 0; i < 5; i++) h[i] += r[i];
