@@ -38,6 +38,12 @@ sys.path.insert(0, ROOT)
 from torrent_amd import _native  # noqa: E402  (load the HIP library before torch)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# SHA-1 VALU roofline: 1024 SIMDs x 64 lanes / 4 cycles per wave64 integer VOP3 instruction
+# (measured: tools/ubench_sha1.hip) x 2.4 GHz, 613 VALU per 64-B compression.
+CLOCK_HZ = 2.4e9
+VALU_PEAK_GBPS = 1024 * 64 / 4 * CLOCK_HZ / 613 * 64 / 1e9
+LONE_WAVE_CYC = 4.34          # cycles per VALU instruction of a lone wave (measured)
+SERIAL_INSTR = {1: 613, 2: 405}  # per-block serial stream: lane kernel / split rounds wave
 
 WORKLOADS = {
     # name: (piece_length, pieces per GPU, description)
@@ -176,6 +182,7 @@ def main() -> int:
     bytes_per_gpu = L * per_gpu
     value = bytes_per_gpu * ws * a.steps / elapsed / 1e9
     achieved = bytes_per_gpu / (avg_kernel_ms / 1e3) / 1e9
+    piece_ceiling = min(VALU_PEAK_GBPS, per_gpu * 64 * CLOCK_HZ / (SERIAL_INSTR.get(kernel, 613) * LONE_WAVE_CYC) / 1e9)
 
     if rank == 0:
         traffic = None
@@ -205,7 +212,14 @@ def main() -> int:
             "bitfield_exact": all_correct,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel_ms_avg": round(avg_kernel_ms, 3), "kernel_ms_max_over_ranks": round(worst_kernel_ms, 3)},
+                         "kernel_ms_avg": round(avg_kernel_ms, 3), "kernel_ms_max_over_ranks": round(worst_kernel_ms, 3),
+                         "algorithmic_bytes_per_launch": bytes_per_gpu,
+                         "valu_peak": round(VALU_PEAK_GBPS, 1),
+                         "frac_of_valu_peak": round(achieved / VALU_PEAK_GBPS, 4),
+                         "piece_parallelism_ceiling": round(piece_ceiling, 1),
+                         "frac_of_piece_ceiling": round(achieved / piece_ceiling, 4),
+                         "note": "SHA-1 is VALU-bound on MI355X (4 cyc/wave64 int VOP3); serial per piece, so "
+                                 "P pieces cap the rate at P x 64 B / (serial instr x 4.34 cyc) per GPU"},
         }
         if ws == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(L, total, P, first, shard_digests, a.cpu_seconds)

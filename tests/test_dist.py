@@ -1,0 +1,74 @@
+"""N>1 path on CPU: world_size-2 gloo processes, each verifying its 8-aligned piece shard.
+
+This is the multi-GPU decomposition of bench.py / verify.shard_ranges: contiguous shards,
+no data-path collective, bitfield slices concatenated by byte position; torch.distributed only for
+barrier / max-over-ranks timing / correctness sum (bench._max, bench._sum).  The per-shard verify
+here is the CPU oracle (the checker), since this container has no GPU; the GPU shard path itself is
+tests/test_gpu_parity.py::test_shards_concatenate.
+"""
+import os
+import socket
+
+import pytest
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws),
+                      LOCAL_RANK=str(rank))
+    import bench
+    from oracle import oracle as O
+    from torrent_amd.verify import shard_ranges
+    dist, r, w, _ = bench._dist()
+    assert (r, w) == (rank, ws)
+    L, P = 4096, 203
+    total = L * (P - 1) + 999
+    payload = O.synth_fill(9, 0, total)
+    pieces = bytearray(O.hash_pieces(payload, total, L, P))
+    for i in range(0, P, 17):
+        pieces[20 * i + 3] ^= 1
+    first, count = shard_ranges(P, w)[r]
+    assert first % 8 == 0
+    full = O.verify_linear(payload, total, L, bytes(pieces))
+    # shard-local verify: bits of pieces [first, first+count) (oracle as the stand-in worker)
+    sl = bytearray((count + 7) // 8)
+    for j in range(count):
+        i = first + j
+        if (full[i >> 3] >> (7 - (i & 7))) & 1:
+            sl[j >> 3] |= 0x80 >> (j & 7)
+    bench._barrier(dist)
+    t = bench._max(dist, float(r + 1))
+    ok = bench._sum(dist, 1.0)
+    gathered = [None] * w
+    dist.all_gather_object(gathered, (first, bytes(sl)))
+    out = bytearray((P + 7) // 8)
+    for f, b in gathered:
+        out[f // 8:f // 8 + len(b)] = b
+    q.put((r, t, ok, bytes(out) == full))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ws", [2])
+def test_gloo_two_ranks_shard_and_reduce(ws):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(ws)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r, t, ok, match in res:
+        assert t == float(ws)      # max over ranks
+        assert ok == float(ws)     # sum over ranks
+        assert match               # concatenated slices == single-shard bitfield

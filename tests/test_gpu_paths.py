@@ -1,0 +1,162 @@
+"""GPU parity through the host-side API (verify_pieces / verify_payload / verify_piece / hash_pieces)
+on the reference's own fixtures, the seeded multi-file layouts (incl. BASELINE config 3) and a
+full-size config-2 run checked through size-independent properties."""
+import hashlib
+import json
+import os
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _load(name):
+    with open(os.path.join(GOLDEN, name), "rb") as f:
+        return f.read()
+
+
+def _ref_payload(name):
+    rd = json.load(open(os.path.join(GOLDEN, "refdata.json")))[name]
+    return b"".join(f["pattern"].encode() * (f["length"] // len(f["pattern"])) for f in rd["files"])
+
+
+def _all_ones(P):
+    b = bytearray(b"\xff" * (P // 8))
+    if P % 8:
+        b.append((0xFF00 >> (P % 8)) & 0xFF)
+    return bytes(b)
+
+
+@pytest.mark.parametrize("name", ["singlefile", "multifile"])
+@pytest.mark.parametrize("resident", [True, False])
+def test_reference_fixtures_on_gpu(native, name, resident):
+    """The reference's test_data digests (produced by its own SHA-1 path) verify on the GPU:
+    all 1706 / 1855 pieces, including the short final piece and the file-spanning piece #852."""
+    from torrent_amd import parse_metainfo, verify_payload
+    info = parse_metainfo(_load(f"{name}.torrent")).info
+    payload = bytearray(_ref_payload(name))
+    P = info.n_pieces
+    assert bytes(verify_payload(info, payload, resident=resident)) == _all_ones(P)
+    flips = [0, 852, P - 1]
+    for i in flips:
+        payload[i * info.piece_length + 3] ^= 0x01
+    bf = verify_payload(info, payload, resident=resident)
+    for i in range(P):
+        assert ((bf[i >> 3] >> (7 - (i & 7))) & 1) == (0 if i in flips else 1), i
+
+
+def test_reference_multifile_through_storage(native):
+    """verify_pieces(info, Storage(...)) -- the reference-shaped API over its StorageMethod plugin --
+    on the multifile fixture (two files, piece #852 spans them)."""
+    from torrent_amd import MemoryStorage, Storage, parse_metainfo, verify_pieces
+    info = parse_metainfo(_load("multifile.torrent")).info
+    payload = _ref_payload("multifile")
+    n0 = info.files[0].length
+    mem = MemoryStorage({tuple(info.files[0].path): payload[:n0], tuple(info.files[1].path): payload[n0:]})
+    st = Storage(mem, info, os.getcwd())
+    assert bytes(verify_pieces(info, st)) == _all_ones(info.n_pieces)
+    # truncate file 2 (a short file on disk): pieces touching the missing tail are unreadable -> 0
+    mem.files[tuple(info.files[1].path)] = mem.files[tuple(info.files[1].path)][:1000]
+    bf = verify_pieces(info, Storage(mem, info, os.getcwd()))
+    L = info.piece_length
+    for i in range(info.n_pieces):
+        end = i * L + (info.length % L if i == info.n_pieces - 1 else L)
+        readable = end <= n0 + 1000
+        assert ((bf[i >> 3] >> (7 - (i & 7))) & 1) == (1 if readable else 0), i
+
+
+@pytest.mark.parametrize("layout", ["single_short_last", "multi_zero_tiny", "many_tiny_span",
+                                    "missing_and_short", "exact_multiple", "cfg3"])
+def test_golden_layouts_on_gpu(native, layout):
+    """Seeded layouts: GPU bitfield == committed expected bitfield (hashlib-computed)."""
+    from tests.layouts import build_layout, by_name
+    from torrent_amd import verify_payload
+    rec = {r["name"]: r for r in json.load(open(os.path.join(GOLDEN, "layouts.json")))}[layout]
+    lay = build_layout(by_name(layout))
+    assert hashlib.sha1(lay["pieces_raw"]).hexdigest() == rec["pieces_sha1"]
+    bf = verify_payload(lay["info"], lay["payload"], avail=lay["avail"])
+    assert bytes(bf).hex() == rec["expected_bitfield"]
+    for i in lay["corrupted"]:
+        assert not (bf[i >> 3] >> (7 - (i & 7))) & 1
+
+
+@pytest.mark.parametrize("layout", ["multi_zero_tiny", "missing_and_short"])
+def test_layout_through_fs_storage(native, tmp_path, layout):
+    """Real files on disk through fs_storage (missing / truncated files included)."""
+    from tests.layouts import build_layout, by_name
+    from torrent_amd import Storage, fs_storage, verify_pieces
+    rec = {r["name"]: r for r in json.load(open(os.path.join(GOLDEN, "layouts.json")))}[layout]
+    lay = build_layout(by_name(layout))
+    for path, data in lay["disk_files"]().items():
+        p = tmp_path.joinpath(*path)
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_bytes(data)
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        bf = verify_pieces(lay["info"], Storage(fs_storage, lay["info"], str(tmp_path)))
+    finally:
+        os.chdir(cwd)
+    assert bytes(bf).hex() == rec["expected_bitfield"]
+
+
+def test_creation_mode_matches_reference_digests(native):
+    """hash_pieces (GPU creation mode, make_torrent.ts:147-173) reproduces info.pieces."""
+    from torrent_amd import hash_pieces, parse_metainfo
+    info = parse_metainfo(_load("multifile.torrent")).info
+    assert hash_pieces(_ref_payload("multifile"), info.piece_length) == info.pieces_raw
+
+
+def test_verify_piece_api(native):
+    from torrent_amd import parse_metainfo, verify_piece
+    info = parse_metainfo(_load("singlefile.torrent")).info
+    payload = _ref_payload("singlefile")
+    L, P = info.piece_length, info.n_pieces
+    assert verify_piece(info, 0, payload[:L])
+    assert verify_piece(info, P - 1, payload[(P - 1) * L:])          # short final piece
+    assert not verify_piece(info, 1, payload[:L - 1])                # wrong length
+    bad = bytearray(payload[:L]); bad[5] ^= 1
+    assert not verify_piece(info, 0, bad)
+    with pytest.raises(ValueError):
+        verify_piece(info, P, b"x")
+
+
+def test_multi_device_api_on_one_gpu(native, oracle):
+    """devices=[0, 0, 0]: three shards on the same GPU, concatenated (the multi-GPU host path)."""
+    from torrent_amd import make_info, verify_payload
+    L, P = 8192, 300
+    total = L * (P - 1) + 4000
+    payload = oracle.synth_fill(31, 0, total)
+    pieces = bytearray(oracle.hash_pieces(payload, total, L, P))
+    for i in (5, 150, 299):
+        pieces[20 * i] ^= 2
+    info = make_info(L, bytes(pieces), "x", length=total)
+    exp = oracle.verify_linear(payload, total, L, bytes(pieces))
+    assert bytes(verify_payload(info, payload, devices=[0, 0, 0])) == exp
+
+
+def test_full_size_cfg2_properties(native, oracle):
+    """BASELINE config 2 at full size (16 GiB, 16,384 x 1 MiB, HBM-resident), checked through
+    size-independent properties: creation-mode digests of a sample match the oracle; verify with
+    those digests is all ones; corrupting 1 % of digests clears exactly those bits; both kernels agree."""
+    L, P = 1 << 20, 16384
+    total = L * P
+    sample = list(range(0, 64)) + [8191, 8192, P - 1]
+    with native.Context(0) as ctx:
+        ctx.set_layout(total, L, P)
+        ctx.fill_synthetic(2)
+        dig = ctx.hash()
+        for i in sample:
+            assert dig[20 * i:20 * i + 20] == oracle.synth_piece_digests(2, total, L, P, i, 1), i
+        bad = set(range(3, P, 97))
+        d2 = bytearray(dig)
+        for i in bad:
+            d2[20 * i + 19] ^= 0x80
+        ctx.set_digests(bytes(d2))
+        for k in (1, 2):
+            ctx.set_option(native.TV_OPT_KERNEL, k)
+            bf = ctx.verify()
+            for i in range(P):
+                assert ((bf[i >> 3] >> (7 - (i & 7))) & 1) == (0 if i in bad else 1)

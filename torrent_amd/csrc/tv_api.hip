@@ -158,9 +158,10 @@ int upload_avail(tv_ctx* c, const uint8_t* avail_bits) {
 
 int choose_kernel(const tv_ctx* c) {
     if (c->kernel_opt == TV_KERNEL_LANE || c->kernel_opt == TV_KERNEL_SPLIT) return c->kernel_opt;
-    // Split (schedule offload) while the split workgroups fit co-resident: 4 x 40 KiB LDS per
-    // CU x 256 CUs x 64 pieces.  Above that the lane kernel fills >= 1 wave per SIMD on its own.
-    return c->count <= 65536 ? TV_KERNEL_SPLIT : TV_KERNEL_LANE;
+    // Split (schedule offload) while its rounds waves and helper waves do not share SIMDs
+    // (<= 2 workgroups of 64 pieces per CU, 256 CUs); with more pieces the lane kernel already has
+    // about one wave per SIMD and the SIMDs' VALU, not the per-lane stream, is the bound.
+    return c->count <= 40000 ? TV_KERNEL_SPLIT : TV_KERNEL_LANE;
 }
 
 TvPieces resident_launch(const tv_ctx* c) {

@@ -18,6 +18,7 @@ contiguous in HBM (see verify.py).
 """
 from __future__ import annotations
 
+import bisect
 import os
 from typing import Callable, List, Optional, Protocol, Tuple
 
@@ -53,16 +54,29 @@ class Storage:
         self.info = info
         self.dir_path = _split_dir(dir_path)
         self._written: dict = {}
+        self._ends: Optional[List[int]] = None  # cumulative file ends (lazy)
 
     # -- mapping ---------------------------------------------------------------------
     def segments(self, offset: int, length: int) -> Optional[List[Segment]]:
         """findAndDo's walk (storage.ts:89-137) without the action.  None = unmappable."""
         if self.info.files is None:
             return [([*self.dir_path, self.info.name], offset, length, 0)]
+        if self._ends is None:
+            ends, acc = [], 0
+            for f in self.info.files:
+                acc += f.length
+                ends.append(acc)
+            self._ends = ends
+        ends = self._ends
+        # the reference walks every file from the first (storage.ts:105-128) and acts on the first
+        # file whose end is >= offset; files before it do nothing, so start there (bisect).
+        k = bisect.bisect_left(ends, offset)
         out: List[Segment] = []
         i = 0
-        file_start = 0
-        for f in self.info.files:
+        file_start = ends[k - 1] if k > 0 else 0
+        files = self.info.files
+        for idx in range(k, len(files)):
+            f = files[idx]
             file_end = file_start + f.length
             if file_end >= offset:
                 n_bytes = min(file_end - offset - i, length - i)

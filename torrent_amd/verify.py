@@ -67,13 +67,14 @@ _ctx_cache: dict = {}
 _ctx_lock = threading.Lock()
 
 
-def _context(device: int) -> _native.Context:
-    """One cached context per device per process (device memory is reused across calls)."""
+def _context(device: int, slot: int = 0) -> _native.Context:
+    """One cached context per (device, shard slot) per process: device memory is reused across
+    calls, and concurrent shards never share a context (a device may appear several times)."""
     with _ctx_lock:
-        c = _ctx_cache.get(device)
+        c = _ctx_cache.get((device, slot))
         if c is None:
             c = _native.Context(device)
-            _ctx_cache[device] = c
+            _ctx_cache[(device, slot)] = c
         return c
 
 
@@ -86,11 +87,13 @@ def _devices(devices) -> List[int]:
 
 
 def _run_shards(devs: List[int], n_pieces: int, fn):
+    """fn(ctx, first, count) for each shard, one thread per shard (ctypes releases the GIL)."""
     ranges = shard_ranges(n_pieces, len(devs))
+    ctxs = [_context(d, s) for s, d in enumerate(devs)]
     if len(devs) == 1:
-        return ranges, [fn(devs[0], *ranges[0])]
-    with ThreadPoolExecutor(len(devs)) as ex:  # ctypes releases the GIL inside each call
-        futs = [ex.submit(fn, d, f, c) for d, (f, c) in zip(devs, ranges)]
+        return ranges, [fn(ctxs[0], *ranges[0])]
+    with ThreadPoolExecutor(len(devs)) as ex:
+        futs = [ex.submit(fn, c, f, n) for c, (f, n) in zip(ctxs, ranges)]
         return ranges, [f.result() for f in futs]
 
 
@@ -99,8 +102,7 @@ def verify_pieces(info: InfoDict, storage, devices=None) -> bytearray:
     (a torrent_amd.storage.Storage, i.e. the reference's Storage over any StorageMethod)."""
     P, L = info.n_pieces, info.piece_length
 
-    def shard(dev: int, first: int, count: int) -> bytes:
-        ctx = _context(dev)
+    def shard(ctx, first: int, count: int) -> bytes:
         ctx.set_layout(info.length, L, P, first, count)
         ctx.set_digests(info.pieces_raw)
         avail = bytearray((count + 7) // 8)
@@ -138,8 +140,7 @@ def verify_payload(info: InfoDict, payload, devices=None, resident: bool = True,
     P, L = info.n_pieces, info.piece_length
     mv = memoryview(payload).cast("B")
 
-    def shard(dev: int, first: int, count: int) -> bytes:
-        ctx = _context(dev)
+    def shard(ctx, first: int, count: int) -> bytes:
         ctx.set_layout(info.length, L, P, first, count)
         ctx.set_digests(info.pieces_raw)
         av = None
@@ -193,8 +194,7 @@ def hash_pieces(payload, piece_length_: int, devices=None) -> bytes:
     total = len(mv)
     P = -(-total // piece_length_) if total else 0
 
-    def shard(dev: int, first: int, count: int) -> bytes:
-        ctx = _context(dev)
+    def shard(ctx, first: int, count: int) -> bytes:
         ctx.set_layout(total, piece_length_, P, first, count)
         lo, hi = first * piece_length_, min(total, (first + count) * piece_length_)
         if hi > lo:

@@ -1,0 +1,174 @@
+// ts/verify.ts -- Deno binding of libtorrent_verify.so: the new verify module for rclarey/torrent.
+//
+// Drop-in position: next to piece.ts / storage.ts in the reference.  It imports only the
+// reference's own types (InfoDict from metainfo.ts:12-44, Storage from storage.ts:34-138,
+// pieceLength rule of piece.ts:16-19) and replaces nothing: callers of Storage / InfoDict /
+// Torrent are unaffected.  The SHA-1 arithmetic that the reference runs through
+// crypto.subtle.digest("SHA-1", content) (tools/make_torrent.ts:28-31) runs on the GPU here.
+//
+// Requires: deno run --unstable --allow-ffi (Deno 1.x, as the reference CI: .github/workflows/main.yml:14).
+// NOTE: Deno is not installed in the build container, so this file is exercised only through the
+// identical C ABI from Python (torrent_amd/_native.py, tests/test_gpu_parity.py).
+
+import type { InfoDict } from "../metainfo.ts";
+import type { Storage } from "../storage.ts";
+
+const SYMBOLS = {
+  tv_abi_version: { parameters: [], result: "i32" },
+  tv_device_count: { parameters: ["pointer"], result: "i32" },
+  tv_create: { parameters: ["pointer", "i32"], result: "i32" },
+  tv_destroy: { parameters: ["pointer"], result: "void" },
+  tv_last_error: { parameters: ["pointer", "pointer", "usize"], result: "i32" },
+  tv_set_layout: { parameters: ["pointer", "u64", "u64", "u64", "u64", "u64"], result: "i32" },
+  tv_set_digests: { parameters: ["pointer", "pointer", "u64"], result: "i32" },
+  tv_stage: { parameters: ["pointer", "u64", "pointer", "u64"], result: "i32", nonblocking: true },
+  tv_fill_synthetic: { parameters: ["pointer", "u64"], result: "i32" },
+  tv_verify: { parameters: ["pointer", "pointer", "pointer"], result: "i32", nonblocking: true },
+  tv_verify_host: {
+    parameters: ["pointer", "pointer", "u64", "pointer", "pointer"],
+    result: "i32",
+    nonblocking: true,
+  },
+  tv_hash: { parameters: ["pointer", "pointer"], result: "i32", nonblocking: true },
+  tv_set_option: { parameters: ["pointer", "i32", "i64"], result: "i32" },
+  tv_get_option: { parameters: ["pointer", "i32", "pointer"], result: "i32" },
+  tv_last_timing: { parameters: ["pointer", "pointer", "pointer"], result: "i32" },
+  tv_last_kernel: { parameters: ["pointer", "pointer", "pointer"], result: "i32" },
+  tv_synchronize: { parameters: ["pointer"], result: "i32" },
+} as const;
+
+export interface VerifyOptions {
+  /** path of libtorrent_verify.so (default: ./torrent_amd/libtorrent_verify.so) */
+  libPath?: string;
+  /** GPU indices; pieces are sharded over them in contiguous, 8-aligned ranges */
+  devices?: number[];
+  /** pieces read through storage.get per staging batch */
+  batchBytes?: number;
+}
+
+type Lib = Deno.DynamicLibrary<typeof SYMBOLS>;
+let lib: Lib | null = null;
+
+function load(path?: string): Lib {
+  if (!lib) {
+    lib = Deno.dlopen(path ?? "./torrent_amd/libtorrent_verify.so", SYMBOLS);
+    if (lib.symbols.tv_abi_version() !== 1) throw new Error("libtorrent_verify ABI mismatch");
+  }
+  return lib;
+}
+
+function ptr(a: Uint8Array | null): Deno.PointerValue {
+  return a ? Deno.UnsafePointer.of(a) : null;
+}
+
+function check(l: Lib, ctx: Deno.PointerValue, rc: number): void {
+  if (rc !== 0) {
+    const buf = new Uint8Array(1024);
+    const n = l.symbols.tv_last_error(ctx, ptr(buf), BigInt(buf.length));
+    throw new Error(`torrent_verify error ${rc}: ${new TextDecoder().decode(buf.subarray(0, Math.min(n, 1023)))}`);
+  }
+}
+
+/** piece.ts:16-19 (private there; restated) */
+function pieceLength(n: number, info: InfoDict): number {
+  return (n === info.pieces.length - 1 && info.length % info.pieceLength) || info.pieceLength;
+}
+
+/** contiguous shards of whole bitfield bytes (first % 8 === 0) */
+export function shardRanges(nPieces: number, nShards: number): [number, number][] {
+  const per = Math.ceil(Math.ceil(nPieces / nShards) / 8) * 8;
+  const out: [number, number][] = [];
+  for (let s = 0, first = 0; s < nShards; s++) {
+    const count = Math.max(0, Math.min(per, nPieces - first));
+    out.push([first, count]);
+    first += count;
+  }
+  return out;
+}
+
+function piecesRaw(info: InfoDict): Uint8Array {
+  // metainfo.ts:111 partition() returns contiguous views of the .torrent buffer; rebuild the string
+  const total = info.pieces.reduce((n, p) => n + p.length, 0);
+  const out = new Uint8Array(total);
+  let o = 0;
+  for (const p of info.pieces) {
+    out.set(p, o);
+    o += p.length;
+  }
+  return out;
+}
+
+/**
+ * verifyPieces(info, storage) -> have-bitfield (Uint8Array of ceil(P/8) bytes, MSB-first:
+ * torrent.ts:53,60,147-149).  Piece i's bit is set iff storage.get(i*pieceLength, len_i) is
+ * non-null (storage.ts:50-65) and its SHA-1 equals info.pieces[i].  Unreadable pieces are 0, not
+ * errors (the reference swallows I/O failures into null); GPU / ABI failures throw Error.
+ */
+export async function verifyPieces(
+  info: InfoDict,
+  storage: Storage,
+  opts: VerifyOptions = {},
+): Promise<Uint8Array> {
+  const l = load(opts.libPath);
+  const P = info.pieces.length;
+  const L = info.pieceLength;
+  const devices = opts.devices ?? [0];
+  const raw = piecesRaw(info);
+  const bitfield = new Uint8Array(Math.ceil(P / 8));
+  const batch = Math.max(1, Math.floor((opts.batchBytes ?? 256 * 2 ** 20) / L));
+
+  await Promise.all(shardRanges(P, devices.length).map(async ([first, count], s) => {
+    if (count === 0) return;
+    const h = new BigUint64Array(1);
+    check(l, null, l.symbols.tv_create(ptr(new Uint8Array(h.buffer)), devices[s]));
+    const ctx = Deno.UnsafePointer.create(h[0]);
+    try {
+      check(l, ctx, l.symbols.tv_set_layout(ctx, BigInt(info.length), BigInt(L), BigInt(P), BigInt(first), BigInt(count)));
+      check(l, ctx, l.symbols.tv_set_digests(ctx, ptr(raw), BigInt(raw.length)));
+      const avail = new Uint8Array(Math.ceil(count / 8));
+      for (let j = 0; j < count; j += batch) {
+        const k = Math.min(batch, count - j);
+        const buf = new Uint8Array(k * L);
+        let hi = 0;
+        // all reads outstanding at once, like make_torrent.ts:96,111 keeps its digests in flight
+        const got = await Promise.all(
+          Array.from({ length: k }, (_, q) => storage.get((first + j + q) * L, pieceLength(first + j + q, info))),
+        );
+        got.forEach((bytes, q) => {
+          if (!bytes) return;
+          buf.set(bytes, q * L);
+          hi = q * L + bytes.length;
+          avail[(j + q) >> 3] |= 128 >> ((j + q) % 8);
+        });
+        if (hi) check(l, ctx, await l.symbols.tv_stage(ctx, BigInt((first + j) * L), ptr(buf), BigInt(hi)));
+      }
+      const out = new Uint8Array(Math.ceil(count / 8));
+      check(l, ctx, await l.symbols.tv_verify(ctx, ptr(avail), ptr(out)));
+      bitfield.set(out, first / 8);
+    } finally {
+      l.symbols.tv_destroy(ctx);
+    }
+  }));
+  return bitfield;
+}
+
+/** verifyPiece(info, index, bytes): one piece (e.g. on completion of its last 16 KiB block). */
+export async function verifyPiece(info: InfoDict, index: number, bytes: Uint8Array, opts: VerifyOptions = {}): Promise<boolean> {
+  if (index >= info.pieces.length) throw new Error(`verifyPiece: invalid piece index ${index}`);
+  if (bytes.length !== pieceLength(index, info) || info.pieces[index].length !== 20) return false;
+  const l = load(opts.libPath);
+  const h = new BigUint64Array(1);
+  check(l, null, l.symbols.tv_create(ptr(new Uint8Array(h.buffer)), (opts.devices ?? [0])[0]));
+  const ctx = Deno.UnsafePointer.create(h[0]);
+  try {
+    const n = BigInt(bytes.length);
+    check(l, ctx, l.symbols.tv_set_layout(ctx, n, n, 1n, 0n, 1n));
+    check(l, ctx, l.symbols.tv_set_digests(ctx, ptr(info.pieces[index]), 20n));
+    check(l, ctx, await l.symbols.tv_stage(ctx, 0n, ptr(bytes), n));
+    const out = new Uint8Array(1);
+    check(l, ctx, await l.symbols.tv_verify(ctx, null, ptr(out)));
+    return (out[0] & 0x80) !== 0;
+  } finally {
+    l.symbols.tv_destroy(ctx);
+  }
+}
