@@ -89,12 +89,12 @@ def _sum(dist, x: float) -> float:
     return float(t.item())
 
 
-def _device_sync(ctx, local: int) -> None:
+def _device_sync(ctx, device: int) -> None:
     ctx.synchronize()
     try:
         import torch
         if torch.cuda.is_available():
-            torch.cuda.synchronize(local)
+            torch.cuda.synchronize(device)
     except Exception:
         pass
 
@@ -133,6 +133,8 @@ def main() -> int:
     ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 lane, 2 split")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--e2e-steps", type=int, default=3,
+                    help="timed end-to-end passes from pinned host memory over PCIe (0 = skip)")
     a = ap.parse_args()
 
     dist, rank, ws, local = _dist()
@@ -141,7 +143,8 @@ def main() -> int:
     total = L * P
     first = rank * per_gpu
 
-    ctx = _native.Context(local)
+    device = local % max(1, _native.device_count())
+    ctx = _native.Context(device)
     ctx.set_option(_native.TV_OPT_KERNEL, a.kernel)
     ctx.set_layout(total, L, P, first, per_gpu)
     ctx.fill_synthetic(SEED)
@@ -162,14 +165,14 @@ def main() -> int:
 
     for _ in range(a.warmup):
         bf = ctx.verify()
-    _device_sync(ctx, local)
+    _device_sync(ctx, device)
     _barrier(dist)
     kernel_ms = []
     t0 = time.perf_counter()
     for _ in range(a.steps):
         bf = ctx.verify()
         kernel_ms.append(ctx.last_timing()[0])
-    _device_sync(ctx, local)
+    _device_sync(ctx, device)
     t1 = time.perf_counter()
     _barrier(dist)
     elapsed = _max(dist, t1 - t0)
@@ -180,6 +183,30 @@ def main() -> int:
     worst_kernel_ms = _max(dist, avg_kernel_ms)
 
     bytes_per_gpu = L * per_gpu
+
+    # End-to-end leg (reported beside `value`, never as it): the same shard streamed from a pinned
+    # host copy over PCIe with copy/compute overlap (tv_verify_host; SURVEY 8d config 5 form).
+    e2e = None
+    if a.e2e_steps > 0:
+        host = _native.PinnedBuffer(bytes_per_gpu)
+        ctx.read(first * L, host.mv)            # host copy of the resident synthetic payload
+        bf2 = ctx.verify_host(host.mv)          # warmup
+        _device_sync(ctx, device)
+        _barrier(dist)
+        e0 = time.perf_counter()
+        for _ in range(a.e2e_steps):
+            bf2 = ctx.verify_host(host.mv)
+        _device_sync(ctx, device)
+        e1 = time.perf_counter()
+        _barrier(dist)
+        e_el = _max(dist, e1 - e0)
+        e_ok = _sum(dist, 1.0 if bf2 == bytes(expect) else 0.0) == ws
+        e2e = {"value": round(bytes_per_gpu * ws * a.e2e_steps / e_el / 1e9, 2), "unit": "GB/s",
+               "steps": a.e2e_steps, "ms_per_step": round(e_el * 1e3 / a.e2e_steps, 2), "bitfield_exact": e_ok,
+               "launches_per_step": ctx.last_kernel()[1],
+               "mode": "pinned host -> HBM column stream (2D DMA) overlapped with the verify kernel; PCIe-inclusive"}
+        host.close()
+
     value = bytes_per_gpu * ws * a.steps / elapsed / 1e9
     achieved = bytes_per_gpu / (avg_kernel_ms / 1e3) / 1e9
     piece_ceiling = min(VALU_PEAK_GBPS, per_gpu * 64 * CLOCK_HZ / (SERIAL_INSTR.get(kernel, 613) * LONE_WAVE_CYC) / 1e9)
@@ -221,13 +248,15 @@ def main() -> int:
                          "note": "SHA-1 is VALU-bound on MI355X (4 cyc/wave64 int VOP3); serial per piece, so "
                                  "P pieces cap the rate at P x 64 B / (serial instr x 4.34 cyc) per GPU"},
         }
+        if e2e is not None:
+            out["e2e_pinned_host"] = e2e
         if ws == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(L, total, P, first, shard_digests, a.cpu_seconds)
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
-    return 0 if all_correct else 1
+    return 0 if all_correct and (e2e is None or e2e["bitfield_exact"]) else 1
 
 
 if __name__ == "__main__":

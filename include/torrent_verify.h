@@ -87,6 +87,11 @@ int tv_set_digests(tv_ctx *ctx, const uint8_t *pieces, uint64_t pieces_len);
  */
 int tv_stage(tv_ctx *ctx, uint64_t linear_offset, const uint8_t *src, uint64_t len);
 
+/* The inverse of tv_stage: copy `len` resident bytes at LINEAR offset `linear_offset` to host
+ * `dst` (HBM as the piece store serving block requests, torrent.ts:164-167 Storage.get).  Bytes
+ * outside the shard are left untouched in dst. */
+int tv_read(tv_ctx *ctx, uint64_t linear_offset, uint8_t *dst, uint64_t len);
+
 /* Fill the resident shard with the synthetic payload of `seed` (benchmarks / GPU tests):
  * byte at linear offset o = byte (o & 7) of splitmix64(seed, o >> 3), little-endian. */
 int tv_fill_synthetic(tv_ctx *ctx, uint64_t seed);
@@ -112,6 +117,14 @@ int tv_verify_host(tv_ctx *ctx, const uint8_t *src, uint64_t src_len, const uint
 /* Creation mode (make_torrent.ts:28-31, :147-173): 20-byte SHA-1 of every resident piece of the
  * shard, written to digests_out (20*shard_count bytes), in piece order. */
 int tv_hash(tv_ctx *ctx, uint8_t *digests_out);
+
+/* Page-locked host memory for tv_verify_host / tv_stage sources.  A pinned source is read by
+ * DMA directly (no staging memcpy); pageable memory goes through the library's pinned ring.
+ * tv_host_register pins an existing range (e.g. a caller's buffer), tv_host_unregister undoes it. */
+int tv_host_alloc(uint64_t bytes, void **out);
+int tv_host_free(void *ptr);
+int tv_host_register(void *ptr, uint64_t bytes);
+int tv_host_unregister(void *ptr);
 
 /* Options (tv_set_option keys). */
 #define TV_OPT_KERNEL 1      /* 0 = auto, 1 = lane kernel, 2 = split (schedule-offload) kernel */

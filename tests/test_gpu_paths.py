@@ -160,3 +160,32 @@ def test_full_size_cfg2_properties(native, oracle):
             bf = ctx.verify()
             for i in range(P):
                 assert ((bf[i >> 3] >> (7 - (i & 7))) & 1) == (0 if i in bad else 1)
+
+
+def test_read_back_and_pinned_stream(native, oracle):
+    """tv_read returns exactly the staged linear bytes (incl. a short last piece and a shard
+    window), and tv_verify_host from a pinned (tv_host_alloc) source matches the oracle."""
+    L, P = 65536, 130
+    total = L * (P - 1) + 12345
+    payload = oracle.synth_fill(41, 0, total)
+    pieces = bytearray(oracle.hash_pieces(payload, total, L, P))
+    pieces[20 * 77] ^= 1
+    payload[5 * L + 9] ^= 4
+    with native.Context(0) as ctx:
+        ctx.set_layout(total, L, P, 8, 120)
+        ctx.stage(0, payload)
+        out = bytearray(total)
+        ctx.read(0, out)
+        lo, hi = 8 * L, 128 * L
+        assert out[lo:hi] == payload[lo:hi] and out[:lo] == bytes(lo)
+        part = bytearray(1000)
+        ctx.read(9 * L - 500, part)
+        assert part == payload[9 * L - 500:9 * L + 500]
+    exp = oracle.verify_linear(payload, total, L, bytes(pieces))
+    with native.Context(0) as ctx, native.PinnedBuffer(total) as pb:
+        pb.mv[:] = payload
+        ctx.set_option(native.TV_OPT_STREAM_CHUNK, 16384)
+        ctx.set_layout(total, L, P)
+        ctx.set_digests(bytes(pieces))
+        assert ctx.verify_host(pb.mv) == exp
+        assert ctx.last_kernel()[1] == 4  # 64 KiB pieces in 16 KiB columns

@@ -41,8 +41,8 @@ M32 = 0xFFFFFFFF
 # be split in AMDGPU asm).  The kernel's VGPR count is therefore >= RING_BASE + 4*RING_QUADS.
 RING_BASE = 64
 RING_QUADS = 8
-READ_AHEAD = 6      # quads in flight ahead of the one being consumed
-WAIT_EVERY = 2      # one s_waitcnt per 2 quads (8 rounds)
+READ_AHEAD = 7      # quads in flight ahead of the one being consumed
+WAIT_EVERY = 4      # one s_waitcnt per 4 quads (16 rounds)
 # physical VGPRs of the helper (schedule) block: 16-word W window, xor3 temp, 3 output quads
 HW_BASE = 80
 HT = 96
@@ -116,13 +116,13 @@ def ring_reg(q: int, j: int) -> str:
     return f"v{RING_BASE + 4 * (q % RING_QUADS) + j}"
 
 
-def gen_lds():
+def gen_lds(off_base: int = 0, lead_wait: bool = True):
     """SHA1_LDS instruction list. Operands: r0-4 (out), t0-1 (tmp), h0-4 (in), addr (vgpr in).
-    Quad g (K+W[4g..4g+3], K pre-added by the helper) is read from addr + g*1024."""
-    ins = [("s_waitcnt_lgkm", 0)]
+    Quad g (K+W[4g..4g+3], K pre-added by the helper) is read from addr + off_base + g*1024."""
+    ins = [("s_waitcnt_lgkm", 0)] if lead_wait else []
     issued = -1
     for g in range(min(READ_AHEAD, 20)):
-        ins.append(("ds_read_b128", g, g * 1024))
+        ins.append(("ds_read_b128", g, off_base + g * 1024))
         issued = g
     R = Regs()
     for t in range(80):
@@ -134,7 +134,7 @@ def gen_lds():
         e_src = R.rd(E)
         ins.append(("v_add_u32", R.wr(E), ring_reg(g, t % 4), e_src))
         if t % 4 == 3 and g + READ_AHEAD < 20:
-            ins.append(("ds_read_b128", g + READ_AHEAD, (g + READ_AHEAD) * 1024))
+            ins.append(("ds_read_b128", g + READ_AHEAD, off_base + (g + READ_AHEAD) * 1024))
             issued = g + READ_AHEAD
         ins.append(("v_alignbit_b32", "t0", R.rd(A), R.rd(A), 27))
         ins.append(_fop(t, "t1", R.rd(B), R.rd(C), R.rd(D)))
@@ -173,8 +173,27 @@ def gen_helper(src=None, off_base: int = 0):
     return ins
 
 
+def rounds_loop_text() -> str:
+    """The split kernel's rounds wave over nsteps (>= 1) blocks in which every lane updates: per
+    block the 80 rounds from K+W in LDS (buffer (step & 1)), h += r, barrier.  One asm statement,
+    so no compiler bookkeeping or asm-boundary s_nop between blocks."""
+    L = ["s_waitcnt lgkmcnt(0)", "s_mov_b32 %[cnt], %[nsteps]", "L_rloop_%=:"]
+
+    def step(off):
+        L.extend(_emit_lines(gen_lds(off, lead_wait=False)))
+        for i in range(5):
+            L.append(f"v_add_u32 %[h{i}], %[h{i}], %[r{i}]")
+        L.append("s_barrier")
+
+    step(0)
+    L += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_eq_u32 %[cnt], 0", "s_cbranch_scc1 L_rdone_%="]
+    step(RING_BYTES)
+    L += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_lg_u32 %[cnt], 0", "s_cbranch_scc1 L_rloop_%=", "L_rdone_%=:"]
+    return "\n".join(f'    "{l}\\n"' for l in L)
+
+
 P0_BASE, P1_BASE, VL = 112, 128, 144   # prefetch buffers (2 blocks) and the running load pointer
-RING_BYTES = 80 * 64 * 4               # one K+W buffer
+RING_BYTES = 80 * 64 * 4               # one K+W buffer (also used by rounds_loop_text)
 
 
 def helper_loop_text() -> str:
@@ -230,49 +249,70 @@ def helper_loop_text() -> str:
 # ---------------------------------------------------------------- emulator -------------
 
 def emulate(ins, regs: dict, lds: dict | None = None, addr: int = 0):
-    """Execute an instruction list on a dict of 32-bit registers (one lane)."""
+    """Execute an instruction list on a dict of 32-bit registers (one lane).  ds_read results
+    land only when an s_waitcnt lgkmcnt(N) retires them (in order); reading a register whose
+    load is still in flight, or overwriting one, raises -- so the wait counts are checked too."""
+    pending = []  # [(regs, values)] oldest first
 
     def v(x):
-        return regs[x] if isinstance(x, str) else x
+        if isinstance(x, str):
+            for rs, _ in pending:
+                if x in rs:
+                    raise AssertionError(f"read of {x} before its ds_read retired")
+            return regs[x]
+        return x
+
+    def wr(x, val):
+        for rs, _ in pending:
+            if x in rs:
+                raise AssertionError(f"write of {x} while its ds_read is in flight")
+        regs[x] = val
 
     for op in ins:
         o = op[0]
         if o == "v_add3_u32":
-            regs[op[1]] = (v(op[2]) + v(op[3]) + v(op[4])) & M32
+            wr(op[1], (v(op[2]) + v(op[3]) + v(op[4])) & M32)
         elif o == "v_alignbit_b32":
-            s = op[4] & 31
+            s_ = op[4] & 31
             cat = (v(op[2]) << 32) | v(op[3])
-            regs[op[1]] = (cat >> s) & M32
+            wr(op[1], (cat >> s_) & M32)
         elif o == "v_bfi_b32":
             a, b, c = v(op[2]), v(op[3]), v(op[4])
-            regs[op[1]] = ((a & b) | (~a & c)) & M32
+            wr(op[1], ((a & b) | (~a & c)) & M32)
         elif o == "v_bitop3_b32":
             a, b, c, imm = v(op[2]), v(op[3]), v(op[4]), op[5]
             r = 0
             for bit in range(32):
                 idx = (((a >> bit) & 1) << 2) | (((b >> bit) & 1) << 1) | ((c >> bit) & 1)
                 r |= ((imm >> idx) & 1) << bit
-            regs[op[1]] = r
+            wr(op[1], r)
         elif o == "v_xor_b32":
-            regs[op[1]] = v(op[2]) ^ v(op[3])
+            wr(op[1], v(op[2]) ^ v(op[3]))
         elif o == "v_add_u32":
-            regs[op[1]] = (v(op[2]) + v(op[3])) & M32
+            wr(op[1], (v(op[2]) + v(op[3])) & M32)
         elif o == "v_perm_b32":
             assert op[2] == 0 and regs[op[4]] == 0x00010203
             x = v(op[3])
-            regs[op[1]] = int.from_bytes(x.to_bytes(4, "little"), "big")
+            wr(op[1], int.from_bytes(x.to_bytes(4, "little"), "big"))
         elif o == "ds_write_b128":
             base, off = op[1], op[2]
             for j in range(4):
-                lds[addr + off + 4 * j] = regs[f"v{base + j}"]
+                lds[addr + off + 4 * j] = v(f"v{base + j}")
         elif o == "ds_read_b128":
             q, off = op[1], op[2]
-            for j in range(4):
-                regs[ring_reg(q, j)] = lds[addr + off + 4 * j]
+            rs = [ring_reg(q, j) for j in range(4)]
+            for x in rs:
+                for prs, _ in pending:
+                    assert x not in prs, f"ds_read into {x} while it is in flight"
+            pending.append((rs, [lds[addr + off + 4 * j] for j in range(4)]))
         elif o == "s_waitcnt_lgkm":
-            pass
+            while len(pending) > op[1]:
+                rs, vals = pending.pop(0)
+                for x, val in zip(rs, vals):
+                    regs[x] = val
         else:
             raise ValueError(o)
+    assert not pending, "ds_read still in flight at the end of the block"
     return regs
 
 
@@ -433,6 +473,19 @@ __device__ __forceinline__ void tv_sha1_helper_loop(const void* va, uint32_t nra
     : {loop_clobbers}, "scc", "memory");
 }}
 
+// The split kernel's rounds wave over nsteps (>= 1) consecutive blocks starting with ring buffer 0,
+// in which every lane updates its chaining value: 80 rounds from LDS, h += r, workgroup barrier.
+__device__ __forceinline__ void tv_sha1_rounds_loop(uint32_t h[5], uint32_t addr, uint32_t nsteps) {{
+    uint32_t r[5], t0, t1, cnt;
+    asm volatile(
+{rounds_loop}
+    : [h0] "+v"(h[0]), [h1] "+v"(h[1]), [h2] "+v"(h[2]), [h3] "+v"(h[3]), [h4] "+v"(h[4]),
+      [r0] "=&v"(r[0]), [r1] "=&v"(r[1]), [r2] "=&v"(r[2]), [r3] "=&v"(r[3]), [r4] "=&v"(r[4]),
+      [t0] "=&v"(t0), [t1] "=&v"(t1), [cnt] "=&s"(cnt)
+    : [addr] "v"(addr), [nsteps] "s"(nsteps)
+    : {ring_clobbers}, "scc", "memory");
+}}
+
 // Message schedule of one block for the split kernel's helper wave: raw[16] are the block's words
 // as loaded (little-endian); writes K+W[0..79] to LDS at `addr` (+ q*1024 for quad q).  The LDS
 // writes are left in flight (the caller's barrier waits lgkmcnt(0)).
@@ -458,7 +511,8 @@ def render() -> str:
     loop = ", ".join(f'"v{i}"' for i in hregs + list(range(P0_BASE, VL + 2)))
     return HEADER.format(ring_base=RING_BASE, ring_quads=RING_QUADS, full=emit(gen_full(), True),
                          lds=emit(gen_lds(), False), helper=emit(gen_helper(), False),
-                         helper_loop=helper_loop_text(), ring_clobbers=ring, helper_clobbers=helper,
+                         helper_loop=helper_loop_text(), rounds_loop=rounds_loop_text(),
+                         ring_clobbers=ring, helper_clobbers=helper,
                          loop_clobbers=loop)
 
 

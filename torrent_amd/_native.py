@@ -36,6 +36,7 @@ SYMBOLS = [
     ("tv_set_layout", _int, [_p, _u64, _u64, _u64, _u64, _u64]),
     ("tv_set_digests", _int, [_p, _p, _u64]),
     ("tv_stage", _int, [_p, _u64, _p, _u64]),
+    ("tv_read", _int, [_p, _u64, _p, _u64]),
     ("tv_fill_synthetic", _int, [_p, _u64]),
     ("tv_verify", _int, [_p, _p, _p]),
     ("tv_verify_host", _int, [_p, _p, _u64, _p, _p]),
@@ -45,6 +46,10 @@ SYMBOLS = [
     ("tv_last_timing", _int, [_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     ("tv_last_kernel", _int, [_p, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
     ("tv_synchronize", _int, [_p]),
+    ("tv_host_alloc", _int, [_u64, ctypes.POINTER(_p)]),
+    ("tv_host_free", _int, [_p]),
+    ("tv_host_register", _int, [_p, _u64]),
+    ("tv_host_unregister", _int, [_p]),
 ]
 
 _lib = None
@@ -102,6 +107,38 @@ def _thread_error() -> str:
     buf = ctypes.create_string_buffer(1024)
     lib().tv_last_error(None, buf, len(buf))
     return buf.value.decode(errors="replace")
+
+
+class PinnedBuffer:
+    """Page-locked host buffer (tv_host_alloc); exposes a writable memoryview `mv`."""
+
+    def __init__(self, nbytes: int):
+        self._L = lib()
+        p = _p()
+        rc = self._L.tv_host_alloc(nbytes, ctypes.byref(p))
+        if rc:
+            raise NativeError(rc, _thread_error())
+        self.ptr = p.value
+        self.nbytes = nbytes
+        self.mv = memoryview((ctypes.c_char * nbytes).from_address(self.ptr)).cast("B") if nbytes else memoryview(b"")
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            self.mv.release()
+            self._L.tv_host_free(self.ptr)
+            self.ptr = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Context:
@@ -170,6 +207,13 @@ class Context:
         a, keep = _addr(data)
         n = memoryview(data).nbytes
         self._check(self._L.tv_stage(self._h, linear_offset, a, n))
+        del keep
+
+    def read(self, linear_offset: int, out) -> None:
+        """Copy resident bytes at linear_offset into the writable buffer `out` (tv_read)."""
+        a, keep = _addr(out)
+        n = memoryview(out).nbytes
+        self._check(self._L.tv_read(self._h, linear_offset, a, n))
         del keep
 
     def fill_synthetic(self, seed: int) -> None:

@@ -451,6 +451,42 @@ int tv_stage(tv_ctx* c, uint64_t linear_offset, const uint8_t* src, uint64_t len
     return TV_OK;
 }
 
+int tv_read(tv_ctx* c, uint64_t linear_offset, uint8_t* dst, uint64_t len) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = require_layout(c, false);
+    if (rc) return rc;
+    if (!dst && len) return fail(c, TV_ERR_ARG, "dst is NULL");
+    if (linear_offset + len < linear_offset) return fail(c, TV_ERR_ARG, "offset + len overflows");
+    if (c->count == 0 || len == 0) return TV_OK;
+    TV_HIP(c, hipSetDevice(c->device));
+    const uint64_t lo = c->first * c->L;
+    const uint64_t last = c->first + c->count - 1;
+    const uint64_t hi = last * c->L + piece_len(c, last);
+    uint64_t pos = std::max(linear_offset, lo);
+    const uint64_t b = std::min(linear_offset + len, hi);
+    while (pos < b) {
+        const uint64_t i = pos / c->L, within = pos % c->L;
+        const uint64_t plen = piece_len(c, i);
+        if (within >= plen) { pos = (i + 1) * c->L; continue; }
+        const uint8_t* src = c->d_payload + (i - c->first) * c->stride + within;
+        uint8_t* out = dst + (pos - linear_offset);
+        if (within == 0 && plen == c->L && b - pos >= c->L) {
+            uint64_t k = (b - pos) / c->L;
+            const uint64_t last_full = (c->total % c->L) ? c->P - 1 : c->P;
+            k = std::min<uint64_t>(k, last_full > i ? last_full - i : 1);
+            TV_HIP(c, hipMemcpy2DAsync(out, c->L, src, c->stride, c->L, k, hipMemcpyDeviceToHost, c->copy_stream));
+            pos += k * c->L;
+        } else {
+            const uint64_t n = std::min(b - pos, plen - within);
+            TV_HIP(c, hipMemcpyAsync(out, src, n, hipMemcpyDeviceToHost, c->copy_stream));
+            pos += n;
+        }
+    }
+    TV_HIP(c, hipStreamSynchronize(c->copy_stream));
+    return TV_OK;
+}
+
 int tv_fill_synthetic(tv_ctx* c, uint64_t seed) {
     if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
     std::lock_guard<std::mutex> g(c->mu);
@@ -644,6 +680,38 @@ int tv_verify_host(tv_ctx* c, const uint8_t* src, uint64_t src_len, const uint8_
     c->last_kernel = kernel;
     c->last_launches = (int)ncol;
     return finish_timing(c);
+}
+
+int tv_host_alloc(uint64_t bytes, void** out) {
+    if (!out) return fail(nullptr, TV_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    if (bytes == 0) return TV_OK;
+    hipError_t e = hipHostMalloc(out, bytes, hipHostMallocDefault);
+    if (e != hipSuccess)
+        return fail(nullptr, e == hipErrorOutOfMemory ? TV_ERR_NOMEM : TV_ERR_HIP, "hipHostMalloc(%llu): %s",
+                    (unsigned long long)bytes, hipGetErrorString(e));
+    return TV_OK;
+}
+
+int tv_host_free(void* ptr) {
+    if (!ptr) return TV_OK;
+    hipError_t e = hipHostFree(ptr);
+    if (e != hipSuccess) return fail(nullptr, TV_ERR_HIP, "hipHostFree: %s", hipGetErrorString(e));
+    return TV_OK;
+}
+
+int tv_host_register(void* ptr, uint64_t bytes) {
+    if (!ptr || !bytes) return fail(nullptr, TV_ERR_ARG, "NULL or empty range");
+    hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterDefault);
+    if (e != hipSuccess) return fail(nullptr, TV_ERR_HIP, "hipHostRegister: %s", hipGetErrorString(e));
+    return TV_OK;
+}
+
+int tv_host_unregister(void* ptr) {
+    if (!ptr) return fail(nullptr, TV_ERR_ARG, "ptr is NULL");
+    hipError_t e = hipHostUnregister(ptr);
+    if (e != hipSuccess) return fail(nullptr, TV_ERR_HIP, "hipHostUnregister: %s", hipGetErrorString(e));
+    return TV_OK;
 }
 
 int tv_last_timing(tv_ctx* c, double* kernel_ms, double* total_ms) {

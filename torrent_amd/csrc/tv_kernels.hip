@@ -285,10 +285,18 @@ __global__ __launch_bounds__(128) void tv_split_kernel(TvPieces p) {
     const uint32_t ring_base = (uint32_t)(uintptr_t)(void*)ring + lane * 16u;
     const uint32_t nb_min = g.nb_min;
     lds_barrier();
-    for (uint32_t b = b0; b < end; b++) {
+    uint32_t b = b0;
+    // blocks where every lane of the wave updates: one asm loop (rounds, h += r, barrier)
+    const uint32_t full_end = end < nb_min ? end : nb_min;
+    if (b < full_end) {
+        tv_sha1_rounds_loop(h, ring_base, full_end - b);
+        b = full_end;
+    }
+    // the short last piece's wave: lanes past their final block keep their digest
+    for (; b < end; b++) {
         uint32_t r[5];
         tv_sha1_lds(h, r, ring_base + ((b - b0) & 1u) * (kRingWords * 4u));
-        if (b < nb_min || b < nb) {
+        if (b < nb) {
 #pragma unroll
             for (int i = 0; i < 5; i++) h[i] += r[i];
         }

@@ -22,6 +22,7 @@ const SYMBOLS = {
   tv_set_layout: { parameters: ["pointer", "u64", "u64", "u64", "u64", "u64"], result: "i32" },
   tv_set_digests: { parameters: ["pointer", "pointer", "u64"], result: "i32" },
   tv_stage: { parameters: ["pointer", "u64", "pointer", "u64"], result: "i32", nonblocking: true },
+  tv_read: { parameters: ["pointer", "u64", "pointer", "u64"], result: "i32", nonblocking: true },
   tv_fill_synthetic: { parameters: ["pointer", "u64"], result: "i32" },
   tv_verify: { parameters: ["pointer", "pointer", "pointer"], result: "i32", nonblocking: true },
   tv_verify_host: {
@@ -35,6 +36,10 @@ const SYMBOLS = {
   tv_last_timing: { parameters: ["pointer", "pointer", "pointer"], result: "i32" },
   tv_last_kernel: { parameters: ["pointer", "pointer", "pointer"], result: "i32" },
   tv_synchronize: { parameters: ["pointer"], result: "i32" },
+  tv_host_alloc: { parameters: ["u64", "pointer"], result: "i32" },
+  tv_host_free: { parameters: ["pointer"], result: "i32" },
+  tv_host_register: { parameters: ["pointer", "u64"], result: "i32" },
+  tv_host_unregister: { parameters: ["pointer"], result: "i32" },
 } as const;
 
 export interface VerifyOptions {
