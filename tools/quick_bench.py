@@ -24,8 +24,15 @@ def run(total, L, kernels=(1, 2), reps=3, pad=None):
     ctx.close()
 
 if __name__ == "__main__":
-    run(16 << 30, 1 << 20)           # cfg2: 16384 pieces
-    run(16 << 30, 256 << 10)         # 65536 pieces
-    run(16 << 30, 128 << 10, (1,))   # 131072 pieces (lane)
-    run(16 << 30, 64 << 10, (1,))    # 262144 pieces (lane)
-    run(50 << 30, 4 << 20)           # cfg4 on one GPU: 12800 pieces x 4 MiB (quarter of cfg4)
+    import sys as _s
+    which = _s.argv[1] if len(_s.argv) > 1 else "all"
+    if which in ("all", "cfg2"):
+        run(16 << 30, 1 << 20)           # cfg2: 16384 pieces
+    if which in ("all", "mid"):
+        run(25 << 30, 1 << 20)           # 25600 pieces (cfg4 per GPU at N=2, 1 MiB pieces)
+        run(16 << 30, 512 << 10)         # 32768 pieces
+        run(20 << 30, 512 << 10)         # 40960 pieces
+        run(16 << 30, 256 << 10)         # 65536 pieces
+    if which in ("all", "big"):
+        run(16 << 30, 64 << 10, (1,))    # 262144 pieces (lane)
+        run(50 << 30, 4 << 20)           # 12800 pieces x 4 MiB (cfg4 per GPU at N=4)

@@ -158,10 +158,11 @@ int upload_avail(tv_ctx* c, const uint8_t* avail_bits) {
 
 int choose_kernel(const tv_ctx* c) {
     if (c->kernel_opt == TV_KERNEL_LANE || c->kernel_opt == TV_KERNEL_SPLIT) return c->kernel_opt;
-    // Split (schedule offload) while its rounds waves and helper waves do not share SIMDs
-    // (<= 2 workgroups of 64 pieces per CU, 256 CUs); with more pieces the lane kernel already has
-    // about one wave per SIMD and the SIMDs' VALU, not the per-lane stream, is the bound.
-    return c->count <= 40000 ? TV_KERNEL_SPLIT : TV_KERNEL_LANE;
+    // Split (schedule offload) while every split workgroup (128 pieces, 4 waves on 4 SIMDs) has a
+    // CU to itself: <= 256 x 128 pieces.  Beyond that workgroups share CUs, a rounds wave shares
+    // its SIMD with another wave, and the lane kernel (about one wave per SIMD, VALU-bound) wins:
+    // measured 40,960 pieces split 1.62 vs lane 2.33 TB/s; 32,768 split 2.50 vs lane 1.87.
+    return c->count <= 32768 ? TV_KERNEL_SPLIT : TV_KERNEL_LANE;
 }
 
 TvPieces resident_launch(const tv_ctx* c) {

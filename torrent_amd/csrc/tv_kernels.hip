@@ -9,7 +9,7 @@
 // Parallelism is one LANE per piece (SHA-1 is serial inside a piece).  Two kernels:
 //   lane  : each lane loads its own 64-byte blocks (register prefetch, 2 blocks ahead) and runs
 //           the full compression (schedule + rounds) as one generated asm block (613 VALU/block).
-//   split : schedule offload.  A workgroup is 2 waves for 64 pieces: the helper wave loads the
+//   split : schedule offload.  A workgroup is 2 x (rounds, helper) waves for 128 pieces: a helper loads the
 //           blocks and writes K+W[0..79] into an LDS double buffer (generated asm: v_perm bswap,
 //           v_bitop3 xor3, ds_write_b128); the rounds wave runs only the 80 rounds from LDS
 //           (400 VALU + 20 ds_read_b128 + 10 waits per block).  A lone wave issues one VALU per
@@ -55,9 +55,11 @@ __device__ __forceinline__ uint32_t uni(uint64_t x) {
     return __builtin_amdgcn_readfirstlane((uint32_t)x);
 }
 
-// j0 must be wave-uniform (first piece of the wave).
-__device__ __forceinline__ WaveGeom wave_geom(const TvPieces& p, uint32_t j0) {
-    const bool has_last = p.last_idx != 0xFFFFFFFFu && (p.last_idx >> 6) == (j0 >> 6);
+// j0 must be wave-uniform: the first piece of the group of `span` pieces (a wave, or a split
+// workgroup) that must agree on block counts.  Lanes past the launch's end are clamped to its last
+// piece, so a group "has" the last piece iff last_idx falls inside [j0, j0 + span).
+__device__ __forceinline__ WaveGeom wave_geom(const TvPieces& p, uint32_t j0, uint32_t span = 64) {
+    const bool has_last = p.last_idx != 0xFFFFFFFFu && p.last_idx >= j0 && p.last_idx - j0 < span;
     const bool only_last = has_last && p.last_idx == j0;
     const uint64_t nfull_min = (has_last ? p.last_len : p.L) / 64;
     const uint64_t nb_max = nblocks(only_last ? p.last_len : p.L);
@@ -244,25 +246,32 @@ __device__ __forceinline__ void lds_barrier() {
 }  // namespace
 
 template <bool HASH>
-__global__ __launch_bounds__(128) void tv_split_kernel(TvPieces p) {
-    __shared__ __attribute__((aligned(16))) uint4 ring[2 * kRingWords / 4];
+__global__ __launch_bounds__(256) void tv_split_kernel(TvPieces p) {
+    // 4 waves = 2 pairs x {rounds, helper}; 128 pieces.  A workgroup's waves go to 4 distinct SIMDs,
+    // so with <= 1 workgroup per CU no rounds wave shares its SIMD.  Each pair has its own 2 x 20 KiB
+    // K+W ring; the barrier is workgroup-wide, so both pairs run the same (workgroup) block range.
+    __shared__ __attribute__((aligned(16))) uint4 ring[4 * kRingWords / 4];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t j0 = blockIdx.x * 64u;
+    const uint32_t pair = wave & 1u;
+    const uint32_t role = wave >> 1;           // 0 = rounds, 1 = helper
+    const uint32_t wg0 = blockIdx.x * 128u;
+    const uint32_t j0 = wg0 + pair * 64u;
     const uint32_t j = j0 + lane;
     const uint32_t jj = j < p.n ? j : p.n - 1;
-    const WaveGeom g = wave_geom(p, j0);
+    const WaveGeom g = wave_geom(p, wg0, 128);
     const uint64_t len = lane_len(p, jj);
     const uint32_t nb = (uint32_t)nblocks(len);
     const uint8_t* piece = p.data + (uint64_t)jj * p.stride - p.data_off;
     const uint32_t b0 = g.fast_begin, end = g.end, fast_end = g.fast_end;
+    uint4* const pring = ring + pair * 2 * (kRingWords / 4);
 
-    if (wave != 0) {
+    if (role != 0) {
         // ---------------- helper wave ----------------
         // Raw blocks [b0, fast_end): one asm loop (loads 2 blocks ahead into registers the compiler
         // never allocates, schedule, K+W -> LDS, barrier per block).  Then the 1-2 padded tail blocks
         // (and one spare block past `end` that the rounds wave never reads) in C++.
-        const uint32_t lds_lane = (uint32_t)(uintptr_t)(void*)ring + lane * 16u;
+        const uint32_t lds_lane = (uint32_t)(uintptr_t)(void*)pring + lane * 16u;
         uint32_t b = b0;
         if (fast_end > b0) {
             tv_sha1_helper_loop(piece + (uint64_t)b0 * 64, fast_end - b0, lds_lane, TV_K0, TV_K1, TV_K2, TV_K3);
@@ -282,7 +291,7 @@ __global__ __launch_bounds__(128) void tv_split_kernel(TvPieces p) {
     // ---------------- rounds wave ----------------
     uint32_t h[5];
     start_state(p, jj, h);
-    const uint32_t ring_base = (uint32_t)(uintptr_t)(void*)ring + lane * 16u;
+    const uint32_t ring_base = (uint32_t)(uintptr_t)(void*)pring + lane * 16u;
     const uint32_t nb_min = g.nb_min;
     lds_barrier();
     uint32_t b = b0;
@@ -343,9 +352,9 @@ __global__ __launch_bounds__(256) void tv_fill_bytes_kernel(uint8_t* payload, ui
 hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_t s) {
     if (p.n == 0) return hipSuccess;
     if (kernel == TV_KERNEL_SPLIT) {
-        const unsigned grid = (p.n + 63) / 64;
-        if (hash) hipLaunchKernelGGL(tv_split_kernel<true>, dim3(grid), dim3(128), 0, s, p);
-        else hipLaunchKernelGGL(tv_split_kernel<false>, dim3(grid), dim3(128), 0, s, p);
+        const unsigned grid = (p.n + 127) / 128;
+        if (hash) hipLaunchKernelGGL(tv_split_kernel<true>, dim3(grid), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL(tv_split_kernel<false>, dim3(grid), dim3(256), 0, s, p);
     } else {
         const unsigned grid = (p.n + 255) / 256;
         if (hash) hipLaunchKernelGGL(tv_lane_kernel<true>, dim3(grid), dim3(256), 0, s, p);
