@@ -106,6 +106,15 @@ int tv_fill_synthetic(tv_ctx *ctx, uint64_t seed);
 int tv_verify(tv_ctx *ctx, const uint8_t *avail_bits, uint8_t *bitfield_out);
 
 /*
+ * Verify a LIST of resident pieces (incremental verify on piece completion, SURVEY 8f row f1: the
+ * piece-message handler torrent.ts:183-193 is where a completed piece is checked).  pieces[k] are
+ * GLOBAL piece indices inside this ctx's shard (any order, duplicates allowed); ok_out[k] = 1 iff
+ * SHA-1 of the resident bytes of piece pieces[k] equals info.pieces[pieces[k]], else 0.  Only pieces
+ * whose bytes were staged should be listed.
+ */
+int tv_verify_list(tv_ctx *ctx, const uint64_t *pieces, uint64_t n, uint8_t *ok_out);
+
+/*
  * Verify the shard from a HOST buffer (end-to-end resume check): `src` holds the
  * shard's linear bytes [shard_first*piece_length, ...) (src_len bytes; pieces extending past
  * src_len are unreadable).  Data streams host -> pinned ring -> HBM over PCIe with copy/compute

@@ -189,3 +189,73 @@ def test_read_back_and_pinned_stream(native, oracle):
         ctx.set_digests(bytes(pieces))
         assert ctx.verify_host(pb.mv) == exp
         assert ctx.last_kernel()[1] == 4  # 64 KiB pieces in 16 KiB columns
+
+
+def test_verify_list_matches_oracle(native, oracle):
+    """tv_verify_list: arbitrary order, duplicates, the short last piece in any lane position,
+    corrupted pieces, a shard offset; > 256 entries (several workgroups)."""
+    import random
+    L, P = 16384, 700
+    total = L * (P - 1) + 333
+    payload = oracle.synth_fill(55, 0, total)
+    pieces = bytearray(oracle.hash_pieces(payload, total, L, P))
+    bad = {3, 64, 65, 400, P - 1}
+    for i in bad:
+        pieces[20 * i + 1] ^= 0x40
+    rng = random.Random(5)
+    with native.Context(0) as ctx:
+        ctx.set_layout(total, L, P, 8, P - 8)
+        ctx.set_digests(bytes(pieces))
+        ctx.stage(0, payload)
+        lst = [rng.randrange(8, P) for _ in range(600)] + [P - 1, P - 1, 8, 9]
+        rng.shuffle(lst)
+        got = ctx.verify_list(lst)
+        assert list(got) == [0 if i in bad else 1 for i in lst]
+        with pytest.raises(native.NativeError):
+            ctx.verify_list([0])          # outside the shard
+        # only the last piece (a wave whose every lane is the short piece)
+        assert ctx.verify_list([P - 1] * 70) == bytes(70)
+        pieces[20 * (P - 1) + 1] ^= 0x40
+        ctx.set_digests(bytes(pieces))
+        assert ctx.verify_list([P - 1] * 70) == b"\x01" * 70
+
+
+def test_incremental_verifier_flow(native, oracle):
+    """Blocks arrive in random order through the reference-shaped handler; completed pieces are
+    verified in batches; a corrupted block yields a 0 and the piece can be re-received."""
+    import random
+    from torrent_amd import MemoryStorage, Storage, make_info
+    from torrent_amd.incremental import IncrementalVerifier
+    from torrent_amd.piece import BLOCK_SIZE, PieceMsg
+    L, P = 4 * BLOCK_SIZE, 37
+    total = L * (P - 1) + BLOCK_SIZE + 100       # last piece: 2 blocks, the second short
+    payload = bytes(oracle.synth_fill(77, 0, total))
+    info = make_info(L, oracle.hash_pieces(payload, total, L, P), "t.bin", length=total)
+    st = Storage(MemoryStorage(), info, os.getcwd())
+    v = IncrementalVerifier(info, st)
+    msgs = []
+    for i in range(P):
+        n = L if i < P - 1 else total - (P - 1) * L
+        for off in range(0, n, BLOCK_SIZE):
+            msgs.append(PieceMsg(i, off, payload[i * L + off:i * L + min(n, off + BLOCK_SIZE)]))
+    rng = random.Random(9)
+    rng.shuffle(msgs)
+    corrupt = msgs[10]
+    msgs[10] = PieceMsg(corrupt.index, corrupt.offset, bytes(b ^ 1 for b in corrupt.block))
+    results = {}
+    for k, m in enumerate(msgs):
+        v.on_block(m)
+        if k % 25 == 0:
+            results.update(dict(v.flush()))
+    results.update(dict(v.flush()))
+    assert results[corrupt.index] is False
+    assert all(ok for i, ok in results.items() if i != corrupt.index) and len(results) == P
+    # re-receive the corrupted piece correctly
+    i = corrupt.index
+    n = L if i < P - 1 else total - (P - 1) * L
+    for off in range(0, n, BLOCK_SIZE):
+        v.on_block(PieceMsg(i, off, payload[i * L + off:i * L + min(n, off + BLOCK_SIZE)]))
+    assert v.flush() == [(i, True)]
+    assert bytes(v.bitfield) == bytes(b"\xff" * (P // 8) + bytes([(0xFF00 >> (P % 8)) & 0xFF]))
+    assert st.get(0, total) is not None   # blocks also went through Storage.set
+    v.close()

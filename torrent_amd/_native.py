@@ -40,6 +40,7 @@ SYMBOLS = [
     ("tv_fill_synthetic", _int, [_p, _u64]),
     ("tv_verify", _int, [_p, _p, _p]),
     ("tv_verify_host", _int, [_p, _p, _u64, _p, _p]),
+    ("tv_verify_list", _int, [_p, _p, _u64, _p]),
     ("tv_hash", _int, [_p, _p]),
     ("tv_set_option", _int, [_p, _int, _i64]),
     ("tv_get_option", _int, [_p, _int, ctypes.POINTER(_i64)]),
@@ -237,6 +238,16 @@ class Context:
         self._check(self._L.tv_verify_host(self._h, a, n, b, out))
         del k1, k2
         return out.raw[: self._nbits()]
+
+    def verify_list(self, pieces) -> bytes:
+        """tv_verify_list: one byte (0/1) per listed global piece index."""
+        n = len(pieces)
+        if n == 0:
+            return b""
+        arr = (ctypes.c_uint64 * n)(*pieces)
+        out = ctypes.create_string_buffer(n)
+        self._check(self._L.tv_verify_list(self._h, ctypes.cast(arr, _p), n, out))
+        return out.raw[:n]
 
     def hash(self) -> bytes:
         out = ctypes.create_string_buffer(max(1, 20 * self.shard_count))

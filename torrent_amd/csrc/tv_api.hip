@@ -52,6 +52,9 @@ struct tv_ctx {
     uint32_t* d_state = nullptr;      // [5][count]
     uint32_t* d_hash = nullptr;       // [5][count]
     uint8_t* d_chunk[2] = {nullptr, nullptr};
+    uint32_t* d_list = nullptr;       // tv_verify_list indices
+    uint8_t* d_list_out = nullptr;
+    uint64_t list_cap = 0;
     uint64_t chunk_bytes = 0;
     size_t bit_words = 0;
 
@@ -108,6 +111,9 @@ void free_device(tv_ctx* c) {
     (void)hipFree(c->d_hash); c->d_hash = nullptr;
     for (auto& p : c->d_chunk) { (void)hipFree(p); p = nullptr; }
     c->chunk_bytes = 0;
+    (void)hipFree(c->d_list); c->d_list = nullptr;
+    (void)hipFree(c->d_list_out); c->d_list_out = nullptr;
+    c->list_cap = 0;
 }
 
 int ensure_ring(tv_ctx* c) {
@@ -178,6 +184,7 @@ TvPieces resident_launch(const tv_ctx* c) {
     p.blk_begin = 0;
     p.blk_end = UINT64_MAX;
     p.finalize = 1;
+    p.dcount = (uint32_t)c->count;
     p.state = c->d_state;
     p.digests = c->d_digests;
     p.avail64 = c->d_avail;
@@ -519,6 +526,51 @@ int tv_verify(tv_ctx* c, const uint8_t* avail_bits, uint8_t* bitfield_out) {
     rc = read_bits(c, bitfield_out);
     if (rc) return rc;
     c->last_kernel = kernel;
+    c->last_launches = 1;
+    return finish_timing(c);
+}
+
+int tv_verify_list(tv_ctx* c, const uint64_t* pieces, uint64_t n, uint8_t* ok_out) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = require_layout(c, true);
+    if (rc) return rc;
+    if (n == 0) return TV_OK;
+    if (!pieces || !ok_out) return fail(c, TV_ERR_ARG, "NULL argument");
+    if (n >= 0xFFFFFFFFull) return fail(c, TV_ERR_ARG, "list too long");
+    std::vector<uint32_t> local(n);
+    for (uint64_t k = 0; k < n; k++) {
+        if (pieces[k] < c->first || pieces[k] >= c->first + c->count)
+            return fail(c, TV_ERR_ARG, "piece %llu is not in this context's shard [%llu, %llu)",
+                        (unsigned long long)pieces[k], (unsigned long long)c->first,
+                        (unsigned long long)(c->first + c->count));
+        local[k] = (uint32_t)(pieces[k] - c->first);
+    }
+    TV_HIP(c, hipSetDevice(c->device));
+    if (c->list_cap < n) {
+        (void)hipFree(c->d_list); c->d_list = nullptr;
+        (void)hipFree(c->d_list_out); c->d_list_out = nullptr;
+        c->list_cap = 0;
+        const uint64_t cap = std::max<uint64_t>(n, 1024);
+        TV_HIP(c, hipMalloc((void**)&c->d_list, cap * 4));
+        TV_HIP(c, hipMalloc((void**)&c->d_list_out, cap));
+        c->list_cap = cap;
+    }
+    TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
+    rc = upload_avail(c, nullptr);  // digest slice complete & bytes inside the torrent
+    if (rc) return rc;
+    TV_HIP(c, hipMemcpyAsync(c->d_list, local.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+    TvPieces p = resident_launch(c);
+    p.n = (uint32_t)n;
+    p.idx = c->d_list;
+    p.out_bytes = c->d_list_out;
+    TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
+    TV_HIP(c, tv_launch_verify_list(p, c->stream));
+    TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
+    TV_HIP(c, hipMemcpyAsync(ok_out, c->d_list_out, n, hipMemcpyDeviceToHost, c->stream));
+    TV_HIP(c, hipEventRecord(c->ev_call1, c->stream));
+    TV_HIP(c, hipEventSynchronize(c->ev_call1));
+    c->last_kernel = TV_KERNEL_LANE;
     c->last_launches = 1;
     return finish_timing(c);
 }

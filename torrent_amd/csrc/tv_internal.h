@@ -20,14 +20,17 @@ struct TvPieces {
     uint32_t n;
     uint32_t last_idx;       // launch-local index of the torrent's last piece, 0xFFFFFFFF if absent
     uint32_t finalize;       // 1: compare / emit digests; 0: store chaining values to `state`
-    uint32_t pad_;
-    uint32_t* state;         // [5][n] chaining values (read when blk_begin > 0, written when !finalize)
-    const uint32_t* digests; // [5][n] expected digest words (big-endian values)
-    const uint64_t* avail64; // per 64 pieces, MSB-first bitfield bytes; may be null
+    uint32_t dcount;         // row stride of state / digests / out_digests (= shard piece count)
+    uint32_t* state;         // [5][dcount] chaining values (read when blk_begin > 0, written when !finalize)
+    const uint32_t* digests; // [5][dcount] expected digest words (big-endian values)
+    const uint64_t* avail64; // MSB-first bitfield bytes over the shard (64-bit words); may be null
     uint64_t* out64;         // per 64 pieces, MSB-first bitfield bytes (sized to whole 256-piece groups)
-    uint32_t* out_digests;   // hash mode: [5][n]
+    uint32_t* out_digests;   // hash mode: [5][dcount]
+    const uint32_t* idx;     // list mode: lane j verifies shard piece idx[j] (data = base + idx*stride)
+    uint8_t* out_bytes;      // list mode: out_bytes[j] = 1 iff piece idx[j] matches
 };
 
 hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_t s);
+hipError_t tv_launch_verify_list(const TvPieces& p, hipStream_t s);
 hipError_t tv_launch_fill(uint8_t* payload, uint64_t stride, uint64_t first, uint32_t n, uint64_t L,
                           uint64_t seed, hipStream_t s);

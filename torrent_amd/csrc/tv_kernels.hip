@@ -58,9 +58,16 @@ __device__ __forceinline__ uint32_t uni(uint64_t x) {
 // j0 must be wave-uniform: the first piece of the group of `span` pieces (a wave, or a split
 // workgroup) that must agree on block counts.  Lanes past the launch's end are clamped to its last
 // piece, so a group "has" the last piece iff last_idx falls inside [j0, j0 + span).
+__device__ __forceinline__ WaveGeom wave_geom_flags(const TvPieces& p, bool has_last, bool only_last);
+
 __device__ __forceinline__ WaveGeom wave_geom(const TvPieces& p, uint32_t j0, uint32_t span = 64) {
     const bool has_last = p.last_idx != 0xFFFFFFFFu && p.last_idx >= j0 && p.last_idx - j0 < span;
     const bool only_last = has_last && p.last_idx == j0;
+    return wave_geom_flags(p, has_last, only_last);
+}
+
+// has_last: some lane's piece is the short last piece; only_last: every lane's is.
+__device__ __forceinline__ WaveGeom wave_geom_flags(const TvPieces& p, bool has_last, bool only_last) {
     const uint64_t nfull_min = (has_last ? p.last_len : p.L) / 64;
     const uint64_t nb_max = nblocks(only_last ? p.last_len : p.L);
     const uint64_t nb_min = nblocks(has_last ? p.last_len : p.L);
@@ -145,20 +152,20 @@ __device__ __forceinline__ void finish(const TvPieces& p, uint32_t j, uint32_t j
     if (!p.finalize) {
         if (j < p.n) {
 #pragma unroll
-            for (int k = 0; k < 5; k++) p.state[(uint64_t)k * p.n + j] = h[k];
+            for (int k = 0; k < 5; k++) p.state[(uint64_t)k * p.dcount + j] = h[k];
         }
         return;
     }
     if (HASH) {
         if (j < p.n) {
 #pragma unroll
-            for (int k = 0; k < 5; k++) p.out_digests[(uint64_t)k * p.n + j] = h[k];
+            for (int k = 0; k < 5; k++) p.out_digests[(uint64_t)k * p.dcount + j] = h[k];
         }
         return;
     }
     bool ok = j < p.n;
 #pragma unroll
-    for (int k = 0; k < 5; k++) ok &= (h[k] == p.digests[(uint64_t)k * p.n + jj]);
+    for (int k = 0; k < 5; k++) ok &= (h[k] == p.digests[(uint64_t)k * p.dcount + jj]);
     const uint64_t mask = __ballot(ok);
     if ((threadIdx.x & 63) == 0) {
         // ballot bit l = piece j0+l  ->  MSB-first bytes: byte m holds pieces j0+8m .. j0+8m+7
@@ -173,7 +180,7 @@ __device__ __forceinline__ void start_state(const TvPieces& p, uint32_t jj, uint
         sha1_iv(h);
     } else {
 #pragma unroll
-        for (int k = 0; k < 5; k++) h[k] = p.state[(uint64_t)k * p.n + jj];
+        for (int k = 0; k < 5; k++) h[k] = p.state[(uint64_t)k * p.dcount + jj];
     }
 }
 
@@ -315,6 +322,62 @@ __global__ __launch_bounds__(256) void tv_split_kernel(TvPieces p) {
 }
 
 // ------------------------------------------------------------------------------------------
+// list kernel (incremental verify): lane j verifies shard piece idx[j]; same compression path as
+// the lane kernel, geometry from wave ballots (the short last piece may sit in any lane).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool avail_bit(const uint64_t* a, uint32_t i) {
+    // MSB-first bitfield bytes held in little-endian 64-bit words
+    return (a[i >> 6] >> (((i >> 3) & 7) * 8 + (7 - (i & 7)))) & 1;
+}
+
+__global__ __launch_bounds__(256) void tv_list_kernel(TvPieces p) {
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t j0 = blockIdx.x * 256u + wave * 64u;
+    if (j0 >= p.n) return;
+    const uint32_t j = j0 + (threadIdx.x & 63u);
+    const uint32_t jj = p.idx[j < p.n ? j : p.n - 1];
+    const bool is_last = jj == p.last_idx;
+    const WaveGeom g = wave_geom_flags(p, __ballot(is_last) != 0, __ballot(!is_last) == 0);
+    const uint64_t len = is_last ? p.last_len : p.L;
+    const uint32_t nb = (uint32_t)nblocks(len);
+    const uint8_t* piece = p.data + (uint64_t)jj * p.stride;
+    uint32_t h[5];
+    sha1_iv(h);
+    uint32_t b = 0, w[16];
+    if (b < g.fast_end) {
+        const uint32_t last = g.fast_end - 1;
+        uint4 A[4], B[4];
+        load_block(piece, 0, A);
+        load_block(piece, 1 < last ? 1 : last, B);
+        for (;;) {
+            bswap_block(A, w);
+            load_block(piece, b + 2 < last ? b + 2 : last, A);
+            compress_full(h, w);
+            if (++b >= g.fast_end) break;
+            bswap_block(B, w);
+            load_block(piece, b + 2 < last ? b + 2 : last, B);
+            compress_full(h, w);
+            if (++b >= g.fast_end) break;
+        }
+    }
+    for (; b < g.end; b++) {
+        build_tail_block(piece, len, b, w);
+        uint32_t r[5];
+        tv_sha1_full(h, r, w, TV_K0, TV_K1, TV_K2, TV_K3);
+        if (b < nb) {
+#pragma unroll
+            for (int i = 0; i < 5; i++) h[i] += r[i];
+        }
+    }
+    if (j < p.n) {
+        bool ok = p.avail64 ? avail_bit(p.avail64, jj) : true;
+#pragma unroll
+        for (int k = 0; k < 5; k++) ok &= (h[k] == p.digests[(uint64_t)k * p.dcount + jj]);
+        p.out_bytes[j] = ok ? 1 : 0;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // synthetic payload fill: byte at linear offset o = byte (o & 7) of splitmix64(seed, o >> 3).
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t splitmix64(uint64_t seed, uint64_t idx) {
@@ -360,6 +423,12 @@ hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_
         if (hash) hipLaunchKernelGGL(tv_lane_kernel<true>, dim3(grid), dim3(256), 0, s, p);
         else hipLaunchKernelGGL(tv_lane_kernel<false>, dim3(grid), dim3(256), 0, s, p);
     }
+    return hipGetLastError();
+}
+
+hipError_t tv_launch_verify_list(const TvPieces& p, hipStream_t s) {
+    if (p.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(tv_list_kernel, dim3((p.n + 255) / 256), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 

@@ -30,6 +30,7 @@ const SYMBOLS = {
     result: "i32",
     nonblocking: true,
   },
+  tv_verify_list: { parameters: ["pointer", "pointer", "u64", "pointer"], result: "i32", nonblocking: true },
   tv_hash: { parameters: ["pointer", "pointer"], result: "i32", nonblocking: true },
   tv_set_option: { parameters: ["pointer", "i32", "i64"], result: "i32" },
   tv_get_option: { parameters: ["pointer", "i32", "pointer"], result: "i32" },
