@@ -259,3 +259,41 @@ def test_incremental_verifier_flow(native, oracle):
     assert bytes(v.bitfield) == bytes(b"\xff" * (P // 8) + bytes([(0xFF00 >> (P % 8)) & 0xFF]))
     assert st.get(0, total) is not None   # blocks also went through Storage.set
     v.close()
+
+
+@pytest.mark.parametrize("layout", ["multi_zero_tiny", "missing_and_short", "single_short_last"])
+def test_verify_files_resume_from_disk(native, tmp_path, layout):
+    """verify_files (f2 resume from disk: parallel preads into pinned buffers, direct DMA) gives the
+    same bits as the committed expectation and as verify_pieces over fs_storage."""
+    from tests.layouts import build_layout, by_name
+    from torrent_amd import verify_files
+    from torrent_amd.verify import _STAGE_BATCH_BYTES  # noqa: F401
+    rec = {r["name"]: r for r in json.load(open(os.path.join(GOLDEN, "layouts.json")))}[layout]
+    lay = build_layout(by_name(layout))
+    for path, data in lay["disk_files"]().items():
+        p = tmp_path.joinpath(*path)
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_bytes(data)
+    before = sorted(str(x) for x in tmp_path.rglob("*"))
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        # small batches + 2 devices slots on GPU 0: exercises batching, double buffering, shards
+        bf = verify_files(lay["info"], str(tmp_path), devices=[0, 0], batch_bytes=3 * lay["info"].piece_length)
+    finally:
+        os.chdir(cwd)
+    assert bytes(bf).hex() == rec["expected_bitfield"]
+    assert sorted(str(x) for x in tmp_path.rglob("*")) == before   # no files created
+
+
+def test_verify_files_reference_singlefile(native, tmp_path):
+    from torrent_amd import parse_metainfo, verify_files
+    info = parse_metainfo(_load("singlefile.torrent")).info
+    (tmp_path / info.name).write_bytes(_ref_payload("singlefile"))
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        bf = verify_files(info, str(tmp_path))
+    finally:
+        os.chdir(cwd)
+    assert bytes(bf) == _all_ones(info.n_pieces)

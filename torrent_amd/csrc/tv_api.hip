@@ -219,37 +219,49 @@ int finish_timing(tv_ctx* c) {
 
 // Stage one contiguous range of LINEAR bytes that lies inside a single piece or covers whole
 // pieces; src is host memory.  Rows of whole pieces use one 2D copy (src pitch L, dst pitch stride).
-int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n) {
+// A page-locked src is read by DMA directly; pageable memory is copied through the pinned ring.
+int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n, bool pinned) {
     while (n) {
         const uint64_t i = pos / c->L, within = pos % c->L;
         const uint64_t plen = piece_len(c, i);
         uint8_t* dst = c->d_payload + (i - c->first) * c->stride + within;
-        int slot;
-        int rc = take_slot(c, &slot);
-        if (rc) return rc;
+        const uint64_t cap = pinned ? UINT64_MAX : (uint64_t)kRingSlotBytes;
+        int slot = -1;
+        if (!pinned) {
+            int rc = take_slot(c, &slot);
+            if (rc) return rc;
+        }
+        const uint8_t* from = pinned ? src : c->ring[slot];
         uint64_t bytes;
-        if (within == 0 && plen == c->L && n >= c->L && c->L <= kRingSlotBytes) {
+        if (within == 0 && plen == c->L && n >= c->L && c->L <= cap) {
             // k whole pieces (none of them the short last piece)
-            uint64_t k = std::min<uint64_t>(n / c->L, kRingSlotBytes / c->L);
+            uint64_t k = std::min<uint64_t>(n / c->L, cap / c->L);
             const uint64_t last_full = (c->total % c->L) ? c->P - 1 : c->P;  // first index that is not full
             k = std::min<uint64_t>(k, (last_full > i) ? last_full - i : 1);
             bytes = k * c->L;
-            memcpy(c->ring[slot], src, bytes);
-            TV_HIP(c, hipMemcpy2DAsync(dst, c->stride, c->ring[slot], c->L, c->L, k, hipMemcpyHostToDevice,
-                                       c->copy_stream));
+            if (!pinned) memcpy(c->ring[slot], src, bytes);
+            TV_HIP(c, hipMemcpy2DAsync(dst, c->stride, from, c->L, c->L, k, hipMemcpyHostToDevice, c->copy_stream));
         } else {
-            bytes = std::min<uint64_t>({n, plen > within ? plen - within : 0, (uint64_t)kRingSlotBytes});
+            bytes = std::min<uint64_t>({n, plen > within ? plen - within : 0, cap});
             if (bytes == 0) return fail(c, TV_ERR_ARG, "stage offset %llu is past piece %llu", (unsigned long long)pos,
                                         (unsigned long long)i);
-            memcpy(c->ring[slot], src, bytes);
-            TV_HIP(c, hipMemcpyAsync(dst, c->ring[slot], bytes, hipMemcpyHostToDevice, c->copy_stream));
+            if (!pinned) memcpy(c->ring[slot], src, bytes);
+            TV_HIP(c, hipMemcpyAsync(dst, from, bytes, hipMemcpyHostToDevice, c->copy_stream));
         }
-        TV_HIP(c, hipEventRecord(c->ring_ev[slot], c->copy_stream));
+        if (!pinned) TV_HIP(c, hipEventRecord(c->ring_ev[slot], c->copy_stream));
         pos += bytes;
         src += bytes;
         n -= bytes;
     }
     return TV_OK;
+}
+
+bool is_pinned(const void* p) {
+    hipPointerAttribute_t attr{};
+    const bool ok = hipPointerGetAttributes(&attr, p) == hipSuccess && attr.type == hipMemoryTypeHost &&
+                    attr.devicePointer != nullptr;
+    (void)hipGetLastError();
+    return ok;
 }
 
 }  // namespace
@@ -436,6 +448,7 @@ int tv_stage(tv_ctx* c, uint64_t linear_offset, const uint8_t* src, uint64_t len
     if (linear_offset + len < linear_offset) return fail(c, TV_ERR_ARG, "offset + len overflows");
     if (a >= b) return TV_OK;
     // piece by piece segments (a piece may be shorter than L only at the end of the torrent)
+    const bool pinned = is_pinned(src);
     uint64_t pos = a;
     while (pos < b) {
         const uint64_t i = pos / c->L, within = pos % c->L;
@@ -451,7 +464,7 @@ int tv_stage(tv_ctx* c, uint64_t linear_offset, const uint8_t* src, uint64_t len
         } else {
             n = std::min(b - pos, plen - within);
         }
-        rc = stage_copy(c, pos, src + (pos - linear_offset), n);
+        rc = stage_copy(c, pos, src + (pos - linear_offset), n, pinned);
         if (rc) return rc;
         pos += n;
     }
@@ -645,12 +658,9 @@ int tv_verify_host(tv_ctx* c, const uint8_t* src, uint64_t src_len, const uint8_
         for (auto& p : c->d_chunk) TV_HIP(c, hipMalloc((void**)&p, row * n + kSlack));
         c->chunk_bytes = row * n + kSlack;
     }
-    hipPointerAttribute_t attr{};
     // DMA straight from the caller's buffer only when it is page-locked (hipHostMalloc or
     // hipHostRegister): such memory has a device mapping.  Pageable memory goes through the ring.
-    bool pinned = hipPointerGetAttributes(&attr, src) == hipSuccess && attr.type == hipMemoryTypeHost &&
-                  attr.devicePointer != nullptr;
-    (void)hipGetLastError();
+    const bool pinned = is_pinned(src);
 
     const uint64_t ncol = (c->L + C - 1) / C;
     const int kernel = choose_kernel(c);
