@@ -139,6 +139,7 @@ int tv_host_unregister(void *ptr);
 #define TV_OPT_KERNEL 1      /* 0 = auto, 1 = lane kernel, 2 = split (schedule-offload) kernel */
 #define TV_OPT_STRIDE_PAD 2  /* bytes of padding between resident pieces (default 256) */
 #define TV_OPT_STREAM_CHUNK 3 /* tv_verify_host: bytes of each piece per streamed column chunk */
+#define TV_OPT_SPLIT_PAIRS 4  /* split kernel: (rounds, helper) wave pairs per workgroup, 0 = auto, 1, 2 */
 int tv_set_option(tv_ctx *ctx, int key, int64_t value);
 int tv_get_option(tv_ctx *ctx, int key, int64_t *value);
 

@@ -22,6 +22,7 @@ TV_ERR_NOMEM = -4
 TV_OPT_KERNEL = 1
 TV_OPT_STRIDE_PAD = 2
 TV_OPT_STREAM_CHUNK = 3
+TV_OPT_SPLIT_PAIRS = 4
 
 KERNEL_AUTO, KERNEL_LANE, KERNEL_SPLIT = 0, 1, 2
 

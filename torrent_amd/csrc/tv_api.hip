@@ -43,6 +43,7 @@ struct tv_ctx {
     int kernel_opt = TV_KERNEL_AUTO;
     uint64_t pad = 256;
     uint64_t stream_chunk = 0;  // 0 = automatic
+    int split_pairs = 0;        // 0 = automatic
 
     // device memory
     uint8_t* d_payload = nullptr;
@@ -351,6 +352,10 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
             if (value < 0 || value % 64) return fail(c, TV_ERR_ARG, "TV_OPT_STREAM_CHUNK must be a multiple of 64");
             c->stream_chunk = (uint64_t)value;
             return TV_OK;
+        case TV_OPT_SPLIT_PAIRS:
+            if (value < 0 || value > 2) return fail(c, TV_ERR_ARG, "TV_OPT_SPLIT_PAIRS must be 0, 1 or 2");
+            c->split_pairs = (int)value;
+            return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
@@ -362,6 +367,7 @@ int tv_get_option(tv_ctx* c, int key, int64_t* value) {
         case TV_OPT_KERNEL: *value = c->kernel_opt; return TV_OK;
         case TV_OPT_STRIDE_PAD: *value = (int64_t)c->pad; return TV_OK;
         case TV_OPT_STREAM_CHUNK: *value = (int64_t)c->stream_chunk; return TV_OK;
+        case TV_OPT_SPLIT_PAIRS: *value = c->split_pairs; return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
@@ -534,7 +540,7 @@ int tv_verify(tv_ctx* c, const uint8_t* avail_bits, uint8_t* bitfield_out) {
     const int kernel = choose_kernel(c);
     TvPieces p = resident_launch(c);
     TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
-    TV_HIP(c, tv_launch_verify(p, kernel, false, c->stream));
+    TV_HIP(c, tv_launch_verify(p, kernel, false, c->stream, c->split_pairs));
     TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
     rc = read_bits(c, bitfield_out);
     if (rc) return rc;
@@ -601,7 +607,7 @@ int tv_hash(tv_ctx* c, uint8_t* digests_out) {
     TvPieces p = resident_launch(c);
     p.avail64 = nullptr;
     TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
-    TV_HIP(c, tv_launch_verify(p, kernel, true, c->stream));
+    TV_HIP(c, tv_launch_verify(p, kernel, true, c->stream, c->split_pairs));
     TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
     std::vector<uint32_t> soa(5 * c->count);
     TV_HIP(c, hipMemcpyAsync(soa.data(), c->d_hash, soa.size() * 4, hipMemcpyDeviceToHost, c->stream));
@@ -730,7 +736,7 @@ int tv_verify_host(tv_ctx* c, const uint8_t* src, uint64_t src_len, const uint8_
         const bool last_col = col + 1 == ncol;
         p.blk_end = last_col ? UINT64_MAX : (off + C) / 64;
         p.finalize = last_col ? 1 : 0;
-        TV_HIP(c, tv_launch_verify(p, kernel, false, c->stream));
+        TV_HIP(c, tv_launch_verify(p, kernel, false, c->stream, c->split_pairs));
         TV_HIP(c, hipEventRecord(done_ev[buf], c->stream));
     }
     TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));

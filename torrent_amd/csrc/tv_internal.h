@@ -30,7 +30,7 @@ struct TvPieces {
     uint8_t* out_bytes;      // list mode: out_bytes[j] = 1 iff piece idx[j] matches
 };
 
-hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_t s);
+hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_t s, int split_pairs = 0);
 hipError_t tv_launch_verify_list(const TvPieces& p, hipStream_t s);
 hipError_t tv_launch_fill(uint8_t* payload, uint64_t stride, uint64_t first, uint32_t n, uint64_t L,
                           uint64_t seed, hipStream_t s);

@@ -252,21 +252,21 @@ __device__ __forceinline__ void lds_barrier() {
 
 }  // namespace
 
-template <bool HASH>
-__global__ __launch_bounds__(256) void tv_split_kernel(TvPieces p) {
-    // 4 waves = 2 pairs x {rounds, helper}; 128 pieces.  A workgroup's waves go to 4 distinct SIMDs,
-    // so with <= 1 workgroup per CU no rounds wave shares its SIMD.  Each pair has its own 2 x 20 KiB
+template <bool HASH, int PAIRS>
+__global__ __launch_bounds__(128 * PAIRS) void tv_split_kernel(TvPieces p) {
+    // PAIRS x {rounds, helper} waves; 64*PAIRS pieces.  A workgroup's waves go to distinct SIMDs, so
+    // with <= 1 workgroup per CU no rounds wave shares its SIMD.  Each pair has its own 2 x 20 KiB
     // K+W ring; the barrier is workgroup-wide, so both pairs run the same (workgroup) block range.
-    __shared__ __attribute__((aligned(16))) uint4 ring[4 * kRingWords / 4];
+    __shared__ __attribute__((aligned(16))) uint4 ring[2 * PAIRS * kRingWords / 4];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t pair = wave & 1u;
-    const uint32_t role = wave >> 1;           // 0 = rounds, 1 = helper
-    const uint32_t wg0 = blockIdx.x * 128u;
+    const uint32_t pair = wave % PAIRS;
+    const uint32_t role = wave / PAIRS;        // 0 = rounds, 1 = helper
+    const uint32_t wg0 = blockIdx.x * (64u * PAIRS);
     const uint32_t j0 = wg0 + pair * 64u;
     const uint32_t j = j0 + lane;
     const uint32_t jj = j < p.n ? j : p.n - 1;
-    const WaveGeom g = wave_geom(p, wg0, 128);
+    const WaveGeom g = wave_geom(p, wg0, 64u * PAIRS);
     const uint64_t len = lane_len(p, jj);
     const uint32_t nb = (uint32_t)nblocks(len);
     const uint8_t* piece = p.data + (uint64_t)jj * p.stride - p.data_off;
@@ -412,12 +412,20 @@ __global__ __launch_bounds__(256) void tv_fill_bytes_kernel(uint8_t* payload, ui
 // ------------------------------------------------------------------------------------------
 // host-side launchers (called by tv_api.hip)
 // ------------------------------------------------------------------------------------------
-hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_t s) {
+hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_t s, int split_pairs) {
     if (p.n == 0) return hipSuccess;
     if (kernel == TV_KERNEL_SPLIT) {
-        const unsigned grid = (p.n + 127) / 128;
-        if (hash) hipLaunchKernelGGL(tv_split_kernel<true>, dim3(grid), dim3(256), 0, s, p);
-        else hipLaunchKernelGGL(tv_split_kernel<false>, dim3(grid), dim3(256), 0, s, p);
+        // one pair per workgroup while that still gives <= 1 workgroup per CU (256 CUs); two pairs
+        // (4 waves on the CU's 4 SIMDs) up to 32768 pieces
+        const int pairs = split_pairs ? split_pairs : (p.n <= 256 * 64 ? 1 : 2);
+        const unsigned grid = (p.n + 64 * pairs - 1) / (64 * pairs);
+        if (pairs == 1) {
+            if (hash) hipLaunchKernelGGL((tv_split_kernel<true, 1>), dim3(grid), dim3(128), 0, s, p);
+            else hipLaunchKernelGGL((tv_split_kernel<false, 1>), dim3(grid), dim3(128), 0, s, p);
+        } else {
+            if (hash) hipLaunchKernelGGL((tv_split_kernel<true, 2>), dim3(grid), dim3(256), 0, s, p);
+            else hipLaunchKernelGGL((tv_split_kernel<false, 2>), dim3(grid), dim3(256), 0, s, p);
+        }
     } else {
         const unsigned grid = (p.n + 255) / 256;
         if (hash) hipLaunchKernelGGL(tv_lane_kernel<true>, dim3(grid), dim3(256), 0, s, p);
