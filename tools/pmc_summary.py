@@ -17,7 +17,7 @@ def load(tag_dir):
         per = defaultdict(lambda: defaultdict(float))
         for row in csv.DictReader(open(f)):
             k = row.get("Kernel_Name", "")
-            if "kernel<false>" not in k:
+            if "kernel<false" not in k:
                 continue
             d = row.get("Dispatch_Id") or row.get("Correlation_Id")
             per[d][row["Counter_Name"]] += float(row["Counter_Value"])
