@@ -172,18 +172,96 @@ def verify_payload(info: InfoDict, payload, devices=None, resident: bool = True,
     return _concat(slices, ranges, P)
 
 
+def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: int,
+                 batch_bytes: int) -> bytearray:
+    """Stage the shard's pieces from files (storage.segments mapping) into HBM and return the
+    shard's readability bits.  Parallel preads go straight into two alternating page-locked
+    buffers; batch i is DMA'd while batch i+1 is read.  A piece touching a missing or short file
+    is unreadable (fsStorage.get -> null, storage.ts:150-172); zero-length reads succeed; missing
+    files are never created."""
+    import os
+    L = info.piece_length
+    avail = bytearray(b"\xff" * ((count + 7) // 8))
+    if count % 8:
+        avail[-1] = (0xFF00 >> (count % 8)) & 0xFF
+    per = max(1, batch_bytes // L)
+    bufs = [_native.PinnedBuffer(per * L), _native.PinnedBuffer(per * L)]
+    fds: dict = {}
+    lock = threading.Lock()
+
+    def fd_of(path):
+        key = os.path.join(*path)
+        with lock:
+            if key not in fds:
+                try:
+                    fd = os.open(key, os.O_RDONLY)
+                    fds[key] = (fd, os.fstat(fd).st_size)
+                except OSError:
+                    fds[key] = (None, -1)
+            return fds[key]
+
+    def clear(j_lo: int, j_hi: int) -> None:   # shard-relative pieces [j_lo, j_hi] unreadable
+        for j in range(max(0, j_lo), min(count - 1, j_hi) + 1):
+            avail[j >> 3] &= ~(0x80 >> (j & 7)) & 0xFF
+
+    def read_batch(b: int, buf) -> int:
+        j = b * per
+        k = min(per, count - j)
+        lo = (first + j) * L
+        hi = lo + (k - 1) * L + piece_length(first + j + k - 1, info)
+        for jj in range(j, j + k):       # bytes past the last file (more digests than data)
+            if (first + jj) * L + piece_length(first + jj, info) > info.length:
+                clear(jj, jj)
+        segs = storage.segments(lo, max(0, min(hi, info.length) - lo)) or []
+
+        def one(seg):
+            path, foff, n, start = seg
+            if n == 0:
+                return True
+            fd, size = fd_of(path)
+            if fd is None or foff + n > size:
+                return (start, n)
+            got = os.preadv(fd, [buf.mv[start:start + n]], foff)
+            return True if got == n else (start, n)
+
+        with ThreadPoolExecutor(max(1, threads)) as ex:
+            for r in ex.map(one, segs):
+                if r is not True:
+                    s0, n = r
+                    clear(j + s0 // L, j + (s0 + n - 1) // L)
+        return hi - lo
+
+    nb = -(-count // per)
+    stager = ThreadPoolExecutor(1)
+    fut = None
+    try:
+        for b in range(nb):
+            buf = bufs[b & 1]
+            n = read_batch(b, buf)
+            if fut is not None:
+                fut.result()           # the other buffer's DMA is done before it is reused
+            fut = stager.submit(ctx.stage, (first + b * per) * L, buf.mv[:n])
+        if fut is not None:
+            fut.result()
+    finally:
+        stager.shutdown()
+        for fd, _ in fds.values():
+            if fd is not None:
+                os.close(fd)
+        for bb in bufs:
+            bb.close()
+    return avail
+
+
 def verify_files(info: InfoDict, dir_path: str, devices=None, threads: int = 8,
                  batch_bytes: int = 256 << 20) -> bytearray:
     """Resume check from disk: the have-bitfield of the files under dir_path,
     laid out as Storage(fs_storage, info, dir_path) maps them (storage.ts:89-137; single-file
     torrents are [dir, name], multi-file [dir, *path] without info.name).
 
-    Same bits as verify_pieces(info, Storage(fs_storage, info, dir_path)): a piece touching a
-    missing or short file is unreadable (fsStorage.get -> null, storage.ts:150-172), zero-length
-    reads succeed.  Unlike fsStorage.get it never creates missing files (no side effects).  Reads
-    go straight into page-locked buffers (parallel preads over `threads`), two buffers alternate so
-    the next batch is read while the previous one is DMA'd into HBM."""
-    import os
+    Same bits as verify_pieces(info, Storage(fs_storage, info, dir_path)), without fsStorage.get's
+    side effect of creating missing files, and with the file reads streamed into page-locked
+    buffers (see _files_shard) instead of one open/seek/read per piece."""
     from .storage import Storage, fs_storage
 
     P, L = info.n_pieces, info.piece_length
@@ -194,81 +272,40 @@ def verify_files(info: InfoDict, dir_path: str, devices=None, threads: int = 8,
         ctx.set_digests(info.pieces_raw)
         if count == 0:
             return b""
-        avail = bytearray(b"\xff" * ((count + 7) // 8))
-        per = max(1, batch_bytes // L)
-        bufs = [_native.PinnedBuffer(per * L), _native.PinnedBuffer(per * L)]
-        fds: dict = {}
-        lock = threading.Lock()
-
-        def fd_of(path):
-            key = os.path.join(*path)
-            with lock:
-                if key not in fds:
-                    try:
-                        fd = os.open(key, os.O_RDONLY)
-                        fds[key] = (fd, os.fstat(fd).st_size)
-                    except OSError:
-                        fds[key] = (None, -1)
-                return fds[key]
-
-        def clear(j_lo: int, j_hi: int) -> None:   # shard-relative pieces [j_lo, j_hi] unreadable
-            for j in range(max(0, j_lo), min(count - 1, j_hi) + 1):
-                avail[j >> 3] &= ~(0x80 >> (j & 7)) & 0xFF
-
-        def read_batch(b: int, buf) -> int:
-            j = b * per
-            k = min(per, count - j)
-            lo = (first + j) * L
-            hi = lo + (k - 1) * L + piece_length(first + j + k - 1, info)
-            segs = storage.segments(lo, hi - lo) if hi <= info.length else None
-            if segs is None:      # bytes past the last file: every piece of the batch is checked below
-                segs = storage.segments(lo, max(0, min(hi, info.length) - lo)) or []
-                for jj in range(j, j + k):
-                    if (first + jj) * L + piece_length(first + jj, info) > info.length:
-                        clear(jj, jj)
-
-            def one(seg):
-                path, foff, n, start = seg
-                if n == 0:
-                    return True
-                fd, size = fd_of(path)
-                if fd is None or foff + n > size:
-                    return (start, n)
-                got = os.preadv(fd, [buf.mv[start:start + n]], foff)
-                return True if got == n else (start, n)
-
-            with ThreadPoolExecutor(max(1, threads)) as ex:
-                for r in ex.map(one, segs):
-                    if r is not True:
-                        s0, n = r
-                        clear(j + s0 // L, j + (s0 + n - 1) // L)
-            return hi - lo
-
-        nb = -(-count // per)
-        stager = ThreadPoolExecutor(1)
-        fut = None
-        try:
-            for b in range(nb):
-                buf = bufs[b & 1]
-                n = read_batch(b, buf)
-                if fut is not None:
-                    fut.result()           # the other buffer's DMA is done before it is reused
-                fut = stager.submit(ctx.stage, (first + b * per) * L, buf.mv[:n])
-            if fut is not None:
-                fut.result()
-        finally:
-            stager.shutdown()
-            for fd, _ in fds.values():
-                if fd is not None:
-                    os.close(fd)
-            for bb in bufs:
-                bb.close()
-        return ctx.verify(avail)
+        return ctx.verify(_files_shard(ctx, info, storage, first, count, threads, batch_bytes))
 
     if P == 0:
         return bytearray()
     ranges, slices = _run_shards(_devices(devices), P, shard)
     return _concat(slices, ranges, P)
+
+
+def hash_files(info: InfoDict, dir_path: str, devices=None, threads: int = 8,
+               batch_bytes: int = 256 << 20) -> bytes:
+    """Creation mode from disk: the `pieces` string of the files info describes under dir_path
+    (info.pieces is ignored; only the geometry is used).  Raises if a file is missing or short."""
+    from .storage import Storage, fs_storage
+
+    L = info.piece_length
+    P = -(-info.length // L) if info.length else 0
+    storage = Storage(fs_storage, info, dir_path)
+
+    def shard(ctx, first: int, count: int) -> bytes:
+        ctx.set_layout(info.length, L, P, first, count)
+        if count == 0:
+            return b""
+        avail = _files_shard(ctx, info, storage, first, count, threads, batch_bytes)
+        full = bytearray(b"\xff" * ((count + 7) // 8))
+        if count % 8:
+            full[-1] = (0xFF00 >> (count % 8)) & 0xFF
+        if avail != full:
+            raise FileNotFoundError("hash_files: a file is missing or shorter than its declared length")
+        return ctx.hash()
+
+    if P == 0:
+        return b""
+    _, slices = _run_shards(_devices(devices), P, shard)
+    return b"".join(slices)
 
 
 def verify_piece(info: InfoDict, index: int, data) -> bool:
