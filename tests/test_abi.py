@@ -69,3 +69,76 @@ def test_no_oracle_in_product_path():
             if f.endswith((".py", ".hip", ".h", ".cpp")):
                 txt = open(os.path.join(dp, f)).read()
                 assert "oracle" not in txt.replace("Oracle", "").lower() or f == "__init__.py", f
+
+
+def _header_prototypes():
+    """(name -> (result C type, [param C types])) for every function include/torrent_verify.h declares."""
+    import re
+    src = open(os.path.join(ROOT, "include", "torrent_verify.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    out = {}
+    for m in re.finditer(r"^\s*(void|int)\s+(tv_\w+)\s*\(([^)]*)\)\s*;", src, flags=re.M):
+        params = [p.strip() for p in m.group(3).split(",") if p.strip() and p.strip() != "void"]
+        types = [re.sub(r"\s*\b\w+$", "", p) if not p.endswith("*") else p for p in params]
+        out[m.group(2)] = (m.group(1), [" ".join(t.replace("*", " * ").split()) for t in types])
+    return out
+
+
+def _deno_type(c):
+    if "*" in c:
+        return "pointer"
+    return {"int": "i32", "uint64_t": "u64", "int64_t": "i64", "size_t": "usize", "void": "void"}[c]
+
+
+def test_deno_and_ctypes_bindings_match_header():
+    """ts/verify.ts (the Deno.dlopen table a maintainer adds) and
+    torrent_amd/_native.py (its ctypes twin) declare exactly the header's functions with the same
+    parameter kinds.  Deno is absent from the image, so this is how the TS binding is checked."""
+    import ctypes
+    import re
+    protos = _header_prototypes()
+    assert len(protos) >= 20
+    ts = open(os.path.join(ROOT, "ts", "verify.ts")).read()
+    table = ts[ts.index("const SYMBOLS = {"):ts.index("} as const;")]
+    deno = {}
+    for m in re.finditer(r"(tv_\w+):\s*\{\s*parameters:\s*\[([^\]]*)\],\s*result:\s*\"(\w+)\"", table, flags=re.S):
+        deno[m.group(1)] = (m.group(3), re.findall(r"\"(\w+)\"", m.group(2)))
+    assert set(deno) == set(protos)
+    for name, (res, params) in protos.items():
+        assert deno[name] == (_deno_type(res), [_deno_type(p) for p in params]), name
+
+    from torrent_amd import _native
+    ct = {n: (r, a) for n, r, a in _native.SYMBOLS}
+    assert set(ct) == set(protos)
+    size = {"int": 4, "uint64_t": 8, "int64_t": 8, "size_t": 8}
+    for name, (res, params) in protos.items():
+        r, args = ct[name]
+        assert (r is None) == (res == "void"), name
+        assert len(args) == len(params), name
+        for c, a in zip(params, args):
+            if "*" in c:
+                assert a in (ctypes.c_void_p, ctypes.c_char_p) or hasattr(a, "contents") or a.__name__.startswith("LP_"), (name, c)
+            else:
+                assert ctypes.sizeof(a) == size[c], (name, c)
+
+
+def test_product_path_fails_loudly_without_the_library(tmp_path):
+    """No CPU fallback: with the HIP library absent, verify_pieces / hash_pieces raise ImportError
+    instead of computing anything (a silent fallback would void the parity claims)."""
+    code = (
+        "from torrent_amd import make_info, verify_pieces, hash_pieces\n"
+        "info = make_info(64, bytes(20), 'x', length=64)\n"
+        "class S:\n"
+        "    def get(self, off, n): return bytes(n)\n"
+        "for fn, a in ((verify_pieces, (info, S())), (hash_pieces, (bytes(64), 64))):\n"
+        "    try:\n"
+        "        fn(*a)\n"
+        "    except ImportError as e:\n"
+        "        assert 'no CPU fallback' in str(e), e\n"
+        "    else:\n"
+        "        raise SystemExit(fn.__name__ + ' returned without the library')\n"
+        "print('raised')\n")
+    env = dict(os.environ, TORRENT_VERIFY_LIB=str(tmp_path / "missing.so"))
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "raised" in r.stdout, r.stdout + r.stderr
