@@ -42,8 +42,25 @@ def lib():
         L.orc_synth_fill.argtypes = [_u64, _u64, _u64, _p]
         L.orc_synth_piece_digests.argtypes = [_u64, _u64, _u64, _u64, _u64, _u64, ctypes.c_int, _p]
         L.orc_hash_pieces.argtypes = [_p, _u64, _u64, _u64, _u64, _u64, ctypes.c_int, _p]
+        L.orc_set_impl.argtypes = [ctypes.c_int]
+        L.orc_set_impl.restype = ctypes.c_int
+        L.orc_get_impl.restype = ctypes.c_int
         _lib = L
     return _lib
+
+
+IMPL_NAMES = {1: "scalar", 2: "sha-ni"}
+
+
+def set_impl(name: str) -> bool:
+    """Select the compression: "best", "scalar" (plain FIPS 180-4 restatement) or "sha-ni"
+    (x86 SHA extensions).  Returns False if the host lacks the requested one."""
+    code = {"best": 0, "scalar": 1, "sha-ni": 2}[name]
+    return lib().orc_set_impl(code) > 0
+
+
+def impl() -> str:
+    return IMPL_NAMES[lib().orc_get_impl()]
 
 
 def _buf(b):

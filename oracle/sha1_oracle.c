@@ -26,6 +26,7 @@
  * splitmix64(seed, o >> 3).  The device fill kernel implements the same function.
  */
 #include <pthread.h>
+#include <stddef.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -57,10 +58,89 @@ static void orc_compress(uint32_t h[5], const uint8_t *blk) {
     h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
 }
 
+/* Same compression with the x86 SHA extensions (SHA-NI): sha1rnds4 runs 4 rounds, sha1nexte
+ * derives the next E (rotl30 of the old A) plus 4 message words, and sha1msg1/2 expand the
+ * schedule W[t] = rotl1(W[t-3]^W[t-8]^W[t-14]^W[t-16]).  It is the CPU baseline's fast path: the
+ * reference's own SHA-1 (WebCrypto in the Deno runtime) is native code of this class, and the
+ * SURVEY (sec. 8d) asks for the baseline at that speed, not a slow scalar port.  The scalar
+ * orc_compress above stays as the plain FIPS restatement; tests check both. */
+#if defined(__x86_64__)
+#include <immintrin.h>
+#define ORC_NI_GROUP(g, f)                                                                          \
+    do {                                                                                            \
+        __m128i mg;                                                                                 \
+        if ((g) < 4)                                                                                \
+            mg = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i *)(blk + 16 * (g))), rev);        \
+        else                                                                                        \
+            mg = _mm_sha1msg2_epu32(_mm_xor_si128(_mm_sha1msg1_epu32(m[((g) - 4) & 3], m[((g) - 3) & 3]), \
+                                                  m[((g) - 2) & 3]),                                \
+                                    m[((g) - 1) & 3]);                                              \
+        m[(g) & 3] = mg;                                                                            \
+        __m128i ev = (g) == 0 ? _mm_add_epi32(e0, mg) : _mm_sha1nexte_epu32(prev, mg);              \
+        prev = abcd;                                                                                \
+        abcd = _mm_sha1rnds4_epu32(abcd, ev, f);                                                    \
+    } while (0)
+__attribute__((target("sha,ssse3,sse4.1"))) static void orc_compress_ni(uint32_t h[5], const uint8_t *blk,
+                                                                         size_t nblocks) {
+    const __m128i rev = _mm_set_epi64x(0x0001020304050607ll, 0x08090a0b0c0d0e0fll);
+    __m128i abcd = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i *)h), 0x1B);
+    __m128i e0 = _mm_set_epi32((int)h[4], 0, 0, 0);
+    for (; nblocks; nblocks--, blk += 64) {
+        const __m128i abcd0 = abcd, e00 = e0;
+        __m128i m[4], prev = abcd;
+        ORC_NI_GROUP(0, 0); ORC_NI_GROUP(1, 0); ORC_NI_GROUP(2, 0); ORC_NI_GROUP(3, 0); ORC_NI_GROUP(4, 0);
+        ORC_NI_GROUP(5, 1); ORC_NI_GROUP(6, 1); ORC_NI_GROUP(7, 1); ORC_NI_GROUP(8, 1); ORC_NI_GROUP(9, 1);
+        ORC_NI_GROUP(10, 2); ORC_NI_GROUP(11, 2); ORC_NI_GROUP(12, 2); ORC_NI_GROUP(13, 2); ORC_NI_GROUP(14, 2);
+        ORC_NI_GROUP(15, 3); ORC_NI_GROUP(16, 3); ORC_NI_GROUP(17, 3); ORC_NI_GROUP(18, 3); ORC_NI_GROUP(19, 3);
+        e0 = _mm_sha1nexte_epu32(prev, e00);
+        abcd = _mm_add_epi32(abcd, abcd0);
+    }
+    _mm_storeu_si128((__m128i *)h, _mm_shuffle_epi32(abcd, 0x1B));
+    h[4] = (uint32_t)_mm_extract_epi32(e0, 3);
+}
+#endif
+
+static void orc_compress_scalar(uint32_t h[5], const uint8_t *blk, size_t nblocks) {
+    for (; nblocks; nblocks--, blk += 64) orc_compress(h, blk);
+}
+
+/* 1 = scalar FIPS restatement, 2 = SHA-NI.  Default: the fastest the host supports. */
+static void (*orc_blocks)(uint32_t *, const uint8_t *, size_t) = 0;
+static int orc_impl_id = 0;
+
+static int orc_have_ni(void) {
+#if defined(__x86_64__)
+    __builtin_cpu_init();
+    return __builtin_cpu_supports("sha") && __builtin_cpu_supports("sse4.1");
+#else
+    return 0;
+#endif
+}
+
+/* Select the compression: 0 = best available, 1 = scalar, 2 = SHA-NI.  Returns the selected
+ * implementation, or -1 if the request is unsupported on this host (selection unchanged). */
+int orc_set_impl(int impl) {
+    if (impl == 0) impl = orc_have_ni() ? 2 : 1;
+    if (impl == 2 && !orc_have_ni()) return -1;
+    if (impl != 1 && impl != 2) return -1;
+#if defined(__x86_64__)
+    orc_blocks = impl == 2 ? orc_compress_ni : orc_compress_scalar;
+#else
+    orc_blocks = orc_compress_scalar;
+#endif
+    orc_impl_id = impl;
+    return impl;
+}
+int orc_get_impl(void) {
+    if (!orc_blocks) orc_set_impl(0);
+    return orc_impl_id;
+}
+
 /* Incremental interface (FIPS 180-4 5.1.1 padding). */
 typedef struct { uint32_t h[5]; uint64_t n; uint8_t buf[64]; uint32_t fill; } orc_sha1_ctx;
 
 static void orc_init(orc_sha1_ctx *c) {
+    if (!orc_blocks) orc_set_impl(0);
     c->h[0] = 0x67452301u; c->h[1] = 0xEFCDAB89u; c->h[2] = 0x98BADCFEu;
     c->h[3] = 0x10325476u; c->h[4] = 0xC3D2E1F0u; c->n = 0; c->fill = 0;
 }
@@ -68,9 +148,13 @@ static void orc_update(orc_sha1_ctx *c, const uint8_t *p, uint64_t len) {
     c->n += len;
     if (c->fill) {
         while (len && c->fill < 64) { c->buf[c->fill++] = *p++; len--; }
-        if (c->fill == 64) { orc_compress(c->h, c->buf); c->fill = 0; }
+        if (c->fill == 64) { orc_blocks(c->h, c->buf, 1); c->fill = 0; }
     }
-    while (len >= 64) { orc_compress(c->h, p); p += 64; len -= 64; }
+    if (len >= 64) {
+        size_t nb = (size_t)(len / 64);
+        orc_blocks(c->h, p, nb);
+        p += 64 * (uint64_t)nb; len -= 64 * (uint64_t)nb;
+    }
     while (len) { c->buf[c->fill++] = *p++; len--; }
 }
 static void orc_final(orc_sha1_ctx *c, uint8_t out[20]) {

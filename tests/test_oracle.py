@@ -32,7 +32,17 @@ def _payload(files):
     return b"".join(f["pattern"].encode() * (f["length"] // len(f["pattern"])) for f in files)
 
 
-def test_fips_kats(oracle):
+@pytest.fixture(params=["scalar", "sha-ni"])
+def impl(request, oracle):
+    """Run a test under each compression of the oracle: the scalar FIPS restatement and the
+    SHA-NI path the bench's cpu_baseline uses."""
+    if not oracle.set_impl(request.param):
+        pytest.skip(f"host lacks {request.param}")
+    yield request.param
+    oracle.set_impl("best")
+
+
+def test_fips_kats(oracle, impl):
     kats = json.loads(_load("kats.json"))
     assert len(kats) >= 5
     for k in kats:
@@ -41,7 +51,7 @@ def test_fips_kats(oracle):
         assert hashlib.sha1(msg).hexdigest() == k["sha1"]
 
 
-def test_oracle_vs_hashlib_random(oracle):
+def test_oracle_vs_hashlib_random(oracle, impl):
     import random
     rng = random.Random(0)
     for n in list(range(0, 200)) + [1000, 4095, 4096, 65537]:
@@ -50,7 +60,7 @@ def test_oracle_vs_hashlib_random(oracle):
 
 
 @pytest.mark.parametrize("name", ["singlefile", "multifile"])
-def test_reference_fixture_digests(oracle, name):
+def test_reference_fixture_digests(oracle, impl, name):
     """All digests of the reference's own .torrent fixtures reproduce from the reconstructed
     payload (parity with the reference's SHA-1 path is pinned here)."""
     meta = parse_metainfo(_load(f"{name}.torrent"))
