@@ -161,3 +161,57 @@ def test_fill_synthetic_matches_oracle(native, oracle):
         ctx.fill_synthetic(77)
         got = ctx.hash()
     assert got == oracle.synth_piece_digests(77, total, L, P, 8, 16)
+
+
+def _bits(bf, P):
+    return [(bf[i >> 3] >> (7 - (i & 7))) & 1 for i in range(P)]
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("L,P,last", [
+    (1, 100, 1),                         # one-byte pieces: every piece is a single padded block
+    (100, 1000, 37),                     # piece length not a multiple of 64, 2-block pieces
+    (1000, 333, 999),                    # odd length, short last piece one byte shorter
+    (16 << 20, 5, (16 << 20) - 3),       # large pieces (16 MiB; 262,144 blocks each)
+    (96 << 20, 2, (5 << 20) + 1),        # pieces larger than a 64 MiB staging-ring slot (chunked stage)
+])
+def test_edge_geometries(native, oracle, kernel, L, P, last):
+    """Extreme piece geometries: tiny, unaligned and very large pieces.  Verify, hash and the
+    incremental list kernel all equal the oracle; corrupted pieces (first, last, one inside) fail."""
+    total = L * (P - 1) + last
+    payload = oracle.synth_fill(L ^ P, 0, total)
+    pieces = bytearray(oracle.hash_pieces(payload, total, L, P, threads=8))
+    bad = sorted({0, P // 2, P - 1})
+    for i in bad:
+        pieces[20 * i + 19] ^= 0x80
+    expect = oracle.verify_linear(payload, total, L, bytes(pieces))
+    assert [i for i, b in enumerate(_bits(expect, P)) if not b] == bad
+    with _ctx(native, kernel) as ctx:
+        ctx.set_layout(total, L, P)
+        ctx.set_digests(bytes(pieces))
+        ctx.stage(0, payload)
+        assert ctx.verify() == expect
+        assert ctx.hash() == oracle.hash_pieces(payload, total, L, P, threads=8)
+        order = list(range(P))[::-1]
+        assert list(ctx.verify_list(order)) == [_bits(expect, P)[i] for i in order]
+
+
+def test_empty_and_zero_length_torrents(native, oracle):
+    """P = 0 (an empty `pieces` string): empty bitfield, no digests (torrent.ts:60 allocates
+    ceil(0/8) bytes).  length 0 with one digest: piece 0 has length L (piece.ts:16-19: 0 % L is
+    falsy) and lies past the end of the data, so it is unreadable -> bit 0 (storage.ts:130-136)."""
+    with _ctx(native) as ctx:
+        ctx.set_layout(0, 16384, 0)
+        ctx.set_digests(b"")
+        assert ctx.verify() == b""
+        assert ctx.hash() == b""
+        assert ctx.verify_host(b"") == b""
+    empty_digest = hashlib.sha1(b"").digest()
+    expect = oracle.verify_linear(b"", 0, 16384, empty_digest)
+    assert expect == b"\x00"
+    for k in KERNELS:
+        with _ctx(native, k) as ctx:
+            ctx.set_layout(0, 16384, 1)
+            ctx.set_digests(empty_digest)
+            assert ctx.verify() == expect
+            assert ctx.verify_host(b"") == expect

@@ -178,3 +178,84 @@ export async function verifyPiece(info: InfoDict, index: number, bytes: Uint8Arr
     l.symbols.tv_destroy(ctx);
   }
 }
+
+/**
+ * hashPieces(payload, pieceLength) -> the `pieces` string (20 B per piece) of a linear payload:
+ * creation mode (SURVEY 8f row f3), the GPU form of make_torrent.ts:147-173 (single file) and
+ * :62-113 (files concatenated in order).
+ */
+export async function hashPieces(payload: Uint8Array, pieceLength: number, opts: VerifyOptions = {}): Promise<Uint8Array> {
+  const P = Math.ceil(payload.length / pieceLength);
+  if (P === 0) return new Uint8Array(0);
+  const l = load(opts.libPath);
+  const h = new BigUint64Array(1);
+  check(l, null, l.symbols.tv_create(ptr(new Uint8Array(h.buffer)), (opts.devices ?? [0])[0]));
+  const ctx = Deno.UnsafePointer.create(h[0]);
+  try {
+    check(l, ctx, l.symbols.tv_set_layout(ctx, BigInt(payload.length), BigInt(pieceLength), BigInt(P), 0n, BigInt(P)));
+    check(l, ctx, l.symbols.tv_set_digests(ctx, null, 0n));
+    check(l, ctx, await l.symbols.tv_stage(ctx, 0n, ptr(payload), BigInt(payload.length)));
+    const out = new Uint8Array(20 * P);
+    check(l, ctx, await l.symbols.tv_hash(ctx, ptr(out)));
+    return out;
+  } finally {
+    l.symbols.tv_destroy(ctx);
+  }
+}
+
+/**
+ * Incremental verification on piece completion (SURVEY 8f row f1), for the MsgId.piece handler
+ * (torrent.ts:183-193): onBlock() per received 16 KiB block (after validateReceivedBlock and
+ * storage.set), flush() verifies every completed piece in ONE list launch (tv_verify_list) and
+ * sets its have-bit (torrent.ts:147-149).  Same behaviour as torrent_amd/incremental.py.
+ */
+export class PieceVerifier {
+  readonly bitfield: Uint8Array;
+  #l: Lib;
+  #ctx: Deno.PointerValue;
+  #bufs = new Map<number, { bytes: Uint8Array; blocks: Set<number> }>();
+  #pending: number[] = [];
+
+  constructor(readonly info: InfoDict, opts: VerifyOptions = {}) {
+    this.#l = load(opts.libPath);
+    const P = info.pieces.length;
+    const h = new BigUint64Array(1);
+    check(this.#l, null, this.#l.symbols.tv_create(ptr(new Uint8Array(h.buffer)), (opts.devices ?? [0])[0]));
+    this.#ctx = Deno.UnsafePointer.create(h[0]);
+    const raw = piecesRaw(info);
+    check(this.#l, this.#ctx, this.#l.symbols.tv_set_layout(this.#ctx, BigInt(info.length), BigInt(info.pieceLength), BigInt(P), 0n, BigInt(P)));
+    check(this.#l, this.#ctx, this.#l.symbols.tv_set_digests(this.#ctx, ptr(raw), BigInt(raw.length)));
+    this.bitfield = new Uint8Array(Math.ceil(P / 8));
+  }
+
+  /** One received block (already validated); true when it completed its piece. */
+  async onBlock(index: number, offset: number, block: Uint8Array): Promise<boolean> {
+    if (this.bitfield[index >> 3] & (128 >> (index % 8))) return false;
+    const len = pieceLength(index, this.info);
+    let e = this.#bufs.get(index);
+    if (!e) this.#bufs.set(index, e = { bytes: new Uint8Array(len), blocks: new Set() });
+    e.bytes.set(block, offset);
+    e.blocks.add(Math.floor(offset / 16384));
+    if (e.blocks.size < Math.ceil(len / 16384)) return false;
+    check(this.#l, this.#ctx, await this.#l.symbols.tv_stage(this.#ctx, BigInt(index * this.info.pieceLength), ptr(e.bytes), BigInt(len)));
+    this.#bufs.delete(index);
+    this.#pending.push(index);
+    return true;
+  }
+
+  /** Verify all completed pieces in one launch; returns [index, ok] and sets the have-bits. */
+  async flush(): Promise<[number, boolean][]> {
+    if (this.#pending.length === 0) return [];
+    const idx = BigUint64Array.from(this.#pending.map(BigInt));
+    const ok = new Uint8Array(idx.length);
+    check(this.#l, this.#ctx, await this.#l.symbols.tv_verify_list(this.#ctx, ptr(new Uint8Array(idx.buffer)), BigInt(idx.length), ptr(ok)));
+    const out: [number, boolean][] = this.#pending.map((i, k) => [i, ok[k] === 1]);
+    for (const [i, good] of out) if (good) this.bitfield[i >> 3] |= 128 >> (i % 8);
+    this.#pending = [];
+    return out;
+  }
+
+  close(): void {
+    this.#l.symbols.tv_destroy(this.#ctx);
+  }
+}
