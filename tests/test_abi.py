@@ -142,3 +142,22 @@ def test_product_path_fails_loudly_without_the_library(tmp_path):
     env = dict(os.environ, TORRENT_VERIFY_LIB=str(tmp_path / "missing.so"))
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "raised" in r.stdout, r.stdout + r.stderr
+
+
+def build_c_consumer(out_dir) -> str:
+    """gcc-compile tests/c/abi_consumer.c against include/ and the in-tree library (no Python in
+    the consumer: the shape of a Deno FFI / cgo binding)."""
+    exe = os.path.join(str(out_dir), "abi_consumer")
+    lib_dir = os.path.join(ROOT, "torrent_amd")
+    subprocess.check_call(["gcc", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "c", "abi_consumer.c"), "-L", lib_dir, "-ltorrent_verify",
+                           f"-Wl,-rpath,{lib_dir}", "-lpthread", "-o", exe])
+    return exe
+
+
+def test_c_consumer_error_paths(native, tmp_path):
+    """A plain-C program links the library and gets statuses + messages (never a crash) for NULL
+    arguments and, without a GPU, for tv_create."""
+    exe = build_c_consumer(tmp_path)
+    r = subprocess.run([exe, "cpu"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr

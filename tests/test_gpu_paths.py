@@ -339,3 +339,13 @@ def test_make_torrent_small_directory_quirk(native, tmp_path):
     (d / "a.txt").write_bytes(b"hello")
     out = parse_metainfo(make_torrent(str(d), "http://t/announce", creation_date=1))
     assert out.info.pieces_raw == bytes(20) and out.info.piece_length == 1 << 15
+
+
+def test_c_consumer_full_path(native, tmp_path):
+    """tests/c/abi_consumer.c on the GPU: verify / hash / verify_list / verify_host (pageable and
+    pinned) / read-back on the reference's conventions, and two contexts on two host threads."""
+    import subprocess
+    from tests.test_abi import build_c_consumer
+    exe = build_c_consumer(tmp_path)
+    r = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
