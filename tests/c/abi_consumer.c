@@ -144,7 +144,7 @@ static int run_gpu(void) {
     CHECK(kms >= 0 && tms >= kms, "timings %f %f", kms, tms);
 
     /* errors come back as status + message, never a crash */
-    CHECK(tv_set_layout(c, 7, 3, 3, 3, 1) == TV_ERR_ARG, "shard_first %% 8 != 0 must be TV_ERR_ARG");
+    CHECK(tv_set_layout(c, 60, 3, 20, 3, 1) == TV_ERR_ARG, "shard_first %% 8 != 0 must be TV_ERR_ARG");
     char msg[256];
     CHECK(tv_last_error(c, msg, sizeof msg) > 0 && strstr(msg, "multiple of 8"), "message: %s", msg);
     tv_destroy(c);
