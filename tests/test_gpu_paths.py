@@ -280,9 +280,12 @@ def test_verify_files_resume_from_disk(native, tmp_path, layout):
     try:
         # small batches + 2 devices slots on GPU 0: exercises batching, double buffering, shards
         bf = verify_files(lay["info"], str(tmp_path), devices=[0, 0], batch_bytes=3 * lay["info"].piece_length)
+        # odd-sized read chunks: every file segment is split across the read threads
+        bf2 = verify_files(lay["info"], str(tmp_path), batch_bytes=5 * lay["info"].piece_length, read_chunk=1000)
     finally:
         os.chdir(cwd)
     assert bytes(bf).hex() == rec["expected_bitfield"]
+    assert bytes(bf2).hex() == rec["expected_bitfield"]
     assert sorted(str(x) for x in tmp_path.rglob("*")) == before   # no files created
 
 

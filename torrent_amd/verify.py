@@ -173,7 +173,7 @@ def verify_payload(info: InfoDict, payload, devices=None, resident: bool = True,
 
 
 def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: int,
-                 batch_bytes: int) -> bytearray:
+                 batch_bytes: int, read_chunk: int = 8 << 20) -> bytearray:
     """Stage the shard's pieces from files (storage.segments mapping) into HBM and return the
     shard's readability bits.  Parallel preads go straight into two alternating page-locked
     buffers; batch i is DMA'd while batch i+1 is read.  A piece touching a missing or short file
@@ -213,25 +213,36 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
             if (first + jj) * L + piece_length(first + jj, info) > info.length:
                 clear(jj, jj)
         segs = storage.segments(lo, max(0, min(hi, info.length) - lo)) or []
-
-        def one(seg):
-            path, foff, n, start = seg
+        # a file segment is split into read_chunk pieces so all threads copy even when one
+        # large file covers the whole batch (a single pread would run on one core)
+        tasks = []
+        for path, foff, n, start in segs:
             if n == 0:
-                return True
+                continue
             fd, size = fd_of(path)
             if fd is None or foff + n > size:
-                return (start, n)
-            got = os.preadv(fd, [buf.mv[start:start + n]], foff)
-            return True if got == n else (start, n)
+                clear(j + start // L, j + (start + n - 1) // L)
+                continue
+            for s0 in range(0, n, read_chunk):
+                c = min(read_chunk, n - s0)
+                tasks.append((fd, foff + s0, start + s0, c))
 
-        with ThreadPoolExecutor(max(1, threads)) as ex:
-            for r in ex.map(one, segs):
-                if r is not True:
-                    s0, n = r
-                    clear(j + s0 // L, j + (s0 + n - 1) // L)
+        def one(t):
+            fd, foff, start, c = t
+            try:
+                got = os.preadv(fd, [buf.mv[start:start + c]], foff)
+            except OSError:
+                got = -1
+            return None if got == c else (start, c)
+
+        for r in pool.map(one, tasks):
+            if r is not None:
+                s0, n = r
+                clear(j + s0 // L, j + (s0 + n - 1) // L)
         return hi - lo
 
     nb = -(-count // per)
+    pool = ThreadPoolExecutor(max(1, threads))
     stager = ThreadPoolExecutor(1)
     fut = None
     try:
@@ -245,6 +256,7 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
             fut.result()
     finally:
         stager.shutdown()
+        pool.shutdown()
         for fd, _ in fds.values():
             if fd is not None:
                 os.close(fd)
@@ -253,8 +265,8 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
     return avail
 
 
-def verify_files(info: InfoDict, dir_path: str, devices=None, threads: int = 8,
-                 batch_bytes: int = 256 << 20) -> bytearray:
+def verify_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
+                 batch_bytes: int = 256 << 20, read_chunk: int = 8 << 20) -> bytearray:
     """Resume check from disk: the have-bitfield of the files under dir_path,
     laid out as Storage(fs_storage, info, dir_path) maps them (storage.ts:89-137; single-file
     torrents are [dir, name], multi-file [dir, *path] without info.name).
@@ -272,7 +284,7 @@ def verify_files(info: InfoDict, dir_path: str, devices=None, threads: int = 8,
         ctx.set_digests(info.pieces_raw)
         if count == 0:
             return b""
-        return ctx.verify(_files_shard(ctx, info, storage, first, count, threads, batch_bytes))
+        return ctx.verify(_files_shard(ctx, info, storage, first, count, threads, batch_bytes, read_chunk))
 
     if P == 0:
         return bytearray()
@@ -280,8 +292,8 @@ def verify_files(info: InfoDict, dir_path: str, devices=None, threads: int = 8,
     return _concat(slices, ranges, P)
 
 
-def hash_files(info: InfoDict, dir_path: str, devices=None, threads: int = 8,
-               batch_bytes: int = 256 << 20) -> bytes:
+def hash_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
+               batch_bytes: int = 256 << 20, read_chunk: int = 8 << 20) -> bytes:
     """Creation mode from disk: the `pieces` string of the files info describes under dir_path
     (info.pieces is ignored; only the geometry is used).  Raises if a file is missing or short."""
     from .storage import Storage, fs_storage
@@ -294,7 +306,7 @@ def hash_files(info: InfoDict, dir_path: str, devices=None, threads: int = 8,
         ctx.set_layout(info.length, L, P, first, count)
         if count == 0:
             return b""
-        avail = _files_shard(ctx, info, storage, first, count, threads, batch_bytes)
+        avail = _files_shard(ctx, info, storage, first, count, threads, batch_bytes, read_chunk)
         full = bytearray(b"\xff" * ((count + 7) // 8))
         if count % 8:
             full[-1] = (0xFF00 >> (count % 8)) & 0xFF
