@@ -352,3 +352,38 @@ def test_c_consumer_full_path(native, tmp_path):
     exe = build_c_consumer(tmp_path)
     r = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_concurrent_calls_do_not_interleave(native, oracle):
+    """Many verify_pieces / verify_piece / hash_pieces calls at once (threads via the asyncio
+    wrappers) share the cached per-device contexts; each job holds its context for its whole
+    set_layout -> stage -> verify sequence, so every result is exact."""
+    import asyncio
+    from torrent_amd import (MemoryStorage, Storage, hash_pieces, make_info, release_contexts,
+                             verify_piece_async, verify_pieces_async)
+    jobs = []
+    for k in range(6):
+        L, P = 4096 * (k + 1), 40 + 13 * k
+        total = L * (P - 1) + 1 + k
+        payload = bytes(oracle.synth_fill(100 + k, 0, total))
+        pieces = bytearray(oracle.hash_pieces(payload, total, L, P))
+        pieces[20 * (k * 5) + 1] ^= 1
+        info = make_info(L, bytes(pieces), f"t{k}", length=total)
+        st = MemoryStorage()
+        st.files[(f"t{k}",)] = bytearray(payload)
+        jobs.append((info, Storage(st, info, os.getcwd()), payload, oracle.verify_linear(payload, total, L, bytes(pieces))))
+
+    async def main():
+        coros = []
+        for info, storage, payload, _ in jobs:
+            coros.append(verify_pieces_async(info, storage, devices=[0, 0]))
+            coros.append(verify_piece_async(info, 1, payload[info.piece_length:2 * info.piece_length]))
+        return await asyncio.gather(*coros)
+
+    out = asyncio.run(main())
+    for n, (info, _, payload, expect) in enumerate(jobs):
+        assert bytes(out[2 * n]) == expect
+        assert out[2 * n + 1] is bool((expect[0] >> 6) & 1)
+        assert hash_pieces(payload, info.piece_length) == oracle.hash_pieces(
+            payload, info.length, info.piece_length, info.n_pieces)
+    release_contexts()

@@ -26,6 +26,7 @@ from __future__ import annotations
 import asyncio
 import threading
 from concurrent.futures import ThreadPoolExecutor
+from contextlib import contextmanager
 from typing import List, Optional, Sequence
 
 from . import _native
@@ -63,19 +64,36 @@ def _concat(slices: Sequence[bytes], ranges: Sequence[tuple], n_pieces: int) -> 
     return out
 
 
-_ctx_cache: dict = {}
+_ctx_cache: dict = {}          # (device, slot) -> (Context, Lock)
 _ctx_lock = threading.Lock()
 
 
-def _context(device: int, slot: int = 0) -> _native.Context:
-    """One cached context per (device, shard slot) per process: device memory is reused across
-    calls, and concurrent shards never share a context (a device may appear several times)."""
+@contextmanager
+def _context(device: int, slot: int = 0):
+    """The cached context of (device, shard slot), held exclusively for one whole job.  Device
+    memory is reused across calls.  Concurrent shards of one call never share a context (a device
+    may appear several times in `devices`).  Concurrent CALLS (threads, the async wrappers) take
+    turns: a job's set_layout -> set_digests -> stage -> verify sequence is never interleaved with
+    another job's."""
     with _ctx_lock:
-        c = _ctx_cache.get((device, slot))
-        if c is None:
-            c = _native.Context(device)
-            _ctx_cache[(device, slot)] = c
-        return c
+        e = _ctx_cache.get((device, slot))
+        if e is None:
+            e = (_native.Context(device), threading.Lock())
+            _ctx_cache[(device, slot)] = e
+    ctx, lock = e
+    with lock:
+        yield ctx
+
+
+def release_contexts() -> None:
+    """Free every cached context (its HBM payload buffer and pinned staging ring).  The next call
+    creates new ones.  Waits for jobs still running on them."""
+    with _ctx_lock:
+        entries = list(_ctx_cache.values())
+        _ctx_cache.clear()
+    for ctx, lock in entries:
+        with lock:
+            ctx.close()
 
 
 def _devices(devices) -> List[int]:
@@ -89,11 +107,15 @@ def _devices(devices) -> List[int]:
 def _run_shards(devs: List[int], n_pieces: int, fn):
     """fn(ctx, first, count) for each shard, one thread per shard (ctypes releases the GIL)."""
     ranges = shard_ranges(n_pieces, len(devs))
-    ctxs = [_context(d, s) for s, d in enumerate(devs)]
+
+    def run(slot: int, first: int, count: int):
+        with _context(devs[slot], slot) as ctx:
+            return fn(ctx, first, count)
+
     if len(devs) == 1:
-        return ranges, [fn(ctxs[0], *ranges[0])]
+        return ranges, [run(0, *ranges[0])]
     with ThreadPoolExecutor(len(devs)) as ex:
-        futs = [ex.submit(fn, c, f, n) for c, (f, n) in zip(ctxs, ranges)]
+        futs = [ex.submit(run, s, f, n) for s, (f, n) in enumerate(ranges)]
         return ranges, [f.result() for f in futs]
 
 
@@ -328,11 +350,11 @@ def verify_piece(info: InfoDict, index: int, data) -> bool:
     n = memoryview(data).nbytes
     if n != piece_length(index, info) or len(info.pieces[index]) != 20 or n == 0:
         return False
-    ctx = _context(0)
-    ctx.set_layout(n, n, 1, 0, 1)
-    ctx.set_digests(bytes(info.pieces[index]))
-    ctx.stage(0, data)
-    return bool(ctx.verify()[0] & 0x80)
+    with _context(0) as ctx:
+        ctx.set_layout(n, n, 1, 0, 1)
+        ctx.set_digests(bytes(info.pieces[index]))
+        ctx.stage(0, data)
+        return bool(ctx.verify()[0] & 0x80)
 
 
 def hash_pieces(payload, piece_length_: int, devices=None) -> bytes:
