@@ -257,6 +257,24 @@ int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n, bool pin
     return TV_OK;
 }
 
+// Every exit of a call that queued copies from caller memory drains both streams, so no DMA
+// still reads the caller's buffer after the call returns (also on error paths), and destroys
+// the call's own events.
+struct DrainGuard {
+    tv_ctx* c;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    explicit DrainGuard(tv_ctx* ctx) : c(ctx) {}
+    ~DrainGuard() {
+        (void)hipStreamSynchronize(c->copy_stream);
+        (void)hipStreamSynchronize(c->stream);
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
+        (void)hipGetLastError();
+    }
+    DrainGuard(const DrainGuard&) = delete;
+    DrainGuard& operator=(const DrainGuard&) = delete;
+};
+
 bool is_pinned(const void* p) {
     hipPointerAttribute_t attr{};
     const bool ok = hipPointerGetAttributes(&attr, p) == hipSuccess && attr.type == hipMemoryTypeHost &&
@@ -454,6 +472,7 @@ int tv_stage(tv_ctx* c, uint64_t linear_offset, const uint8_t* src, uint64_t len
     if (linear_offset + len < linear_offset) return fail(c, TV_ERR_ARG, "offset + len overflows");
     if (a >= b) return TV_OK;
     // piece by piece segments (a piece may be shorter than L only at the end of the torrent)
+    DrainGuard drain(c);
     const bool pinned = is_pinned(src);
     uint64_t pos = a;
     while (pos < b) {
@@ -474,7 +493,7 @@ int tv_stage(tv_ctx* c, uint64_t linear_offset, const uint8_t* src, uint64_t len
         if (rc) return rc;
         pos += n;
     }
-    TV_HIP(c, hipStreamSynchronize(c->copy_stream));
+    TV_HIP(c, hipStreamSynchronize(c->copy_stream));   // report a copy failure as this call's error
     return TV_OK;
 }
 
@@ -492,6 +511,7 @@ int tv_read(tv_ctx* c, uint64_t linear_offset, uint8_t* dst, uint64_t len) {
     const uint64_t hi = last * c->L + piece_len(c, last);
     uint64_t pos = std::max(linear_offset, lo);
     const uint64_t b = std::min(linear_offset + len, hi);
+    DrainGuard drain(c);  // no D2H copy into dst outlives the call, also on error paths
     while (pos < b) {
         const uint64_t i = pos / c->L, within = pos % c->L;
         const uint64_t plen = piece_len(c, i);
@@ -566,6 +586,7 @@ int tv_verify_list(tv_ctx* c, const uint64_t* pieces, uint64_t n, uint8_t* ok_ou
         local[k] = (uint32_t)(pieces[k] - c->first);
     }
     TV_HIP(c, hipSetDevice(c->device));
+    DrainGuard drain(c);  // after `local`: its H2D copy and the ok_out D2H copy end before return
     if (c->list_cap < n) {
         (void)hipFree(c->d_list); c->d_list = nullptr;
         (void)hipFree(c->d_list_out); c->d_list_out = nullptr;
@@ -610,6 +631,7 @@ int tv_hash(tv_ctx* c, uint8_t* digests_out) {
     TV_HIP(c, tv_launch_verify(p, kernel, true, c->stream, c->split_pairs));
     TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
     std::vector<uint32_t> soa(5 * c->count);
+    DrainGuard drain(c);  // declared after soa: drains before soa is freed, also on error paths
     TV_HIP(c, hipMemcpyAsync(soa.data(), c->d_hash, soa.size() * 4, hipMemcpyDeviceToHost, c->stream));
     TV_HIP(c, hipEventRecord(c->ev_call1, c->stream));
     TV_HIP(c, hipEventSynchronize(c->ev_call1));
@@ -672,12 +694,10 @@ int tv_verify_host(tv_ctx* c, const uint8_t* src, uint64_t src_len, const uint8_
     const int kernel = choose_kernel(c);
     TvPieces p = resident_launch(c);
     p.stride = row;
-    hipEvent_t col_ev[2];
-    TV_HIP(c, hipEventCreateWithFlags(&col_ev[0], hipEventDisableTiming));
-    TV_HIP(c, hipEventCreateWithFlags(&col_ev[1], hipEventDisableTiming));
-    hipEvent_t done_ev[2];
-    TV_HIP(c, hipEventCreateWithFlags(&done_ev[0], hipEventDisableTiming));
-    TV_HIP(c, hipEventCreateWithFlags(&done_ev[1], hipEventDisableTiming));
+    DrainGuard drain(c);
+    hipEvent_t* col_ev = drain.ev;       // copy of column -> buffer k done
+    hipEvent_t* done_ev = drain.ev + 2;  // kernel that read buffer k done
+    for (int k = 0; k < 4; k++) TV_HIP(c, hipEventCreateWithFlags(&drain.ev[k], hipEventDisableTiming));
     TV_HIP(c, hipEventRecord(done_ev[0], c->stream));
     TV_HIP(c, hipEventRecord(done_ev[1], c->stream));
     bool k0_recorded = false;
@@ -741,10 +761,6 @@ int tv_verify_host(tv_ctx* c, const uint8_t* src, uint64_t src_len, const uint8_
     }
     TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
     rc = read_bits(c, bitfield_out);
-    for (int k = 0; k < 2; k++) {
-        (void)hipEventDestroy(col_ev[k]);
-        (void)hipEventDestroy(done_ev[k]);
-    }
     if (rc) return rc;
     c->last_kernel = kernel;
     c->last_launches = (int)ncol;
