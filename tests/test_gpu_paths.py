@@ -387,3 +387,34 @@ def test_concurrent_calls_do_not_interleave(native, oracle):
         assert hash_pieces(payload, info.piece_length) == oracle.hash_pieces(
             payload, info.length, info.piece_length, info.n_pieces)
     release_contexts()
+
+
+def test_verify_files_read_faults_are_unreadable_pieces(native, tmp_path, monkeypatch):
+    """Fault injection (the storage_test.ts:96-108 idea, applied to verify_files' own reads): a
+    read that raises makes exactly the pieces it covers unreadable (bit 0), never an exception."""
+    from torrent_amd import make_info, verify_files
+    L, P = 4096, 24
+    total = L * P
+    payload = bytes(range(256)) * (total // 256)
+    import hashlib as _h
+    pieces = b"".join(_h.sha1(payload[i * L:(i + 1) * L]).digest() for i in range(P))
+    info = make_info(L, pieces, "f.bin", length=total)
+    (tmp_path / "f.bin").write_bytes(payload)
+    real = os.preadv
+    bad_lo, bad_hi = 5 * L + 100, 9 * L + 7          # file bytes whose reads fail
+
+    def flaky(fd, bufs, off):
+        n = sum(memoryview(b).nbytes for b in bufs)
+        if off < bad_hi and off + n > bad_lo:
+            raise OSError(5, "injected I/O error")
+        return real(fd, bufs, off)
+
+    monkeypatch.setattr(os, "preadv", flaky)
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        bf = verify_files(info, str(tmp_path), batch_bytes=8 * L, read_chunk=L)
+    finally:
+        os.chdir(cwd)
+    bits = [(bf[i >> 3] >> (7 - (i & 7))) & 1 for i in range(P)]
+    assert bits == [0 if 5 <= i <= 9 else 1 for i in range(P)]

@@ -182,6 +182,27 @@ def test_fs_storage(tmp_path):  # storage_test.ts:41-62
     assert fs.exists([str(p)]) and not fs.exists([str(tmp_path / "zz")])
 
 
+def test_fs_storage_fault_injection(tmp_path, monkeypatch):
+    """storage_test.ts:96-108 patches Deno.FsFile.prototype.seek to throw: get -> null, set ->
+    false.  Here the positional read/write itself throws.  verify_files uses its own preads and
+    turns the same failure into an unreadable piece (bit 0)."""
+    import torrent_amd.storage as S
+    p = tmp_path / "f.bin"
+    p.write_bytes(b"x" * 64)
+
+    def boom(*a, **k):
+        raise OSError(5, "injected I/O error")
+
+    monkeypatch.setattr(S.os, "pread", boom)
+    monkeypatch.setattr(S.os, "pwrite", boom)
+    fs = S.FsStorage()
+    assert fs.get([str(p)], 0, 8) is None
+    assert fs.set([str(p)], 0, b"abc") is False
+    info = make_info(32, bytes(40), "f.bin", length=64)
+    st = Storage(fs, info, str(tmp_path))
+    assert st.get(0, 32) is None and st.set(0, b"y" * 16) is False
+
+
 def test_layout_segments_agree_with_storage(oracle):
     """The seeded multi-file layouts: Storage.get over a MemoryStorage of the on-disk files
     returns exactly the layout's expected piece bytes (including missing / short files)."""
