@@ -1,0 +1,60 @@
+"""Piece-count sweep: HBM-resident verify throughput of every kernel variant vs pieces per GPU
+(16 GiB payload per point, piece length = 16 GiB / P rounded to 64 B).  Substantiates the
+auto kernel choice (tv_api.hip choose_kernel) and the piece-parallelism ceiling of DESIGN.md 4.
+usage: python tools/sweep_pieces.py [out.jsonl]"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from torrent_amd import _native as N  # noqa: E402
+
+VARIANTS = [("lane", 1, 0), ("split1", 2, 1), ("split2", 2, 2), ("auto", 0, 0)]
+PS = [1024, 2048, 4096, 8192, 12800, 16384, 20480, 25600, 32768, 40960, 51200, 65536, 131072, 262144]
+
+
+def main():
+    out = open(sys.argv[1], "w") if len(sys.argv) > 1 else None
+    rows = []
+    for P in PS:
+        L = ((16 << 30) // P) // 64 * 64
+        total = L * P
+        ctx = N.Context(0)
+        ctx.set_layout(total, L, P)
+        ctx.fill_synthetic(2)
+        ctx.set_option(N.TV_OPT_KERNEL, 1)
+        d = bytearray(ctx.hash())
+        for i in range(0, P, 100):
+            d[20 * i] ^= 1
+        ctx.set_digests(bytes(d))
+        expect = [0 if i % 100 == 0 else 1 for i in range(P)]
+        row = {"pieces": P, "piece_length": L, "bytes": total}
+        for name, k, pairs in VARIANTS:
+            ctx.set_option(N.TV_OPT_KERNEL, k)
+            ctx.set_option(N.TV_OPT_SPLIT_PAIRS, pairs)
+            best = 1e9
+            for _ in range(3):
+                bf = ctx.verify()
+                best = min(best, ctx.last_timing()[0])
+            bits = [(bf[i >> 3] >> (7 - (i & 7))) & 1 for i in range(P)]
+            assert bits == expect, (P, name)
+            row[name] = round(total / best / 1e6, 1)   # GB/s
+            if name == "auto":
+                row["auto_kernel"] = {1: "lane", 2: "split"}[ctx.last_kernel()[0]]
+        ctx.close()
+        row["best"] = max((row[n], n) for n, _, _ in VARIANTS[:3])[1]
+        rows.append(row)
+        line = json.dumps(row)
+        print(line, flush=True)
+        if out:
+            out.write(line + "\n")
+            out.flush()
+    print("| pieces | piece length | lane | split 1 pair | split 2 pairs | auto (choice) |")
+    print("|---|---|---|---|---|---|")
+    for r in rows:
+        print(f"| {r['pieces']:,} | {r['piece_length']:,} | {r['lane']:,} | {r['split1']:,} | {r['split2']:,} | "
+              f"{r['auto']:,} ({r['auto_kernel']}) |")
+
+
+if __name__ == "__main__":
+    main()
