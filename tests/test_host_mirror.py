@@ -246,3 +246,18 @@ def test_shard_ranges_byte_aligned():
             for f, c in rs:
                 assert f == pos and (f % 8 == 0 or c == 0)
                 pos += c
+
+
+@pytest.mark.parametrize("name", ["singlefile", "multifile"])
+def test_info_hash_is_sha1_of_the_original_info_bytes(name):
+    """f4 (metainfo.ts:141-143): infoHash = SHA-1(bencode(decoded.info)).  Re-encoding in
+    insertion order reproduces the .torrent's own info bytes, so the hash equals SHA-1 of the
+    info slice of the file (what every BitTorrent peer and tracker uses)."""
+    import hashlib
+    data = _load(f"{name}.torrent")
+    m = parse_metainfo(data)
+    start = data.index(b"4:info") + len(b"4:info")
+    assert data.endswith(b"e")
+    raw_info = data[start:-1]                       # "info" is the last key of the top-level dict
+    assert _bencode(_bdecode(raw_info)) == raw_info
+    assert m.info_hash == hashlib.sha1(raw_info).digest()
