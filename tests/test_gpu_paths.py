@@ -162,6 +162,46 @@ def test_full_size_cfg2_properties(native, oracle):
                 assert ((bf[i >> 3] >> (7 - (i & 7))) & 1) == (0 if i in bad else 1)
 
 
+def test_full_size_cfg4_properties(native, oracle):
+    """BASELINE config 4 at its largest single-GPU size: 200 GiB, 51,200 x 4 MiB pieces resident in
+    HBM (linear offsets to 214,748,364,800), and the 8-GPU shard geometry of the same torrent (the last
+    shard, pieces [44800, 51200), staged at linear offsets > 187 GB).  Properties: sampled creation-mode
+    digests equal the oracle's; verify with them is all ones except 1 % corrupted digests; lane and
+    split kernels agree; the shard's digests equal the whole-torrent run's slice."""
+    from torrent_amd import release_contexts, shard_ranges
+    release_contexts()  # no cached context may hold HBM while 200 GiB is resident
+    L, P = 4 << 20, 51200
+    total = L * P
+    sample = [0, 1, 63, 64, 25599, 25600, 44800, P - 2, P - 1]
+    with native.Context(0) as ctx:
+        ctx.set_layout(total, L, P)
+        ctx.fill_synthetic(4)
+        dig = ctx.hash()
+        for i in sample:
+            assert dig[20 * i:20 * i + 20] == oracle.synth_piece_digests(4, total, L, P, i, 1), i
+        bad = set(range(5, P, 100)) | {P - 1}
+        d2 = bytearray(dig)
+        for i in bad:
+            d2[20 * i] ^= 0x01
+        ctx.set_digests(bytes(d2))
+        for k in (1, 2):
+            ctx.set_option(native.TV_OPT_KERNEL, k)
+            bf = ctx.verify()
+            assert ctx.last_kernel()[0] == k
+            got = {i for i in range(P) if not (bf[i >> 3] >> (7 - (i & 7))) & 1}
+            assert got == bad, (k, sorted(got ^ bad)[:10])
+    first, count = shard_ranges(P, 8)[7]
+    assert (first, count) == (44800, 6400)
+    with native.Context(0) as ctx:
+        ctx.set_layout(total, L, P, first, count)
+        ctx.fill_synthetic(4)
+        assert ctx.hash() == dig[20 * first:20 * (first + count)]
+        ctx.set_digests(bytes(d2))
+        bf = ctx.verify()
+        for j in range(count):
+            assert ((bf[j >> 3] >> (7 - (j & 7))) & 1) == (0 if first + j in bad else 1), j
+
+
 def test_read_back_and_pinned_stream(native, oracle):
     """tv_read returns exactly the staged linear bytes (incl. a short last piece and a shard
     window), and tv_verify_host from a pinned (tv_host_alloc) source matches the oracle."""
