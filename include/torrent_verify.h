@@ -39,6 +39,8 @@ extern "C" {
 #define TV_ERR_HIP (-2)     /* HIP runtime failure (message has the hipError string) */
 #define TV_ERR_STATE (-3)   /* call out of order (e.g. verify before set_layout) */
 #define TV_ERR_NOMEM (-4)   /* device or pinned host allocation failed */
+#define TV_ERR_IO (-5)      /* tv_stage_file: file missing, unreadable or shorter than the read
+                               (the reference's fsStorage.get -> null, storage.ts:163-171) */
 
 typedef struct tv_ctx tv_ctx;
 
@@ -86,6 +88,23 @@ int tv_set_digests(tv_ctx *ctx, const uint8_t *pieces, uint64_t pieces_len);
  * when the call returns.  Replaces: fsStorage.get reads feeding Storage.get (storage.ts:150-172).
  */
 int tv_stage(tv_ctx *ctx, uint64_t linear_offset, const uint8_t *src, uint64_t len);
+
+/*
+ * Stage `len` bytes of the file at `path` (a NUL-terminated path), starting at byte `file_offset`,
+ * as LINEAR torrent bytes [linear_offset, linear_offset + len).  This is one file segment of
+ * Storage.get's mapping (storage.ts:89-137: path, offset in the file, length) read the way
+ * fsStorage.get reads it (storage.ts:150-172: open, seek, read).  The file is processed in windows of
+ * TV_OPT_FILE_CHUNK bytes.  A window whose pages are mostly in the page cache (mincore) is mapped, its
+ * pages registered read-only and DMA'd straight to HBM, with no host copy.  A window mostly on disk is
+ * read by parallel preads (8 MiB requests, 8 in flight) into the pinned ring and DMA'd from there.
+ * TV_OPT_FILE_DIRECT = 0 forces the second form.  Either way, window k+1 is read while window k
+ * copies.  Bytes outside the shard are skipped.  A missing or short file returns TV_ERR_IO before
+ * anything is staged (a read error part-way also returns TV_ERR_IO): the host marks the pieces the
+ * segment touches unreadable, as Storage.get returning null makes them.  Unlike
+ * fsStorage.get (which opens with create: true, storage.ts:28-32,158) a missing file is never created.
+ * len == 0 succeeds without opening the file.
+ */
+int tv_stage_file(tv_ctx *ctx, const char *path, uint64_t file_offset, uint64_t linear_offset, uint64_t len);
 
 /* The inverse of tv_stage: copy `len` resident bytes at LINEAR offset `linear_offset` to host
  * `dst` (HBM as the piece store serving block requests, torrent.ts:164-167 Storage.get).  Bytes
@@ -140,6 +159,8 @@ int tv_host_unregister(void *ptr);
 #define TV_OPT_STRIDE_PAD 2  /* bytes of padding between resident pieces (default 256) */
 #define TV_OPT_STREAM_CHUNK 3 /* tv_verify_host: bytes of each piece per streamed column chunk */
 #define TV_OPT_SPLIT_PAIRS 4  /* split kernel: (rounds, helper) wave pairs per workgroup, 0 = auto, 1, 2 */
+#define TV_OPT_FILE_DIRECT 5  /* tv_stage_file: 1 (default) = warm windows DMA'd from registered page-cache pages, 0 = all via the pinned ring */
+#define TV_OPT_FILE_CHUNK 6   /* tv_stage_file: bytes per mapped file window (default 256 MiB, >= 64 KiB) */
 int tv_set_option(tv_ctx *ctx, int key, int64_t value);
 int tv_get_option(tv_ctx *ctx, int key, int64_t *value);
 

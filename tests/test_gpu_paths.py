@@ -322,11 +322,64 @@ def test_verify_files_resume_from_disk(native, tmp_path, layout):
         bf = verify_files(lay["info"], str(tmp_path), devices=[0, 0], batch_bytes=3 * lay["info"].piece_length)
         # odd-sized read chunks: every file segment is split across the read threads
         bf2 = verify_files(lay["info"], str(tmp_path), batch_bytes=5 * lay["info"].piece_length, read_chunk=1000)
+        # every non-empty file segment through tv_stage_file (page-cache DMA), 2 shards
+        bf3 = verify_files(lay["info"], str(tmp_path), devices=[0, 0], direct_min=0)
+        # a mix: segments >= 3 KiB direct, the rest in pread runs
+        bf4 = verify_files(lay["info"], str(tmp_path), batch_bytes=4 * lay["info"].piece_length, direct_min=3072)
     finally:
         os.chdir(cwd)
     assert bytes(bf).hex() == rec["expected_bitfield"]
     assert bytes(bf2).hex() == rec["expected_bitfield"]
+    assert bytes(bf3).hex() == rec["expected_bitfield"]
+    assert bytes(bf4).hex() == rec["expected_bitfield"]
     assert sorted(str(x) for x in tmp_path.rglob("*")) == before   # no files created
+
+
+@pytest.mark.parametrize("direct", [1, 0])
+def test_stage_file_windows_offsets_and_failures(native, oracle, tmp_path, direct):
+    """tv_stage_file: the torrent bytes sit at an unaligned offset inside the file; windows of
+    200,000 bytes (not a page multiple) over a shard window [8, 128) of 130 pieces with a short last
+    piece; registered page-cache DMA (direct=1) and the pinned-ring copy (direct=0) stage the same
+    bytes.  A short or missing file stages nothing and returns False; len 0 needs no file."""
+    L, P = 65536, 130
+    total = L * (P - 1) + 12345
+    payload = oracle.synth_fill(77, 0, total)
+    pieces = bytearray(oracle.hash_pieces(payload, total, L, P))
+    pieces[20 * 40 + 5] ^= 2
+    prefix = 12345
+    f = tmp_path / "blob.bin"
+    f.write_bytes(b"\xaa" * prefix + bytes(payload))
+    short = tmp_path / "short.bin"
+    short.write_bytes(b"\x01" * 1000)
+    exp = oracle.verify_linear(payload, total, L, bytes(pieces))
+    with native.Context(0) as ctx:
+        ctx.set_option(native.TV_OPT_FILE_DIRECT, direct)
+        ctx.set_option(native.TV_OPT_FILE_CHUNK, 200000)
+        assert ctx.get_option(native.TV_OPT_FILE_CHUNK) == 200000
+        ctx.set_layout(total, L, P, 8, 122)
+        ctx.set_digests(bytes(pieces))
+        assert ctx.stage_file(str(f), prefix, 0, total)
+        out = bytearray(total)
+        ctx.read(0, out)
+        assert out[8 * L:] == payload[8 * L:] and out[:8 * L] == bytes(8 * L)
+        bf = ctx.verify()
+        want = bytearray((122 + 7) // 8)
+        for j in range(122):
+            i = 8 + j
+            if (exp[i >> 3] >> (7 - (i & 7))) & 1:
+                want[j >> 3] |= 0x80 >> (j & 7)
+        assert bf == bytes(want)
+        # failures: nothing is staged, False is returned (fsStorage.get -> null), no file is created
+        assert not ctx.stage_file(str(short), 0, 9 * L, 2000)
+        assert not ctx.stage_file(str(tmp_path / "missing.bin"), 0, 9 * L, 10)
+        assert not (tmp_path / "missing.bin").exists()
+        assert ctx.stage_file(str(tmp_path / "missing.bin"), 0, 9 * L, 0)
+        ctx.read(0, out)
+        assert out[8 * L:] == payload[8 * L:]
+        # a range partly outside the shard: only the shard's bytes are staged
+        ctx.stage_file(str(short), 0, 8 * L - 500, 1000)
+        ctx.read(0, out)
+        assert out[8 * L:8 * L + 500] == b"\x01" * 500 and out[8 * L + 500:] == payload[8 * L + 500:]
 
 
 def test_verify_files_reference_singlefile(native, tmp_path):

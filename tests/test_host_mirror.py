@@ -261,3 +261,87 @@ def test_info_hash_is_sha1_of_the_original_info_bytes(name):
     raw_info = data[start:-1]                       # "info" is the last key of the top-level dict
     assert _bencode(_bdecode(raw_info)) == raw_info
     assert m.info_hash == hashlib.sha1(raw_info).digest()
+
+
+class _ImageCtx:
+    """Stand-in for a tv_ctx on CPU: tv_stage / tv_stage_file write into a linear image of the shard,
+    so verify_files' staging plan (file segments -> pread runs + direct segments) is checked without a
+    GPU.  stage_file reads the file the way the library does (missing / short -> False, nothing staged)."""
+
+    def __init__(self, total, lo, hi):
+        self.img = bytearray(total)
+        self.written = bytearray(total)
+        self.lo, self.hi = lo, hi
+        self.direct = 0
+
+    def _put(self, off, data):
+        a, b = max(off, self.lo), min(off + len(data), self.hi)
+        if b > a:
+            self.img[a:b] = data[a - off:b - off]
+            for k in range(a, b):
+                assert not self.written[k], f"byte {k} staged twice"
+                self.written[k] = 1
+
+    def stage(self, off, mv):
+        self._put(off, bytes(mv))
+
+    def stage_file(self, path, foff, off, n):
+        self.direct += 1
+        try:
+            with open(path, "rb") as f:
+                f.seek(foff)
+                data = f.read(n)
+        except OSError:
+            return False
+        if len(data) < n:
+            return False
+        self._put(off, data)
+        return True
+
+
+@pytest.mark.parametrize("layout", ["missing_and_short", "multi_zero_tiny", "single_short_last"])
+@pytest.mark.parametrize("direct_min,batch", [(None, 3), (0, 2), (3072, 1), (1 << 62, 1)])
+def test_files_shard_staging_plan(tmp_path, monkeypatch, layout, direct_min, batch):
+    """verify_files' staging plan on CPU: every readable byte of the shard is staged exactly once at its
+    linear offset (pread runs and direct segments together), and the availability bits are exactly the
+    pieces whose bytes are all on disk (storage.ts:150-172 null -> 0), over 3 shards."""
+    from tests.layouts import build_layout, by_name
+    from torrent_amd import _native, verify
+    from torrent_amd.storage import Storage, fs_storage
+
+    class _Buf:
+        def __init__(self, n):
+            self.mv = memoryview(bytearray(n))
+
+        def close(self):
+            pass
+
+    monkeypatch.setattr(_native, "PinnedBuffer", _Buf)
+    lay = build_layout(by_name(layout))
+    info = lay["info"]
+    for path, data in lay["disk_files"]().items():
+        p = tmp_path.joinpath(*path)
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_bytes(data)
+    monkeypatch.chdir(tmp_path)
+    st = Storage(fs_storage, info, str(tmp_path))
+    L, P, total = info.piece_length, info.n_pieces, info.length
+    for first, count in verify.shard_ranges(P, 3):
+        if not count:
+            continue
+        hi = (first + count - 1) * L + (total % L if first + count == P and total % L else L)
+        ctx = _ImageCtx(total, first * L, hi)
+        avail = verify._files_shard(ctx, info, st, first, count, threads=4, batch_bytes=batch * L,
+                                    read_chunk=1000, direct_min=direct_min)
+        for j in range(count):
+            i = first + j
+            want = (lay["avail"][i >> 3] >> (7 - (i & 7))) & 1
+            assert (avail[j >> 3] >> (7 - (j & 7))) & 1 == want, (layout, i)
+            if want:
+                a, b = i * L, min(total, (i + 1) * L)
+                assert ctx.img[a:b] == lay["payload"][a:b], (layout, i)
+                assert all(ctx.written[a:b]), (layout, i)
+        if direct_min == 0:
+            assert ctx.direct > 0
+        if direct_min == 1 << 62:
+            assert ctx.direct == 0

@@ -1,6 +1,8 @@
 """Resume-from-disk throughput: write a synthetic multi-file torrent to a directory,
-then time verify_files (disk -> pinned -> HBM -> verify).  The files were just written, so the page
-cache is warm: this measures the host pipeline + PCIe, not cold NVMe reads.
+then time verify_files (disk -> HBM -> verify) with its two staging paths: direct (tv_stage_file, the
+page-cache pages DMA'd to HBM) and pread runs (parallel preads into pinned buffers, then DMA).  Each
+is timed with the page cache warm (the files were just written) and cold (posix_fadvise DONTNEED
+after fsync, so the reads go to the box's disk).
 usage: python tools/resume_bench.py <dir> <GiB> [n_files]"""
 import os
 import sys
@@ -10,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from torrent_amd import _native, make_info, FileInfo, verify_files  # noqa: E402
 
 d, gib = sys.argv[1], float(sys.argv[2])
-nf = int(sys.argv[3]) if len(sys.argv) > 3 else 64
+nf = int(sys.argv[3]) if len(sys.argv) > 3 and not sys.argv[3].startswith("-") else 64
 L = 1 << 20
 total = int(gib * (1 << 30)) // L * L
 P = total // L
@@ -37,15 +39,38 @@ for f in files:
 buf.close()
 ctx.close()
 wt = time.perf_counter() - t0
+
+
+def evict():
+    """Drop the files' clean pages from the page cache (posix_fadvise DONTNEED: no root needed)."""
+    for f in files:
+        fd = os.open(os.path.join(d, *f.path), os.O_RDONLY)
+        os.fsync(fd)
+        os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+        os.close(fd)
+
+
+def exact(bf):
+    return all(((bf[i >> 3] >> (7 - (i & 7))) & 1) == (0 if i % 100 == 0 else 1) for i in range(P))
+
+
 cwd = os.getcwd()
 os.chdir(d)
-best = None
-for rep in range(3):
-    t0 = time.perf_counter()
-    bf = verify_files(info, d, threads=16)
-    el = time.perf_counter() - t0
-    best = el if best is None else min(best, el)
+modes = [("direct (tv_stage_file: page-cache DMA)", None), ("pread runs -> pinned -> DMA", 1 << 62)]
+if "--pread-first" in sys.argv:
+    modes = modes[::-1] + modes[1:]
+for cold in ((False,) if "--warm-only" in sys.argv else (False, True)):
+    for name, dmin in modes:
+        best, ok = None, True
+        for rep in range(2 if cold else 3):
+            if cold:
+                evict()
+            t0 = time.perf_counter()
+            bf = verify_files(info, d, threads=16, direct_min=dmin)
+            el = time.perf_counter() - t0
+            ok = ok and exact(bf)
+            best = el if best is None else min(best, el)
+        print(f"resume_from_disk: {total / 2**30:.1f} GiB in {nf} files, write {total / wt / 1e9:.2f} GB/s, "
+              f"{'COLD (fadvise DONTNEED)' if cold else 'page cache warm'}, {name}: best {best * 1e3:.0f} ms = "
+              f"{total / best / 1e9:.2f} GB/s, exact={ok}", flush=True)
 os.chdir(cwd)
-ok = all(((bf[i >> 3] >> (7 - (i & 7))) & 1) == (0 if i % 100 == 0 else 1) for i in range(P))
-print(f"resume_from_disk: {total / 2**30:.1f} GiB in {nf} files, write {total / wt / 1e9:.2f} GB/s, "
-      f"verify_files best {best * 1e3:.0f} ms = {total / best / 1e9:.2f} GB/s (page cache warm), exact={ok}")

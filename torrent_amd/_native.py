@@ -18,11 +18,14 @@ TV_ERR_ARG = -1
 TV_ERR_HIP = -2
 TV_ERR_STATE = -3
 TV_ERR_NOMEM = -4
+TV_ERR_IO = -5
 
 TV_OPT_KERNEL = 1
 TV_OPT_STRIDE_PAD = 2
 TV_OPT_STREAM_CHUNK = 3
 TV_OPT_SPLIT_PAIRS = 4
+TV_OPT_FILE_DIRECT = 5
+TV_OPT_FILE_CHUNK = 6
 
 KERNEL_AUTO, KERNEL_LANE, KERNEL_SPLIT = 0, 1, 2
 
@@ -37,6 +40,7 @@ SYMBOLS = [
     ("tv_set_layout", _int, [_p, _u64, _u64, _u64, _u64, _u64]),
     ("tv_set_digests", _int, [_p, _p, _u64]),
     ("tv_stage", _int, [_p, _u64, _p, _u64]),
+    ("tv_stage_file", _int, [_p, ctypes.c_char_p, _u64, _u64, _u64]),
     ("tv_read", _int, [_p, _u64, _p, _u64]),
     ("tv_fill_synthetic", _int, [_p, _u64]),
     ("tv_verify", _int, [_p, _p, _p]),
@@ -210,6 +214,16 @@ class Context:
         n = memoryview(data).nbytes
         self._check(self._L.tv_stage(self._h, linear_offset, a, n))
         del keep
+
+    def stage_file(self, path, file_offset: int, linear_offset: int, length: int) -> bool:
+        """tv_stage_file: stage `length` bytes of file `path` from `file_offset` as linear bytes
+        [linear_offset, +length).  False when the file is missing or short (TV_ERR_IO: the
+        reference's fsStorage.get -> null, so the pieces it touches are unreadable)."""
+        rc = self._L.tv_stage_file(self._h, os.fsencode(path), file_offset, linear_offset, length)
+        if rc == TV_ERR_IO:
+            return False
+        self._check(rc)
+        return True
 
     def read(self, linear_offset: int, out) -> None:
         """Copy resident bytes at linear_offset into the writable buffer `out` (tv_read)."""

@@ -3,14 +3,20 @@
 // Owns, per context (= per GPU): the compute and copy HIP streams, timing events, a ring of
 // pinned host staging buffers, and the device allocations (resident payload with padded piece
 // stride, digests, availability / output bitfields, chaining state for streamed runs).
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/torrent_verify.h"
@@ -44,6 +50,8 @@ struct tv_ctx {
     uint64_t pad = 256;
     uint64_t stream_chunk = 0;  // 0 = automatic
     int split_pairs = 0;        // 0 = automatic
+    uint64_t file_chunk = 256ull << 20;  // tv_stage_file: bytes per mapped window
+    bool file_direct = true;             // tv_stage_file: DMA from registered page-cache pages
 
     // device memory
     uint8_t* d_payload = nullptr;
@@ -283,6 +291,118 @@ bool is_pinned(const void* p) {
     return ok;
 }
 
+// Clip the LINEAR range [off, off + len) to this ctx's shard: [*a, *b) (empty when *a >= *b).
+void clip_to_shard(const tv_ctx* c, uint64_t off, uint64_t len, uint64_t* a, uint64_t* b) {
+    const uint64_t lo = c->first * c->L;
+    const uint64_t last = c->first + c->count - 1;
+    const uint64_t hi = last * c->L + piece_len(c, last);
+    *a = std::max(off, lo);
+    *b = std::min(off + len, hi);
+}
+
+// Queue the copies of LINEAR bytes [a, b) (inside the shard) on the copy stream; byte `pos` is read
+// from base + (pos - base_off).  Pieces are split at piece boundaries (a piece is shorter than L only
+// at the end of the torrent, piece.ts:16-19); bytes in a short last piece's missing tail are skipped.
+int stage_range(tv_ctx* c, uint64_t a, uint64_t b, const uint8_t* base, uint64_t base_off, bool pinned) {
+    uint64_t pos = a;
+    while (pos < b) {
+        const uint64_t i = pos / c->L, within = pos % c->L;
+        const uint64_t plen = piece_len(c, i);
+        if (within >= plen) {  // inside a short last piece's missing tail: nothing to store
+            pos = (i + 1) * c->L;
+            continue;
+        }
+        uint64_t n;
+        if (within == 0 && plen == c->L) {
+            n = ((b - pos) / c->L) * c->L;  // whole pieces
+            if (n == 0) n = b - pos;
+        } else {
+            n = std::min(b - pos, plen - within);
+        }
+        int rc = stage_copy(c, pos, base + (pos - base_off), n, pinned);
+        if (rc) return rc;
+        pos += n;
+    }
+    return TV_OK;
+}
+
+#ifndef MADV_POPULATE_READ
+#define MADV_POPULATE_READ 22  // Linux >= 5.14; older kernels fall back to touching every page
+#endif
+
+// Fault in the pages of a mapped file window [m, m + n) (the MAP_POPULATE equivalent, after the
+// residency check).  One thread: splitting it over 8 was 27 % slower on a warm page cache (mm lock
+// contention; tools/stage_file_bench.py, profiles/r01/stage_file_bench.log).
+void populate_window(void* m, uint64_t n) {
+    if (madvise(m, n, MADV_POPULATE_READ) == 0) return;
+    volatile uint8_t sink = 0;
+    for (uint64_t o = 0; o < n; o += 4096) sink = sink ^ ((const uint8_t*)m)[o];
+    (void)sink;
+}
+
+// Fraction of the pages of the mapped window [m, m + n) that are in the page cache (mincore).
+double resident_fraction(void* m, uint64_t n, uint64_t page) {
+    std::vector<unsigned char> vec((n + page - 1) / page);
+    if (mincore(m, n, vec.data()) != 0) return 0.0;
+    size_t r = 0;
+    for (unsigned char v : vec) r += v & 1;
+    return vec.empty() ? 1.0 : (double)r / (double)vec.size();
+}
+
+// Read file bytes [fo, fo + n) into dst with parallel preads (8 MiB parts on up to 8 threads: a cold
+// file is read with many large requests in flight).  Returns 0 or an errno value (EIO for a short read).
+int pread_parallel(int fd, uint8_t* dst, uint64_t fo, uint64_t n) {
+    const uint64_t part = 8ull << 20;
+    const uint64_t nparts = (n + part - 1) / part;
+    const int threads = (int)std::min<uint64_t>(8, nparts);
+    std::vector<int> err(threads, 0);
+    auto work = [&](int t) {
+        for (uint64_t q = t; q < nparts; q += threads) {
+            uint64_t o = q * part;
+            const uint64_t e = std::min(n, o + part);
+            while (o < e) {
+                const ssize_t got = pread(fd, dst + o, e - o, (off_t)(fo + o));
+                if (got < 0 && errno == EINTR) continue;
+                if (got <= 0) {
+                    err[t] = got < 0 ? errno : EIO;
+                    return;
+                }
+                o += (uint64_t)got;
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < threads; t++) th.emplace_back(work, t);
+    if (threads > 0) work(0);
+    for (auto& t : th) t.join();
+    for (int e : err)
+        if (e) return e;
+    return 0;
+}
+
+// Memory-mapped windows of a file for tv_stage_file; released (unregistered, unmapped) on every exit.
+// Declared BEFORE the call's DrainGuard, so the streams are drained before any window goes away.
+struct FileWindows {
+    struct W {
+        void* ptr = nullptr;
+        size_t len = 0;
+        bool registered = false;
+    };
+    W w[2];
+    int fd = -1;
+    void release(int k) {
+        if (w[k].registered) (void)hipHostUnregister(w[k].ptr);
+        if (w[k].ptr) munmap(w[k].ptr, w[k].len);
+        w[k] = W{};
+        (void)hipGetLastError();
+    }
+    ~FileWindows() {
+        release(0);
+        release(1);
+        if (fd >= 0) close(fd);
+    }
+};
+
 }  // namespace
 
 // ============================================================================================
@@ -374,6 +494,14 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
             if (value < 0 || value > 2) return fail(c, TV_ERR_ARG, "TV_OPT_SPLIT_PAIRS must be 0, 1 or 2");
             c->split_pairs = (int)value;
             return TV_OK;
+        case TV_OPT_FILE_DIRECT:
+            if (value < 0 || value > 1) return fail(c, TV_ERR_ARG, "TV_OPT_FILE_DIRECT must be 0 or 1");
+            c->file_direct = value != 0;
+            return TV_OK;
+        case TV_OPT_FILE_CHUNK:
+            if (value < (64 << 10)) return fail(c, TV_ERR_ARG, "TV_OPT_FILE_CHUNK must be >= 65536");
+            c->file_chunk = (uint64_t)value;
+            return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
@@ -386,6 +514,8 @@ int tv_get_option(tv_ctx* c, int key, int64_t* value) {
         case TV_OPT_STRIDE_PAD: *value = (int64_t)c->pad; return TV_OK;
         case TV_OPT_STREAM_CHUNK: *value = (int64_t)c->stream_chunk; return TV_OK;
         case TV_OPT_SPLIT_PAIRS: *value = c->split_pairs; return TV_OK;
+        case TV_OPT_FILE_DIRECT: *value = c->file_direct ? 1 : 0; return TV_OK;
+        case TV_OPT_FILE_CHUNK: *value = (int64_t)c->file_chunk; return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
@@ -462,38 +592,87 @@ int tv_stage(tv_ctx* c, uint64_t linear_offset, const uint8_t* src, uint64_t len
     int rc = require_layout(c, false);
     if (rc) return rc;
     if (!src && len) return fail(c, TV_ERR_ARG, "src is NULL");
+    if (linear_offset + len < linear_offset) return fail(c, TV_ERR_ARG, "offset + len overflows");
     if (c->count == 0 || len == 0) return TV_OK;
     TV_HIP(c, hipSetDevice(c->device));
-    // clip to the shard's linear range
-    const uint64_t lo = c->first * c->L;
-    const uint64_t last = c->first + c->count - 1;
-    const uint64_t hi = last * c->L + piece_len(c, last);
-    uint64_t a = std::max(linear_offset, lo), b = std::min(linear_offset + len, hi);
-    if (linear_offset + len < linear_offset) return fail(c, TV_ERR_ARG, "offset + len overflows");
+    uint64_t a, b;
+    clip_to_shard(c, linear_offset, len, &a, &b);
     if (a >= b) return TV_OK;
-    // piece by piece segments (a piece may be shorter than L only at the end of the torrent)
     DrainGuard drain(c);
-    const bool pinned = is_pinned(src);
-    uint64_t pos = a;
-    while (pos < b) {
-        const uint64_t i = pos / c->L, within = pos % c->L;
-        const uint64_t plen = piece_len(c, i);
-        if (within >= plen) {  // inside a short last piece's missing tail: nothing to store
-            pos = (i + 1) * c->L;
-            continue;
-        }
-        uint64_t n;
-        if (within == 0 && plen == c->L) {
-            n = ((b - pos) / c->L) * c->L;  // whole pieces
-            if (n == 0) n = b - pos;
-        } else {
-            n = std::min(b - pos, plen - within);
-        }
-        rc = stage_copy(c, pos, src + (pos - linear_offset), n, pinned);
-        if (rc) return rc;
-        pos += n;
-    }
+    rc = stage_range(c, a, b, src, linear_offset, is_pinned(src));
+    if (rc) return rc;
     TV_HIP(c, hipStreamSynchronize(c->copy_stream));   // report a copy failure as this call's error
+    return TV_OK;
+}
+
+int tv_stage_file(tv_ctx* c, const char* path, uint64_t file_offset, uint64_t linear_offset, uint64_t len) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = require_layout(c, false);
+    if (rc) return rc;
+    if (!path) return fail(c, TV_ERR_ARG, "path is NULL");
+    if (linear_offset + len < linear_offset || file_offset + len < file_offset)
+        return fail(c, TV_ERR_ARG, "offset + len overflows");
+    if (len == 0) return TV_OK;  // a zero-length read succeeds without touching the file
+    FileWindows win;  // before `drain`: destroyed after the streams are drained
+    win.fd = open(path, O_RDONLY | O_CLOEXEC);
+    if (win.fd < 0) return fail(c, TV_ERR_IO, "open %s: %s", path, strerror(errno));
+    struct stat st;
+    if (fstat(win.fd, &st) != 0) return fail(c, TV_ERR_IO, "fstat %s: %s", path, strerror(errno));
+    if ((uint64_t)st.st_size < file_offset + len)
+        return fail(c, TV_ERR_IO, "%s has %llu bytes, the read needs %llu", path, (unsigned long long)st.st_size,
+                    (unsigned long long)(file_offset + len));
+    if (c->count == 0) return TV_OK;
+    uint64_t a, b;
+    clip_to_shard(c, linear_offset, len, &a, &b);
+    if (a >= b) return TV_OK;
+    TV_HIP(c, hipSetDevice(c->device));
+    DrainGuard drain(c);
+    for (int k = 0; k < 2; k++) TV_HIP(c, hipEventCreateWithFlags(&drain.ev[k], hipEventDisableTiming));
+    const uint64_t page = (uint64_t)sysconf(_SC_PAGESIZE);
+    const uint64_t chunk = c->file_chunk;
+    int idx = 0;
+    for (uint64_t p = a; p < b; p += chunk, idx++) {
+        const int k = idx & 1;
+        const uint64_t n = std::min(chunk, b - p);
+        const uint64_t fo = file_offset + (p - linear_offset);
+        // the window used two chunks ago must be DMA-complete before it is unmapped
+        if (win.w[k].ptr) {
+            TV_HIP(c, hipEventSynchronize(drain.ev[k]));
+            win.release(k);
+        }
+        const uint64_t map_off = fo / page * page, delta = fo - map_off;
+        void* m = mmap(nullptr, delta + n, PROT_READ, MAP_SHARED, win.fd, (off_t)map_off);
+        if (m == MAP_FAILED) return fail(c, TV_ERR_IO, "mmap %s at %llu: %s", path, (unsigned long long)map_off, strerror(errno));
+        win.w[k].ptr = m;
+        win.w[k].len = delta + n;
+        if (c->file_direct && resident_fraction(m, delta + n, page) >= 0.5) {
+            // warm window: register its page-cache pages read-only and DMA them to HBM directly
+            populate_window(m, delta + n);
+            win.w[k].registered = hipHostRegister(m, delta + n, hipHostRegisterReadOnly) == hipSuccess;
+            (void)hipGetLastError();
+        }
+        if (win.w[k].registered) {
+            rc = stage_range(c, p, p + n, (const uint8_t*)m + delta, p, true);
+            if (rc) return rc;
+        } else {
+            // cold window (or direct DMA off / refused): parallel preads into the pinned ring, then DMA
+            win.release(k);
+            for (uint64_t q = 0; q < n; q += kRingSlotBytes) {
+                const uint64_t kq = std::min<uint64_t>(kRingSlotBytes, n - q);
+                int slot;
+                rc = take_slot(c, &slot);
+                if (rc) return rc;
+                const int e = pread_parallel(win.fd, c->ring[slot], fo + q, kq);
+                if (e) return fail(c, TV_ERR_IO, "read %s at %llu: %s", path, (unsigned long long)(fo + q), strerror(e));
+                rc = stage_range(c, p + q, p + q + kq, c->ring[slot], p + q, true);
+                if (rc) return rc;
+                TV_HIP(c, hipEventRecord(c->ring_ev[slot], c->copy_stream));
+            }
+        }
+        TV_HIP(c, hipEventRecord(drain.ev[k], c->copy_stream));
+    }
+    TV_HIP(c, hipStreamSynchronize(c->copy_stream));
     return TV_OK;
 }
 

@@ -35,6 +35,8 @@ from .piece import piece_length
 
 # pieces gathered per tv_stage call when reading through a Storage
 _STAGE_BATCH_BYTES = 256 << 20
+# verify_files: file segments at least this long are DMA'd from the page cache (tv_stage_file)
+_DIRECT_MIN_BYTES = 32 << 20
 
 
 def shard_ranges(n_pieces: int, n_shards: int) -> List[tuple]:
@@ -195,19 +197,26 @@ def verify_payload(info: InfoDict, payload, devices=None, resident: bool = True,
 
 
 def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: int,
-                 batch_bytes: int, read_chunk: int = 8 << 20) -> bytearray:
-    """Stage the shard's pieces from files (storage.segments mapping) into HBM and return the
-    shard's readability bits.  Parallel preads go straight into two alternating page-locked
-    buffers; batch i is DMA'd while batch i+1 is read.  A piece touching a missing or short file
-    is unreadable (fsStorage.get -> null, storage.ts:150-172); zero-length reads succeed; missing
-    files are never created."""
+                 batch_bytes: int, read_chunk: int = 8 << 20, direct_min: Optional[int] = None) -> bytearray:
+    """Stage the shard's pieces from files into HBM and return the shard's readability bits.
+
+    The shard's linear range is mapped to file segments exactly as Storage.get maps it
+    (storage.ts:89-137).  Then:
+      * a segment of >= direct_min bytes is staged by tv_stage_file: its page-cache pages are mapped,
+        registered read-only and DMA'd straight to HBM (no host copy), on a thread of its own;
+      * shorter segments that are adjacent in the linear space are grouped into runs of at most
+        batch_bytes; a run is read by parallel preads (read_chunk pieces, so all threads copy even
+        when one file covers the run) into one of two alternating page-locked buffers and DMA'd
+        while the next run is read.
+    A piece touching a missing or short file is unreadable (fsStorage.get -> null,
+    storage.ts:150-172); zero-length segments succeed; missing files are never created."""
     import os
     L = info.piece_length
+    if direct_min is None:
+        direct_min = _DIRECT_MIN_BYTES
     avail = bytearray(b"\xff" * ((count + 7) // 8))
     if count % 8:
         avail[-1] = (0xFF00 >> (count % 8)) & 0xFF
-    per = max(1, batch_bytes // L)
-    bufs = [_native.PinnedBuffer(per * L), _native.PinnedBuffer(per * L)]
     fds: dict = {}
     lock = threading.Lock()
 
@@ -223,59 +232,92 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
             return fds[key]
 
     def clear(j_lo: int, j_hi: int) -> None:   # shard-relative pieces [j_lo, j_hi] unreadable
-        for j in range(max(0, j_lo), min(count - 1, j_hi) + 1):
-            avail[j >> 3] &= ~(0x80 >> (j & 7)) & 0xFF
+        with lock:
+            for j in range(max(0, j_lo), min(count - 1, j_hi) + 1):
+                avail[j >> 3] &= ~(0x80 >> (j & 7)) & 0xFF
 
-    def read_batch(b: int, buf) -> int:
-        j = b * per
-        k = min(per, count - j)
-        lo = (first + j) * L
-        hi = lo + (k - 1) * L + piece_length(first + j + k - 1, info)
-        for jj in range(j, j + k):       # bytes past the last file (more digests than data)
-            if (first + jj) * L + piece_length(first + jj, info) > info.length:
-                clear(jj, jj)
-        segs = storage.segments(lo, max(0, min(hi, info.length) - lo)) or []
-        # a file segment is split into read_chunk pieces so all threads copy even when one
-        # large file covers the whole batch (a single pread would run on one core)
+    lo = first * L
+    last = first + count - 1
+    hi = last * L + piece_length(last, info)
+    # pieces whose bytes extend past the last file (more digests than data) are unreadable
+    j = count - 1
+    while j >= 0 and (first + j) * L + piece_length(first + j, info) > info.length:
+        clear(j, j)
+        j -= 1
+    span = max(0, min(hi, info.length) - lo)
+    segs = storage.segments(lo, span) if span else []
+    if segs is None:                  # unmappable (Storage.get -> null for every piece)
+        clear(0, count - 1)
+        segs = []
+
+    direct: list = []                 # (path, file offset, shard-relative start, n)
+    runs: list = []                   # [start, n, [(fd, file offset, run-relative start, n)]]
+    run_cap = max(1, batch_bytes)
+    for path, foff, n, start in segs:
+        if n == 0:
+            continue
+        fd, size = fd_of(path)
+        if fd is None or foff + n > size:
+            clear(start // L, (start + n - 1) // L)
+            continue
+        if n >= direct_min:
+            direct.append((os.path.join(*path), foff, start, n))
+            continue
+        while n:                      # a segment longer than a run is cut across runs
+            cur = runs[-1] if runs else None
+            if cur is not None and cur[0] + cur[1] == start and cur[1] < run_cap:
+                k = min(n, run_cap - cur[1])
+                cur[2].append((fd, foff, start - cur[0], k))
+                cur[1] += k
+            else:
+                k = min(n, run_cap)
+                runs.append([start, k, [(fd, foff, 0, k)]])
+            foff, start, n = foff + k, start + k, n - k
+
+    def stage_direct() -> None:
+        for path, foff, start, n in direct:
+            if not ctx.stage_file(path, foff, lo + start, n):
+                clear(start // L, (start + n - 1) // L)
+
+    def read_run(run, buf) -> None:
+        start0, _, parts = run
         tasks = []
-        for path, foff, n, start in segs:
-            if n == 0:
-                continue
-            fd, size = fd_of(path)
-            if fd is None or foff + n > size:
-                clear(j + start // L, j + (start + n - 1) // L)
-                continue
+        for fd, foff, rel, n in parts:
             for s0 in range(0, n, read_chunk):
-                c = min(read_chunk, n - s0)
-                tasks.append((fd, foff + s0, start + s0, c))
+                tasks.append((fd, foff + s0, rel + s0, min(read_chunk, n - s0)))
 
         def one(t):
-            fd, foff, start, c = t
+            fd, foff, rel, c = t
             try:
-                got = os.preadv(fd, [buf.mv[start:start + c]], foff)
+                got = os.preadv(fd, [buf.mv[rel:rel + c]], foff)
             except OSError:
                 got = -1
-            return None if got == c else (start, c)
+            return None if got == c else (rel, c)
 
         for r in pool.map(one, tasks):
             if r is not None:
-                s0, n = r
-                clear(j + s0 // L, j + (s0 + n - 1) // L)
-        return hi - lo
+                rel, c = r
+                clear((start0 + rel) // L, (start0 + rel + c - 1) // L)
 
-    nb = -(-count // per)
     pool = ThreadPoolExecutor(max(1, threads))
-    stager = ThreadPoolExecutor(1)
-    fut = None
+    stager = ThreadPoolExecutor(2)    # one thread for direct segments, one for run DMAs
+    bufs = []
     try:
-        for b in range(nb):
+        dfut = stager.submit(stage_direct) if direct else None
+        if runs:
+            size = max(r[1] for r in runs)
+            bufs = [_native.PinnedBuffer(size)] + ([_native.PinnedBuffer(size)] if len(runs) > 1 else [])
+        fut = None
+        for b, run in enumerate(runs):
             buf = bufs[b & 1]
-            n = read_batch(b, buf)
+            read_run(run, buf)
             if fut is not None:
                 fut.result()           # the other buffer's DMA is done before it is reused
-            fut = stager.submit(ctx.stage, (first + b * per) * L, buf.mv[:n])
+            fut = stager.submit(ctx.stage, lo + run[0], buf.mv[:run[1]])
         if fut is not None:
             fut.result()
+        if dfut is not None:
+            dfut.result()
     finally:
         stager.shutdown()
         pool.shutdown()
@@ -288,14 +330,16 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
 
 
 def verify_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
-                 batch_bytes: int = 256 << 20, read_chunk: int = 8 << 20) -> bytearray:
+                 batch_bytes: int = 256 << 20, read_chunk: int = 8 << 20,
+                 direct_min: Optional[int] = None) -> bytearray:
     """Resume check from disk: the have-bitfield of the files under dir_path,
     laid out as Storage(fs_storage, info, dir_path) maps them (storage.ts:89-137; single-file
     torrents are [dir, name], multi-file [dir, *path] without info.name).
 
     Same bits as verify_pieces(info, Storage(fs_storage, info, dir_path)), without fsStorage.get's
-    side effect of creating missing files, and with the file reads streamed into page-locked
-    buffers (see _files_shard) instead of one open/seek/read per piece."""
+    side effect of creating missing files.  Long file segments (>= direct_min bytes, default 32 MiB)
+    are DMA'd to HBM straight from the page cache; shorter ones are read by parallel preads into
+    page-locked buffers (see _files_shard) instead of one open/seek/read per piece."""
     from .storage import Storage, fs_storage
 
     P, L = info.n_pieces, info.piece_length
@@ -306,7 +350,8 @@ def verify_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
         ctx.set_digests(info.pieces_raw)
         if count == 0:
             return b""
-        return ctx.verify(_files_shard(ctx, info, storage, first, count, threads, batch_bytes, read_chunk))
+        return ctx.verify(_files_shard(ctx, info, storage, first, count, threads, batch_bytes, read_chunk,
+                                       direct_min))
 
     if P == 0:
         return bytearray()
@@ -315,7 +360,8 @@ def verify_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
 
 
 def hash_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
-               batch_bytes: int = 256 << 20, read_chunk: int = 8 << 20) -> bytes:
+               batch_bytes: int = 256 << 20, read_chunk: int = 8 << 20,
+               direct_min: Optional[int] = None) -> bytes:
     """Creation mode from disk: the `pieces` string of the files info describes under dir_path
     (info.pieces is ignored; only the geometry is used).  Raises if a file is missing or short."""
     from .storage import Storage, fs_storage
@@ -328,7 +374,8 @@ def hash_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
         ctx.set_layout(info.length, L, P, first, count)
         if count == 0:
             return b""
-        avail = _files_shard(ctx, info, storage, first, count, threads, batch_bytes, read_chunk)
+        avail = _files_shard(ctx, info, storage, first, count, threads, batch_bytes, read_chunk,
+                             direct_min)
         full = bytearray(b"\xff" * ((count + 7) // 8))
         if count % 8:
             full[-1] = (0xFF00 >> (count % 8)) & 0xFF

@@ -22,6 +22,7 @@ const SYMBOLS = {
   tv_set_layout: { parameters: ["pointer", "u64", "u64", "u64", "u64", "u64"], result: "i32" },
   tv_set_digests: { parameters: ["pointer", "pointer", "u64"], result: "i32" },
   tv_stage: { parameters: ["pointer", "u64", "pointer", "u64"], result: "i32", nonblocking: true },
+  tv_stage_file: { parameters: ["pointer", "pointer", "u64", "u64", "u64"], result: "i32", nonblocking: true },
   tv_read: { parameters: ["pointer", "u64", "pointer", "u64"], result: "i32", nonblocking: true },
   tv_fill_synthetic: { parameters: ["pointer", "u64"], result: "i32" },
   tv_verify: { parameters: ["pointer", "pointer", "pointer"], result: "i32", nonblocking: true },
@@ -147,6 +148,70 @@ export async function verifyPieces(
           avail[(j + q) >> 3] |= 128 >> ((j + q) % 8);
         });
         if (hi) check(l, ctx, await l.symbols.tv_stage(ctx, BigInt((first + j) * L), ptr(buf), BigInt(hi)));
+      }
+      const out = new Uint8Array(Math.ceil(count / 8));
+      check(l, ctx, await l.symbols.tv_verify(ctx, ptr(avail), ptr(out)));
+      bitfield.set(out, first / 8);
+    } finally {
+      l.symbols.tv_destroy(ctx);
+    }
+  }));
+  return bitfield;
+}
+
+const TV_ERR_IO = -5;
+
+/**
+ * verifyFiles(info, dir) -> have-bitfield of the files under `dir` (resume from disk, SURVEY 8f
+ * row f2), laid out as new Storage(fsStorage, info, dir) maps them (storage.ts:89-137: single-file
+ * [dir, name], multi-file [dir, ...path]).  Every file segment of a shard is staged by tv_stage_file:
+ * page-cache pages are DMA'd to HBM directly when the file is warm, read by parallel preads when it is
+ * cold.  A missing or short file (TV_ERR_IO) makes the pieces it touches 0, like fsStorage.get
+ * returning null (storage.ts:163-171); unlike fsStorage.get, no missing file is created.  Same
+ * behaviour as torrent_amd.verify_files.
+ */
+export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptions = {}): Promise<Uint8Array> {
+  const l = load(opts.libPath);
+  const P = info.pieces.length;
+  const L = info.pieceLength;
+  const devices = opts.devices ?? [0];
+  const raw = piecesRaw(info);
+  const files = "files" in info
+    ? info.files.map((f) => ({ length: f.length, path: [dir, ...f.path].join("/") }))
+    : [{ length: info.length, path: [dir, info.name].join("/") }];
+  const bitfield = new Uint8Array(Math.ceil(P / 8));
+
+  await Promise.all(shardRanges(P, devices.length).map(async ([first, count], s) => {
+    if (count === 0) return;
+    const h = new BigUint64Array(1);
+    check(l, null, l.symbols.tv_create(ptr(new Uint8Array(h.buffer)), devices[s]));
+    const ctx = Deno.UnsafePointer.create(h[0]);
+    try {
+      check(l, ctx, l.symbols.tv_set_layout(ctx, BigInt(info.length), BigInt(L), BigInt(P), BigInt(first), BigInt(count)));
+      check(l, ctx, l.symbols.tv_set_digests(ctx, ptr(raw), BigInt(raw.length)));
+      const avail = new Uint8Array(Math.ceil(count / 8)).fill(0xff);
+      if (count % 8) avail[avail.length - 1] = (0xff00 >> (count % 8)) & 0xff;
+      const clear = (lo: number, hi: number) => {
+        for (let j = Math.max(0, lo); j <= Math.min(count - 1, hi); j++) avail[j >> 3] &= ~(128 >> (j % 8));
+      };
+      // pieces whose bytes extend past the last file (more digests than data) are unreadable
+      for (let j = count - 1; j >= 0 && (first + j) * L + pieceLength(first + j, info) > info.length; j--) clear(j, j);
+      const lo = first * L;
+      const hi = Math.min(info.length, (first + count - 1) * L + pieceLength(first + count - 1, info));
+      // findAndDo's walk over the files in order (storage.ts:105-128), restricted to [lo, hi)
+      let fileStart = 0;
+      for (const f of files) {
+        const fileEnd = fileStart + f.length;
+        const a = Math.max(lo, fileStart);
+        const b = Math.min(hi, fileEnd);
+        if (b > a) {
+          const path = new TextEncoder().encode(f.path + "\0");
+          const rc = await l.symbols.tv_stage_file(ctx, ptr(path), BigInt(a - fileStart), BigInt(a), BigInt(b - a));
+          if (rc === TV_ERR_IO) clear(Math.floor((a - lo) / L), Math.floor((b - 1 - lo) / L));
+          else check(l, ctx, rc);
+        }
+        fileStart = fileEnd;
+        if (fileStart >= hi) break;
       }
       const out = new Uint8Array(Math.ceil(count / 8));
       check(l, ctx, await l.symbols.tv_verify(ctx, ptr(avail), ptr(out)));
