@@ -9,7 +9,8 @@
  *                      pieces "abc" | "def" | "g" (L = 3, short last piece, piece.ts:16-19), the
  *                      middle digest corrupted, MSB-first bitfield (torrent.ts:147-149) = 0xA0.
  *                      It covers verify, hash, verify_list, verify_host from pageable and pinned
- *                      memory, read-back, and two contexts driven from two threads at once.
+ *                      memory, read-back, stage_file (incl. short / missing files -> TV_ERR_IO),
+ *                      and two contexts driven from two threads at once.
  *
  * Build: gcc -O2 -Iinclude tests/c/abi_consumer.c -Ltorrent_amd -ltorrent_verify \
  *            -Wl,-rpath,$PWD/torrent_amd -lpthread -o abi_consumer
@@ -18,6 +19,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "torrent_verify.h"
 
@@ -139,6 +141,26 @@ static int run_gpu(void) {
         CHECK(bf == 0xA0, "verify_host (pinned) bitfield %02x", bf);
         OK(tv_host_free(pinned), NULL);
     }
+    char msg0[256];
+    /* from a file: "xx" + payload at file offset 2 (fsStorage.get's open/seek/read, storage.ts:150-172) */
+    char path[] = "/tmp/tv_abi_consumer_XXXXXX";
+    int fd = mkstemp(path);
+    CHECK(fd >= 0, "mkstemp");
+    if (fd >= 0) {
+        CHECK(write(fd, "xxabcdefg", 9) == 9, "write");
+        close(fd);
+        OK(tv_set_layout(c, 7, 3, 3, 0, 3), c);
+        OK(tv_set_digests(c, digests, 60), c);
+        OK(tv_stage_file(c, path, 2, 0, 7), c);
+        OK(tv_verify(c, NULL, &bf), c);
+        CHECK(bf == 0xA0, "stage_file bitfield %02x, want a0", bf);
+        CHECK(tv_stage_file(c, path, 5, 0, 7) == TV_ERR_IO, "short file must be TV_ERR_IO");
+        CHECK(tv_last_error(c, msg0, sizeof msg0) > 0 && strstr(msg0, "bytes"), "message: %s", msg0);
+        CHECK(tv_stage_file(c, "/nonexistent/tv_file", 0, 0, 7) == TV_ERR_IO, "missing file must be TV_ERR_IO");
+        OK(tv_stage_file(c, "/nonexistent/tv_file", 0, 0, 0), c); /* zero-length read: no file needed */
+        unlink(path);
+    }
+
     double kms = -1, tms = -1;
     OK(tv_last_timing(c, &kms, &tms), c);
     CHECK(kms >= 0 && tms >= kms, "timings %f %f", kms, tms);
