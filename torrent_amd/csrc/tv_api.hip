@@ -56,7 +56,10 @@ struct tv_ctx {
     // device memory
     uint8_t* d_payload = nullptr;
     uint32_t* d_digests = nullptr;    // [5][count]
-    uint64_t* d_avail = nullptr;      // bit words, sized to whole 256-piece groups
+    uint64_t* d_avail = nullptr;      // bit words, sized to whole 256-piece groups (caller-masked)
+    uint64_t* d_base_avail = nullptr; // same shape: digest slice complete & piece inside the torrent
+    uint8_t* h_avail = nullptr;       // pinned bounce buffer for caller-masked availability
+    hipEvent_t ev_avail = nullptr;    // the last H2D copy out of h_avail
     uint64_t* d_out = nullptr;
     uint32_t* d_state = nullptr;      // [5][count]
     uint32_t* d_hash = nullptr;       // [5][count]
@@ -69,6 +72,7 @@ struct tv_ctx {
 
     bool digests_set = false;
     std::vector<uint8_t> digest_ok;   // shard-relative MSB-first bits: digest slice is 20 bytes
+    std::vector<uint8_t> base_avail;  // host copy of d_base_avail (bit_words * 8 bytes)
 
     // pinned staging ring
     uint8_t* ring[kRingSlots] = {nullptr, nullptr, nullptr};
@@ -115,6 +119,9 @@ void free_device(tv_ctx* c) {
     (void)hipFree(c->d_payload); c->d_payload = nullptr;
     (void)hipFree(c->d_digests); c->d_digests = nullptr;
     (void)hipFree(c->d_avail); c->d_avail = nullptr;
+    (void)hipFree(c->d_base_avail); c->d_base_avail = nullptr;
+    if (c->ev_avail) (void)hipEventSynchronize(c->ev_avail);
+    (void)hipHostFree(c->h_avail); c->h_avail = nullptr;
     (void)hipFree(c->d_out); c->d_out = nullptr;
     (void)hipFree(c->d_state); c->d_state = nullptr;
     (void)hipFree(c->d_hash); c->d_hash = nullptr;
@@ -154,20 +161,35 @@ int take_slot(tv_ctx* c, int* slot) {
     return TV_OK;
 }
 
-// Effective availability of every shard piece: caller bit & digest slice complete & bytes
-// inside the torrent (piece.ts:16-19 length at offset i*L must end <= total).
-int upload_avail(tv_ctx* c, const uint8_t* avail_bits) {
+// Base availability of every shard piece, computed once per tv_set_digests and kept in HBM: the
+// digest slice is complete (metainfo.ts:111) and the piece's bytes lie inside the torrent (piece.ts:16-19
+// length at offset i*L must end <= total).
+int upload_base_avail(tv_ctx* c) {
     const size_t nbytes = c->bit_words * 8;
     std::vector<uint8_t> bits(nbytes, 0);
     for (uint64_t j = 0; j < c->count; j++) {
         const uint64_t i = c->first + j;
-        bool ok = get_bit(c->digest_ok.data(), j);
-        ok = ok && (i * c->L + piece_len(c, i) <= c->total);
-        ok = ok && (!avail_bits || get_bit(avail_bits, j));
-        if (ok) set_bit(bits.data(), j);
+        if (get_bit(c->digest_ok.data(), j) && i * c->L + piece_len(c, i) <= c->total) set_bit(bits.data(), j);
     }
-    TV_HIP(c, hipMemcpyAsync(c->d_avail, bits.data(), nbytes, hipMemcpyHostToDevice, c->stream));
+    TV_HIP(c, hipMemcpyAsync(c->d_base_avail, bits.data(), nbytes, hipMemcpyHostToDevice, c->stream));
     TV_HIP(c, hipStreamSynchronize(c->stream));
+    c->base_avail.swap(bits);
+    return TV_OK;
+}
+
+// Availability for one launch: the base bits, or base & the caller's bits (Storage.get -> null for
+// a missing / short file) queued on the compute stream from the pinned bounce buffer (no host sync).
+int launch_avail(tv_ctx* c, const uint8_t* avail_bits, const uint64_t** out) {
+    if (!avail_bits) {
+        *out = c->d_base_avail;
+        return TV_OK;
+    }
+    TV_HIP(c, hipEventSynchronize(c->ev_avail));  // the previous copy out of h_avail is done
+    const size_t nbytes = c->bit_words * 8, used = (c->count + 7) / 8;
+    for (size_t k = 0; k < nbytes; k++) c->h_avail[k] = c->base_avail[k] & (k < used ? avail_bits[k] : 0);
+    TV_HIP(c, hipMemcpyAsync(c->d_avail, c->h_avail, nbytes, hipMemcpyHostToDevice, c->stream));
+    TV_HIP(c, hipEventRecord(c->ev_avail, c->stream));
+    *out = c->d_avail;
     return TV_OK;
 }
 
@@ -196,7 +218,7 @@ TvPieces resident_launch(const tv_ctx* c) {
     p.dcount = (uint32_t)c->count;
     p.state = c->d_state;
     p.digests = c->d_digests;
-    p.avail64 = c->d_avail;
+    p.avail64 = c->d_base_avail;
     p.out64 = c->d_out;
     p.out_digests = c->d_hash;
     return p;
@@ -436,6 +458,7 @@ int tv_create(tv_ctx** out, int device) {
     if (e == hipSuccess) e = hipEventCreate(&c->ev_k0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev_k1);
     if (e == hipSuccess) e = hipEventCreate(&c->ev_call1);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_avail, hipEventDisableTiming);
     if (e != hipSuccess) {
         fail(nullptr, TV_ERR_HIP, "tv_create: %s", hipGetErrorString(e));
         tv_destroy(c);
@@ -456,7 +479,7 @@ void tv_destroy(tv_ctx* c) {
         if (c->ring_ev[s]) (void)hipEventDestroy(c->ring_ev[s]);
     }
     if (c->h_bits) (void)hipHostFree(c->h_bits);
-    for (hipEvent_t ev : {c->ev_call0, c->ev_k0, c->ev_k1, c->ev_call1})
+    for (hipEvent_t ev : {c->ev_call0, c->ev_k0, c->ev_k1, c->ev_call1, c->ev_avail})
         if (ev) (void)hipEventDestroy(ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -551,6 +574,8 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
         TV_HIP(c, hipMalloc((void**)&c->d_state, 5 * shard_count * sizeof(uint32_t)));
         TV_HIP(c, hipMalloc((void**)&c->d_hash, 5 * shard_count * sizeof(uint32_t)));
         TV_HIP(c, hipMalloc((void**)&c->d_avail, c->bit_words * 8));
+        TV_HIP(c, hipMalloc((void**)&c->d_base_avail, c->bit_words * 8));
+        TV_HIP(c, hipHostMalloc((void**)&c->h_avail, c->bit_words * 8, hipHostMallocDefault));
         TV_HIP(c, hipMalloc((void**)&c->d_out, c->bit_words * 8));
         TV_HIP(c, hipMemsetAsync(c->d_payload + shard_count * c->stride, 0, kSlack, c->stream));
         TV_HIP(c, hipStreamSynchronize(c->stream));
@@ -581,6 +606,10 @@ int tv_set_digests(tv_ctx* c, const uint8_t* pieces, uint64_t pieces_len) {
         TV_HIP(c, hipSetDevice(c->device));
         TV_HIP(c, hipMemcpyAsync(c->d_digests, soa.data(), soa.size() * 4, hipMemcpyHostToDevice, c->stream));
         TV_HIP(c, hipStreamSynchronize(c->stream));
+    }
+    if (c->count) {
+        rc = upload_base_avail(c);
+        if (rc) return rc;
     }
     c->digests_set = true;
     return TV_OK;
@@ -734,10 +763,12 @@ int tv_verify(tv_ctx* c, const uint8_t* avail_bits, uint8_t* bitfield_out) {
     if (!c->count) return TV_OK;
     TV_HIP(c, hipSetDevice(c->device));
     TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
-    rc = upload_avail(c, avail_bits);
+    const uint64_t* av = nullptr;
+    rc = launch_avail(c, avail_bits, &av);
     if (rc) return rc;
     const int kernel = choose_kernel(c);
     TvPieces p = resident_launch(c);
+    p.avail64 = av;
     TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
     TV_HIP(c, tv_launch_verify(p, kernel, false, c->stream, c->split_pairs));
     TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
@@ -776,8 +807,6 @@ int tv_verify_list(tv_ctx* c, const uint64_t* pieces, uint64_t n, uint8_t* ok_ou
         c->list_cap = cap;
     }
     TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
-    rc = upload_avail(c, nullptr);  // digest slice complete & bytes inside the torrent
-    if (rc) return rc;
     TV_HIP(c, hipMemcpyAsync(c->d_list, local.data(), n * 4, hipMemcpyHostToDevice, c->stream));
     TvPieces p = resident_launch(c);
     p.n = (uint32_t)n;
@@ -848,7 +877,8 @@ int tv_verify_host(tv_ctx* c, const uint8_t* src, uint64_t src_len, const uint8_
         if (end <= src_len && (!avail_bits || get_bit(avail_bits, j))) set_bit(av.data(), j);
     }
     TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
-    rc = upload_avail(c, av.data());
+    const uint64_t* av_dev = nullptr;
+    rc = launch_avail(c, av.data(), &av_dev);
     if (rc) return rc;
 
     const uint64_t n = c->count;
@@ -873,6 +903,7 @@ int tv_verify_host(tv_ctx* c, const uint8_t* src, uint64_t src_len, const uint8_
     const int kernel = choose_kernel(c);
     TvPieces p = resident_launch(c);
     p.stride = row;
+    p.avail64 = av_dev;
     DrainGuard drain(c);
     hipEvent_t* col_ev = drain.ev;       // copy of column -> buffer k done
     hipEvent_t* done_ev = drain.ev + 2;  // kernel that read buffer k done
