@@ -671,11 +671,13 @@ int tv_stage_file(tv_ctx* c, const char* path, uint64_t file_offset, uint64_t li
             win.release(k);
         }
         const uint64_t map_off = fo / page * page, delta = fo - map_off;
-        void* m = mmap(nullptr, delta + n, PROT_READ, MAP_SHARED, win.fd, (off_t)map_off);
-        if (m == MAP_FAILED) return fail(c, TV_ERR_IO, "mmap %s at %llu: %s", path, (unsigned long long)map_off, strerror(errno));
-        win.w[k].ptr = m;
-        win.w[k].len = delta + n;
-        if (c->file_direct && resident_fraction(m, delta + n, page) >= 0.5) {
+        // (a file that cannot be mapped, e.g. on a filesystem without mmap, takes the pread path)
+        void* m = c->file_direct ? mmap(nullptr, delta + n, PROT_READ, MAP_SHARED, win.fd, (off_t)map_off) : MAP_FAILED;
+        if (m != MAP_FAILED) {
+            win.w[k].ptr = m;
+            win.w[k].len = delta + n;
+        }
+        if (m != MAP_FAILED && resident_fraction(m, delta + n, page) >= 0.5) {
             // warm window: register its page-cache pages read-only and DMA them to HBM directly
             populate_window(m, delta + n);
             win.w[k].registered = hipHostRegister(m, delta + n, hipHostRegisterReadOnly) == hipSuccess;
