@@ -231,9 +231,11 @@ def test_read_back_and_pinned_stream(native, oracle):
         assert ctx.last_kernel()[1] == 4  # 64 KiB pieces in 16 KiB columns
 
 
-def test_verify_list_matches_oracle(native, oracle):
-    """tv_verify_list: arbitrary order, duplicates, the short last piece in any lane position,
-    corrupted pieces, a shard offset; > 256 entries (several workgroups)."""
+@pytest.mark.parametrize("kernel", [0, 1, 2])
+def test_verify_list_matches_oracle(native, oracle, kernel):
+    """tv_verify_list (auto / lane list kernel / split kernel in list mode): arbitrary order,
+    duplicates, the short last piece in any lane position, corrupted pieces, a shard offset;
+    > 256 entries (several workgroups)."""
     import random
     L, P = 16384, 700
     total = L * (P - 1) + 333
@@ -244,12 +246,14 @@ def test_verify_list_matches_oracle(native, oracle):
         pieces[20 * i + 1] ^= 0x40
     rng = random.Random(5)
     with native.Context(0) as ctx:
+        ctx.set_option(native.TV_OPT_KERNEL, kernel)
         ctx.set_layout(total, L, P, 8, P - 8)
         ctx.set_digests(bytes(pieces))
         ctx.stage(0, payload)
         lst = [rng.randrange(8, P) for _ in range(600)] + [P - 1, P - 1, 8, 9]
         rng.shuffle(lst)
         got = ctx.verify_list(lst)
+        assert ctx.last_kernel()[0] == (kernel or 2)
         assert list(got) == [0 if i in bad else 1 for i in lst]
         with pytest.raises(native.NativeError):
             ctx.verify_list([0])          # outside the shard

@@ -590,6 +590,7 @@ int tv_set_digests(tv_ctx* c, const uint8_t* pieces, uint64_t pieces_len) {
     int rc = require_layout(c, false);
     if (rc) return rc;
     if (!pieces && pieces_len) return fail(c, TV_ERR_ARG, "pieces is NULL");
+    c->digests_set = false;  // until the digests AND their base availability are both on the device
     // partition(info.pieces, 20) (metainfo.ts:111, _bytes.ts:92-99): slice i = [20i, 20i+20)
     std::vector<uint32_t> soa(5 * c->count, 0);
     std::fill(c->digest_ok.begin(), c->digest_ok.end(), 0);
@@ -815,12 +816,17 @@ int tv_verify_list(tv_ctx* c, const uint64_t* pieces, uint64_t n, uint8_t* ok_ou
     p.idx = c->d_list;
     p.out_bytes = c->d_list_out;
     TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
-    TV_HIP(c, tv_launch_verify_list(p, c->stream));
+    // split (rounds + helper pair, ~30 % shorter serial stream per block) while one pair per CU
+    // suffices, like choose_kernel; the lane list kernel for longer lists
+    const int kernel = (c->kernel_opt == TV_KERNEL_LANE || c->kernel_opt == TV_KERNEL_SPLIT)
+                           ? c->kernel_opt
+                           : (n <= 256 * 64 ? TV_KERNEL_SPLIT : TV_KERNEL_LANE);
+    TV_HIP(c, tv_launch_verify_list(p, kernel, c->stream));
     TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
     TV_HIP(c, hipMemcpyAsync(ok_out, c->d_list_out, n, hipMemcpyDeviceToHost, c->stream));
     TV_HIP(c, hipEventRecord(c->ev_call1, c->stream));
     TV_HIP(c, hipEventSynchronize(c->ev_call1));
-    c->last_kernel = TV_KERNEL_LANE;
+    c->last_kernel = kernel;
     c->last_launches = 1;
     return finish_timing(c);
 }

@@ -31,6 +31,6 @@ struct TvPieces {
 };
 
 hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_t s, int split_pairs = 0);
-hipError_t tv_launch_verify_list(const TvPieces& p, hipStream_t s);
+hipError_t tv_launch_verify_list(const TvPieces& p, int kernel, hipStream_t s);
 hipError_t tv_launch_fill(uint8_t* payload, uint64_t stride, uint64_t first, uint32_t n, uint64_t L,
                           uint64_t seed, hipStream_t s);

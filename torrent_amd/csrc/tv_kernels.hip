@@ -252,11 +252,20 @@ __device__ __forceinline__ void lds_barrier() {
 
 }  // namespace
 
-template <bool HASH, int PAIRS>
+__device__ __forceinline__ bool avail_bit(const uint64_t* a, uint32_t i) {
+    // MSB-first bitfield bytes held in little-endian 64-bit words
+    return (a[i >> 6] >> (((i >> 3) & 7) * 8 + (7 - (i & 7)))) & 1;
+}
+
+// LIST = incremental verify (tv_verify_list): lane j verifies shard piece idx[j]; one pair per
+// workgroup, geometry from the pair's ballots (the short last piece may sit in any lane; the
+// helper and rounds waves see the same 64 pieces, so their ballots agree).
+template <bool HASH, int PAIRS, bool LIST = false>
 __global__ __launch_bounds__(128 * PAIRS) void tv_split_kernel(TvPieces p) {
     // PAIRS x {rounds, helper} waves; 64*PAIRS pieces.  A workgroup's waves go to distinct SIMDs, so
     // with <= 1 workgroup per CU no rounds wave shares its SIMD.  Each pair has its own 2 x 20 KiB
     // K+W ring; the barrier is workgroup-wide, so both pairs run the same (workgroup) block range.
+    static_assert(!LIST || PAIRS == 1, "list mode runs one pair per workgroup");
     __shared__ __attribute__((aligned(16))) uint4 ring[2 * PAIRS * kRingWords / 4];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -265,8 +274,11 @@ __global__ __launch_bounds__(128 * PAIRS) void tv_split_kernel(TvPieces p) {
     const uint32_t wg0 = blockIdx.x * (64u * PAIRS);
     const uint32_t j0 = wg0 + pair * 64u;
     const uint32_t j = j0 + lane;
-    const uint32_t jj = j < p.n ? j : p.n - 1;
-    const WaveGeom g = wave_geom(p, wg0, 64u * PAIRS);
+    const uint32_t jl = j < p.n ? j : p.n - 1;
+    const uint32_t jj = LIST ? p.idx[jl] : jl;
+    const bool is_last = jj == p.last_idx;
+    const WaveGeom g = LIST ? wave_geom_flags(p, __ballot(is_last) != 0, __ballot(!is_last) == 0)
+                            : wave_geom(p, wg0, 64u * PAIRS);
     const uint64_t len = lane_len(p, jj);
     const uint32_t nb = (uint32_t)nblocks(len);
     const uint8_t* piece = p.data + (uint64_t)jj * p.stride - p.data_off;
@@ -297,7 +309,8 @@ __global__ __launch_bounds__(128 * PAIRS) void tv_split_kernel(TvPieces p) {
 
     // ---------------- rounds wave ----------------
     uint32_t h[5];
-    start_state(p, jj, h);
+    if (LIST) sha1_iv(h);
+    else start_state(p, jj, h);
     const uint32_t ring_base = (uint32_t)(uintptr_t)(void*)pring + lane * 16u;
     const uint32_t nb_min = g.nb_min;
     lds_barrier();
@@ -318,6 +331,15 @@ __global__ __launch_bounds__(128 * PAIRS) void tv_split_kernel(TvPieces p) {
         }
         lds_barrier();
     }
+    if (LIST) {
+        if (j < p.n) {
+            bool ok = p.avail64 ? avail_bit(p.avail64, jj) : true;
+#pragma unroll
+            for (int k = 0; k < 5; k++) ok &= (h[k] == p.digests[(uint64_t)k * p.dcount + jj]);
+            p.out_bytes[j] = ok ? 1 : 0;
+        }
+        return;
+    }
     finish<HASH>(p, j, jj, j0, h);
 }
 
@@ -325,11 +347,6 @@ __global__ __launch_bounds__(128 * PAIRS) void tv_split_kernel(TvPieces p) {
 // list kernel (incremental verify): lane j verifies shard piece idx[j]; same compression path as
 // the lane kernel, geometry from wave ballots (the short last piece may sit in any lane).
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ bool avail_bit(const uint64_t* a, uint32_t i) {
-    // MSB-first bitfield bytes held in little-endian 64-bit words
-    return (a[i >> 6] >> (((i >> 3) & 7) * 8 + (7 - (i & 7)))) & 1;
-}
-
 __global__ __launch_bounds__(256) void tv_list_kernel(TvPieces p) {
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t j0 = blockIdx.x * 256u + wave * 64u;
@@ -434,9 +451,12 @@ hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_
     return hipGetLastError();
 }
 
-hipError_t tv_launch_verify_list(const TvPieces& p, hipStream_t s) {
+hipError_t tv_launch_verify_list(const TvPieces& p, int kernel, hipStream_t s) {
     if (p.n == 0) return hipSuccess;
-    hipLaunchKernelGGL(tv_list_kernel, dim3((p.n + 255) / 256), dim3(256), 0, s, p);
+    if (kernel == TV_KERNEL_SPLIT)
+        hipLaunchKernelGGL((tv_split_kernel<false, 1, true>), dim3((p.n + 63) / 64), dim3(128), 0, s, p);
+    else
+        hipLaunchKernelGGL(tv_list_kernel, dim3((p.n + 255) / 256), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
