@@ -38,10 +38,13 @@ sys.path.insert(0, ROOT)
 from torrent_amd import _native  # noqa: E402  (load the HIP library before torch)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-# SHA-1 VALU roofline: 1024 SIMDs x 64 lanes / 4 cycles per wave64 integer VOP3 instruction
-# (measured: tools/ubench_sha1.hip) x 2.4 GHz, 613 VALU per 64-B compression.
+# SHA-1 VALU roofline from the measured SIMD cost per wave64 instruction (tools/ubench_simd.hip,
+# profiles/r01/ubench_simd.log): v_alignbit / v_add3 / v_perm 4 cycles (half rate), v_bitop3 / VOP2 2
+# cycles (full rate).  Minimal mix per 64-B block: 224 alignbit + 160 add3 + 16 perm (400 x 4) + 144
+# bitop3 + 64 xor + 5 add (213 x 2) = 2,026 SIMD cycles per 64 lanes.
 CLOCK_HZ = 2.4e9
-VALU_PEAK_GBPS = 1024 * 64 / 4 * CLOCK_HZ / 613 * 64 / 1e9
+SIMD_CYC_PER_BLOCK = 400 * 4 + 213 * 2
+VALU_PEAK_GBPS = 1024 * 64 * 64 * CLOCK_HZ / SIMD_CYC_PER_BLOCK / 1e9
 LONE_WAVE_CYC = 4.34          # cycles per VALU instruction of a lone wave (measured)
 SERIAL_INSTR = {1: 613, 2: 405}  # per-block serial stream: lane kernel / split rounds wave
 
@@ -276,8 +279,9 @@ def main() -> int:
                          "frac_of_valu_peak": round(achieved / VALU_PEAK_GBPS, 4),
                          "piece_parallelism_ceiling": round(piece_ceiling, 1),
                          "frac_of_piece_ceiling": round(achieved / piece_ceiling, 4),
-                         "note": "SHA-1 is VALU-bound on MI355X (4 cyc/wave64 int VOP3); serial per piece, so "
-                                 "P pieces cap the rate at P x 64 B / (serial instr x 4.34 cyc) per GPU"},
+                         "note": "SHA-1 is VALU-bound on MI355X (valu_peak from measured per-op SIMD costs), not "
+                                 "HBM-bound; it is serial per piece, so P pieces cap the rate at P x 64 B / "
+                                 "(serial instr x 4.34 cyc) per GPU (piece_parallelism_ceiling)"},
         }
         if e2e is not None:
             out["e2e_pinned_host"] = e2e

@@ -20,7 +20,7 @@ SHA1_LDS    the 80 rounds only (400 VALU); W[0..79] comes from LDS as 20 ds_read
 Round (roles rotate statically; the new `a` is written into the old `e` register):
     E  = v_add3_u32(E, K, W[t])          # off the critical path
     T0 = v_alignbit_b32(A, A, 27)        # rotl5(a)
-    T1 = f(B, C, D)                      # v_bfi_b32 (Ch) | v_bitop3_b32 0x96 (Parity) / 0xE8 (Maj)
+    T1 = f(B, C, D)                      # v_bitop3_b32 0xCA (Ch) / 0x96 (Parity) / 0xE8 (Maj)
     B  = v_alignbit_b32(B, B, 2)         # rotl30(b)
     E  = v_add3_u32(E, T0, T1)           # new a
 Chaining values H are read-only inputs: the first write to each working register goes to its
@@ -79,9 +79,9 @@ def roles(t: int):
 
 def _fop(t, dst, b, c, d):
     k = f_kind(t)
-    if k == "ch":
-        return ("v_bfi_b32", dst, b, c, d)
-    return ("v_bitop3_b32", dst, b, c, d, 0x96 if k == "par" else 0xE8)
+    # Ch as v_bitop3 0xCA, not v_bfi_b32: same 8-byte issue cost, but v_bitop3 runs at full rate on
+    # the SIMD (2 cyc per wave64) and v_bfi at half rate (4 cyc; tools/ubench_simd.hip)
+    return ("v_bitop3_b32", dst, b, c, d, {"ch": 0xCA, "par": 0x96}.get(k, 0xE8))
 
 
 def gen_full():

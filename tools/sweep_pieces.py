@@ -10,7 +10,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from torrent_amd import _native as N  # noqa: E402
 
 VARIANTS = [("lane", 1, 0), ("split1", 2, 1), ("split2", 2, 2), ("auto", 0, 0)]
-PS = [1024, 2048, 4096, 8192, 12800, 16384, 20480, 25600, 32768, 40960, 51200, 65536, 131072, 262144]
+PS = [1024, 2048, 4096, 8192, 12800, 16384, 20480, 25600, 32768, 40960, 49152, 51200, 65536, 131072, 262144]
+if os.environ.get("SWEEP_PS"):
+    PS = [int(x) for x in os.environ["SWEEP_PS"].split(",")]
 
 
 def main():
@@ -39,10 +41,13 @@ def main():
             bits = [(bf[i >> 3] >> (7 - (i & 7))) & 1 for i in range(P)]
             assert bits == expect, (P, name)
             row[name] = round(total / best / 1e6, 1)   # GB/s
+            ctx.set_digests(bytes(len(d)))             # all-zero digests: every bit must now read 0
+            assert not any(ctx.verify()), (P, name)    # (no stale bits from the previous variant)
+            ctx.set_digests(bytes(d))
             if name == "auto":
                 row["auto_kernel"] = {1: "lane", 2: "split"}[ctx.last_kernel()[0]]
         ctx.close()
-        row["best"] = max((row[n], n) for n, _, _ in VARIANTS[:3])[1]
+        row["best"] = max((row[n], n) for n, _, _ in VARIANTS[:-1])[1]
         rows.append(row)
         line = json.dumps(row)
         print(line, flush=True)

@@ -772,6 +772,8 @@ int tv_verify(tv_ctx* c, const uint8_t* avail_bits, uint8_t* bitfield_out) {
     const int kernel = choose_kernel(c);
     TvPieces p = resident_launch(c);
     p.avail64 = av;
+    // fail closed: a piece the launch does not write reads as 0, never as a stale 1
+    TV_HIP(c, hipMemsetAsync(c->d_out, 0, c->bit_words * 8, c->stream));
     TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
     TV_HIP(c, tv_launch_verify(p, kernel, false, c->stream, c->split_pairs));
     TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
@@ -913,6 +915,7 @@ int tv_verify_host(tv_ctx* c, const uint8_t* src, uint64_t src_len, const uint8_
     p.stride = row;
     p.avail64 = av_dev;
     DrainGuard drain(c);
+    TV_HIP(c, hipMemsetAsync(c->d_out, 0, c->bit_words * 8, c->stream));  // fail closed, as tv_verify
     hipEvent_t* col_ev = drain.ev;       // copy of column -> buffer k done
     hipEvent_t* done_ev = drain.ev + 2;  // kernel that read buffer k done
     for (int k = 0; k < 4; k++) TV_HIP(c, hipEventCreateWithFlags(&drain.ev[k], hipEventDisableTiming));

@@ -434,7 +434,7 @@ hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_
     if (kernel == TV_KERNEL_SPLIT) {
         // one pair per workgroup while that still gives <= 1 workgroup per CU (256 CUs); two pairs
         // (4 waves on the CU's 4 SIMDs) up to 32768 pieces
-        const int pairs = split_pairs ? split_pairs : (p.n <= 256 * 64 ? 1 : 2);
+        const int pairs = (split_pairs == 1 || split_pairs == 2) ? split_pairs : (p.n <= 256 * 64 ? 1 : 2);
         const unsigned grid = (p.n + 64 * pairs - 1) / (64 * pairs);
         if (pairs == 1) {
             if (hash) hipLaunchKernelGGL((tv_split_kernel<true, 1>), dim3(grid), dim3(128), 0, s, p);
