@@ -212,6 +212,9 @@ TvPieces resident_launch(const tv_ctx* c) {
     const uint64_t last = c->P - 1;
     p.last_idx = (last >= c->first && last < c->first + c->count) ? (uint32_t)(last - c->first) : 0xFFFFFFFFu;
     p.last_len = piece_len(c, last);
+    // a short last piece hashes in a group of its own: in a main group its short tail would put every
+    // other lane of the group on the slow padded-block path for the rest of the piece
+    p.n_main = (p.last_idx != 0xFFFFFFFFu && p.last_len != c->L) ? p.n - 1 : p.n;
     p.blk_begin = 0;
     p.blk_end = UINT64_MAX;
     p.finalize = 1;
@@ -800,21 +803,44 @@ int tv_verify_list(tv_ctx* c, const uint64_t* pieces, uint64_t n, uint8_t* ok_ou
                         (unsigned long long)(c->first + c->count));
         local[k] = (uint32_t)(pieces[k] - c->first);
     }
+    // A short last piece (piece.ts:16-19) listed together with full pieces goes into waves of its own:
+    // the launch list is [full pieces..., padding to a multiple of 64, last-piece entries...], so no
+    // wave mixes the short piece's padding blocks with the others' raw blocks (the slow path).
+    const uint64_t lastj = c->first + c->count - 1 == c->P - 1 ? c->count - 1 : UINT64_MAX;
+    std::vector<uint32_t> launch;  // shard-relative pieces in launch order
+    std::vector<int64_t> origin;   // launch position -> index in `pieces` (-1 = padding)
+    bool reordered = false;
+    if (lastj != UINT64_MAX && piece_len(c, c->P - 1) != c->L) {
+        uint64_t nlast = 0;
+        for (uint64_t k = 0; k < n; k++) nlast += local[k] == lastj;
+        if (nlast && nlast < n) {
+            reordered = true;
+            for (uint64_t k = 0; k < n; k++)
+                if (local[k] != lastj) { launch.push_back(local[k]); origin.push_back((int64_t)k); }
+            while (launch.size() % 64) { launch.push_back(launch[0]); origin.push_back(-1); }
+            for (uint64_t k = 0; k < n; k++)
+                if (local[k] == lastj) { launch.push_back(local[k]); origin.push_back((int64_t)k); }
+        }
+    }
+    if (!reordered) launch.swap(local);
+    const uint64_t m = launch.size();
+    std::vector<uint8_t> ok_launch(reordered ? m : 0);
     TV_HIP(c, hipSetDevice(c->device));
-    DrainGuard drain(c);  // after `local`: its H2D copy and the ok_out D2H copy end before return
-    if (c->list_cap < n) {
+    DrainGuard drain(c);  // after the host vectors: their H2D / D2H copies end before return
+    if (c->list_cap < m) {
         (void)hipFree(c->d_list); c->d_list = nullptr;
         (void)hipFree(c->d_list_out); c->d_list_out = nullptr;
         c->list_cap = 0;
-        const uint64_t cap = std::max<uint64_t>(n, 1024);
+        const uint64_t cap = std::max<uint64_t>(m, 1024);
         TV_HIP(c, hipMalloc((void**)&c->d_list, cap * 4));
         TV_HIP(c, hipMalloc((void**)&c->d_list_out, cap));
         c->list_cap = cap;
     }
     TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
-    TV_HIP(c, hipMemcpyAsync(c->d_list, local.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+    TV_HIP(c, hipMemcpyAsync(c->d_list, launch.data(), m * 4, hipMemcpyHostToDevice, c->stream));
     TvPieces p = resident_launch(c);
-    p.n = (uint32_t)n;
+    p.n = (uint32_t)m;
+    p.n_main = (uint32_t)m;
     p.idx = c->d_list;
     p.out_bytes = c->d_list_out;
     TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
@@ -822,12 +848,15 @@ int tv_verify_list(tv_ctx* c, const uint64_t* pieces, uint64_t n, uint8_t* ok_ou
     // suffices, like choose_kernel; the lane list kernel for longer lists
     const int kernel = (c->kernel_opt == TV_KERNEL_LANE || c->kernel_opt == TV_KERNEL_SPLIT)
                            ? c->kernel_opt
-                           : (n <= 256 * 64 ? TV_KERNEL_SPLIT : TV_KERNEL_LANE);
+                           : (m <= 256 * 64 ? TV_KERNEL_SPLIT : TV_KERNEL_LANE);
     TV_HIP(c, tv_launch_verify_list(p, kernel, c->stream));
     TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
-    TV_HIP(c, hipMemcpyAsync(ok_out, c->d_list_out, n, hipMemcpyDeviceToHost, c->stream));
+    TV_HIP(c, hipMemcpyAsync(reordered ? ok_launch.data() : ok_out, c->d_list_out, m, hipMemcpyDeviceToHost, c->stream));
     TV_HIP(c, hipEventRecord(c->ev_call1, c->stream));
     TV_HIP(c, hipEventSynchronize(c->ev_call1));
+    if (reordered)
+        for (uint64_t i = 0; i < m; i++)
+            if (origin[i] >= 0) ok_out[origin[i]] = ok_launch[i];
     c->last_kernel = kernel;
     c->last_launches = 1;
     return finish_timing(c);

@@ -18,6 +18,8 @@ struct TvPieces {
     uint64_t blk_begin;
     uint64_t blk_end;        // UINT64_MAX = through the end of every piece
     uint32_t n;
+    uint32_t n_main;         // main groups cover pieces [0, n_main); n_main = n - 1 when the short last
+                             // piece (last_len < L) gets a group of its own, else n (list mode: n)
     uint32_t last_idx;       // launch-local index of the torrent's last piece, 0xFFFFFFFF if absent
     uint32_t finalize;       // 1: compare / emit digests; 0: store chaining values to `state`
     uint32_t dcount;         // row stride of state / digests / out_digests (= shard piece count)

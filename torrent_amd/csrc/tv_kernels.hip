@@ -61,7 +61,8 @@ __device__ __forceinline__ uint32_t uni(uint64_t x) {
 __device__ __forceinline__ WaveGeom wave_geom_flags(const TvPieces& p, bool has_last, bool only_last);
 
 __device__ __forceinline__ WaveGeom wave_geom(const TvPieces& p, uint32_t j0, uint32_t span = 64) {
-    const bool has_last = p.last_idx != 0xFFFFFFFFu && p.last_idx >= j0 && p.last_idx - j0 < span;
+    // (a SHORT last piece is never in a main group: it has a dedicated group, see TvPieces::n_main)
+    const bool has_last = p.last_idx < p.n_main && p.last_idx >= j0 && p.last_idx - j0 < span;
     const bool only_last = has_last && p.last_idx == j0;
     return wave_geom_flags(p, has_last, only_last);
 }
@@ -145,33 +146,37 @@ __device__ __forceinline__ uint64_t lane_len(const TvPieces& p, uint32_t jj) {
 }
 
 // Final step shared by both kernels: compare (verify) or store (hash) the digest, or keep the
-// chaining value for the next launch of a streamed run.
+// chaining value for the next launch of a streamed run.  `writer`: this lane owns piece jj's outputs
+// (a main-group lane below n_main, or lane 0 of the short last piece's dedicated group).  Bitfield
+// words are OR-ed into the zeroed output (the last group may share a word with a main group).
 template <bool HASH>
-__device__ __forceinline__ void finish(const TvPieces& p, uint32_t j, uint32_t jj, uint32_t j0,
-                                       const uint32_t h[5]) {
+__device__ __forceinline__ void finish(const TvPieces& p, bool writer, uint32_t jj, uint32_t j0,
+                                       const uint32_t h[5], bool last_grp) {
     if (!p.finalize) {
-        if (j < p.n) {
+        if (writer) {
 #pragma unroll
-            for (int k = 0; k < 5; k++) p.state[(uint64_t)k * p.dcount + j] = h[k];
+            for (int k = 0; k < 5; k++) p.state[(uint64_t)k * p.dcount + jj] = h[k];
         }
         return;
     }
     if (HASH) {
-        if (j < p.n) {
+        if (writer) {
 #pragma unroll
-            for (int k = 0; k < 5; k++) p.out_digests[(uint64_t)k * p.dcount + j] = h[k];
+            for (int k = 0; k < 5; k++) p.out_digests[(uint64_t)k * p.dcount + jj] = h[k];
         }
         return;
     }
-    bool ok = j < p.n;
+    bool ok = writer;
 #pragma unroll
     for (int k = 0; k < 5; k++) ok &= (h[k] == p.digests[(uint64_t)k * p.dcount + jj]);
     const uint64_t mask = __ballot(ok);
     if ((threadIdx.x & 63) == 0) {
         // ballot bit l = piece j0+l  ->  MSB-first bytes: byte m holds pieces j0+8m .. j0+8m+7
-        uint64_t bits = __builtin_bswap64(__builtin_bitreverse64(mask));
-        if (p.avail64) bits &= p.avail64[j0 >> 6];
-        p.out64[j0 >> 6] = bits;
+        const uint32_t w = (last_grp ? jj : j0) >> 6;
+        uint64_t bits = last_grp ? ((mask & 1) ? 1ull << (((jj >> 3) & 7) * 8 + 7 - (jj & 7)) : 0)
+                                 : __builtin_bswap64(__builtin_bitreverse64(mask));
+        if (p.avail64) bits &= p.avail64[w];
+        if (bits) atomicOr(reinterpret_cast<unsigned long long*>(p.out64 + w), (unsigned long long)bits);
     }
 }
 
@@ -192,11 +197,16 @@ __device__ __forceinline__ void start_state(const TvPieces& p, uint32_t jj, uint
 template <bool HASH>
 __global__ __launch_bounds__(256) void tv_lane_kernel(TvPieces p) {
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t j0 = blockIdx.x * 256u + wave * 64u;
-    if (j0 >= p.n) return;  // wave-uniform: no piece in this wave
-    const uint32_t j = j0 + (threadIdx.x & 63u);
-    const uint32_t jj = j < p.n ? j : p.n - 1;
-    const WaveGeom g = wave_geom(p, j0);
+    const uint32_t lane = threadIdx.x & 63u;
+    // main waves cover [0, n_main); a short last piece (n_main < n) gets the wave after them alone
+    const uint32_t gw = blockIdx.x * 4u + wave, nw_main = (p.n_main + 63u) / 64u;
+    const bool last_grp = gw >= nw_main;
+    if (last_grp && (gw > nw_main || p.n_main == p.n)) return;  // wave-uniform: no piece here
+    const uint32_t j0 = last_grp ? p.last_idx : gw * 64u;
+    const uint32_t j = last_grp ? p.last_idx : j0 + lane;
+    const uint32_t jj = last_grp ? p.last_idx : (j < p.n_main ? j : p.n_main - 1);
+    const bool writer = last_grp ? lane == 0 : j < p.n_main;
+    const WaveGeom g = last_grp ? wave_geom_flags(p, true, true) : wave_geom(p, j0);
     const uint64_t len = lane_len(p, jj);
     const uint32_t nb = (uint32_t)nblocks(len);
     const uint8_t* piece = p.data + (uint64_t)jj * p.stride - p.data_off;
@@ -233,7 +243,7 @@ __global__ __launch_bounds__(256) void tv_lane_kernel(TvPieces p) {
             for (int i = 0; i < 5; i++) h[i] += r[i];
         }
     }
-    finish<HASH>(p, j, jj, j0, h);
+    finish<HASH>(p, writer, jj, j0, h, last_grp);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -271,14 +281,20 @@ __global__ __launch_bounds__(128 * PAIRS) void tv_split_kernel(TvPieces p) {
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t pair = wave % PAIRS;
     const uint32_t role = wave / PAIRS;        // 0 = rounds, 1 = helper
-    const uint32_t wg0 = blockIdx.x * (64u * PAIRS);
-    const uint32_t j0 = wg0 + pair * 64u;
-    const uint32_t j = j0 + lane;
-    const uint32_t jl = j < p.n ? j : p.n - 1;
+    // main workgroups cover [0, n_main); a short last piece (n_main < n) gets one workgroup after
+    // them, whose every lane (and pair) hashes it, so no main group runs its short tail.  List mode
+    // has no last group (the host puts the last piece's entries in waves of their own).
+    const uint32_t span = 64u * PAIRS;
+    const uint32_t nlim = LIST ? p.n : p.n_main;
+    const bool last_grp = !LIST && blockIdx.x >= (nlim + span - 1) / span;
+    const uint32_t wg0 = last_grp ? p.last_idx : blockIdx.x * span;
+    const uint32_t j0 = last_grp ? p.last_idx : wg0 + pair * 64u;
+    const uint32_t j = last_grp ? p.last_idx : j0 + lane;
+    const uint32_t jl = last_grp ? p.last_idx : (j < nlim ? j : nlim - 1);
     const uint32_t jj = LIST ? p.idx[jl] : jl;
     const bool is_last = jj == p.last_idx;
     const WaveGeom g = LIST ? wave_geom_flags(p, __ballot(is_last) != 0, __ballot(!is_last) == 0)
-                            : wave_geom(p, wg0, 64u * PAIRS);
+                            : last_grp ? wave_geom_flags(p, true, true) : wave_geom(p, wg0, span);
     const uint64_t len = lane_len(p, jj);
     const uint32_t nb = (uint32_t)nblocks(len);
     const uint8_t* piece = p.data + (uint64_t)jj * p.stride - p.data_off;
@@ -340,7 +356,7 @@ __global__ __launch_bounds__(128 * PAIRS) void tv_split_kernel(TvPieces p) {
         }
         return;
     }
-    finish<HASH>(p, j, jj, j0, h);
+    finish<HASH>(p, last_grp ? (lane == 0 && pair == 0) : j < p.n_main, jj, j0, h, last_grp);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -435,7 +451,7 @@ hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_
         // one pair per workgroup while that still gives <= 1 workgroup per CU (256 CUs); two pairs
         // (4 waves on the CU's 4 SIMDs) up to 32768 pieces
         const int pairs = (split_pairs == 1 || split_pairs == 2) ? split_pairs : (p.n <= 256 * 64 ? 1 : 2);
-        const unsigned grid = (p.n + 64 * pairs - 1) / (64 * pairs);
+        const unsigned grid = (p.n_main + 64 * pairs - 1) / (64 * pairs) + (p.n_main < p.n ? 1 : 0);
         if (pairs == 1) {
             if (hash) hipLaunchKernelGGL((tv_split_kernel<true, 1>), dim3(grid), dim3(128), 0, s, p);
             else hipLaunchKernelGGL((tv_split_kernel<false, 1>), dim3(grid), dim3(128), 0, s, p);
@@ -444,7 +460,8 @@ hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_
             else hipLaunchKernelGGL((tv_split_kernel<false, 2>), dim3(grid), dim3(256), 0, s, p);
         }
     } else {
-        const unsigned grid = (p.n + 255) / 256;
+        const unsigned waves = (p.n_main + 63) / 64 + (p.n_main < p.n ? 1 : 0);
+        const unsigned grid = (waves + 3) / 4;
         if (hash) hipLaunchKernelGGL(tv_lane_kernel<true>, dim3(grid), dim3(256), 0, s, p);
         else hipLaunchKernelGGL(tv_lane_kernel<false>, dim3(grid), dim3(256), 0, s, p);
     }
