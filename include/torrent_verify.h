@@ -106,6 +106,23 @@ int tv_stage(tv_ctx *ctx, uint64_t linear_offset, const uint8_t *src, uint64_t l
  */
 int tv_stage_file(tv_ctx *ctx, const char *path, uint64_t file_offset, uint64_t linear_offset, uint64_t len);
 
+/*
+ * Stage MANY file segments in one call: a shard's whole Storage.get mapping (storage.ts:89-137), each
+ * segment read as fsStorage.get reads it (storage.ts:150-172).  Segment k is `lens[k]` bytes of file
+ * `paths[k]` from byte `file_offsets[k]`, staged as LINEAR bytes [linear_offsets[k], +lens[k]).
+ *   - Segments of >= TV_OPT_FILE_DIRECT_MIN bytes (default 32 MiB) take the tv_stage_file path.
+ *   - Shorter ones are packed into the pinned ring's 64 MiB slots. TV_OPT_FILE_THREADS threads read
+ *     them (open, pread, close; default 16), and each run of linear-contiguous segments is one DMA.
+ *     A slot's DMA overlaps the reads of the next slot. This is the many-small-files case: a
+ *     10,000-file torrent is one call, not 10,000.
+ * status_out[k] = TV_OK, or TV_ERR_IO when the file is missing, unreadable or shorter than the
+ * segment; the host marks the pieces that segment touches unreadable (Storage.get -> null).  The call
+ * itself returns TV_OK unless an argument or HIP error occurs; the first I/O failure's message is
+ * kept for tv_last_error.  Bytes outside the shard are skipped; zero-length segments succeed.
+ */
+int tv_stage_files(tv_ctx *ctx, uint64_t n, const char *const *paths, const uint64_t *file_offsets,
+                   const uint64_t *linear_offsets, const uint64_t *lens, int32_t *status_out);
+
 /* The inverse of tv_stage: copy `len` resident bytes at LINEAR offset `linear_offset` to host
  * `dst` (HBM as the piece store serving block requests, torrent.ts:164-167 Storage.get).  Bytes
  * outside the shard are left untouched in dst. */
@@ -161,6 +178,8 @@ int tv_host_unregister(void *ptr);
 #define TV_OPT_SPLIT_PAIRS 4  /* split kernel: (rounds, helper) wave pairs per workgroup, 0 = auto, 1, 2 */
 #define TV_OPT_FILE_DIRECT 5  /* tv_stage_file: 1 (default) = warm windows DMA'd from registered page-cache pages, 0 = all via the pinned ring */
 #define TV_OPT_FILE_CHUNK 6   /* tv_stage_file: bytes per mapped file window (default 256 MiB, >= 64 KiB) */
+#define TV_OPT_FILE_DIRECT_MIN 7 /* tv_stage_files: segment length that takes the tv_stage_file path (default 32 MiB) */
+#define TV_OPT_FILE_THREADS 8    /* tv_stage_files: reader threads for short segments (default 16) */
 int tv_set_option(tv_ctx *ctx, int key, int64_t value);
 int tv_get_option(tv_ctx *ctx, int key, int64_t *value);
 

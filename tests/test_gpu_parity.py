@@ -129,7 +129,8 @@ def test_shards_concatenate(native, oracle, kernel):
 
 
 @pytest.mark.parametrize("chunk", [0, 64, 4096, 65536])
-def test_stream_from_host_matches(native, oracle, chunk):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_stream_from_host_matches(native, oracle, chunk, kernel):
     L, P = 65536, 97
     total = L * (P - 1) + 4321
     payload = oracle.synth_fill(23, 0, total)
@@ -137,7 +138,7 @@ def test_stream_from_host_matches(native, oracle, chunk):
     payload[3 * L + 100] ^= 0x10
     pieces[20 * 50 + 3] ^= 0x01
     expect = oracle.verify_linear(payload, total, L, bytes(pieces))
-    with _ctx(native) as ctx:
+    with _ctx(native, kernel) as ctx:
         ctx.set_option(native.TV_OPT_STREAM_CHUNK, chunk)
         ctx.set_layout(total, L, P)
         ctx.set_digests(bytes(pieces))

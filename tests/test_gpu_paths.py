@@ -307,11 +307,10 @@ def test_incremental_verifier_flow(native, oracle):
 
 @pytest.mark.parametrize("layout", ["multi_zero_tiny", "missing_and_short", "single_short_last"])
 def test_verify_files_resume_from_disk(native, tmp_path, layout):
-    """verify_files (f2 resume from disk: parallel preads into pinned buffers, direct DMA) gives the
-    same bits as the committed expectation and as verify_pieces over fs_storage."""
+    """verify_files (f2 resume from disk: one tv_stage_files call per shard) gives the same bits as the
+    committed expectation and as verify_pieces over fs_storage, whichever path the segments take."""
     from tests.layouts import build_layout, by_name
     from torrent_amd import verify_files
-    from torrent_amd.verify import _STAGE_BATCH_BYTES  # noqa: F401
     rec = {r["name"]: r for r in json.load(open(os.path.join(GOLDEN, "layouts.json")))}[layout]
     lay = build_layout(by_name(layout))
     for path, data in lay["disk_files"]().items():
@@ -322,14 +321,14 @@ def test_verify_files_resume_from_disk(native, tmp_path, layout):
     cwd = os.getcwd()
     os.chdir(tmp_path)
     try:
-        # small batches + 2 devices slots on GPU 0: exercises batching, double buffering, shards
-        bf = verify_files(lay["info"], str(tmp_path), devices=[0, 0], batch_bytes=3 * lay["info"].piece_length)
-        # odd-sized read chunks: every file segment is split across the read threads
-        bf2 = verify_files(lay["info"], str(tmp_path), batch_bytes=5 * lay["info"].piece_length, read_chunk=1000)
-        # every non-empty file segment through tv_stage_file (page-cache DMA), 2 shards
+        # default: every segment is short, so all go through the reader pool; 2 shards on GPU 0
+        bf = verify_files(lay["info"], str(tmp_path), devices=[0, 0])
+        # one reader thread
+        bf2 = verify_files(lay["info"], str(tmp_path), threads=1)
+        # every non-empty file segment through the tv_stage_file path (page-cache DMA), 2 shards
         bf3 = verify_files(lay["info"], str(tmp_path), devices=[0, 0], direct_min=0)
-        # a mix: segments >= 3 KiB direct, the rest in pread runs
-        bf4 = verify_files(lay["info"], str(tmp_path), batch_bytes=4 * lay["info"].piece_length, direct_min=3072)
+        # a mix: segments >= 3 KiB take the tv_stage_file path, the rest the reader pool
+        bf4 = verify_files(lay["info"], str(tmp_path), direct_min=3072)
     finally:
         os.chdir(cwd)
     assert bytes(bf).hex() == rec["expected_bitfield"]
@@ -486,32 +485,38 @@ def test_concurrent_calls_do_not_interleave(native, oracle):
     release_contexts()
 
 
-def test_verify_files_read_faults_are_unreadable_pieces(native, tmp_path, monkeypatch):
-    """Fault injection (the storage_test.ts:96-108 idea, applied to verify_files' own reads): a
-    read that raises makes exactly the pieces it covers unreadable (bit 0), never an exception."""
-    from torrent_amd import make_info, verify_files
-    L, P = 4096, 24
-    total = L * P
-    payload = bytes(range(256)) * (total // 256)
+def test_verify_files_read_faults_are_unreadable_pieces(native, tmp_path):
+    """Read faults (the storage_test.ts:96-108 idea, applied to verify_files' own reads): a path that
+    opens but cannot be read (a directory where a file should be: EISDIR), a short file and a missing
+    file make exactly the pieces they touch unreadable (bit 0), never an exception, through both the
+    reader pool and the tv_stage_file path; tv_stage_files reports each as TV_ERR_IO."""
     import hashlib as _h
+    from torrent_amd import FileInfo, make_info, verify_files
+    L = 4096
+    sizes = [5 * L + 100, 3 * L, 4 * L + 7, 2 * L, 6 * L]         # files f0 .. f4
+    payload = bytes((i * 7 + 3) & 0xFF for i in range(sum(sizes)))
+    total = len(payload)
+    P = -(-total // L)
     pieces = b"".join(_h.sha1(payload[i * L:(i + 1) * L]).digest() for i in range(P))
-    info = make_info(L, pieces, "f.bin", length=total)
-    (tmp_path / "f.bin").write_bytes(payload)
-    real = os.preadv
-    bad_lo, bad_hi = 5 * L + 100, 9 * L + 7          # file bytes whose reads fail
-
-    def flaky(fd, bufs, off):
-        n = sum(memoryview(b).nbytes for b in bufs)
-        if off < bad_hi and off + n > bad_lo:
-            raise OSError(5, "injected I/O error")
-        return real(fd, bufs, off)
-
-    monkeypatch.setattr(os, "preadv", flaky)
+    info = make_info(L, pieces, "t", files=[FileInfo(n, [f"f{k}"]) for k, n in enumerate(sizes)])
+    starts = [sum(sizes[:k]) for k in range(len(sizes) + 1)]
+    (tmp_path / "f0").write_bytes(payload[starts[0]:starts[1]])
+    (tmp_path / "f1").mkdir()                                      # a directory: open ok, read fails
+    (tmp_path / "f2").write_bytes(payload[starts[2]:starts[3] - 1])  # one byte short
+    (tmp_path / "f4").write_bytes(payload[starts[4]:starts[5]])       # f3 missing
+    bad = set()
+    for k in (1, 2, 3):
+        bad |= set(range(starts[k] // L, (starts[k + 1] - 1) // L + 1))
     cwd = os.getcwd()
     os.chdir(tmp_path)
     try:
-        bf = verify_files(info, str(tmp_path), batch_bytes=8 * L, read_chunk=L)
+        for dmin in (None, 0):
+            bf = verify_files(info, str(tmp_path), direct_min=dmin)
+            bits = [(bf[i >> 3] >> (7 - (i & 7))) & 1 for i in range(P)]
+            assert bits == [0 if i in bad else 1 for i in range(P)], dmin
     finally:
         os.chdir(cwd)
-    bits = [(bf[i >> 3] >> (7 - (i & 7))) & 1 for i in range(P)]
-    assert bits == [0 if 5 <= i <= 9 else 1 for i in range(P)]
+    with native.Context(0) as ctx:
+        ctx.set_layout(total, L, P)
+        st = ctx.stage_files([str(tmp_path / f"f{k}") for k in range(5)], [0] * 5, starts[:5], sizes)
+        assert st == [0, native.TV_ERR_IO, native.TV_ERR_IO, native.TV_ERR_IO, 0]

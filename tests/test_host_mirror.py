@@ -264,15 +264,19 @@ def test_info_hash_is_sha1_of_the_original_info_bytes(name):
 
 
 class _ImageCtx:
-    """Stand-in for a tv_ctx on CPU: tv_stage / tv_stage_file write into a linear image of the shard,
-    so verify_files' staging plan (file segments -> pread runs + direct segments) is checked without a
-    GPU.  stage_file reads the file the way the library does (missing / short -> False, nothing staged)."""
+    """Stand-in for a tv_ctx on CPU: tv_stage_files writes into a linear image of the shard, so
+    verify_files' staging plan (the storage.ts segment mapping, one batched call, status -> unreadable
+    pieces) is checked without a GPU.  Files are read the way the library reads them (missing / short /
+    unreadable -> TV_ERR_IO, nothing staged for that segment)."""
 
     def __init__(self, total, lo, hi):
         self.img = bytearray(total)
         self.written = bytearray(total)
         self.lo, self.hi = lo, hi
-        self.direct = 0
+        self.calls = 0
+
+    def set_option(self, key, value):
+        pass
 
     def _put(self, off, data):
         a, b = max(off, self.lo), min(off + len(data), self.hi)
@@ -282,41 +286,34 @@ class _ImageCtx:
                 assert not self.written[k], f"byte {k} staged twice"
                 self.written[k] = 1
 
-    def stage(self, off, mv):
-        self._put(off, bytes(mv))
-
-    def stage_file(self, path, foff, off, n):
-        self.direct += 1
-        try:
-            with open(path, "rb") as f:
-                f.seek(foff)
-                data = f.read(n)
-        except OSError:
-            return False
-        if len(data) < n:
-            return False
-        self._put(off, data)
-        return True
+    def stage_files(self, paths, file_offsets, linear_offsets, lens):
+        self.calls += 1
+        out = []
+        for path, foff, off, n in zip(paths, file_offsets, linear_offsets, lens):
+            try:
+                with open(path, "rb") as f:
+                    f.seek(foff)
+                    data = f.read(n)
+            except OSError:
+                out.append(-5)
+                continue
+            if len(data) < n:
+                out.append(-5)
+                continue
+            self._put(off, data)
+            out.append(0)
+        return out
 
 
 @pytest.mark.parametrize("layout", ["missing_and_short", "multi_zero_tiny", "single_short_last"])
-@pytest.mark.parametrize("direct_min,batch", [(None, 3), (0, 2), (3072, 1), (1 << 62, 1)])
-def test_files_shard_staging_plan(tmp_path, monkeypatch, layout, direct_min, batch):
-    """verify_files' staging plan on CPU: every readable byte of the shard is staged exactly once at its
-    linear offset (pread runs and direct segments together), and the availability bits are exactly the
-    pieces whose bytes are all on disk (storage.ts:150-172 null -> 0), over 3 shards."""
+def test_files_shard_staging_plan(tmp_path, monkeypatch, layout):
+    """verify_files' staging plan on CPU: one tv_stage_files call per shard stages every readable byte
+    of the shard exactly once at its linear offset, and the availability bits are exactly the pieces
+    whose bytes are all on disk (storage.ts:150-172 null -> 0), over 3 shards."""
     from tests.layouts import build_layout, by_name
-    from torrent_amd import _native, verify
+    from torrent_amd import verify
     from torrent_amd.storage import Storage, fs_storage
 
-    class _Buf:
-        def __init__(self, n):
-            self.mv = memoryview(bytearray(n))
-
-        def close(self):
-            pass
-
-    monkeypatch.setattr(_native, "PinnedBuffer", _Buf)
     lay = build_layout(by_name(layout))
     info = lay["info"]
     for path, data in lay["disk_files"]().items():
@@ -331,8 +328,8 @@ def test_files_shard_staging_plan(tmp_path, monkeypatch, layout, direct_min, bat
             continue
         hi = (first + count - 1) * L + (total % L if first + count == P and total % L else L)
         ctx = _ImageCtx(total, first * L, hi)
-        avail = verify._files_shard(ctx, info, st, first, count, threads=4, batch_bytes=batch * L,
-                                    read_chunk=1000, direct_min=direct_min)
+        avail = verify._files_shard(ctx, info, st, first, count, threads=4)
+        assert ctx.calls == 1
         for j in range(count):
             i = first + j
             want = (lay["avail"][i >> 3] >> (7 - (i & 7))) & 1
@@ -341,7 +338,3 @@ def test_files_shard_staging_plan(tmp_path, monkeypatch, layout, direct_min, bat
                 a, b = i * L, min(total, (i + 1) * L)
                 assert ctx.img[a:b] == lay["payload"][a:b], (layout, i)
                 assert all(ctx.written[a:b]), (layout, i)
-        if direct_min == 0:
-            assert ctx.direct > 0
-        if direct_min == 1 << 62:
-            assert ctx.direct == 0

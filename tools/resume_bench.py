@@ -1,6 +1,7 @@
 """Resume-from-disk throughput: write a synthetic multi-file torrent to a directory,
-then time verify_files (disk -> HBM -> verify) with its two staging paths: direct (tv_stage_file, the
-page-cache pages DMA'd to HBM) and pread runs (parallel preads into pinned buffers, then DMA).  Each
+then time verify_files (disk -> HBM -> verify; one tv_stage_files call) with its two staging paths:
+direct (the tv_stage_file path: page-cache pages DMA'd to HBM) and the reader pool (library threads
+pread into pinned slots, then DMA).  Each
 is timed with the page cache warm (the files were just written) and cold (posix_fadvise DONTNEED
 after fsync, so the reads go to the box's disk).
 usage: python tools/resume_bench.py <dir> <GiB> [n_files]"""
@@ -56,7 +57,7 @@ def exact(bf):
 
 cwd = os.getcwd()
 os.chdir(d)
-modes = [("direct (tv_stage_file: page-cache DMA)", None), ("pread runs -> pinned -> DMA", 1 << 62)]
+modes = [("direct (tv_stage_file path: page-cache DMA)", None), ("reader pool (preads -> pinned slots -> DMA)", 1 << 62)]
 if "--pread-first" in sys.argv:
     modes = modes[::-1] + modes[1:]
 for cold in ((False,) if "--warm-only" in sys.argv else (False, True)):

@@ -26,6 +26,8 @@ TV_OPT_STREAM_CHUNK = 3
 TV_OPT_SPLIT_PAIRS = 4
 TV_OPT_FILE_DIRECT = 5
 TV_OPT_FILE_CHUNK = 6
+TV_OPT_FILE_DIRECT_MIN = 7
+TV_OPT_FILE_THREADS = 8
 
 KERNEL_AUTO, KERNEL_LANE, KERNEL_SPLIT = 0, 1, 2
 
@@ -41,6 +43,7 @@ SYMBOLS = [
     ("tv_set_digests", _int, [_p, _p, _u64]),
     ("tv_stage", _int, [_p, _u64, _p, _u64]),
     ("tv_stage_file", _int, [_p, ctypes.c_char_p, _u64, _u64, _u64]),
+    ("tv_stage_files", _int, [_p, _u64, _p, _p, _p, _p, _p]),
     ("tv_read", _int, [_p, _u64, _p, _u64]),
     ("tv_fill_synthetic", _int, [_p, _u64]),
     ("tv_verify", _int, [_p, _p, _p]),
@@ -224,6 +227,22 @@ class Context:
             return False
         self._check(rc)
         return True
+
+    def stage_files(self, paths, file_offsets, linear_offsets, lens) -> list:
+        """tv_stage_files: stage many file segments in one call.  Returns one status per segment:
+        TV_OK, or TV_ERR_IO for a missing / unreadable / short file (its pieces are unreadable)."""
+        n = len(paths)
+        if n == 0:
+            return []
+        enc = [os.fsencode(x) for x in paths]
+        cpaths = (ctypes.c_char_p * n)(*enc)
+        arr = lambda v: (ctypes.c_uint64 * n)(*v)  # noqa: E731
+        fo, lo, ln = arr(file_offsets), arr(linear_offsets), arr(lens)
+        st = (ctypes.c_int32 * n)()
+        self._check(self._L.tv_stage_files(self._h, n, ctypes.cast(cpaths, _p), ctypes.cast(fo, _p),
+                                           ctypes.cast(lo, _p), ctypes.cast(ln, _p), ctypes.cast(st, _p)))
+        del enc
+        return list(st)
 
     def read(self, linear_offset: int, out) -> None:
         """Copy resident bytes at linear_offset into the writable buffer `out` (tv_read)."""

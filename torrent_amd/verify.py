@@ -196,45 +196,25 @@ def verify_payload(info: InfoDict, payload, devices=None, resident: bool = True,
     return _concat(slices, ranges, P)
 
 
-def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: int,
-                 batch_bytes: int, read_chunk: int = 8 << 20, direct_min: Optional[int] = None) -> bytearray:
+def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: int = 16,
+                 direct_min: Optional[int] = None) -> bytearray:
     """Stage the shard's pieces from files into HBM and return the shard's readability bits.
 
     The shard's linear range is mapped to file segments exactly as Storage.get maps it
-    (storage.ts:89-137).  Then:
-      * a segment of >= direct_min bytes is staged by tv_stage_file: its page-cache pages are mapped,
-        registered read-only and DMA'd straight to HBM (no host copy), on a thread of its own;
-      * shorter segments that are adjacent in the linear space are grouped into runs of at most
-        batch_bytes; a run is read by parallel preads (read_chunk pieces, so all threads copy even
-        when one file covers the run) into one of two alternating page-locked buffers and DMA'd
-        while the next run is read.
+    (storage.ts:89-137), and ALL segments go to the library in one tv_stage_files call: segments of
+    >= direct_min bytes (default 32 MiB) are DMA'd from the page cache (tv_stage_file's path), shorter
+    ones are read by `threads` library threads into pinned slots, one DMA per run of adjacent bytes.
     A piece touching a missing or short file is unreadable (fsStorage.get -> null,
     storage.ts:150-172); zero-length segments succeed; missing files are never created."""
     import os
     L = info.piece_length
-    if direct_min is None:
-        direct_min = _DIRECT_MIN_BYTES
     avail = bytearray(b"\xff" * ((count + 7) // 8))
     if count % 8:
         avail[-1] = (0xFF00 >> (count % 8)) & 0xFF
-    fds: dict = {}
-    lock = threading.Lock()
-
-    def fd_of(path):
-        key = os.path.join(*path)
-        with lock:
-            if key not in fds:
-                try:
-                    fd = os.open(key, os.O_RDONLY)
-                    fds[key] = (fd, os.fstat(fd).st_size)
-                except OSError:
-                    fds[key] = (None, -1)
-            return fds[key]
 
     def clear(j_lo: int, j_hi: int) -> None:   # shard-relative pieces [j_lo, j_hi] unreadable
-        with lock:
-            for j in range(max(0, j_lo), min(count - 1, j_hi) + 1):
-                avail[j >> 3] &= ~(0x80 >> (j & 7)) & 0xFF
+        for j in range(max(0, j_lo), min(count - 1, j_hi) + 1):
+            avail[j >> 3] &= ~(0x80 >> (j & 7)) & 0xFF
 
     lo = first * L
     last = first + count - 1
@@ -249,97 +229,26 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
     if segs is None:                  # unmappable (Storage.get -> null for every piece)
         clear(0, count - 1)
         segs = []
-
-    direct: list = []                 # (path, file offset, shard-relative start, n)
-    runs: list = []                   # [start, n, [(fd, file offset, run-relative start, n)]]
-    run_cap = max(1, batch_bytes)
-    for path, foff, n, start in segs:
-        if n == 0:
-            continue
-        fd, size = fd_of(path)
-        if fd is None or foff + n > size:
+    segs = [sg for sg in segs if sg[2] > 0]
+    ctx.set_option(_native.TV_OPT_FILE_THREADS, max(1, threads))
+    ctx.set_option(_native.TV_OPT_FILE_DIRECT_MIN, _DIRECT_MIN_BYTES if direct_min is None else direct_min)
+    status = ctx.stage_files([os.path.join(*path) for path, _, _, _ in segs], [foff for _, foff, _, _ in segs],
+                             [lo + start for _, _, _, start in segs], [n for _, _, n, _ in segs])
+    for (_, _, n, start), st in zip(segs, status):
+        if st != _native.TV_OK:
             clear(start // L, (start + n - 1) // L)
-            continue
-        if n >= direct_min:
-            direct.append((os.path.join(*path), foff, start, n))
-            continue
-        while n:                      # a segment longer than a run is cut across runs
-            cur = runs[-1] if runs else None
-            if cur is not None and cur[0] + cur[1] == start and cur[1] < run_cap:
-                k = min(n, run_cap - cur[1])
-                cur[2].append((fd, foff, start - cur[0], k))
-                cur[1] += k
-            else:
-                k = min(n, run_cap)
-                runs.append([start, k, [(fd, foff, 0, k)]])
-            foff, start, n = foff + k, start + k, n - k
-
-    def stage_direct() -> None:
-        for path, foff, start, n in direct:
-            if not ctx.stage_file(path, foff, lo + start, n):
-                clear(start // L, (start + n - 1) // L)
-
-    def read_run(run, buf) -> None:
-        start0, _, parts = run
-        tasks = []
-        for fd, foff, rel, n in parts:
-            for s0 in range(0, n, read_chunk):
-                tasks.append((fd, foff + s0, rel + s0, min(read_chunk, n - s0)))
-
-        def one(t):
-            fd, foff, rel, c = t
-            try:
-                got = os.preadv(fd, [buf.mv[rel:rel + c]], foff)
-            except OSError:
-                got = -1
-            return None if got == c else (rel, c)
-
-        for r in pool.map(one, tasks):
-            if r is not None:
-                rel, c = r
-                clear((start0 + rel) // L, (start0 + rel + c - 1) // L)
-
-    pool = ThreadPoolExecutor(max(1, threads))
-    stager = ThreadPoolExecutor(2)    # one thread for direct segments, one for run DMAs
-    bufs = []
-    try:
-        dfut = stager.submit(stage_direct) if direct else None
-        if runs:
-            size = max(r[1] for r in runs)
-            bufs = [_native.PinnedBuffer(size)] + ([_native.PinnedBuffer(size)] if len(runs) > 1 else [])
-        fut = None
-        for b, run in enumerate(runs):
-            buf = bufs[b & 1]
-            read_run(run, buf)
-            if fut is not None:
-                fut.result()           # the other buffer's DMA is done before it is reused
-            fut = stager.submit(ctx.stage, lo + run[0], buf.mv[:run[1]])
-        if fut is not None:
-            fut.result()
-        if dfut is not None:
-            dfut.result()
-    finally:
-        stager.shutdown()
-        pool.shutdown()
-        for fd, _ in fds.values():
-            if fd is not None:
-                os.close(fd)
-        for bb in bufs:
-            bb.close()
     return avail
 
 
 def verify_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
-                 batch_bytes: int = 256 << 20, read_chunk: int = 8 << 20,
                  direct_min: Optional[int] = None) -> bytearray:
     """Resume check from disk: the have-bitfield of the files under dir_path,
     laid out as Storage(fs_storage, info, dir_path) maps them (storage.ts:89-137; single-file
     torrents are [dir, name], multi-file [dir, *path] without info.name).
 
     Same bits as verify_pieces(info, Storage(fs_storage, info, dir_path)), without fsStorage.get's
-    side effect of creating missing files.  Long file segments (>= direct_min bytes, default 32 MiB)
-    are DMA'd to HBM straight from the page cache; shorter ones are read by parallel preads into
-    page-locked buffers (see _files_shard) instead of one open/seek/read per piece."""
+    side effect of creating missing files, and with every file segment of a shard staged by ONE
+    tv_stage_files call (see _files_shard) instead of one open/seek/read per piece."""
     from .storage import Storage, fs_storage
 
     P, L = info.n_pieces, info.piece_length
@@ -350,8 +259,7 @@ def verify_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
         ctx.set_digests(info.pieces_raw)
         if count == 0:
             return b""
-        return ctx.verify(_files_shard(ctx, info, storage, first, count, threads, batch_bytes, read_chunk,
-                                       direct_min))
+        return ctx.verify(_files_shard(ctx, info, storage, first, count, threads, direct_min))
 
     if P == 0:
         return bytearray()
@@ -360,7 +268,6 @@ def verify_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
 
 
 def hash_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
-               batch_bytes: int = 256 << 20, read_chunk: int = 8 << 20,
                direct_min: Optional[int] = None) -> bytes:
     """Creation mode from disk: the `pieces` string of the files info describes under dir_path
     (info.pieces is ignored; only the geometry is used).  Raises if a file is missing or short."""
@@ -374,8 +281,7 @@ def hash_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
         ctx.set_layout(info.length, L, P, first, count)
         if count == 0:
             return b""
-        avail = _files_shard(ctx, info, storage, first, count, threads, batch_bytes, read_chunk,
-                             direct_min)
+        avail = _files_shard(ctx, info, storage, first, count, threads, direct_min)
         full = bytearray(b"\xff" * ((count + 7) // 8))
         if count % 8:
             full[-1] = (0xFF00 >> (count % 8)) & 0xFF

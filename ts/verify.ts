@@ -23,6 +23,11 @@ const SYMBOLS = {
   tv_set_digests: { parameters: ["pointer", "pointer", "u64"], result: "i32" },
   tv_stage: { parameters: ["pointer", "u64", "pointer", "u64"], result: "i32", nonblocking: true },
   tv_stage_file: { parameters: ["pointer", "pointer", "u64", "u64", "u64"], result: "i32", nonblocking: true },
+  tv_stage_files: {
+    parameters: ["pointer", "u64", "pointer", "pointer", "pointer", "pointer", "pointer"],
+    result: "i32",
+    nonblocking: true,
+  },
   tv_read: { parameters: ["pointer", "u64", "pointer", "u64"], result: "i32", nonblocking: true },
   tv_fill_synthetic: { parameters: ["pointer", "u64"], result: "i32" },
   tv_verify: { parameters: ["pointer", "pointer", "pointer"], result: "i32", nonblocking: true },
@@ -164,11 +169,12 @@ const TV_ERR_IO = -5;
 /**
  * verifyFiles(info, dir) -> have-bitfield of the files under `dir` (resume from disk, SURVEY 8f
  * row f2), laid out as new Storage(fsStorage, info, dir) maps them (storage.ts:89-137: single-file
- * [dir, name], multi-file [dir, ...path]).  Every file segment of a shard is staged by tv_stage_file:
- * page-cache pages are DMA'd to HBM directly when the file is warm, read by parallel preads when it is
- * cold.  A missing or short file (TV_ERR_IO) makes the pieces it touches 0, like fsStorage.get
- * returning null (storage.ts:163-171); unlike fsStorage.get, no missing file is created.  Same
- * behaviour as torrent_amd.verify_files.
+ * [dir, name], multi-file [dir, ...path]).  All file segments of a shard go to tv_stage_files in one
+ * call: long segments are DMA'd to HBM from the page cache when the file is warm (parallel preads when
+ * cold); short ones (many small files) are read by the library's thread pool into pinned slots.
+ * A missing or short file (TV_ERR_IO) makes the pieces it touches 0, like fsStorage.get returning
+ * null (storage.ts:163-171); unlike fsStorage.get, no missing file is created.  Same behaviour as
+ * torrent_amd.verify_files.
  */
 export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptions = {}): Promise<Uint8Array> {
   const l = load(opts.libPath);
@@ -198,20 +204,36 @@ export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptio
       for (let j = count - 1; j >= 0 && (first + j) * L + pieceLength(first + j, info) > info.length; j--) clear(j, j);
       const lo = first * L;
       const hi = Math.min(info.length, (first + count - 1) * L + pieceLength(first + count - 1, info));
-      // findAndDo's walk over the files in order (storage.ts:105-128), restricted to [lo, hi)
+      // findAndDo's walk over the files in order (storage.ts:105-128), restricted to [lo, hi): every
+      // segment of the shard goes to the library in ONE tv_stage_files call
+      const segs: { path: Uint8Array; fileOffset: number; linear: number; len: number }[] = [];
       let fileStart = 0;
       for (const f of files) {
         const fileEnd = fileStart + f.length;
         const a = Math.max(lo, fileStart);
         const b = Math.min(hi, fileEnd);
-        if (b > a) {
-          const path = new TextEncoder().encode(f.path + "\0");
-          const rc = await l.symbols.tv_stage_file(ctx, ptr(path), BigInt(a - fileStart), BigInt(a), BigInt(b - a));
-          if (rc === TV_ERR_IO) clear(Math.floor((a - lo) / L), Math.floor((b - 1 - lo) / L));
-          else check(l, ctx, rc);
-        }
+        if (b > a) segs.push({ path: new TextEncoder().encode(f.path + "\0"), fileOffset: a - fileStart, linear: a, len: b - a });
         fileStart = fileEnd;
         if (fileStart >= hi) break;
+      }
+      if (segs.length) {
+        const n = segs.length;
+        const paths = new BigUint64Array(n);
+        const fo = new BigUint64Array(n), lin = new BigUint64Array(n), len = new BigUint64Array(n);
+        segs.forEach((sg, k) => {
+          paths[k] = BigInt(Deno.UnsafePointer.value(Deno.UnsafePointer.of(sg.path)));
+          fo[k] = BigInt(sg.fileOffset);
+          lin[k] = BigInt(sg.linear);
+          len[k] = BigInt(sg.len);
+        });
+        const status = new Int32Array(n);
+        const u8 = (a: ArrayBufferView) => new Uint8Array(a.buffer, a.byteOffset, a.byteLength);
+        check(l, ctx, await l.symbols.tv_stage_files(ctx, BigInt(n), ptr(u8(paths)), ptr(u8(fo)), ptr(u8(lin)),
+                                                     ptr(u8(len)), ptr(u8(status))));
+        // `segs` (the path strings) stays referenced until here, after the nonblocking call settled
+        segs.forEach((sg, k) => {
+          if (status[k] === TV_ERR_IO) clear(Math.floor((sg.linear - lo) / L), Math.floor((sg.linear + sg.len - 1 - lo) / L));
+        });
       }
       const out = new Uint8Array(Math.ceil(count / 8));
       check(l, ctx, await l.symbols.tv_verify(ctx, ptr(avail), ptr(out)));
