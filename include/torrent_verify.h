@@ -96,7 +96,8 @@ int tv_stage(tv_ctx *ctx, uint64_t linear_offset, const uint8_t *src, uint64_t l
  * fsStorage.get reads it (storage.ts:150-172: open, seek, read).  The file is processed in windows of
  * TV_OPT_FILE_CHUNK bytes.  A window whose pages are mostly in the page cache (mincore) is mapped, its
  * pages registered read-only and DMA'd straight to HBM, with no host copy.  A window mostly on disk is
- * read by parallel preads (8 MiB requests, 8 in flight) into the pinned ring and DMA'd from there.
+ * read by parallel preads (4 MiB requests, TV_OPT_FILE_THREADS in flight) into the pinned ring and
+ * DMA'd from there.
  * TV_OPT_FILE_DIRECT = 0 forces the second form.  Either way, window k+1 is read while window k
  * copies.  Bytes outside the shard are skipped.  A missing or short file returns TV_ERR_IO before
  * anything is staged (a read error part-way also returns TV_ERR_IO): the host marks the pieces the

@@ -405,12 +405,13 @@ double resident_fraction(void* m, uint64_t n, uint64_t page) {
     return vec.empty() ? 1.0 : (double)r / (double)vec.size();
 }
 
-// Read file bytes [fo, fo + n) into dst with parallel preads (8 MiB parts on up to 8 threads: a cold
-// file is read with many large requests in flight).  Returns 0 or an errno value (EIO for a short read).
-int pread_parallel(int fd, uint8_t* dst, uint64_t fo, uint64_t n) {
-    const uint64_t part = 8ull << 20;
+// Read file bytes [fo, fo + n) into dst with parallel preads (4 MiB parts on up to max_threads threads,
+// TV_OPT_FILE_THREADS: a cold file is read with many large requests in flight).  Returns 0 or an
+// errno value (EIO for a short read).
+int pread_parallel(int fd, uint8_t* dst, uint64_t fo, uint64_t n, int max_threads) {
+    const uint64_t part = 4ull << 20;
     const uint64_t nparts = (n + part - 1) / part;
-    const int threads = (int)std::min<uint64_t>(8, nparts);
+    const int threads = (int)std::min<uint64_t>((uint64_t)std::max(1, max_threads), nparts);
     std::vector<int> err(threads, 0);
     auto work = [&](int t) {
         for (uint64_t q = t; q < nparts; q += threads) {
@@ -738,7 +739,7 @@ int stage_file_locked(tv_ctx* c, const char* path, uint64_t file_offset, uint64_
                 rc = take_slot(c, &slot);
                 if (rc) return rc;
                 uint8_t* at = c->ring[slot] + ((p + q) & 3);  // at the resident bytes' alignment mod 4
-                const int e = pread_parallel(win.fd, at, fo + q, kq);
+                const int e = pread_parallel(win.fd, at, fo + q, kq, c->file_threads);
                 if (e) return fail(c, TV_ERR_IO, "read %s at %llu: %s", path, (unsigned long long)(fo + q), strerror(e));
                 rc = stage_range(c, p + q, p + q + kq, at, p + q, true);
                 if (rc) return rc;
