@@ -35,7 +35,12 @@ def test_hash_lengths_all_tail_cases(native, oracle, kernel):
 
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("L,P,last", [(4096, 300, 4096), (4096, 300, 1), (16384, 129, 9000),
-                                      (65536, 64, 65536 - 9), (1 << 20, 70, 123457), (64, 1000, 55)])
+                                      (65536, 64, 65536 - 9), (1 << 20, 70, 123457), (64, 1000, 55),
+                                      # the short last piece's dedicated group at every boundary: alone
+                                      # (no main group), right after a full wave / split workgroup /
+                                      # 256-thread lane workgroup, and sharing an output word
+                                      (16384, 1, 1000), (4096, 2, 17), (4096, 65, 100), (4096, 129, 4095),
+                                      (4096, 257, 3), (4096, 200, 2048)])
 def test_verify_matches_oracle(native, oracle, kernel, L, P, last):
     total = L * (P - 1) + last
     payload = oracle.synth_fill(L + P, 0, total)
