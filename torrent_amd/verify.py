@@ -121,9 +121,11 @@ def _run_shards(devs: List[int], n_pieces: int, fn):
         return ranges, [f.result() for f in futs]
 
 
-def verify_pieces(info: InfoDict, storage, devices=None) -> bytearray:
+def verify_pieces(info: InfoDict, storage, devices=None, threads: int = 16) -> bytearray:
     """verifyPieces(info, storage): have-bitfield of every piece read through `storage`
-    (a torrent_amd.storage.Storage, i.e. the reference's Storage over any StorageMethod)."""
+    (a torrent_amd.storage.Storage, i.e. the reference's Storage over any StorageMethod).  The gets
+    of a batch are in flight together on `threads` threads, as ts/verify.ts keeps them outstanding
+    with Promise.all (make_torrent.ts:96,111 does the same); threads=1 reads them one by one."""
     P, L = info.n_pieces, info.piece_length
 
     def shard(ctx, first: int, count: int) -> bytes:
@@ -131,23 +133,25 @@ def verify_pieces(info: InfoDict, storage, devices=None) -> bytearray:
         ctx.set_digests(info.pieces_raw)
         avail = bytearray((count + 7) // 8)
         per_batch = max(1, _STAGE_BATCH_BYTES // max(1, L))
-        j = 0
-        while j < count:
-            k = min(per_batch, count - j)
-            buf = bytearray(k * L)
-            hi = 0
-            for q in range(k):
-                i = first + j + q
-                n = piece_length(i, info)
-                data = storage.get(i * L, n)  # storage.ts:50-65; None => unreadable => bit 0
-                if data is None:
-                    continue
-                buf[q * L:q * L + n] = data
-                hi = q * L + n
-                _set_bit(avail, j + q)
-            if hi:
-                ctx.stage((first + j) * L, memoryview(buf)[:hi])
-            j += k
+
+        def get(i: int):
+            return storage.get(i * L, piece_length(i, info))  # storage.ts:50-65; None => bit 0
+
+        with ThreadPoolExecutor(max(1, threads)) as pool:
+            j = 0
+            while j < count:
+                k = min(per_batch, count - j)
+                buf = bytearray(k * L)
+                hi = 0
+                for q, data in enumerate(pool.map(get, range(first + j, first + j + k))):
+                    if data is None:
+                        continue
+                    buf[q * L:q * L + len(data)] = data
+                    hi = q * L + len(data)
+                    _set_bit(avail, j + q)
+                if hi:
+                    ctx.stage((first + j) * L, memoryview(buf)[:hi])
+                j += k
         return ctx.verify(avail)
 
     if P == 0:
