@@ -385,6 +385,33 @@ def test_stage_file_windows_offsets_and_failures(native, oracle, tmp_path, direc
         assert out[8 * L:8 * L + 500] == b"\x01" * 500 and out[8 * L + 500:] == payload[8 * L + 500:]
 
 
+@pytest.mark.parametrize("direct_min", [1 << 62, 0])
+def test_stage_files_long_unaligned_and_gapped(native, oracle, tmp_path, direct_min):
+    """tv_stage_files edge cases, read back byte for byte: a 150 MiB segment (longer than a 64 MiB
+    staging slot: split into slot parts and 4 MiB read parts) at a file offset of 3 (never congruent
+    with its linear offset mod 4), segments given out of linear order with a gap between them, one
+    reaching past the shard's end, a zero-length one for a missing file, and a directory (TV_ERR_IO).
+    direct_min = 2^62: all through the reader pool; 0: all through the tv_stage_file path."""
+    L, P = 1 << 20, 160
+    total = L * P
+    payload = oracle.synth_fill(91, 0, total)
+    (tmp_path / "big.bin").write_bytes(b"xyz" + bytes(payload[:150 * L]))
+    (tmp_path / "tail.bin").write_bytes(bytes(payload[150 * L + 5:]))
+    (tmp_path / "dir").mkdir()
+    with native.Context(0) as ctx:
+        ctx.set_option(native.TV_OPT_FILE_DIRECT_MIN, direct_min)
+        ctx.set_layout(total, L, P, 0, 152)                 # shard: pieces [0, 152)
+        st = ctx.stage_files([str(tmp_path / "tail.bin"), str(tmp_path / "big.bin"),
+                              str(tmp_path / "missing.bin"), str(tmp_path / "dir")],
+                             [0, 3, 0, 0], [150 * L + 5, 0, 17, 150 * L], [total - 150 * L - 5, 150 * L, 0, 5])
+        assert st == [0, 0, 0, native.TV_ERR_IO]
+        out = bytearray(total)
+        ctx.read(0, out)
+    assert out[:150 * L] == payload[:150 * L]               # the long segment
+    assert out[150 * L + 5:152 * L] == payload[150 * L + 5:152 * L]   # clipped at the shard's end
+    assert not (tmp_path / "missing.bin").exists()
+
+
 def test_verify_files_reference_singlefile(native, tmp_path):
     from torrent_amd import parse_metainfo, verify_files
     info = parse_metainfo(_load("singlefile.torrent")).info
