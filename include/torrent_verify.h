@@ -85,7 +85,9 @@ int tv_set_digests(tv_ctx *ctx, const uint8_t *pieces, uint64_t pieces_len);
  * Copy `len` payload bytes at LINEAR torrent offset `linear_offset` (the concatenation of the
  * files in info.files order, storage.ts:89-137) into the resident payload.  Bytes outside the
  * shard are ignored.  The copy goes through the library's pinned staging ring and is complete
- * when the call returns.  Replaces: fsStorage.get reads feeding Storage.get (storage.ts:150-172).
+ * when the call returns.  Pageable memory is copied into the ring by TV_OPT_FILE_THREADS threads; a
+ * page-locked source (tv_host_alloc / tv_host_register) is DMA'd directly.  Replaces: fsStorage.get
+ * reads feeding Storage.get (storage.ts:150-172).
  */
 int tv_stage(tv_ctx *ctx, uint64_t linear_offset, const uint8_t *src, uint64_t len);
 
@@ -180,7 +182,8 @@ int tv_host_unregister(void *ptr);
 #define TV_OPT_FILE_DIRECT 5  /* tv_stage_file: 1 (default) = warm windows DMA'd from registered page-cache pages, 0 = all via the pinned ring */
 #define TV_OPT_FILE_CHUNK 6   /* tv_stage_file: bytes per mapped file window (default 256 MiB, >= 64 KiB) */
 #define TV_OPT_FILE_DIRECT_MIN 7 /* tv_stage_files: segment length that takes the tv_stage_file path (default 32 MiB) */
-#define TV_OPT_FILE_THREADS 8    /* tv_stage_files: reader threads for short segments (default 16) */
+#define TV_OPT_FILE_THREADS 8    /* host threads (default 16): tv_stage_files' readers, and the copies of pageable
+                                    tv_stage sources into the pinned ring (25.8 -> 55.8 GB/s) */
 int tv_set_option(tv_ctx *ctx, int key, int64_t value);
 int tv_get_option(tv_ctx *ctx, int key, int64_t *value);
 

@@ -257,6 +257,29 @@ int finish_timing(tv_ctx* c) {
 // Stage one contiguous range of LINEAR bytes that lies inside a single piece or covers whole
 // pieces; src is host memory.  Rows of whole pieces use one 2D copy (src pitch L, dst pitch stride).
 // A page-locked src is read by DMA directly; pageable memory is copied through the pinned ring.
+// Host memcpy into a pinned ring slot, split over up to `threads` threads in 4 MiB parts when it is
+// long (one core copies pageable memory at well under the PCIe rate).
+void copy_into_ring(uint8_t* dst, const uint8_t* src, uint64_t n, int threads) {
+    constexpr uint64_t kPart = 4ull << 20;
+    const uint64_t parts = (n + kPart - 1) / kPart;
+    const int t = (int)std::min<uint64_t>((uint64_t)std::max(1, threads), parts);
+    if (t <= 1) {
+        memcpy(dst, src, n);
+        return;
+    }
+    std::atomic<uint64_t> next{0};
+    auto work = [&]() {
+        for (uint64_t q = next++; q < parts; q = next++) {
+            const uint64_t o = q * kPart;
+            memcpy(dst + o, src + o, std::min(kPart, n - o));
+        }
+    };
+    std::vector<std::thread> th;
+    for (int i = 1; i < t; i++) th.emplace_back(work);
+    work();
+    for (auto& x : th) x.join();
+}
+
 // One host -> device copy on the copy stream, dword-aligned.  The DMA engine moves 1-byte-aligned
 // data ~10x slower than dword-aligned data (57 vs 5.7 GB/s, tools/dma_align_probe.py): when src and
 // dst agree mod 4, the 0-3 byte head and tail go as separate tiny copies and the body is aligned.
@@ -298,7 +321,7 @@ int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n, bool pin
             k = std::min<uint64_t>(k, (last_full > i) ? last_full - i : 1);
             bytes = k * c->L;
             const uint8_t* from = via_ring ? c->ring[slot] : src;
-            if (via_ring) memcpy(c->ring[slot], src, bytes);
+            if (via_ring) copy_into_ring(c->ring[slot], src, bytes, c->file_threads);
             TV_HIP(c, hipMemcpy2DAsync(dst, c->stride, from, c->L, c->L, k, hipMemcpyHostToDevice, c->copy_stream));
         } else {
             bytes = std::min<uint64_t>({n, plen > within ? plen - within : 0, cap});
@@ -307,7 +330,7 @@ int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n, bool pin
             const uint8_t* from = src;
             if (via_ring) {  // place the bytes at the destination's alignment inside the slot
                 uint8_t* r = c->ring[slot] + ((uintptr_t)dst & 3);
-                memcpy(r, src, bytes);
+                copy_into_ring(r, src, bytes, c->file_threads);
                 from = r;
             }
             int rc = dma_h2d(c, dst, from, bytes);
