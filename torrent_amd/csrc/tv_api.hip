@@ -280,6 +280,22 @@ void copy_into_ring(uint8_t* dst, const uint8_t* src, uint64_t n, int threads) {
     for (auto& x : th) x.join();
 }
 
+// Gather k rows of `width` bytes at pitch `pitch` from src into dst (packed), on up to `threads` threads.
+void gather_rows(uint8_t* dst, const uint8_t* src, uint64_t width, uint64_t pitch, uint64_t k, int threads) {
+    const uint64_t per = std::max<uint64_t>(1, (4ull << 20) / std::max<uint64_t>(1, width));  // rows per task
+    const uint64_t tasks = (k + per - 1) / per;
+    const int t = (int)std::min<uint64_t>((uint64_t)std::max(1, threads), tasks);
+    std::atomic<uint64_t> next{0};
+    auto work = [&]() {
+        for (uint64_t q = next++; q < tasks; q = next++)
+            for (uint64_t r = q * per; r < std::min(k, (q + 1) * per); r++) memcpy(dst + r * width, src + r * pitch, width);
+    };
+    std::vector<std::thread> th;
+    for (int i = 1; i < t; i++) th.emplace_back(work);
+    work();
+    for (auto& x : th) x.join();
+}
+
 // One host -> device copy on the copy stream, dword-aligned.  The DMA engine moves 1-byte-aligned
 // data ~10x slower than dword-aligned data (57 vs 5.7 GB/s, tools/dma_align_probe.py): when src and
 // dst agree mod 4, the 0-3 byte head and tail go as separate tiny copies and the body is aligned.
@@ -1175,7 +1191,7 @@ int tv_verify_host(tv_ctx* c, const uint8_t* src, uint64_t src_len, const uint8_
                 rc = take_slot(c, &slot);
                 if (rc) return rc;
                 const uint64_t k = std::min<uint64_t>(full_rows - r, std::max<uint64_t>(1, kRingSlotBytes / width));
-                for (uint64_t q = 0; q < k; q++) memcpy(c->ring[slot] + q * width, src + (r + q) * c->L + off, width);
+                gather_rows(c->ring[slot], src + r * c->L + off, width, c->L, k, c->file_threads);
                 TV_HIP(c, hipMemcpy2DAsync(c->d_chunk[buf] + r * row, row, c->ring[slot], width, width, k,
                                            hipMemcpyHostToDevice, c->copy_stream));
                 TV_HIP(c, hipEventRecord(c->ring_ev[slot], c->copy_stream));
