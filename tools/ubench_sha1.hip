@@ -1,6 +1,8 @@
 // tools/ubench_sha1.hip -- throughput of the generated SHA-1 compression (no memory traffic) at
 // 1/2/4/8 waves per SIMD: separates the VALU-mix / issue limit from memory and clock effects.
-// Build: hipcc --offload-arch=gfx950 -O3 -I torrent_amd/csrc tools/ubench_sha1.hip -o /tmp/ubench_sha1
+// Build: hipcc --offload-arch=gfx950 -O3 -I torrent_amd/csrc tools/ubench_sha1.hip -o tools/ubench_sha1_bin
+// "SIMD cycles per compression" (event time x clock / compressions per SIMD) is the number to read;
+// 8 waves per SIMD = two 1024-thread blocks per CU.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
@@ -26,8 +28,8 @@ int main() {
     hipMalloc(&out, 4 << 22); hipMalloc(&clk, 8 * 4096);
     const int iters = 2000;
     for (int wps : {1, 2, 4, 8}) {
-        const int threads = 64 * 4 * wps;  // one block per CU: wps waves on each of the 4 SIMDs
-        const int blocks = 256;
+        const int threads = 64 * 4 * (wps > 4 ? 4 : wps);  // wps waves on each of the 4 SIMDs
+        const int blocks = 256 * (wps > 4 ? wps / 4 : 1);
         hipLaunchKernelGGL(kfull, dim3(blocks), dim3(threads), 0, 0, out, 50, clk);
         hipDeviceSynchronize();
         hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
@@ -39,7 +41,8 @@ int main() {
         const double ghz = (double)c[0] / ((double)c[1] / 100e6) / 1e9;  // memtime cycles / realtime(100 MHz)
         const double lanes = (double)blocks * threads;
         const double gbps = lanes * iters * 64.0 / (ms / 1e3) / 1e9;
-        const double instr_per_simd = (double)iters * 597 * wps;  // ~597 VALU per compression incl. feed-forward
+        const double instr_per_simd = (double)iters * 597 * wps;
+        printf("  SIMD cycles per compression (event time x clock): %.0f\n", ms * 1e-3 * ghz * 1e9 / (iters * (double)wps));  // ~597 VALU per compression incl. feed-forward
         printf("waves/SIMD=%d  %.3f ms  clock %.2f GHz  %.1f GB/s-equiv  %.2f cycles/VALU per SIMD  %.2f cycles/VALU per wave\n",
                wps, ms, ghz, gbps, (double)c[0] / instr_per_simd, (double)c[0] / (iters * 597.0));
     }
