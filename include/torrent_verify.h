@@ -113,7 +113,9 @@ int tv_stage_file(tv_ctx *ctx, const char *path, uint64_t file_offset, uint64_t 
  * Stage MANY file segments in one call: a shard's whole Storage.get mapping (storage.ts:89-137), each
  * segment read as fsStorage.get reads it (storage.ts:150-172).  Segment k is `lens[k]` bytes of file
  * `paths[k]` from byte `file_offsets[k]`, staged as LINEAR bytes [linear_offsets[k], +lens[k]).
- *   - Segments of >= TV_OPT_FILE_DIRECT_MIN bytes (default 32 MiB) take the tv_stage_file path.
+ *   - Segments of >= TV_OPT_FILE_DIRECT_MIN bytes (default 32 MiB) take the tv_stage_file path. With
+ *     TV_OPT_FILE_CONCURRENT (default 1) they are split by bytes between two staging lanes (a helper
+ *     thread with its own copy stream and pinned ring, and the calling thread), which DMA side by side.
  *   - Shorter ones are packed into the pinned ring's 64 MiB slots. TV_OPT_FILE_THREADS threads read
  *     them (open, pread, close; default 16), and each run of linear-contiguous segments is one DMA.
  *     A slot's DMA overlaps the reads of the next slot. This is the many-small-files case: a
@@ -184,6 +186,7 @@ int tv_host_unregister(void *ptr);
 #define TV_OPT_FILE_DIRECT_MIN 7 /* tv_stage_files: segment length that takes the tv_stage_file path (default 32 MiB) */
 #define TV_OPT_FILE_THREADS 8    /* host threads (default 16): tv_stage_files' readers, and the copies of pageable
                                     tv_stage sources into the pinned ring (25.8 -> 55.8 GB/s) */
+#define TV_OPT_FILE_CONCURRENT 9 /* tv_stage_files: 1 (default) = long segments on two staging lanes, 0 = one */
 int tv_set_option(tv_ctx *ctx, int key, int64_t value);
 int tv_get_option(tv_ctx *ctx, int key, int64_t *value);
 

@@ -385,13 +385,16 @@ def test_stage_file_windows_offsets_and_failures(native, oracle, tmp_path, direc
         assert out[8 * L:8 * L + 500] == b"\x01" * 500 and out[8 * L + 500:] == payload[8 * L + 500:]
 
 
+@pytest.mark.parametrize("concurrent", [1, 0])
 @pytest.mark.parametrize("direct_min", [1 << 62, 0])
-def test_stage_files_long_unaligned_and_gapped(native, oracle, tmp_path, direct_min):
+def test_stage_files_long_unaligned_and_gapped(native, oracle, tmp_path, direct_min, concurrent):
     """tv_stage_files edge cases, read back byte for byte: a 150 MiB segment (longer than a 64 MiB
     staging slot: split into slot parts and 4 MiB read parts) at a file offset of 3 (never congruent
     with its linear offset mod 4), segments given out of linear order with a gap between them, one
     reaching past the shard's end, a zero-length one for a missing file, and a directory (TV_ERR_IO).
-    direct_min = 2^62: all through the reader pool; 0: all through the tv_stage_file path."""
+    direct_min = 2^62: all through the reader pool; 0: all through the tv_stage_file path (with
+    TV_OPT_FILE_CONCURRENT the 150 MiB segment on the calling thread's lane, the others - the
+    directory's TV_ERR_IO among them - on the helper's)."""
     L, P = 1 << 20, 160
     total = L * P
     payload = oracle.synth_fill(91, 0, total)
@@ -400,6 +403,8 @@ def test_stage_files_long_unaligned_and_gapped(native, oracle, tmp_path, direct_
     (tmp_path / "dir").mkdir()
     with native.Context(0) as ctx:
         ctx.set_option(native.TV_OPT_FILE_DIRECT_MIN, direct_min)
+        ctx.set_option(native.TV_OPT_FILE_CONCURRENT, concurrent)
+        assert ctx.get_option(native.TV_OPT_FILE_CONCURRENT) == concurrent
         ctx.set_layout(total, L, P, 0, 152)                 # shard: pieces [0, 152)
         st = ctx.stage_files([str(tmp_path / "tail.bin"), str(tmp_path / "big.bin"),
                               str(tmp_path / "missing.bin"), str(tmp_path / "dir")],
@@ -410,6 +415,48 @@ def test_stage_files_long_unaligned_and_gapped(native, oracle, tmp_path, direct_
     assert out[:150 * L] == payload[:150 * L]               # the long segment
     assert out[150 * L + 5:152 * L] == payload[150 * L + 5:152 * L]   # clipped at the shard's end
     assert not (tmp_path / "missing.bin").exists()
+
+
+@pytest.mark.parametrize("direct", [1, 0])
+def test_stage_files_two_lanes_many_segments(native, oracle, tmp_path, direct):
+    """Two staging lanes under load: 40 files of ragged sizes at file offsets 0-3 (so the lanes' copies
+    are aligned, head/tail split or routed through each lane's own ring), an odd piece length (no
+    whole-piece row is dword-aligned), 64 KiB windows, half the segments long enough for the
+    tv_stage_file path, staged in one call with and without TV_OPT_FILE_CONCURRENT; every byte read
+    back and the verify bitfield all ones."""
+    import random
+    rnd = random.Random(5)
+    L, P = 65539, 700
+    total = L * P - 1234
+    payload = oracle.synth_fill(17, 0, total)
+    cuts = sorted(rnd.sample(range(1, total), 39))
+    bounds = [0] + cuts + [total]
+    paths, fos, lins, lens = [], [], [], []
+    for k in range(40):
+        a, b = bounds[k], bounds[k + 1]
+        pre = rnd.randrange(4)
+        path = tmp_path / f"s{k:02d}.bin"
+        path.write_bytes(bytes(pre) + bytes(payload[a:b]))
+        paths.append(str(path)); fos.append(pre); lins.append(a); lens.append(b - a)
+    order = list(range(40))
+    rnd.shuffle(order)
+    with native.Context(0) as ctx:
+        ctx.set_option(native.TV_OPT_FILE_DIRECT, direct)
+        ctx.set_option(native.TV_OPT_FILE_CHUNK, 64 << 10)
+        ctx.set_option(native.TV_OPT_FILE_DIRECT_MIN, sorted(lens)[20])
+        ctx.set_layout(total, L, P)
+        ctx.set_digests(oracle.hash_pieces(payload, total, L, P))
+        for conc in (1, 0):
+            ctx.set_option(native.TV_OPT_FILE_CONCURRENT, conc)
+            ctx.fill_synthetic(99)                                  # overwrite what the last round staged
+            st = ctx.stage_files([paths[k] for k in order], [fos[k] for k in order],
+                                 [lins[k] for k in order], [lens[k] for k in order])
+            assert st == [0] * 40
+            out = bytearray(total)
+            ctx.read(0, out)
+            assert out == payload, conc
+            bf = ctx.verify()
+            assert all(bf[i >> 3] >> (7 - (i & 7)) & 1 for i in range(P)), conc
 
 
 def test_verify_files_reference_singlefile(native, tmp_path):

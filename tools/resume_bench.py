@@ -4,13 +4,18 @@ direct (the tv_stage_file path: page-cache pages DMA'd to HBM) and the reader po
 pread into pinned slots, then DMA).  Each
 is timed with the page cache warm (the files were just written) and cold (posix_fadvise DONTNEED
 after fsync, so the reads go to the box's disk).
-usage: python tools/resume_bench.py <dir> <GiB> [n_files]"""
+With --lanes-ab: only the warm direct case, one staging lane against two (TV_OPT_FILE_CONCURRENT on
+the cached context), interleaved over 6 rounds.
+usage: python tools/resume_bench.py <dir> <GiB> [n_files] [--warm-only|--pread-first|--lanes-ab]"""
 import os
 import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import statistics  # noqa: E402
+
 from torrent_amd import _native, make_info, FileInfo, verify_files  # noqa: E402
+from torrent_amd.verify import _context  # noqa: E402
 
 d, gib = sys.argv[1], float(sys.argv[2])
 nf = int(sys.argv[3]) if len(sys.argv) > 3 and not sys.argv[3].startswith("-") else 64
@@ -57,6 +62,22 @@ def exact(bf):
 
 cwd = os.getcwd()
 os.chdir(d)
+if "--lanes-ab" in sys.argv:
+    res = {1: [], 2: []}
+    for rnd in range(6):
+        for lanes in (2, 1):
+            with _context(0) as c:
+                c.set_option(_native.TV_OPT_FILE_CONCURRENT, lanes - 1)
+            t0 = time.perf_counter()
+            bf = verify_files(info, d, threads=16)
+            el = time.perf_counter() - t0
+            assert exact(bf)
+            res[lanes].append(total / el / 1e9)
+    for lanes, v in res.items():
+        print(f"resume_from_disk: {total / 2**30:.1f} GiB in {nf} files, page cache warm, direct, {lanes} staging "
+              f"lane(s): median {statistics.median(v):.2f} GB/s, best {max(v):.2f}  all {[round(x, 1) for x in v]}",
+              flush=True)
+    sys.exit(0)
 modes = [("direct (tv_stage_file path: page-cache DMA)", None), ("reader pool (preads -> pinned slots -> DMA)", 1 << 62)]
 if "--pread-first" in sys.argv:
     modes = modes[::-1] + modes[1:]

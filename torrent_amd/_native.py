@@ -28,6 +28,7 @@ TV_OPT_FILE_DIRECT = 5
 TV_OPT_FILE_CHUNK = 6
 TV_OPT_FILE_DIRECT_MIN = 7
 TV_OPT_FILE_THREADS = 8
+TV_OPT_FILE_CONCURRENT = 9
 
 KERNEL_AUTO, KERNEL_LANE, KERNEL_SPLIT = 0, 1, 2
 

@@ -40,6 +40,7 @@ struct tv_ctx {
 
     hipStream_t stream = nullptr;       // kernels
     hipStream_t copy_stream = nullptr;  // H2D staging
+    hipStream_t copy_stream2 = nullptr; // H2D staging of the second lane (tv_stage_files' long segments)
     hipEvent_t ev_call0 = nullptr, ev_k0 = nullptr, ev_k1 = nullptr, ev_call1 = nullptr;
 
     // geometry
@@ -53,6 +54,7 @@ struct tv_ctx {
     int split_pairs = 0;        // 0 = automatic
     uint64_t file_chunk = 256ull << 20;  // tv_stage_file: bytes per mapped window
     bool file_direct = true;             // tv_stage_file: DMA from registered page-cache pages
+    bool file_concurrent = true;         // tv_stage_files: long segments beside the reader pool
     uint64_t file_direct_min = 32ull << 20;  // tv_stage_files: segments >= this take the tv_stage_file path
     int file_threads = 16;                   // tv_stage_files: reader threads
 
@@ -81,6 +83,11 @@ struct tv_ctx {
     uint8_t* ring[kRingSlots] = {nullptr, nullptr, nullptr};
     hipEvent_t ring_ev[kRingSlots] = {nullptr, nullptr, nullptr};
     int ring_next = 0;
+    // lane 1 (copy_stream2 + ring2): tv_stage_files runs its long segments on it beside the reader pool
+    uint8_t* ring2[kRingSlots] = {nullptr, nullptr, nullptr};
+    hipEvent_t ring2_ev[kRingSlots] = {nullptr, nullptr, nullptr};
+    int ring2_next = 0;
+    std::mutex err_mu;                // fail() may run on a tv_stage_files helper thread
     uint8_t* h_bits = nullptr;        // pinned bitfield bounce buffer
     size_t h_bits_cap = 0;
 
@@ -97,7 +104,10 @@ int fail(tv_ctx* c, int code, const char* fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(buf, sizeof buf, fmt, ap);
     va_end(ap);
-    if (c) c->err = buf;
+    if (c) {
+        std::lock_guard<std::mutex> g(c->err_mu);
+        c->err = buf;
+    }
     g_thread_error = buf;
     return code;
 }
@@ -135,10 +145,24 @@ void free_device(tv_ctx* c) {
     c->list_cap = 0;
 }
 
-int ensure_ring(tv_ctx* c) {
+// Staging lane `which`: 0 = copy_stream + ring, 1 = copy_stream2 + ring2.  Lane 1 is used only by
+// tv_stage_files' helper thread, so the two lanes never share a ring slot or a stream.
+struct RingRef {
+    uint8_t** buf;
+    hipEvent_t* ev;
+    int* next;
+};
+RingRef ring_ref(tv_ctx* c, int which) {
+    return which ? RingRef{c->ring2, c->ring2_ev, &c->ring2_next} : RingRef{c->ring, c->ring_ev, &c->ring_next};
+}
+
+hipStream_t lane_stream(const tv_ctx* c, int which) { return which ? c->copy_stream2 : c->copy_stream; }
+
+int ensure_ring(tv_ctx* c, int which = 0) {
+    RingRef r = ring_ref(c, which);
     for (int s = 0; s < kRingSlots; s++) {
-        if (!c->ring[s]) TV_HIP(c, hipHostMalloc((void**)&c->ring[s], kRingSlotBytes, hipHostMallocDefault));
-        if (!c->ring_ev[s]) TV_HIP(c, hipEventCreateWithFlags(&c->ring_ev[s], hipEventDisableTiming));
+        if (!r.buf[s]) TV_HIP(c, hipHostMalloc((void**)&r.buf[s], kRingSlotBytes, hipHostMallocDefault));
+        if (!r.ev[s]) TV_HIP(c, hipEventCreateWithFlags(&r.ev[s], hipEventDisableTiming));
     }
     return TV_OK;
 }
@@ -154,12 +178,13 @@ int ensure_hbits(tv_ctx* c, size_t bytes) {
 }
 
 // Take the next pinned ring slot (waiting for its previous copy to finish).
-int take_slot(tv_ctx* c, int* slot) {
-    int rc = ensure_ring(c);
+int take_slot(tv_ctx* c, int* slot, int which = 0) {
+    int rc = ensure_ring(c, which);
     if (rc) return rc;
-    int s = c->ring_next;
-    c->ring_next = (s + 1) % kRingSlots;
-    TV_HIP(c, hipEventSynchronize(c->ring_ev[s]));
+    RingRef r = ring_ref(c, which);
+    int s = *r.next;
+    *r.next = (s + 1) % kRingSlots;
+    TV_HIP(c, hipEventSynchronize(r.ev[s]));
     *slot = s;
     return TV_OK;
 }
@@ -299,21 +324,23 @@ void gather_rows(uint8_t* dst, const uint8_t* src, uint64_t width, uint64_t pitc
 // One host -> device copy on the copy stream, dword-aligned.  The DMA engine moves 1-byte-aligned
 // data ~10x slower than dword-aligned data (57 vs 5.7 GB/s, tools/dma_align_probe.py): when src and
 // dst agree mod 4, the 0-3 byte head and tail go as separate tiny copies and the body is aligned.
-int dma_h2d(tv_ctx* c, uint8_t* dst, const uint8_t* src, uint64_t n) {
+int dma_h2d(tv_ctx* c, uint8_t* dst, const uint8_t* src, uint64_t n, int lane = 0) {
+    hipStream_t cs = lane_stream(c, lane);
     const uint64_t mis = (uintptr_t)dst & 3;
     if (n >= 64 && mis == ((uintptr_t)src & 3) && (mis || (n & 3))) {
         const uint64_t head = (4 - mis) & 3, body = (n - head) & ~3ull, tail = n - head - body;
-        if (head) TV_HIP(c, hipMemcpyAsync(dst, src, head, hipMemcpyHostToDevice, c->copy_stream));
-        TV_HIP(c, hipMemcpyAsync(dst + head, src + head, body, hipMemcpyHostToDevice, c->copy_stream));
-        if (tail)
-            TV_HIP(c, hipMemcpyAsync(dst + head + body, src + head + body, tail, hipMemcpyHostToDevice, c->copy_stream));
+        if (head) TV_HIP(c, hipMemcpyAsync(dst, src, head, hipMemcpyHostToDevice, cs));
+        TV_HIP(c, hipMemcpyAsync(dst + head, src + head, body, hipMemcpyHostToDevice, cs));
+        if (tail) TV_HIP(c, hipMemcpyAsync(dst + head + body, src + head + body, tail, hipMemcpyHostToDevice, cs));
         return TV_OK;
     }
-    TV_HIP(c, hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->copy_stream));
+    TV_HIP(c, hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, cs));
     return TV_OK;
 }
 
-int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n, bool pinned) {
+int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n, bool pinned, int lane = 0) {
+    hipStream_t cs = lane_stream(c, lane);
+    RingRef ring = ring_ref(c, lane);
     while (n) {
         const uint64_t i = pos / c->L, within = pos % c->L;
         const uint64_t plen = piece_len(c, i);
@@ -326,7 +353,7 @@ int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n, bool pin
         const uint64_t cap = via_ring ? (uint64_t)kRingSlotBytes - 4 : UINT64_MAX;
         int slot = -1;
         if (via_ring) {
-            int rc = take_slot(c, &slot);
+            int rc = take_slot(c, &slot, lane);
             if (rc) return rc;
         }
         uint64_t bytes;
@@ -336,23 +363,23 @@ int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n, bool pin
             const uint64_t last_full = (c->total % c->L) ? c->P - 1 : c->P;  // first index that is not full
             k = std::min<uint64_t>(k, (last_full > i) ? last_full - i : 1);
             bytes = k * c->L;
-            const uint8_t* from = via_ring ? c->ring[slot] : src;
-            if (via_ring) copy_into_ring(c->ring[slot], src, bytes, c->file_threads);
-            TV_HIP(c, hipMemcpy2DAsync(dst, c->stride, from, c->L, c->L, k, hipMemcpyHostToDevice, c->copy_stream));
+            const uint8_t* from = via_ring ? ring.buf[slot] : src;
+            if (via_ring) copy_into_ring(ring.buf[slot], src, bytes, c->file_threads);
+            TV_HIP(c, hipMemcpy2DAsync(dst, c->stride, from, c->L, c->L, k, hipMemcpyHostToDevice, cs));
         } else {
             bytes = std::min<uint64_t>({n, plen > within ? plen - within : 0, cap});
             if (bytes == 0) return fail(c, TV_ERR_ARG, "stage offset %llu is past piece %llu", (unsigned long long)pos,
                                         (unsigned long long)i);
             const uint8_t* from = src;
             if (via_ring) {  // place the bytes at the destination's alignment inside the slot
-                uint8_t* r = c->ring[slot] + ((uintptr_t)dst & 3);
+                uint8_t* r = ring.buf[slot] + ((uintptr_t)dst & 3);
                 copy_into_ring(r, src, bytes, c->file_threads);
                 from = r;
             }
-            int rc = dma_h2d(c, dst, from, bytes);
+            int rc = dma_h2d(c, dst, from, bytes, lane);
             if (rc) return rc;
         }
-        if (via_ring) TV_HIP(c, hipEventRecord(c->ring_ev[slot], c->copy_stream));
+        if (via_ring) TV_HIP(c, hipEventRecord(ring.ev[slot], cs));
         pos += bytes;
         src += bytes;
         n -= bytes;
@@ -365,10 +392,11 @@ int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n, bool pin
 // the call's own events.
 struct DrainGuard {
     tv_ctx* c;
+    int lane;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    explicit DrainGuard(tv_ctx* ctx) : c(ctx) {}
+    explicit DrainGuard(tv_ctx* ctx, int copy_lane = 0) : c(ctx), lane(copy_lane) {}
     ~DrainGuard() {
-        (void)hipStreamSynchronize(c->copy_stream);
+        (void)hipStreamSynchronize(lane_stream(c, lane));
         (void)hipStreamSynchronize(c->stream);
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
@@ -398,7 +426,8 @@ void clip_to_shard(const tv_ctx* c, uint64_t off, uint64_t len, uint64_t* a, uin
 // Queue the copies of LINEAR bytes [a, b) (inside the shard) on the copy stream; byte `pos` is read
 // from base + (pos - base_off).  Pieces are split at piece boundaries (a piece is shorter than L only
 // at the end of the torrent, piece.ts:16-19); bytes in a short last piece's missing tail are skipped.
-int stage_range(tv_ctx* c, uint64_t a, uint64_t b, const uint8_t* base, uint64_t base_off, bool pinned) {
+int stage_range(tv_ctx* c, uint64_t a, uint64_t b, const uint8_t* base, uint64_t base_off, bool pinned,
+                int lane = 0) {
     uint64_t pos = a;
     while (pos < b) {
         const uint64_t i = pos / c->L, within = pos % c->L;
@@ -414,7 +443,7 @@ int stage_range(tv_ctx* c, uint64_t a, uint64_t b, const uint8_t* base, uint64_t
         } else {
             n = std::min(b - pos, plen - within);
         }
-        int rc = stage_copy(c, pos, base + (pos - base_off), n, pinned);
+        int rc = stage_copy(c, pos, base + (pos - base_off), n, pinned, lane);
         if (rc) return rc;
         pos += n;
     }
@@ -528,6 +557,7 @@ int tv_create(tv_ctx** out, int device) {
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy_stream2, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&c->ev_call0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev_k0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev_k1);
@@ -547,16 +577,20 @@ void tv_destroy(tv_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+    if (c->copy_stream2) (void)hipStreamSynchronize(c->copy_stream2);
     free_device(c);
     for (int s = 0; s < kRingSlots; s++) {
         if (c->ring[s]) (void)hipHostFree(c->ring[s]);
         if (c->ring_ev[s]) (void)hipEventDestroy(c->ring_ev[s]);
+        if (c->ring2[s]) (void)hipHostFree(c->ring2[s]);
+        if (c->ring2_ev[s]) (void)hipEventDestroy(c->ring2_ev[s]);
     }
     if (c->h_bits) (void)hipHostFree(c->h_bits);
     for (hipEvent_t ev : {c->ev_call0, c->ev_k0, c->ev_k1, c->ev_call1, c->ev_avail})
         if (ev) (void)hipEventDestroy(ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+    if (c->copy_stream2) (void)hipStreamDestroy(c->copy_stream2);
     delete c;
 }
 
@@ -607,6 +641,10 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
             if (value < 1 || value > 256) return fail(c, TV_ERR_ARG, "TV_OPT_FILE_THREADS must be 1 .. 256");
             c->file_threads = (int)value;
             return TV_OK;
+        case TV_OPT_FILE_CONCURRENT:
+            if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_FILE_CONCURRENT must be 0 or 1");
+            c->file_concurrent = value != 0;
+            return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
@@ -623,6 +661,7 @@ int tv_get_option(tv_ctx* c, int key, int64_t* value) {
         case TV_OPT_FILE_CHUNK: *value = (int64_t)c->file_chunk; return TV_OK;
         case TV_OPT_FILE_DIRECT_MIN: *value = (int64_t)c->file_direct_min; return TV_OK;
         case TV_OPT_FILE_THREADS: *value = c->file_threads; return TV_OK;
+        case TV_OPT_FILE_CONCURRENT: *value = c->file_concurrent ? 1 : 0; return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
@@ -722,7 +761,9 @@ int tv_stage(tv_ctx* c, uint64_t linear_offset, const uint8_t* src, uint64_t len
 namespace {
 
 // tv_stage_file with the context lock held and the arguments checked.
-int stage_file_locked(tv_ctx* c, const char* path, uint64_t file_offset, uint64_t linear_offset, uint64_t len) {
+int stage_file_locked(tv_ctx* c, const char* path, uint64_t file_offset, uint64_t linear_offset, uint64_t len,
+                      int lane = 0) {
+    hipStream_t cs = lane_stream(c, lane);
     int rc = TV_OK;
     if (len == 0) return TV_OK;  // a zero-length read succeeds without touching the file
     FileWindows win;  // before `drain`: destroyed after the streams are drained
@@ -738,7 +779,7 @@ int stage_file_locked(tv_ctx* c, const char* path, uint64_t file_offset, uint64_
     clip_to_shard(c, linear_offset, len, &a, &b);
     if (a >= b) return TV_OK;
     TV_HIP(c, hipSetDevice(c->device));
-    DrainGuard drain(c);
+    DrainGuard drain(c, lane);
     for (int k = 0; k < 2; k++) TV_HIP(c, hipEventCreateWithFlags(&drain.ev[k], hipEventDisableTiming));
     const uint64_t page = (uint64_t)sysconf(_SC_PAGESIZE);
     const uint64_t chunk = c->file_chunk;
@@ -767,7 +808,7 @@ int stage_file_locked(tv_ctx* c, const char* path, uint64_t file_offset, uint64_
             (void)hipGetLastError();
         }
         if (win.w[k].registered) {
-            rc = stage_range(c, p, p + n, (const uint8_t*)m + delta, p, true);
+            rc = stage_range(c, p, p + n, (const uint8_t*)m + delta, p, true, lane);
             if (rc) return rc;
         } else {
             // cold window (or direct DMA off / refused): parallel preads into the pinned ring, then DMA
@@ -775,19 +816,20 @@ int stage_file_locked(tv_ctx* c, const char* path, uint64_t file_offset, uint64_
             for (uint64_t q = 0; q < n; q += kRingSlotBytes - 4) {
                 const uint64_t kq = std::min<uint64_t>(kRingSlotBytes - 4, n - q);
                 int slot;
-                rc = take_slot(c, &slot);
+                rc = take_slot(c, &slot, lane);
                 if (rc) return rc;
-                uint8_t* at = c->ring[slot] + ((p + q) & 3);  // at the resident bytes' alignment mod 4
+                RingRef ring = ring_ref(c, lane);
+                uint8_t* at = ring.buf[slot] + ((p + q) & 3);  // at the resident bytes' alignment mod 4
                 const int e = pread_parallel(win.fd, at, fo + q, kq, c->file_threads);
                 if (e) return fail(c, TV_ERR_IO, "read %s at %llu: %s", path, (unsigned long long)(fo + q), strerror(e));
-                rc = stage_range(c, p + q, p + q + kq, at, p + q, true);
+                rc = stage_range(c, p + q, p + q + kq, at, p + q, true, lane);
                 if (rc) return rc;
-                TV_HIP(c, hipEventRecord(c->ring_ev[slot], c->copy_stream));
+                TV_HIP(c, hipEventRecord(ring.ev[slot], cs));
             }
         }
-        TV_HIP(c, hipEventRecord(drain.ev[k], c->copy_stream));
+        TV_HIP(c, hipEventRecord(drain.ev[k], cs));
     }
-    TV_HIP(c, hipStreamSynchronize(c->copy_stream));
+    TV_HIP(c, hipStreamSynchronize(cs));
     return TV_OK;
 }
 
@@ -873,23 +915,73 @@ int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64
     TV_HIP(c, hipSetDevice(c->device));
     // Long segments: the windowed page-cache path of tv_stage_file.  Short ones: packed into the pinned
     // ring's 64 MiB slots, read by the thread pool, DMA'd per run of linear-contiguous segments while the
-    // next slot is read.
+    // next slot is read.  With TV_OPT_FILE_CONCURRENT the long segments are split by bytes between a
+    // helper thread on staging lane 1 and this thread (lane 0, before the pool): each lane's copies
+    // queue on its own stream, so the two feed the DMA engines side by side.
     const uint64_t direct_min = c->file_direct_min;
+    struct LongSeg {
+        uint64_t k, fo, a, len;
+    };
+    std::vector<LongSeg> longs;
     std::vector<SmallSeg> small;
+    uint64_t small_bytes = 0;
     for (uint64_t k = 0; k < n; k++) {
         uint64_t a, b;
         clip_to_shard(c, linear_offsets[k], lens[k], &a, &b);
         if (a >= b) continue;  // nothing of this segment is resident here (zero-length reads succeed)
         const uint64_t fo = file_offsets[k] + (a - linear_offsets[k]);
         if (b - a >= direct_min) {
-            rc = stage_file_locked(c, paths[k], fo, a, b - a);
-            if (rc == TV_ERR_IO) status_out[k] = TV_ERR_IO;
-            else if (rc) return rc;
+            longs.push_back({k, fo, a, b - a});
         } else {
             const uint64_t part = kRingSlotBytes - 4;  // (pieces of at most one slot, with room to align)
             for (uint64_t o = 0; o < b - a; o += part)
                 small.push_back({k, fo + o, a + o, std::min<uint64_t>(part, b - a - o), 0});
+            small_bytes += b - a;
         }
+    }
+    // longest first to the lane with fewer bytes so far (lane 0 also carries the pool's bytes)
+    std::vector<LongSeg> lane_segs[2];
+    {
+        std::vector<size_t> order(longs.size());
+        for (size_t q = 0; q < order.size(); q++) order[q] = q;
+        std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return longs[x].len > longs[y].len; });
+        uint64_t load[2] = {small_bytes, 0};
+        for (size_t q : order) {
+            const int l = (c->file_concurrent && load[1] < load[0]) ? 1 : 0;
+            lane_segs[l].push_back(longs[q]);
+            load[l] += longs[q].len;
+        }
+        for (auto& v : lane_segs)  // each lane walks its segments in linear order
+            std::sort(v.begin(), v.end(), [](const LongSeg& x, const LongSeg& y) { return x.a < y.a; });
+    }
+    int helper_rc = TV_OK;
+    std::thread helper;
+    struct Joiner {
+        std::thread& t;
+        ~Joiner() {
+            if (t.joinable()) t.join();
+        }
+    } joiner{helper};  // every exit joins the helper before the ctx lock is released
+    if (!lane_segs[1].empty()) {
+        helper = std::thread([&]() {
+            if (hipSetDevice(c->device) != hipSuccess) {
+                helper_rc = fail(c, TV_ERR_HIP, "tv_stage_files: hipSetDevice(%d) failed", c->device);
+                return;
+            }
+            for (const LongSeg& sg : lane_segs[1]) {
+                const int r = stage_file_locked(c, paths[sg.k], sg.fo, sg.a, sg.len, 1);
+                if (r == TV_ERR_IO) status_out[sg.k] = TV_ERR_IO;
+                else if (r) {
+                    helper_rc = r;
+                    return;
+                }
+            }
+        });
+    }
+    for (const LongSeg& sg : lane_segs[0]) {
+        rc = stage_file_locked(c, paths[sg.k], sg.fo, sg.a, sg.len, 0);
+        if (rc == TV_ERR_IO) status_out[sg.k] = TV_ERR_IO;
+        else if (rc) return rc;
     }
     std::string first_err;
     std::mutex err_mu;
@@ -924,6 +1016,8 @@ int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64
         i = j;
     }
     TV_HIP(c, hipStreamSynchronize(c->copy_stream));
+    if (helper.joinable()) helper.join();
+    if (helper_rc) return helper_rc;
     if (!first_err.empty()) fail(c, TV_OK, "tv_stage_files: %s (and possibly more; see status_out)", first_err.c_str());
     return TV_OK;
 }
