@@ -1,8 +1,9 @@
 // tv_api.hip -- C ABI of libtorrent_verify.so (declared in include/torrent_verify.h).
 //
-// Owns, per context (= per GPU): the compute and copy HIP streams, timing events, a ring of
-// pinned host staging buffers, and the device allocations (resident payload with padded piece
-// stride, digests, availability / output bitfields, chaining state for streamed runs).
+// Owns, per context (= per GPU): the compute stream, two staging lanes (a copy stream and a ring of
+// pinned host staging buffers each), timing events, and the device allocations (resident payload
+// with padded piece stride, digests, availability / output bitfields, chaining state for streamed
+// runs).
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <sys/mman.h>
@@ -54,7 +55,7 @@ struct tv_ctx {
     int split_pairs = 0;        // 0 = automatic
     uint64_t file_chunk = 256ull << 20;  // tv_stage_file: bytes per mapped window
     bool file_direct = true;             // tv_stage_file: DMA from registered page-cache pages
-    bool file_concurrent = true;         // tv_stage_files: long segments beside the reader pool
+    bool file_concurrent = true;         // tv_stage_files: long segments on two staging lanes
     uint64_t file_direct_min = 32ull << 20;  // tv_stage_files: segments >= this take the tv_stage_file path
     int file_threads = 16;                   // tv_stage_files: reader threads
 
@@ -279,9 +280,6 @@ int finish_timing(tv_ctx* c) {
     return TV_OK;
 }
 
-// Stage one contiguous range of LINEAR bytes that lies inside a single piece or covers whole
-// pieces; src is host memory.  Rows of whole pieces use one 2D copy (src pitch L, dst pitch stride).
-// A page-locked src is read by DMA directly; pageable memory is copied through the pinned ring.
 // Host memcpy into a pinned ring slot, split over up to `threads` threads in 4 MiB parts when it is
 // long (one core copies pageable memory at well under the PCIe rate).
 void copy_into_ring(uint8_t* dst, const uint8_t* src, uint64_t n, int threads) {
@@ -321,7 +319,7 @@ void gather_rows(uint8_t* dst, const uint8_t* src, uint64_t width, uint64_t pitc
     for (auto& x : th) x.join();
 }
 
-// One host -> device copy on the copy stream, dword-aligned.  The DMA engine moves 1-byte-aligned
+// One host -> device copy on the lane's copy stream, dword-aligned.  The DMA engine moves 1-byte-aligned
 // data ~10x slower than dword-aligned data (57 vs 5.7 GB/s, tools/dma_align_probe.py): when src and
 // dst agree mod 4, the 0-3 byte head and tail go as separate tiny copies and the body is aligned.
 int dma_h2d(tv_ctx* c, uint8_t* dst, const uint8_t* src, uint64_t n, int lane = 0) {
@@ -338,6 +336,9 @@ int dma_h2d(tv_ctx* c, uint8_t* dst, const uint8_t* src, uint64_t n, int lane = 
     return TV_OK;
 }
 
+// Stage one contiguous range of LINEAR bytes that lies inside a single piece or covers whole
+// pieces; src is host memory.  Rows of whole pieces use one 2D copy (src pitch L, dst pitch stride).
+// A page-locked src is read by DMA directly; pageable memory is copied through the lane's pinned ring.
 int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n, bool pinned, int lane = 0) {
     hipStream_t cs = lane_stream(c, lane);
     RingRef ring = ring_ref(c, lane);
@@ -680,6 +681,7 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
     TV_HIP(c, hipSetDevice(c->device));
     TV_HIP(c, hipStreamSynchronize(c->stream));
     TV_HIP(c, hipStreamSynchronize(c->copy_stream));
+    TV_HIP(c, hipStreamSynchronize(c->copy_stream2));
     free_device(c);
     c->has_layout = false;
     c->digests_set = false;
@@ -1381,6 +1383,7 @@ int tv_synchronize(tv_ctx* c) {
     std::lock_guard<std::mutex> g(c->mu);
     TV_HIP(c, hipSetDevice(c->device));
     TV_HIP(c, hipStreamSynchronize(c->copy_stream));
+    TV_HIP(c, hipStreamSynchronize(c->copy_stream2));
     TV_HIP(c, hipStreamSynchronize(c->stream));
     return TV_OK;
 }
