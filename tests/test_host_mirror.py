@@ -169,6 +169,39 @@ def test_segments_quirks():
     assert Storage(MemoryStorage(), single, os.path.join(os.getcwd(), "dl")).segments(3, 4) == [(["dl", "s.bin"], 3, 4, 0)]
 
 
+@pytest.mark.parametrize("dir_path", ["/tmp/seg", "/", "", "/tmp/seg/"])
+def test_segment_arrays_equal_the_walk(dir_path):
+    """Storage.segment_arrays (the vectorised walk verify_files stages from) equals segments() minus
+    its zero-length entries, with the same None cases, on random layouts full of zero-length and tiny
+    files and random (offset, length) ranges, including past-the-end ones; file_paths() equals
+    os.path.join of each segment's path."""
+    import random
+    rnd = random.Random(11)
+    d = dir_path or os.getcwd()
+    for _ in range(300):
+        sizes = [rnd.choice([0, 0, 1, 5, 64, 100, 4096]) for _ in range(rnd.randrange(1, 12))]
+        total = sum(sizes)
+        if total == 0:
+            continue
+        info = make_info(64, bytes(20 * (-(-total // 64))), "t",
+                         files=[FileInfo(n, [f"d{k % 3}", f"f{k}"]) for k, n in enumerate(sizes)])
+        st = Storage(MemoryStorage(), info, d)
+        paths = st.file_paths()
+        for _ in range(20):
+            off, ln = rnd.randrange(0, total + 3), rnd.randrange(0, total + 3)
+            walk, arrs = st.segments(off, ln), st.segment_arrays(off, ln)
+            if walk is None:
+                assert arrs is None, (sizes, off, ln)
+                continue
+            assert arrs is not None, (sizes, off, ln)
+            want = [(os.path.join(*p), fo, n, s0) for p, fo, n, s0 in walk if n > 0]
+            assert [(paths[k], int(fo), int(n), int(s0)) for k, fo, n, s0 in zip(*arrs)] == want
+    single = make_info(8, bytes(20), "s.bin", length=8)
+    st = Storage(MemoryStorage(), single, os.path.join(os.getcwd(), "dl"))
+    k, fo, n, s0 = st.segment_arrays(3, 4)
+    assert (st.file_paths()[int(k[0])], int(fo[0]), int(n[0]), int(s0[0])) == (os.path.join("dl", "s.bin"), 3, 4, 0)
+
+
 def test_fs_storage(tmp_path):  # storage_test.ts:41-62
     p = tmp_path / "__test.txt"
     p.write_bytes(bytes([1, 2, 3, 4, 5, 6, 7, 8]))

@@ -232,18 +232,30 @@ class Context:
     def stage_files(self, paths, file_offsets, linear_offsets, lens) -> list:
         """tv_stage_files: stage many file segments in one call.  Returns one status per segment:
         TV_OK, or TV_ERR_IO for a missing / unreadable / short file (its pieces are unreadable)."""
+        import numpy as np
+
         n = len(paths)
         if n == 0:
             return []
-        enc = [os.fsencode(x) for x in paths]
-        cpaths = (ctypes.c_char_p * n)(*enc)
-        arr = lambda v: (ctypes.c_uint64 * n)(*v)  # noqa: E731
+        if any(len(v) != n for v in (file_offsets, linear_offsets, lens)):
+            raise ValueError("stage_files: paths, file_offsets, linear_offsets and lens differ in length")
+        # all paths in one NUL-separated buffer (paths hold no NUL), and the char* array pointing into it
+        blob = b"\0".join(os.fsencode(x) for x in paths) + b"\0"
+        if blob.count(b"\0") != n:
+            raise ValueError("stage_files: a path contains a NUL byte")
+        cblob = ctypes.create_string_buffer(blob, len(blob))
+        nul = np.flatnonzero(np.frombuffer(blob, dtype=np.uint8) == 0)
+        starts = np.empty(n, dtype=np.uint64)
+        starts[0] = 0
+        starts[1:] = nul[:-1] + 1
+        ptrs = starts + np.uint64(ctypes.addressof(cblob))
+        arr = lambda v: np.ascontiguousarray(v, dtype=np.uint64)  # noqa: E731
         fo, lo, ln = arr(file_offsets), arr(linear_offsets), arr(lens)
-        st = (ctypes.c_int32 * n)()
-        self._check(self._L.tv_stage_files(self._h, n, ctypes.cast(cpaths, _p), ctypes.cast(fo, _p),
-                                           ctypes.cast(lo, _p), ctypes.cast(ln, _p), ctypes.cast(st, _p)))
-        del enc
-        return list(st)
+        st = np.zeros(n, dtype=np.int32)
+        self._check(self._L.tv_stage_files(self._h, n, ptrs.ctypes.data, fo.ctypes.data, lo.ctypes.data,
+                                           ln.ctypes.data, st.ctypes.data))
+        del cblob
+        return st.tolist()
 
     def read(self, linear_offset: int, out) -> None:
         """Copy resident bytes at linear_offset into the writable buffer `out` (tv_read)."""

@@ -55,6 +55,8 @@ class Storage:
         self.dir_path = _split_dir(dir_path)
         self._written: dict = {}
         self._ends: Optional[List[int]] = None  # cumulative file ends (lazy)
+        self._table = None                       # (starts, ends) as int64 arrays (lazy)
+        self._joined: Optional[List[str]] = None  # os.path.join of every file's path (lazy)
 
     # -- mapping ---------------------------------------------------------------------
     def segments(self, offset: int, length: int) -> Optional[List[Segment]]:
@@ -87,6 +89,57 @@ class Storage:
                     return out
             file_start = file_end
         return None
+
+    def segment_arrays(self, offset: int, length: int):
+        """segments(offset, length) without its zero-length entries, as arrays: (file_index,
+        file_offset, n_bytes, slice_start), int64 each, in walk order; file_index is into info.files
+        (all 0 for a single-file torrent).  None = unmappable, exactly when segments() returns None.
+
+        The same walk, vectorised for many-file shards: the file k that segments() visits contributes
+        the bytes [max(start_k, offset), min(end_k, offset + length)), so every file overlapping the
+        range gives one segment, and the walk completes iff the files reach offset + length."""
+        import numpy as np
+
+        if self.info.files is None:
+            n = length if length > 0 else 0
+            if n == 0:
+                return tuple(np.zeros(0, np.int64) for _ in range(4))
+            return (np.zeros(1, np.int64), np.array([offset], np.int64), np.array([n], np.int64),
+                    np.zeros(1, np.int64))
+        if self._table is None:
+            lens = np.fromiter((f.length for f in self.info.files), dtype=np.int64, count=len(self.info.files))
+            ends = np.cumsum(lens)
+            self._table = (ends - lens, ends)
+        starts, ends = self._table
+        if len(ends) == 0 or int(ends[-1]) < offset + length:
+            return None
+        a = int(np.searchsorted(ends, offset, side="right"))           # first file ending past offset
+        b = int(np.searchsorted(starts, offset + length, side="left"))  # files starting before the end
+        k = np.arange(a, max(a, b), dtype=np.int64)
+        lo = np.maximum(starts[a:b], offset)
+        n = np.minimum(ends[a:b], offset + length) - lo
+        keep = n > 0
+        k, lo, n = k[keep], lo[keep], n[keep]
+        return k, lo - starts[k], n, lo - offset
+
+    def file_paths(self) -> List[str]:
+        """os.path.join(*segment path) for every file index of segment_arrays (fs_storage's paths)."""
+        if self._joined is None:
+            if self.info.files is None:
+                self._joined = [os.path.join(*self.dir_path, self.info.name)]
+            else:
+                base = os.path.join(*self.dir_path) if self.dir_path else ""
+                head = base if (not base or base.endswith(os.sep)) else base + os.sep
+                out = []
+                for f in self.info.files:
+                    parts = f.path
+                    # os.path.join(*dir, *parts) without its per-call cost when no part is empty or absolute
+                    if parts and all(q and not q.startswith(os.sep) for q in parts):
+                        out.append(head + os.sep.join(parts))
+                    else:
+                        out.append(os.path.join(*self.dir_path, *parts))
+                self._joined = out
+        return self._joined
 
     def _find_and_do(self, offset: int, buf: bytearray | memoryview,
                      action: Callable[[List[str], int, memoryview], bool]) -> bool:

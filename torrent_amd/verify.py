@@ -210,7 +210,6 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
     ones are read by `threads` library threads into pinned slots, one DMA per run of adjacent bytes.
     A piece touching a missing or short file is unreadable (fsStorage.get -> null,
     storage.ts:150-172); zero-length segments succeed; missing files are never created."""
-    import os
     L = info.piece_length
     avail = bytearray(b"\xff" * ((count + 7) // 8))
     if count % 8:
@@ -229,18 +228,21 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
         clear(j, j)
         j -= 1
     span = max(0, min(hi, info.length) - lo)
-    segs = storage.segments(lo, span) if span else []
-    if segs is None:                  # unmappable (Storage.get -> null for every piece)
+    # the n_bytes > 0 segments of Storage.segments(lo, span), as arrays (same walk, vectorised)
+    segs = storage.segment_arrays(lo, span) if span else None
+    if span and segs is None:         # unmappable (Storage.get -> null for every piece)
         clear(0, count - 1)
-        segs = []
-    segs = [sg for sg in segs if sg[2] > 0]
+    if segs is None or len(segs[0]) == 0:
+        return avail
+    k, foff, nbytes, start = segs
+    paths = storage.file_paths()
     ctx.set_option(_native.TV_OPT_FILE_THREADS, max(1, threads))
     ctx.set_option(_native.TV_OPT_FILE_DIRECT_MIN, _DIRECT_MIN_BYTES if direct_min is None else direct_min)
-    status = ctx.stage_files([os.path.join(*path) for path, _, _, _ in segs], [foff for _, foff, _, _ in segs],
-                             [lo + start for _, _, _, start in segs], [n for _, _, n, _ in segs])
-    for (_, _, n, start), st in zip(segs, status):
+    status = ctx.stage_files([paths[i] for i in k.tolist()], foff, start + lo, nbytes)
+    for q, st in enumerate(status):
         if st != _native.TV_OK:
-            clear(start // L, (start + n - 1) // L)
+            s0, n = int(start[q]), int(nbytes[q])
+            clear(s0 // L, (s0 + n - 1) // L)
     return avail
 
 
