@@ -15,7 +15,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from tests.layouts import build_layout, by_name  # noqa: E402
-from torrent_amd import _native, verify_files, verify_payload  # noqa: E402
+from torrent_amd import verify_files, verify_payload  # noqa: E402
 from torrent_amd.verify import _context  # noqa: E402
 
 d = sys.argv[1]

@@ -1,5 +1,6 @@
 """Scratch throughput probe: fill a synthetic shard on device, hash it, verify it, per kernel."""
-import sys, time, os
+import os
+import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from torrent_amd import _native as N
 
