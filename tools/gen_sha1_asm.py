@@ -14,7 +14,7 @@ SHA1_FULL   one 64-byte block, message schedule computed in-asm (16-word rolling
             5 VALU per round + 3 per scheduled word = 400 + 192 = 592 (+16 v_perm bswap and
             5 feed-forward adds by the compiler outside) = 613 per block.
 SHA1_LDS    the 80 rounds only (400 VALU); W[0..79] comes from LDS as 20 ds_read_b128
-            (layout [t/4][lane][4 words], conflict-free), kept 3 quads ahead in a 16-VGPR
+            (layout [t/4][lane][4 words], conflict-free), kept 15 quads ahead in a 64-VGPR
             ring of PHYSICAL registers (a 128-bit asm operand cannot be split in AMDGPU asm).
 
 Round (roles rotate statically; the new `a` is written into the old `e` register):
@@ -39,9 +39,12 @@ M32 = 0xFFFFFFFF
 
 # physical VGPRs used by SHA1_LDS for its K+W ring (quad-aligned; a 128-bit asm operand cannot
 # be split in AMDGPU asm).  The kernel's VGPR count is therefore >= RING_BASE + 4*RING_QUADS.
+# A ds_read_b128 of a wave64 returns 1 KiB and its latency under the rounds wave's VALU stream is
+# long: 15 quads in flight (60 rounds ahead, lgkmcnt's 4-bit maximum) run the 80-round block in
+# 1,794 cycles against 1,894 with 7 in flight (tools/gen_ubench_rounds.py, profiles/r01/ubench_rounds.log).
 RING_BASE = 64
-RING_QUADS = 8
-READ_AHEAD = 7      # quads in flight ahead of the one being consumed
+RING_QUADS = 16
+READ_AHEAD = 15     # quads in flight ahead of the one being consumed
 WAIT_EVERY = 4      # one s_waitcnt per 4 quads (16 rounds)
 # physical VGPRs of the helper (schedule) block: 16-word W window, xor3 temp, 3 output quads
 HW_BASE = 80
