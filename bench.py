@@ -45,7 +45,9 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level par
 CLOCK_HZ = 2.4e9
 SIMD_CYC_PER_BLOCK = 400 * 4 + 213 * 2
 VALU_PEAK_GBPS = 1024 * 64 * 64 * CLOCK_HZ / SIMD_CYC_PER_BLOCK / 1e9
-LONE_WAVE_CYC = 4.34          # cycles per VALU instruction of a lone wave (measured)
+# Cycles per VALU instruction of a lone wave: 4.07 for 8-byte VOP3 ops in a long loop body, 4.09 for the
+# SHA-1 round mix (tools/ubench_fetch.hip, profiles/r01/ubench_fetch.log); the wave64 cadence is 4.
+LONE_WAVE_CYC = 4.07
 SERIAL_INSTR = {1: 613, 2: 405}  # per-block serial stream: lane kernel / split rounds wave
 
 WORKLOADS = {
@@ -281,7 +283,7 @@ def main() -> int:
                          "frac_of_piece_ceiling": round(achieved / piece_ceiling, 4),
                          "note": "SHA-1 is VALU-bound on MI355X (valu_peak from measured per-op SIMD costs), not "
                                  "HBM-bound; it is serial per piece, so P pieces cap the rate at P x 64 B / "
-                                 "(serial instr x 4.34 cyc) per GPU (piece_parallelism_ceiling)"},
+                                 "(serial VALU instr x 4.07 cyc) per GPU (piece_parallelism_ceiling)"},
         }
         if e2e is not None:
             out["e2e_pinned_host"] = e2e
