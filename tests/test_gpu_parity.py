@@ -221,3 +221,21 @@ def test_empty_and_zero_length_torrents(native, oracle):
             ctx.set_digests(empty_digest)
             assert ctx.verify() == expect
             assert ctx.verify_host(b"") == expect
+
+
+def test_geometry_that_overflows_offsets_is_rejected(native):
+    """Piece offsets i*L and digest offsets 20*i are 64-bit: a geometry whose offsets would wrap is an
+    argument error (thrown, like piece.ts:22-64's validation), not a silent wrong read.  The context
+    stays usable afterwards."""
+    with _ctx(native) as ctx:
+        for total, L, P, first, count in [
+            (0, 1 << 30, (1 << 34) + 8, (1 << 34), 8),    # i*L wraps past 2^64
+            (0, 64, (1 << 62), (1 << 62) - 8, 8),         # 20*i wraps
+            (0, 1 << 36, 1 << 30, 0, (1 << 30) - 8),      # 2^30 pieces of 64 GiB: offsets and shard bytes wrap
+        ]:
+            with pytest.raises(native.NativeError, match="overflows"):
+                ctx.set_layout(total, L, P, first, count)
+        ctx.set_layout(100, 64, 2)
+        ctx.set_digests(hashlib.sha1(bytes(64)).digest() + hashlib.sha1(bytes(36)).digest())
+        ctx.stage(0, bytes(100))
+        assert ctx.verify() == b"\xc0"

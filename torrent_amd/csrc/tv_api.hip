@@ -596,7 +596,13 @@ void tv_destroy(tv_ctx* c) {
 }
 
 int tv_last_error(const tv_ctx* c, char* buf, size_t n) {
-    const std::string& s = c ? c->err : g_thread_error;
+    std::string s;
+    if (c) {  // a tv_stage_files helper thread may be writing it (fail() takes err_mu)
+        std::lock_guard<std::mutex> g(const_cast<tv_ctx*>(c)->err_mu);
+        s = c->err;
+    } else {
+        s = g_thread_error;
+    }
     if (buf && n) {
         size_t k = std::min(n - 1, s.size());
         memcpy(buf, s.data(), k);
@@ -678,6 +684,13 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
     if (shard_first % 8) return fail(c, TV_ERR_ARG, "shard_first must be a multiple of 8 (whole bitfield bytes)");
     if (shard_count >= 0xFFFFFFFFull) return fail(c, TV_ERR_ARG, "shard_count too large");
     if (piece_length > (1ull << 36)) return fail(c, TV_ERR_ARG, "piece_length must be <= 64 GiB");
+    // every linear offset i*L (+L) and digest offset 20*i (+20) of the torrent must fit in 64 bits, and so
+    // must the resident allocation; otherwise a wrapped offset would index the wrong bytes
+    const uint64_t stride = ((piece_length + 63) / 64) * 64 + c->pad;
+    if (n_pieces >= UINT64_MAX / 20 || n_pieces >= UINT64_MAX / piece_length - 1 ||
+        (shard_count && shard_count > (UINT64_MAX - kSlack) / stride))
+        return fail(c, TV_ERR_ARG, "geometry overflows 64-bit offsets (%llu pieces of %llu bytes)",
+                    (unsigned long long)n_pieces, (unsigned long long)piece_length);
     TV_HIP(c, hipSetDevice(c->device));
     TV_HIP(c, hipStreamSynchronize(c->stream));
     TV_HIP(c, hipStreamSynchronize(c->copy_stream));
@@ -690,7 +703,7 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
     c->P = n_pieces;
     c->first = shard_first;
     c->count = shard_count;
-    c->stride = ((piece_length + 63) / 64) * 64 + c->pad;
+    c->stride = stride;
     c->bit_words = ((shard_count + 255) / 256) * 4;
     c->digest_ok.assign((shard_count + 7) / 8 + 8, 0);
     if (shard_count) {
