@@ -65,7 +65,7 @@ def variant(name: str) -> list[str]:
             out.append(f"s_waitcnt lgkmcnt({min(15, 2 * n)})")
             continue
         out.append(line)
-    if name == "hadd":
+    if name in ("hadd", "pair_rounds"):
         out += [f"v_add_u32 v{50 + i}, v{50 + i}, v{40 + i}" for i in range(5)] + ["s_barrier"]
     out.append("s_waitcnt lgkmcnt(0)")
     return out
@@ -75,10 +75,12 @@ def variant(name: str) -> list[str]:
 SWEEP = {"q8a7w2": (8, 7, 2), "q8a7w1": (8, 7, 1), "q8a4w4": (8, 4, 4), "q8a6w2": (8, 6, 2),
          "q16a15w8": (16, 15, 8), "q16a12w4": (16, 12, 4), "q16a15w4": (16, 15, 4), "q16a8w8": (16, 8, 8)}
 VARIANTS = ["real", "nolds", "nowait", "b64", "late", "hadd"] + list(SWEEP)
+SWEEP["pair_rounds"] = (16, 15, 4)
+PAIR_HELPERS = {"pair_bar": (0, 0), "pair_valu": (0, 300), "pair_wr": (20, 0), "pair_full": (20, 300)}
 
 
 def render() -> str:
-    clob = ", ".join(f'"v{r}"' for r in list(range(40, 56)) + list(range(64, 128)))
+    clob = ", ".join(f'"v{r}"' for r in list(range(40, 56)) + list(range(60, 128)))
     kern = []
     for vi, name in enumerate(VARIANTS):
         body = "\n".join(f'        "{l}\\n"' for l in variant(name))
@@ -107,7 +109,50 @@ __global__ __launch_bounds__(64) void k_{name}(uint64_t* cyc, uint32_t* sink, ui
     if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
     sink[blockIdx.x * 64 + threadIdx.x] = o + lds[threadIdx.x];
 }}""")
-    runs = "\n".join(f'    run(k_{n}, "{n}");' for n in VARIANTS)
+    # two-wave workgroups: wave 0 = the rounds block (16-quad ring) + 5 adds + s_barrier per block;
+    # wave 1 = a helper stand-in per block: PAIR_HELPERS[name] = (ds_write_b128 count, VALU count)
+    rounds = variant("pair_rounds")
+    for name, (nw, nv) in PAIR_HELPERS.items():
+        hb = []
+        for q in range(20):
+            hb += ["v_bitop3_b32 v60, v61, v62, v63 bitop3:0x96"] * (nv // 20)
+            if q < nw:
+                hb.append(f"ds_write_b128 v49, v[64:67] offset:{20480 + q * 1024}")
+        hb += ["s_waitcnt lgkmcnt(0)", "s_barrier"]
+        rbody = "\n".join(f'            "{l}\\n"' for l in rounds)
+        hbody = "\n".join(f'            "{l}\\n"' for l in hb)
+        kern.append(f"""
+__global__ __launch_bounds__(128) void k_{name}(uint64_t* cyc, uint32_t* sink, uint32_t seed) {{
+    __shared__ uint32_t lds[40 * 256 + 64];
+    for (int i = threadIdx.x; i < 40 * 256 + 64; i += 128) lds[i] = i * seed;
+    __syncthreads();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t addr = (threadIdx.x & 63) * 16, a = threadIdx.x ^ seed, o = 0;
+    uint64_t t0, t1;
+    asm volatile("s_waitcnt lgkmcnt(0)\\n s_memtime %0\\n s_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+    if (wave == 0) {{
+        asm volatile(
+            "v_mov_b32 v49, %1\\n v_mov_b32 v40, %2\\n v_mov_b32 v41, %2\\n v_mov_b32 v42, %2\\n"
+            "v_mov_b32 v43, %2\\n v_mov_b32 v44, %2\\n s_mov_b32 s40, {NBLK}\\n s_branch L_top_%=\\n"
+            ".p2align 6\\n L_top_%=:\\n"
+{rbody}
+            "s_sub_u32 s40, s40, 1\\n s_cmp_lg_u32 s40, 0\\n s_cbranch_scc1 L_top_%=\\n"
+            "v_mov_b32 %0, v40\\n"
+            : "=v"(o) : "v"(addr), "v"(a) : "s40", "scc", "memory", {clob});
+    }} else {{
+        asm volatile(
+            "v_mov_b32 v49, %1\\n v_mov_b32 v61, %2\\n v_mov_b32 v62, %2\\n v_mov_b32 v63, %2\\n"
+            "s_mov_b32 s40, {NBLK}\\n s_branch L_top_%=\\n .p2align 6\\n L_top_%=:\\n"
+{hbody}
+            "s_sub_u32 s40, s40, 1\\n s_cmp_lg_u32 s40, 0\\n s_cbranch_scc1 L_top_%=\\n"
+            "v_mov_b32 %0, v60\\n"
+            : "=v"(o) : "v"(addr), "v"(a) : "s40", "scc", "memory", {clob});
+    }}
+    asm volatile("s_waitcnt lgkmcnt(0)\\n s_memtime %0\\n s_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+    if ((threadIdx.x & 63) == 0 && wave == 0) cyc[blockIdx.x] = t1 - t0;
+    sink[blockIdx.x * 128 + threadIdx.x] = o + lds[threadIdx.x];
+}}""")
+    runs = "\n".join(f'    run(k_{n}, "{n}", {128 if n in PAIR_HELPERS else 64});' for n in VARIANTS + list(PAIR_HELPERS))
     return f"""// GENERATED by tools/gen_ubench_rounds.py -- see its docstring.
 #include <hip/hip_runtime.h>
 
@@ -115,15 +160,15 @@ __global__ __launch_bounds__(64) void k_{name}(uint64_t* cyc, uint32_t* sink, ui
 {''.join(kern)}
 
 template <typename K>
-void run(K kern, const char* name) {{
+void run(K kern, const char* name, int threads) {{
     const int blocks = 256;
     uint64_t* cyc;
     uint32_t* sink;
     (void)hipMalloc(&cyc, sizeof(uint64_t) * blocks);
-    (void)hipMalloc(&sink, 4 * blocks * 64);
+    (void)hipMalloc(&sink, 4 * blocks * 128);
     double best = 1e30;
     for (int rep = 0; rep < 4; rep++) {{
-        hipLaunchKernelGGL(kern, dim3(blocks), dim3(64), 0, 0, cyc, sink, 1u);
+        hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, 0, cyc, sink, 1u);
         (void)hipDeviceSynchronize();
         uint64_t h[256];
         (void)hipMemcpy(h, cyc, 8 * blocks, hipMemcpyDeviceToHost);
