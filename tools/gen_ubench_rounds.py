@@ -24,7 +24,7 @@ import gen_sha1_asm as g  # noqa: E402
 
 NBLK = 64
 REG = {**{f"r{i}": f"v{40 + i}" for i in range(5)}, **{f"h{i}": f"v{40 + i}" for i in range(5)},
-       "t0": "v45", "t1": "v46", "addr": "v49"}
+       "t0": "v45", "t1": "v46", "addr": "v49", **{f"k{i}": f"s{44 + i}" for i in range(4)}}
 
 
 def phys(line: str) -> str:
@@ -54,6 +54,12 @@ def variant(name: str) -> list[str]:
             continue
         if name == "nowait" and line.startswith("s_waitcnt"):
             continue
+        if name in ("kadd3", "kadd3v") and line.startswith("v_add_u32"):
+            # e + K + W as one v_add3 with K in an SGPR (kadd3) or a VGPR (kadd3v), W from the ring
+            m = re.match(r"v_add_u32 (v\d+), (v\d+), (v\d+)", line)
+            k = "s44" if name == "kadd3" else "v47"
+            out.append(f"v_add3_u32 {m.group(1)}, {m.group(3)}, {k}, {m.group(2)}")
+            continue
         if name == "b64" and line.startswith("ds_read_b128"):
             m = re.match(r"ds_read_b128 v\[(\d+):(\d+)\], (v\d+) offset:(\d+)", line)
             lo, addr, off = int(m.group(1)), m.group(3), int(m.group(4))
@@ -76,7 +82,10 @@ SWEEP = {"q8a7w2": (8, 7, 2), "q8a7w1": (8, 7, 1), "q8a4w4": (8, 4, 4), "q8a6w2"
          "q16a15w8": (16, 15, 8), "q16a12w4": (16, 12, 4), "q16a15w4": (16, 15, 4), "q16a8w8": (16, 8, 8)}
 VARIANTS = ["real", "nolds", "nowait", "b64", "late", "hadd"] + list(SWEEP)
 SWEEP["pair_rounds"] = (16, 15, 4)
-PAIR_HELPERS = {"pair_bar": (0, 0), "pair_valu": (0, 300), "pair_wr": (20, 0), "pair_full": (20, 300)}
+SWEEP["kadd3"] = SWEEP["kadd3v"] = (16, 15, 4)
+VARIANTS += ["kadd3", "kadd3v"]
+PAIR_HELPERS = {"pair_bar": (0, 0), "pair_valu": (0, 300), "pair_wr": (20, 0), "pair_full": (20, 300),
+                "pair_vop2": (20, 300), "pair_prio": (20, 300), "pair_half": (20, 140)}
 
 
 def render() -> str:
@@ -115,11 +124,13 @@ __global__ __launch_bounds__(64) void k_{name}(uint64_t* cyc, uint32_t* sink, ui
     for name, (nw, nv) in PAIR_HELPERS.items():
         hb = []
         for q in range(20):
-            hb += ["v_bitop3_b32 v60, v61, v62, v63 bitop3:0x96"] * (nv // 20)
+            op = "v_xor_b32 v60, v61, v62" if name == "pair_vop2" else "v_bitop3_b32 v60, v61, v62, v63 bitop3:0x96"
+            hb += [op] * (nv // 20)
             if q < nw:
                 hb.append(f"ds_write_b128 v49, v[64:67] offset:{20480 + q * 1024}")
         hb += ["s_waitcnt lgkmcnt(0)", "s_barrier"]
-        rbody = "\n".join(f'            "{l}\\n"' for l in rounds)
+        rl = (["s_setprio 3"] if name == "pair_prio" else []) + rounds
+        rbody = "\n".join(f'            "{l}\\n"' for l in rl)
         hbody = "\n".join(f'            "{l}\\n"' for l in hb)
         kern.append(f"""
 __global__ __launch_bounds__(128) void k_{name}(uint64_t* cyc, uint32_t* sink, uint32_t seed) {{
