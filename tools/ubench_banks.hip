@@ -1,4 +1,4 @@
-// tools/ubench_banks.hip -- why does a lone wave issue VOP3 at ~4.5 cycles but VOP2 at ~4.1?
+// tools/ubench_banks.hip -- why does a lone wave issue a dependent VOP3 chain at ~4.9 cycles but VOP2 at ~4.1?
 // Build: hipcc --offload-arch=gfx950 -O3 tools/ubench_banks.hip -o /tmp/ubench_banks
 // Candidates: VGPR bank conflicts among the 3 source operands (bank = vgpr index mod 4), the
 // 8-byte encoding (instruction fetch), or VOP3 itself.  Each case is a dependent chain of 64

@@ -1,11 +1,11 @@
 // tools/ubench_fetch.hip -- does a lone wave issue 8-byte VALU instructions faster from a SMALL loop?
 //
-// ubench_banks.hip found a lone wave issuing 8-byte instructions at 4.93 cyc (≈ 1.62 instruction bytes
-// per cycle) against 4.11 cyc for 4-byte ones, in long straight-line code.  The split kernel's rounds
-// wave sits at that fetch bound.  If a loop body small enough to stay in the wave's
-// instruction buffer issued at the 4-cycle cadence, a rounds loop of 5 rounds per trip would beat the
-// 80-round straight-line loop.  Each case: a loop of K instructions per trip (trips x K = 16,384), one
-// wave per CU, timed by s_memtime; reported per VALU instruction and per trip overhead.
+// ubench_banks.hip found a lone wave issuing DEPENDENT chains of 8-byte instructions at 4.93 cyc
+// (≈ 1.62 instruction bytes per cycle) against 4.11 cyc for 4-byte ones, which read like an
+// instruction-fetch bound.  This probe answers it: independent 8-byte instructions in loops of K per
+// trip (trips x K = 16,384), and the SHA-1 round mix, one wave per CU, timed by s_memtime, reported
+// per VALU instruction.  Result (profiles/r01/ubench_fetch.log): 4.07 cyc for long bodies, so there
+// is no fetch bound; the 4.93 is the back-to-back VOP3 dependency.  Also: an SGPR source costs nothing.
 // Build: hipcc --offload-arch=gfx950 -O3 tools/ubench_fetch.hip -o tools/ubench_fetch
 #include <hip/hip_runtime.h>
 

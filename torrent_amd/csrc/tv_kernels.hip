@@ -9,13 +9,12 @@
 // Parallelism is one LANE per piece (SHA-1 is serial inside a piece).  Two kernels:
 //   lane  : each lane loads its own 64-byte blocks (register prefetch, 2 blocks ahead) and runs
 //           the full compression (schedule + rounds) as one generated asm block (613 VALU/block).
-//   split : schedule offload.  A workgroup is 2 x (rounds, helper) waves for 128 pieces: a helper loads the
-//           blocks and writes K+W[0..79] into an LDS double buffer (generated asm: v_perm bswap,
-//           v_bitop3 xor3, ds_write_b128); the rounds wave runs only the 80 rounds from LDS
-//           (400 VALU + 20 ds_read_b128 + 10 waits per block).  A lone wave issues one VALU per
-//           ~4.5 cycles whether or not it is dependent (tools/ubench_valu.hip), so with fewer
-//           pieces than SIMDs the per-lane instruction count IS the bound; this cuts the serial
-//           stream from ~630 to ~445 instructions per block.
+//   split : schedule offload.  A workgroup is PAIRS x (rounds, helper) waves, 64 pieces per pair: a helper
+//           loads the blocks and writes K+W[0..79] into an LDS double buffer (generated asm: v_perm
+//           bswap, v_bitop3 xor3, K adds, ds_write_b128); the rounds wave runs only the 80 rounds from
+//           LDS (405 VALU + 20 ds_read_b128 + 5 waits per block).  A lone wave issues one VALU per
+//           ~4.07 cycles (tools/ubench_fetch.hip), so with fewer pieces than SIMDs the per-lane
+//           instruction count IS the bound; this cuts the serial stream from 613 to 405 VALU per block.
 //
 // HBM layout: resident piece j (shard-local) starts at payload + j*stride, stride = L + pad
 // (pad breaks the power-of-two stride that would put all 64 lanes of a wave on one channel).
