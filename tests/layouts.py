@@ -6,6 +6,8 @@ tests/test_oracle.py).  Digests are hashlib SHA-1 of the CLEAN payload; corrupti
 one bit inside each chosen piece.  `missing` files are absent on disk and `short` files are
 truncated, so pieces touching their bytes are unreadable (Storage.get -> null, storage.ts:50-65).
 
+Config 1 of BASELINE.json is the layout "cfg1" (64 MiB single file, 256 KiB pieces, 256 pieces;
+three corrupted, including piece 0 and the final piece).
 Config 3 of BASELINE.json is the layout "cfg3": 10,000 files of U[0, 524288] bytes (>= 20
 zero-length, >= 5 under 64 B), 256 KiB pieces, short final piece, 1 % corrupted pieces
 including piece 0, the final piece and >= 10 pieces that span a file boundary.
@@ -29,6 +31,8 @@ LAYOUTS = [
      "zero": 3, "tiny": 2, "corrupt_frac": 0.03, "missing": [7, 31], "short": {12: 1000, 40: 0}},
     {"name": "exact_multiple", "seed": 105, "piece_length": 4096, "sizes": [4096 * 33, 4096 * 7],
      "corrupt_frac": 0.0},
+    # BASELINE config 1 (the reference's CPU-runnable case): one 64 MiB file, 256 KiB pieces, 256 pieces
+    {"name": "cfg1", "seed": 1, "piece_length": 262144, "sizes": [64 << 20], "corrupt_frac": 0.01},
     {"name": "cfg3", "seed": 3, "piece_length": 262144, "n_files": 10000, "max_size": 524288,
      "zero": 20, "tiny": 5, "corrupt_frac": 0.01, "span_corrupt": 10, "big": True},
 ]

@@ -68,7 +68,7 @@ def test_reference_multifile_through_storage(native):
 
 
 @pytest.mark.parametrize("layout", ["single_short_last", "multi_zero_tiny", "many_tiny_span",
-                                    "missing_and_short", "exact_multiple", "cfg3"])
+                                    "missing_and_short", "exact_multiple", "cfg1", "cfg3"])
 def test_golden_layouts_on_gpu(native, layout):
     """Seeded layouts: GPU bitfield == committed expected bitfield (hashlib-computed)."""
     from tests.layouts import build_layout, by_name
@@ -305,7 +305,7 @@ def test_incremental_verifier_flow(native, oracle):
     v.close()
 
 
-@pytest.mark.parametrize("layout", ["multi_zero_tiny", "missing_and_short", "single_short_last"])
+@pytest.mark.parametrize("layout", ["multi_zero_tiny", "missing_and_short", "single_short_last", "cfg1"])
 def test_verify_files_resume_from_disk(native, tmp_path, layout):
     """verify_files (f2 resume from disk: one tv_stage_files call per shard) gives the same bits as the
     committed expectation and as verify_pieces over fs_storage, whichever path the segments take."""
