@@ -194,15 +194,24 @@ def main() -> int:
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-saturating", action="store_true",
                     help="skip the piece-saturated leg (N=1 only: 65,536 x 256 KiB pieces against R_valu)")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: the workload's piece count is the WHOLE torrent, split into N contiguous "
+                         "8-aligned shards (BASELINE config 4: 200 GiB over 2/4/8 GPUs); default is weak scaling")
     ap.add_argument("--e2e-steps", type=int, default=3,
                     help="timed end-to-end passes from pinned host memory over PCIe (0 = skip)")
     a = ap.parse_args()
 
     dist, rank, ws, local = _dist()
     L, per_gpu, desc = WORKLOADS[a.workload]
-    P = per_gpu * ws
+    if a.strong:
+        from torrent_amd.verify import shard_ranges
+        P = per_gpu
+        first, per_gpu = shard_ranges(P, ws)[rank]
+        desc = desc.split(" per GPU")[0].split(" (")[0] + f" ({P} pieces in all, {ws} shard(s), strong scaling)"
+    else:
+        P = per_gpu * ws
+        first = rank * per_gpu
     total = L * P
-    first = rank * per_gpu
 
     device = local % max(1, _native.device_count())
     ctx = _native.Context(device)
@@ -273,7 +282,7 @@ def main() -> int:
         _barrier(dist)
         e_el = _max(dist, e1 - e0)
         e_ok = _sum(dist, 1.0 if bf2 == bytes(expect) else 0.0) == ws
-        e2e = {"value": round(bytes_per_gpu * ws * a.e2e_steps / e_el / 1e9, 2), "unit": "GB/s",
+        e2e = {"value": round(total * a.e2e_steps / e_el / 1e9, 2), "unit": "GB/s",
                "steps": a.e2e_steps, "ms_per_step": round(e_el * 1e3 / a.e2e_steps, 2), "bitfield_exact": e_ok,
                "launches_per_step": ctx.last_kernel()[1],
                "mode": "pinned host -> HBM column stream (2D DMA) overlapped with the verify kernel; PCIe-inclusive"}
@@ -286,7 +295,7 @@ def main() -> int:
         except Exception as exc:  # reported, never fatal to the bench line
             sat = {"skipped": f"{type(exc).__name__}: {exc}"}
 
-    value = bytes_per_gpu * ws * a.steps / elapsed / 1e9
+    value = total * a.steps / elapsed / 1e9      # every rank's shard: weak N x per-GPU bytes, strong the whole torrent
     achieved = bytes_per_gpu / (avg_kernel_ms / 1e3) / 1e9
     piece_ceiling = min(VALU_PEAK_GBPS, per_gpu * 64 * CLOCK_HZ / (SERIAL_INSTR.get(kernel, 613) * LONE_WAVE_CYC) / 1e9)
 
@@ -295,7 +304,10 @@ def main() -> int:
         tpath = os.path.join(ROOT, "profiles", f"traffic_{a.workload}.json")
         if os.path.exists(tpath):
             try:
-                traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
+                rec = json.load(open(tpath))
+                # a per-launch PMC figure applies only to the launch geometry it was measured on
+                if rec.get("payload_bytes_per_launch") == bytes_per_gpu:
+                    traffic = rec.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
         out = {
@@ -307,7 +319,7 @@ def main() -> int:
             "warmup": a.warmup,
             "ms_per_step": round(elapsed * 1e3 / a.steps, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if a.strong else "weak",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (device counter-PRNG payload; 1% corrupted digests)",
