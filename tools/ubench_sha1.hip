@@ -46,5 +46,15 @@ int main() {
         printf("waves/SIMD=%d  %.3f ms  clock %.2f GHz  %.1f GB/s-equiv  %.2f cycles/VALU per SIMD  %.2f cycles/VALU per wave\n",
                wps, ms, ghz, gbps, (double)c[0] / instr_per_simd, (double)c[0] / (iters * 597.0));
     }
+    // Lone-wave cadence against CU occupancy: 1, 2, 4 waves per CU (one per SIMD, 256 blocks), cycles
+    // per compression from block 0's own s_memtime span (core clock), so no clock estimate enters.
+    for (int threads : {64, 128, 256}) {
+        hipLaunchKernelGGL(kfull, dim3(256), dim3(threads), 0, 0, out, 50, clk);
+        hipLaunchKernelGGL(kfull, dim3(256), dim3(threads), 0, 0, out, iters, clk);
+        hipDeviceSynchronize();
+        uint64_t c[2]; hipMemcpy(c, clk, 16, hipMemcpyDeviceToHost);
+        printf("waves/CU=%d (1 per SIMD used)  block-0 memtime cycles per compression %.0f  (%.3f per VALU of ~597)\n",
+               threads / 64, (double)c[0] / iters, (double)c[0] / iters / 597.0);
+    }
     return 0;
 }
