@@ -1,0 +1,61 @@
+// tools/ubench_full_variants.hip -- which part of the full compression runs slower than a lone wave's
+// 4.07-cycle cadence?  Timing-only variants of the generated tv_sha1_full (results are not SHA-1):
+//   a  as generated (592 VALU)
+//   b  schedule xor3 (v_bitop3 0x96, 3 VGPR sources) -> VOP2 v_xor (2 sources)
+//   c  schedule rotl1 (v_alignbit w,w,w,31) -> VOP2 v_lshlrev
+//   d  b + c
+//   e  rounds only (schedule removed, 400 VALU)
+//   f  a with K in VGPRs     g  e with K in VGPRs
+//   h  e with e+K+W as VOP2 v_add e, W (K dropped)     i  a with the same VOP2 e + W
+//   j-m  tools/gen_full_sched.py pipelined schedules (real SHA-1): lag 1 plain, lag 1/2/3 f_first
+// Build: python3 tools/ubench_full_variants.py <dir> (writes <dir>/variants.h), then
+//   hipcc --offload-arch=gfx950 -O3 -I <dir of variants.h> tools/ubench_full_variants.hip -o tools/ubench_full_variants_bin
+// One wave per CU, two compressions per loop trip; cycles per compression from block 0's s_memtime.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include "variants.h"
+
+#define KERNEL(V)                                                                               \
+__global__ __launch_bounds__(64) void k_##V(uint32_t* out, int iters, uint64_t* clk) {          \
+    uint32_t h[5] = {threadIdx.x, 2, 3, 4, 5};                                                  \
+    uint32_t w[16];                                                                             \
+    for (int i = 0; i < 16; i++) w[i] = threadIdx.x * (i + 1);                                  \
+    uint64_t t0 = __builtin_amdgcn_s_memtime();                                                 \
+    for (int it = 0; it < iters; it += 2) {                                                     \
+        uint32_t r[5];                                                                          \
+        tv_sha1_full_##V(h, r, w, 0x5A827999u, 0x6ED9EBA1u, 0x8F1BBCDCu, 0xCA62C1D6u);          \
+        for (int i = 0; i < 5; i++) h[i] += r[i];                                               \
+        tv_sha1_full_##V(h, r, w, 0x5A827999u, 0x6ED9EBA1u, 0x8F1BBCDCu, 0xCA62C1D6u);          \
+        for (int i = 0; i < 5; i++) h[i] += r[i];                                               \
+    }                                                                                           \
+    uint64_t t1 = __builtin_amdgcn_s_memtime();                                                 \
+    out[blockIdx.x * 64 + threadIdx.x] = h[0] ^ h[1] ^ h[2] ^ h[3] ^ h[4] ^ w[3];               \
+    if (threadIdx.x == 0) clk[blockIdx.x] = t1 - t0;                                            \
+}
+KERNEL(a) KERNEL(b) KERNEL(c) KERNEL(d) KERNEL(e) KERNEL(f) KERNEL(g) KERNEL(h) KERNEL(i) KERNEL(j) KERNEL(k) KERNEL(l) KERNEL(m)
+
+typedef void (*kfn)(uint32_t*, int, uint64_t*);
+
+int main() {
+    uint32_t* out; uint64_t* clk;
+    if (hipMalloc(&out, 4 << 20) != hipSuccess || hipMalloc(&clk, 8 * 256) != hipSuccess) return 1;
+    const int iters = 2000;
+    struct { const char* name; kfn f; int valu; } v[] = {
+        {"a as generated", k_a, 597}, {"b xor3 -> VOP2 xor", k_b, 597}, {"c rotl1 -> VOP2 lshl", k_c, 597},
+        {"d b + c", k_d, 597}, {"e rounds only", k_e, 405},
+        {"f a, K in VGPR", k_f, 597}, {"g e, K in VGPR", k_g, 405}, {"h e, VOP2 e+W", k_h, 405},
+        {"i a, VOP2 e+W", k_i, 597}, {"j lag1 plain", k_j, 597}, {"k lag1 f_first", k_k, 597},
+        {"l lag2 f_first", k_l, 597}, {"m lag3 f_first", k_m, 597}};
+    for (int rep = 0; rep < 2; rep++)
+        for (auto& x : v) {
+            hipLaunchKernelGGL(x.f, dim3(256), dim3(64), 0, 0, out, 50, clk);
+            hipLaunchKernelGGL(x.f, dim3(256), dim3(64), 0, 0, out, iters, clk);
+            if (hipDeviceSynchronize() != hipSuccess) return 2;
+            uint64_t c = 0;
+            if (hipMemcpy(&c, clk, 8, hipMemcpyDeviceToHost) != hipSuccess) return 3;
+            printf("%-22s cycles per compression %6.0f   %.3f per VALU (%d)\n", x.name, (double)c / iters,
+                   (double)c / iters / x.valu, x.valu);
+        }
+    return 0;
+}
