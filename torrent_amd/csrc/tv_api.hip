@@ -339,7 +339,14 @@ int dma_h2d(tv_ctx* c, uint8_t* dst, const uint8_t* src, uint64_t n, int lane = 
 // Stage one contiguous range of LINEAR bytes that lies inside a single piece or covers whole
 // pieces; src is host memory.  Rows of whole pieces use one 2D copy (src pitch L, dst pitch stride).
 // A page-locked src is read by DMA directly; pageable memory is copied through the lane's pinned ring.
-int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n, bool pinned, int lane = 0) {
+// `src_in_ring`: src already lies in one of the lane's ring slots (tv_stage_files' packed reads, the
+// cold-window preads).  Such a source is never bounced through the ring again: the bounce would take the
+// ring's next slots, and after kRingSlots takes that is the very slot being read (its event is recorded
+// only after these copies are queued), so the bounce would overwrite bytes still to be copied.  The
+// slot bytes sit at their LINEAR offset's alignment mod 4, which is the destination's whenever L % 4 == 0
+// (every power-of-two piece length); with other L the copy is simply not dword-aligned.
+int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n, bool pinned, int lane = 0,
+               bool src_in_ring = false) {
     hipStream_t cs = lane_stream(c, lane);
     RingRef ring = ring_ref(c, lane);
     while (n) {
@@ -349,8 +356,9 @@ int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n, bool pin
         const bool whole = within == 0 && plen == c->L && n >= c->L;
         // A pinned source whose alignment cannot match the destination's (mod 4; whole-piece rows need
         // it at 0 mod 4 and L % 4 == 0) goes through the ring instead: one memcpy, then aligned DMA.
-        const bool via_ring = !pinned || (whole ? (((uintptr_t)src & 3) != 0 && c->L % 4 == 0)
-                                                : (((uintptr_t)src ^ (uintptr_t)dst) & 3) != 0);
+        const bool via_ring = !src_in_ring &&
+                              (!pinned || (whole ? (((uintptr_t)src & 3) != 0 && c->L % 4 == 0)
+                                                 : (((uintptr_t)src ^ (uintptr_t)dst) & 3) != 0));
         const uint64_t cap = via_ring ? (uint64_t)kRingSlotBytes - 4 : UINT64_MAX;
         int slot = -1;
         if (via_ring) {
@@ -428,7 +436,7 @@ void clip_to_shard(const tv_ctx* c, uint64_t off, uint64_t len, uint64_t* a, uin
 // from base + (pos - base_off).  Pieces are split at piece boundaries (a piece is shorter than L only
 // at the end of the torrent, piece.ts:16-19); bytes in a short last piece's missing tail are skipped.
 int stage_range(tv_ctx* c, uint64_t a, uint64_t b, const uint8_t* base, uint64_t base_off, bool pinned,
-                int lane = 0) {
+                int lane = 0, bool src_in_ring = false) {
     uint64_t pos = a;
     while (pos < b) {
         const uint64_t i = pos / c->L, within = pos % c->L;
@@ -444,7 +452,7 @@ int stage_range(tv_ctx* c, uint64_t a, uint64_t b, const uint8_t* base, uint64_t
         } else {
             n = std::min(b - pos, plen - within);
         }
-        int rc = stage_copy(c, pos, base + (pos - base_off), n, pinned, lane);
+        int rc = stage_copy(c, pos, base + (pos - base_off), n, pinned, lane, src_in_ring);
         if (rc) return rc;
         pos += n;
     }
@@ -837,7 +845,7 @@ int stage_file_locked(tv_ctx* c, const char* path, uint64_t file_offset, uint64_
                 uint8_t* at = ring.buf[slot] + ((p + q) & 3);  // at the resident bytes' alignment mod 4
                 const int e = pread_parallel(win.fd, at, fo + q, kq, c->file_threads);
                 if (e) return fail(c, TV_ERR_IO, "read %s at %llu: %s", path, (unsigned long long)(fo + q), strerror(e));
-                rc = stage_range(c, p + q, p + q + kq, at, p + q, true, lane);
+                rc = stage_range(c, p + q, p + q + kq, at, p + q, true, lane, /*src_in_ring=*/true);
                 if (rc) return rc;
                 TV_HIP(c, hipEventRecord(ring.ev[slot], cs));
             }
@@ -1023,7 +1031,7 @@ int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64
             while (r < j && status_out[small[r].k] == TV_OK && small[r].linear == small[r - 1].linear + small[r - 1].len)
                 r++;
             const uint64_t lin_a = small[q].linear, lin_b = small[r - 1].linear + small[r - 1].len;
-            rc = stage_range(c, lin_a, lin_b, c->ring[slot] + small[q].packed, lin_a, true);
+            rc = stage_range(c, lin_a, lin_b, c->ring[slot] + small[q].packed, lin_a, true, 0, /*src_in_ring=*/true);
             if (rc) return rc;
             q = r;
         }
