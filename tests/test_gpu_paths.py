@@ -459,6 +459,44 @@ def test_stage_files_two_lanes_many_segments(native, oracle, tmp_path, direct):
             assert all(bf[i >> 3] >> (7 - (i & 7)) & 1 for i in range(P)), conc
 
 
+@pytest.mark.parametrize("direct_min", [1 << 62, 0])
+def test_stage_files_odd_piece_length_ring_sources(native, oracle, tmp_path, direct_min):
+    """Ring-slot sources at an odd piece length.  The packed reads of the reader pool (direct_min = 2^62)
+    and the pread windows of tv_stage_file (direct_min = 0, direct DMA off) sit in ring slots at their
+    LINEAR offset's alignment mod 4, which is not the device destination's when L % 4 != 0.  Such
+    sources must be DMA'd as they lie: re-bouncing them through the ring took the ring's next slots,
+    which after three takes is the slot being read (a race; the two-lane test caught it once).  300
+    ragged segments put several hundred unaligned piece fragments into one slot."""
+    import random
+    rnd = random.Random(11)
+    L, P = 16387, 300
+    total = L * P - 77
+    payload = oracle.synth_fill(23, 0, total)
+    bounds = [0] + sorted(rnd.sample(range(1, total), 299)) + [total]
+    paths, fos, lins, lens = [], [], [], []
+    for k in range(300):
+        a, b = bounds[k], bounds[k + 1]
+        pre = rnd.randrange(4)
+        path = tmp_path / f"o{k:03d}.bin"
+        path.write_bytes(bytes(pre) + bytes(payload[a:b]))
+        paths.append(str(path)); fos.append(pre); lins.append(a); lens.append(b - a)
+    with native.Context(0) as ctx:
+        ctx.set_option(native.TV_OPT_FILE_DIRECT, 0)
+        ctx.set_option(native.TV_OPT_FILE_CHUNK, 64 << 10)
+        ctx.set_option(native.TV_OPT_FILE_DIRECT_MIN, direct_min)
+        ctx.set_layout(total, L, P)
+        ctx.set_digests(oracle.hash_pieces(payload, total, L, P))
+        for rep in range(3):
+            ctx.fill_synthetic(50 + rep)
+            st = ctx.stage_files(paths, fos, lins, lens)
+            assert st == [0] * 300
+            out = bytearray(total)
+            ctx.read(0, out)
+            assert out == payload, rep
+            bf = ctx.verify()
+            assert all(bf[i >> 3] >> (7 - (i & 7)) & 1 for i in range(P)), rep
+
+
 def test_verify_files_reference_singlefile(native, tmp_path):
     from torrent_amd import parse_metainfo, verify_files
     info = parse_metainfo(_load("singlefile.torrent")).info
