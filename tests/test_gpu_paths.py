@@ -510,6 +510,38 @@ def test_verify_files_reference_singlefile(native, tmp_path):
     assert bytes(bf) == _all_ones(info.n_pieces)
 
 
+def test_cli_make_torrent_then_verify(native, tmp_path):
+    """The two command lines end to end in fresh processes: `python -m torrent_amd.make_torrent -c ... -t
+    ... <file>` (make_torrent.ts:190-250) writes <name>.torrent in the working directory, and
+    `python -m torrent_amd verify <torrent> <dir>` reports every piece verified (exit 0); after a one-byte
+    corruption it reports the bad piece (exit 1) and the bitfield hex shows which."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    data = bytes((i * 7 + 3) & 0xFF for i in range(3_000_001))   # 3 MB: 32 KiB pieces by make_torrent.ts:17-21
+    (tmp_path / "payload.bin").write_bytes(data)
+    r = subprocess.run([sys.executable, "-m", "torrent_amd.make_torrent", "-c", "cli test", "-t",
+                        "http://tracker.example/announce", "payload.bin"], cwd=tmp_path, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "output -> payload.bin.torrent" in r.stdout, r.stdout + r.stderr
+    from torrent_amd import parse_metainfo
+    meta = parse_metainfo((tmp_path / "payload.bin.torrent").read_bytes())
+    L, P = meta.info.piece_length, meta.info.n_pieces
+    assert L == 1 << 15 and P == -(-len(data) // L) and meta.comment == "cli test"
+    assert meta.info.pieces[5] == hashlib.sha1(data[5 * L:6 * L]).digest()
+    cmd = [sys.executable, "-m", "torrent_amd", "verify", str(tmp_path / "payload.bin.torrent"), str(tmp_path)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and f"{P}/{P} pieces verified" in r.stdout, r.stdout + r.stderr
+    bad = bytearray(data)
+    bad[40 * L + 9] ^= 0x20
+    (tmp_path / "payload.bin").write_bytes(bytes(bad))
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 1 and f"{P - 1}/{P} pieces verified" in r.stdout, r.stdout + r.stderr
+    bf = bytes.fromhex(r.stdout.strip().splitlines()[-1])
+    assert [i for i in range(P) if not (bf[i >> 3] >> (7 - (i & 7))) & 1] == [40]
+
+
 @pytest.mark.parametrize("name", ["singlefile", "multifile"])
 def test_make_torrent_reproduces_reference_fixture_bytes(native, tmp_path, name):
     """Creation mode end to end: make_torrent on the reconstructed payload (same comment, tracker,

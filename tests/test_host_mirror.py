@@ -371,3 +371,11 @@ def test_files_shard_staging_plan(tmp_path, monkeypatch, layout):
                 a, b = i * L, min(total, (i + 1) * L)
                 assert ctx.img[a:b] == lay["payload"][a:b], (layout, i)
                 assert all(ctx.written[a:b]), (layout, i)
+
+
+def test_cli_usage_without_a_gpu(capsys):
+    """Both command lines print their usage on bad arguments without touching the library."""
+    from torrent_amd.__main__ import main as verify_main
+    from torrent_amd.make_torrent import main as make_main
+    assert verify_main([]) == 2 and "python -m torrent_amd verify" in capsys.readouterr().out
+    assert make_main(["--help"]) == 0 and "make_torrent [-c <comment>] -t <tracker url> <target>" in capsys.readouterr().out
