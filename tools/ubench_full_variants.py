@@ -51,6 +51,11 @@ def main(out_dir):
     ekw2 = lambda t: re.sub(r"v_add3_u32 (%\[r\d\]), (%\[[rh]\d\]), %\[k\d\], (%\[w\d+\])", r"v_add_u32 \1, \2, \3", t)
     parts = [var("a", fn), var("b", vb), var("c", vc), var("d", vd), var("e", ve), var("f", kv(fn)),
              var("g", kv(ve)), var("h", ekw2(ve)), var("i", ekw2(fn))]
+    # n: rounds only with e+K+W as a 2-source VOP3 (v_add_u32_e64 e, W); o: as v_add3 e, W, 0 (no SGPR);
+    # p: the full block with e+K+W as v_add_u32_e64 (timing only, K dropped)
+    e64 = lambda t: re.sub(r"v_add3_u32 (%\[r\d\]), (%\[[rh]\d\]), %\[k\d\], (%\[w\d+\])", r"v_add_u32_e64 \1, \2, \3", t)
+    z3 = lambda t: re.sub(r"v_add3_u32 (%\[r\d\]), (%\[[rh]\d\]), %\[k\d\], (%\[w\d+\])", r"v_add3_u32 \1, \2, \3, 0", t)
+    parts += [var("n", e64(ve)), var("o", z3(ve)), var("p", e64(fn))]
     for name, (lag, q) in zip("jklm", [(1, "plain"), (1, "f_first"), (2, "f_first"), (3, "f_first")]):
         ins = S.gen_full_pipelined(lag, q)
         S.check(ins)
