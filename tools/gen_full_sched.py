@@ -89,6 +89,35 @@ def gen_full_pipelined(lag: int = 1, quiet_order: str = "f_first"):
     return ins
 
 
+def gen_full_kw_vop2():
+    """gen_sha1_asm.gen_full with e+K+W as two VOP2 adds: kw = K + W[t] (SGPR src0), e = e + kw.  One
+    more instruction per round, but no VOP3 in the e+K+W slot (tools/ubench_full_variants.hip, h/i)."""
+    ins = []
+    R = G.Regs()
+    for t in range(80):
+        A, B, C, D, E = G.roles(t)
+        u = t + 1
+        sched = 16 <= u < 80
+        wt = f"w{t & 15}"
+        wu = f"w{u & 15}"
+        if sched:
+            ins.append(("v_bitop3_b32", "t2", f"w{(u - 3) & 15}", f"w{(u - 8) & 15}", f"w{(u - 14) & 15}", 0x96))
+        ins.append(("v_add_u32", "t3", f"k{t // 20}", wt))
+        e_src = R.rd(E)
+        ins.append(("v_add_u32", R.wr(E), e_src, "t3"))
+        ins.append(("v_alignbit_b32", "t0", R.rd(A), R.rd(A), 27))
+        if sched:
+            ins.append(("v_xor_b32", wu, "t2", wu))
+        ins.append(G._fop(t, "t1", R.rd(B), R.rd(C), R.rd(D)))
+        b_src = R.rd(B)
+        ins.append(("v_alignbit_b32", R.wr(B), b_src, b_src, 2))
+        if sched:
+            ins.append(("v_alignbit_b32", wu, wu, wu, 31))
+        ins.append(("v_add3_u32", R.rd(E), R.rd(E), "t0", "t1"))
+    assert R.cur == [f"r{i}" for i in range(5)]
+    return ins
+
+
 def check(ins, n: int = 20) -> None:
     rng = random.Random(7)
     for _ in range(n):
@@ -119,6 +148,8 @@ def check(ins, n: int = 20) -> None:
 
 
 if __name__ == "__main__":
+    check(gen_full_kw_vop2())
+    print("kw_vop2:", len(gen_full_kw_vop2()), "instr ok")
     for lag in (1, 2, 3):
         for q in ("plain", "f_first"):
             ins = gen_full_pipelined(lag, q)

@@ -56,6 +56,9 @@ def main(out_dir):
     e64 = lambda t: re.sub(r"v_add3_u32 (%\[r\d\]), (%\[[rh]\d\]), %\[k\d\], (%\[w\d+\])", r"v_add_u32_e64 \1, \2, \3", t)
     z3 = lambda t: re.sub(r"v_add3_u32 (%\[r\d\]), (%\[[rh]\d\]), %\[k\d\], (%\[w\d+\])", r"v_add3_u32 \1, \2, \3, 0", t)
     parts += [var("n", e64(ve)), var("o", z3(ve)), var("p", e64(fn))]
+    ins = S.gen_full_kw_vop2()
+    S.check(ins)
+    parts.append(fn_text("q", ins))
     for name, (lag, q) in zip("jklm", [(1, "plain"), (1, "f_first"), (2, "f_first"), (3, "f_first")]):
         ins = S.gen_full_pipelined(lag, q)
         S.check(ins)
