@@ -133,10 +133,11 @@ def test_shards_concatenate(native, oracle, kernel):
     assert bytes(out) == expect
 
 
+@pytest.mark.parametrize("L", [65536, 65539])      # 65,539: no row of the 2D column copies is dword-aligned
 @pytest.mark.parametrize("chunk", [0, 64, 4096, 65536])
 @pytest.mark.parametrize("kernel", KERNELS)
-def test_stream_from_host_matches(native, oracle, chunk, kernel):
-    L, P = 65536, 97
+def test_stream_from_host_matches(native, oracle, chunk, kernel, L):
+    P = 97
     total = L * (P - 1) + 4321
     payload = oracle.synth_fill(23, 0, total)
     pieces = bytearray(oracle.hash_pieces(payload, total, L, P))
@@ -157,6 +158,13 @@ def test_stream_from_host_matches(native, oracle, chunk, kernel):
                 avail[i >> 3] |= 0x80 >> (i & 7)
         assert ctx.verify_host(memoryview(payload)[:cut]) == oracle.verify_linear(
             payload, total, L, bytes(pieces), bytes(avail))
+        # page-locked source: 2D column copies straight from it (src pitch L)
+        hb = native.PinnedBuffer(total)
+        try:
+            hb.mv[:] = payload
+            assert ctx.verify_host(hb.mv) == expect
+        finally:
+            hb.close()
 
 
 def test_fill_synthetic_matches_oracle(native, oracle):
