@@ -23,6 +23,24 @@ __global__ __launch_bounds__(1024) void kfull(uint32_t* out, int iters, uint64_t
     if (threadIdx.x == 0) { clk[2 * blockIdx.x] = t1 - t0; clk[2 * blockIdx.x + 1] = r1 - r0; }
 }
 
+// two compressions per loop trip (the lane kernel's unroll): halves the loop's SALU + branch share
+__global__ __launch_bounds__(1024) void kfull2(uint32_t* out, int iters, uint64_t* clk) {
+    uint32_t h[5] = {threadIdx.x, 2, 3, 4, 5};
+    uint32_t w[16];
+    for (int i = 0; i < 16; i++) w[i] = threadIdx.x * (i + 1);
+    uint64_t t0 = __builtin_amdgcn_s_memtime();
+    for (int it = 0; it < iters; it += 2) {
+        uint32_t r[5];
+        tv_sha1_full(h, r, w, 0x5A827999u, 0x6ED9EBA1u, 0x8F1BBCDCu, 0xCA62C1D6u);
+        for (int i = 0; i < 5; i++) h[i] += r[i];
+        tv_sha1_full(h, r, w, 0x5A827999u, 0x6ED9EBA1u, 0x8F1BBCDCu, 0xCA62C1D6u);
+        for (int i = 0; i < 5; i++) h[i] += r[i];
+    }
+    uint64_t t1 = __builtin_amdgcn_s_memtime();
+    out[blockIdx.x * blockDim.x + threadIdx.x] = h[0] ^ h[1] ^ h[2] ^ h[3] ^ h[4] ^ w[3];
+    if (threadIdx.x == 0) clk[2 * blockIdx.x] = t1 - t0;
+}
+
 int main() {
     uint32_t* out; uint64_t* clk;
     hipMalloc(&out, 4 << 22); hipMalloc(&clk, 8 * 4096);
@@ -55,6 +73,14 @@ int main() {
         uint64_t c[2]; hipMemcpy(c, clk, 16, hipMemcpyDeviceToHost);
         printf("waves/CU=%d (1 per SIMD used)  block-0 memtime cycles per compression %.0f  (%.3f per VALU of ~597)\n",
                threads / 64, (double)c[0] / iters, (double)c[0] / iters / 597.0);
+    }
+    {
+        hipLaunchKernelGGL(kfull2, dim3(256), dim3(64), 0, 0, out, 50, clk);
+        hipLaunchKernelGGL(kfull2, dim3(256), dim3(64), 0, 0, out, iters, clk);
+        hipDeviceSynchronize();
+        uint64_t c[2]; hipMemcpy(c, clk, 16, hipMemcpyDeviceToHost);
+        printf("2 compressions per trip, waves/CU=1  block-0 memtime cycles per compression %.0f  (%.3f per VALU of ~597)\n",
+               (double)c[0] / iters, (double)c[0] / iters / 597.0);
     }
     return 0;
 }
