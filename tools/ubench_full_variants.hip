@@ -10,6 +10,7 @@
 //   j-m  tools/gen_full_sched.py pipelined schedules (real SHA-1): lag 1 plain, lag 1/2/3 f_first
 //   n  e with e+K+W as v_add_u32_e64 e, W   o  e with v_add3 e, W, 0   p  a with v_add_u32_e64 e, W
 //   q  real SHA-1: e+K+W as two VOP2 adds (tools/gen_full_sched.py gen_full_kw_vop2, 672 VALU)
+//   r  e with e+K+W after the rotl5   s  e with s_nop 0 after e+K+W   t  e with a VOP2 v_mov after e+K+W
 // Build: python3 tools/ubench_full_variants.py <dir> (writes <dir>/variants.h), then
 //   hipcc --offload-arch=gfx950 -O3 -I <dir of variants.h> tools/ubench_full_variants.hip -o tools/ubench_full_variants_bin
 // One wave per CU, two compressions per loop trip; cycles per compression from block 0's s_memtime.
@@ -35,7 +36,7 @@ __global__ __launch_bounds__(64) void k_##V(uint32_t* out, int iters, uint64_t* 
     out[blockIdx.x * 64 + threadIdx.x] = h[0] ^ h[1] ^ h[2] ^ h[3] ^ h[4] ^ w[3];               \
     if (threadIdx.x == 0) clk[blockIdx.x] = t1 - t0;                                            \
 }
-KERNEL(a) KERNEL(b) KERNEL(c) KERNEL(d) KERNEL(e) KERNEL(f) KERNEL(g) KERNEL(h) KERNEL(i) KERNEL(j) KERNEL(k) KERNEL(l) KERNEL(m) KERNEL(n) KERNEL(o) KERNEL(p) KERNEL(q)
+KERNEL(a) KERNEL(b) KERNEL(c) KERNEL(d) KERNEL(e) KERNEL(f) KERNEL(g) KERNEL(h) KERNEL(i) KERNEL(j) KERNEL(k) KERNEL(l) KERNEL(m) KERNEL(n) KERNEL(o) KERNEL(p) KERNEL(q) KERNEL(r) KERNEL(s) KERNEL(t)
 
 typedef void (*kfn)(uint32_t*, int, uint64_t*);
 
@@ -50,7 +51,8 @@ int main() {
         {"i a, VOP2 e+W", k_i, 597}, {"j lag1 plain", k_j, 597}, {"k lag1 f_first", k_k, 597},
         {"l lag2 f_first", k_l, 597}, {"m lag3 f_first", k_m, 597}, {"n e, VOP3 add_e64 e+W", k_n, 405},
         {"o e, add3 e,W,0", k_o, 405}, {"p a, VOP3 add_e64 e+W", k_p, 597},
-        {"q real: kw=K+W, e+=kw VOP2", k_q, 677}};
+        {"q real: kw=K+W, e+=kw VOP2", k_q, 677}, {"r e, e+K+W after rotl5", k_r, 405},
+        {"s e, s_nop after e+K+W", k_s, 405}, {"t e, VOP2 mov after e+K+W", k_t, 485}};
     for (int rep = 0; rep < 2; rep++)
         for (auto& x : v) {
             hipLaunchKernelGGL(x.f, dim3(256), dim3(64), 0, 0, out, 50, clk);

@@ -56,6 +56,14 @@ def main(out_dir):
     e64 = lambda t: re.sub(r"v_add3_u32 (%\[r\d\]), (%\[[rh]\d\]), %\[k\d\], (%\[w\d+\])", r"v_add_u32_e64 \1, \2, \3", t)
     z3 = lambda t: re.sub(r"v_add3_u32 (%\[r\d\]), (%\[[rh]\d\]), %\[k\d\], (%\[w\d+\])", r"v_add3_u32 \1, \2, \3, 0", t)
     parts += [var("n", e64(ve)), var("o", z3(ve)), var("p", e64(fn))]
+    # r: rounds only (e) with each e+K+W moved after the round's rotl5; s: e with s_nop 0 after each e+K+W;
+    # t: e with a VOP2 v_mov (t3) after each e+K+W (timing only)
+    ekw_re = r'(\s*"v_add3_u32 %\[r\d\], %\[[rh]\d\], %\[k\d\], %\[w\d+\]\\n"\n)(\s*"v_alignbit_b32 %\[t0\][^\n]*\n)'
+    vr = re.sub(ekw_re, r"\2\1", ve)
+    vs = re.sub(r'(\s*"v_add3_u32 %\[r\d\], %\[[rh]\d\], %\[k\d\], %\[w\d+\]\\n"\n)', r'\1    "s_nop 0\\n"\n', ve)
+    vt = re.sub(r'(\s*"v_add3_u32 %\[r\d\], %\[[rh]\d\], %\[k\d\], %\[w\d+\]\\n"\n)', r'\1    "v_mov_b32 %[t2], %[t1]\\n"\n', ve)
+    print("variants r/s/t:", vr.count("v_add3"), vs.count("s_nop 0"), vt.count("v_mov_b32"))
+    parts += [var("r", vr), var("s", vs), var("t", vt)]
     ins = S.gen_full_kw_vop2()
     S.check(ins)
     parts.append(fn_text("q", ins))
