@@ -118,6 +118,40 @@ def gen_full_kw_vop2():
     return ins
 
 
+def gen_full_bswap_next():
+    """gen_sha1_asm.gen_full plus the NEXT block's 16 byte swaps (v_perm x_t -> n_t, sel = 0x00010203),
+    one right after each of rounds 0-15's e+K+W: tools/ubench_full_variants.hip (t) found ~5 idle
+    cycles per round there that another instruction fills for free."""
+    out = []
+    t = -1
+    for op in G.gen_full():
+        out.append(op)
+        if op[0] == "v_add3_u32" and op[3].startswith("k"):   # this round's e+K+W
+            t += 1
+            if t < 16:
+                out.append(("v_perm_b32", f"n{t}", 0, f"x{t}", "sel"))
+    return out
+
+
+def check_bswap_next(ins, n: int = 8) -> None:
+    rng = random.Random(9)
+    for _ in range(n):
+        x = [rng.randrange(1 << 32) for _ in range(16)]
+        regs = {f"x{i}": x[i] for i in range(16)}
+        regs["sel"] = 0x00010203
+        block = bytes(rng.randrange(256) for _ in range(64))
+        h = [rng.randrange(1 << 32) for _ in range(5)]
+        w = list(struct.unpack(">16I", block))
+        regs.update({f"h{i}": h[i] for i in range(5)})
+        regs.update({f"k{i}": G.K[i] for i in range(4)})
+        regs.update({f"w{i}": w[i] for i in range(16)})
+        ref = dict(regs)
+        G.emulate(ins, regs)
+        G.emulate(G.gen_full(), ref)
+        assert [regs[f"r{i}"] for i in range(5)] == [ref[f"r{i}"] for i in range(5)]
+        assert [regs[f"n{i}"] for i in range(16)] == [int.from_bytes(v.to_bytes(4, "little"), "big") for v in x]
+
+
 def check(ins, n: int = 20) -> None:
     rng = random.Random(7)
     for _ in range(n):
@@ -149,6 +183,8 @@ def check(ins, n: int = 20) -> None:
 
 if __name__ == "__main__":
     check(gen_full_kw_vop2())
+    check_bswap_next(gen_full_bswap_next())
+    print("bswap_next:", len(gen_full_bswap_next()), "instr ok")
     print("kw_vop2:", len(gen_full_kw_vop2()), "instr ok")
     for lag in (1, 2, 3):
         for q in ("plain", "f_first"):

@@ -33,6 +33,28 @@ def fn_text(name, ins):
 """
 
 
+def fn_text_bswap_next(name, ins):
+    body = G.emit(ins, True)
+    n_out = ", ".join(f'[n{i}] "=&v"(n[{i}])' for i in range(16))
+    x_in = ", ".join(f'[x{i}] "v"(x[{i}])' for i in range(16))
+    return f"""__device__ __forceinline__ void tv_sha1_full_{name}(const uint32_t h[5], uint32_t r[5], uint32_t w[16],
+        const uint32_t x[16], uint32_t n[16], uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {{
+    uint32_t t0, t1, t2;
+    asm volatile(
+{body}
+    : [r0] "=&v"(r[0]), [r1] "=&v"(r[1]), [r2] "=&v"(r[2]), [r3] "=&v"(r[3]), [r4] "=&v"(r[4]),
+      [w0] "+v"(w[0]), [w1] "+v"(w[1]), [w2] "+v"(w[2]), [w3] "+v"(w[3]),
+      [w4] "+v"(w[4]), [w5] "+v"(w[5]), [w6] "+v"(w[6]), [w7] "+v"(w[7]),
+      [w8] "+v"(w[8]), [w9] "+v"(w[9]), [w10] "+v"(w[10]), [w11] "+v"(w[11]),
+      [w12] "+v"(w[12]), [w13] "+v"(w[13]), [w14] "+v"(w[14]), [w15] "+v"(w[15]),
+      [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), {n_out}
+    : [h0] "v"(h[0]), [h1] "v"(h[1]), [h2] "v"(h[2]), [h3] "v"(h[3]), [h4] "v"(h[4]), {x_in},
+      [sel] "s"(0x00010203u), [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
+    : "memory");
+}}
+"""
+
+
 def main(out_dir):
     src = open(os.path.join(HERE, "..", "torrent_amd", "csrc", "sha1_asm.h")).read()
     start = src.index("__device__ __forceinline__ void tv_sha1_full(")
@@ -64,6 +86,9 @@ def main(out_dir):
     vt = re.sub(r'(\s*"v_add3_u32 %\[r\d\], %\[[rh]\d\], %\[k\d\], %\[w\d+\]\\n"\n)', r'\1    "v_mov_b32 %[t2], %[t1]\\n"\n', ve)
     print("variants r/s/t:", vr.count("v_add3"), vs.count("s_nop 0"), vt.count("v_mov_b32"))
     parts += [var("r", vr), var("s", vs), var("t", vt)]
+    ins_u = S.gen_full_bswap_next()
+    S.check_bswap_next(ins_u)
+    parts.append(fn_text_bswap_next("u", ins_u))
     ins = S.gen_full_kw_vop2()
     S.check(ins)
     parts.append(fn_text("q", ins))
