@@ -68,7 +68,9 @@ int tv_last_error(const tv_ctx *ctx, char *buf, size_t n);
  *                  piece i has length piece.ts:16-19 and linear offset i*piece_length
  *                  (torrent.ts:165,186)
  *   shard_first, shard_count : pieces resident on this device; shard_first % 8 == 0 so the
- *                  bitfield slice is whole bytes
+ *                  bitfield slice is whole bytes; any shard_first when shard_count == 0
+ * Device and pinned allocations are kept and reused when the new geometry fits them (a run of
+ * single-piece layouts allocates once).
  * Replaces: the per-piece Storage.get(i*pieceLength, pieceLength(i)) walk (storage.ts:50-65).
  */
 int tv_set_layout(tv_ctx *ctx, uint64_t total_length, uint64_t piece_length, uint64_t n_pieces,
@@ -168,6 +170,56 @@ int tv_verify_host(tv_ctx *ctx, const uint8_t *src, uint64_t src_len, const uint
  * shard, written to digests_out (20*shard_count bytes), in piece order. */
 int tv_hash(tv_ctx *ctx, uint8_t *digests_out);
 
+/*
+ * Streamed verify through a BOUNDED pinned ring (end-to-end resume check, SURVEY 8d cfg5: the
+ * resume flow Client.add -> Storage -> bitfield -> sendBitfield, client.ts:53-67, torrent.ts:56-60,101).
+ * No resident payload and no whole-shard host buffer are needed: the library hands out requests in the
+ * order its kernels consume them, the caller (a Storage.get reader, a file reader, a generator) fills
+ * each request's pinned staging slot, and the library DMAs it to HBM over PCIe while the kernels hash the
+ * previous column.  Host memory in flight is the ring (TV_STREAM_RING_SLOTS x TV_STREAM_SLOT_BYTES).
+ *
+ *   tv_stream_begin(ctx, avail)          avail: optional shard-relative MSB-first bits (NULL = all)
+ *   loop: tv_stream_next(ctx, &req)      req.rows == 0 -> every byte has been requested
+ *         fill req.slot (row q at req.slot + q*req.width) and tv_stream_commit(ctx, &req),
+ *         or tv_stream_commit_from(ctx, &req, src, src_pitch) to copy the rows from caller memory
+ *   tv_stream_end(ctx, bitfield_out)     ceil(shard_count/8) bytes, as tv_verify
+ *
+ * A request covers `rows` consecutive pieces starting at GLOBAL piece `piece`, and bytes
+ * [offset, offset + width) of each (piece-relative; every request of one column has the same offset).
+ * Row q holds the LINEAR bytes [(piece+q)*piece_length + offset, ...) of length
+ * row_bytes(q) = min(width, piece_len(piece+q) - offset), which is `width` for every row except
+ * the short last piece's (0 past its end; piece.ts:16-19).  One request is outstanding at a time.  A piece whose bytes cannot be read
+ * (Storage.get -> null, storage.ts:50-65) is reported with tv_stream_unreadable and gets bit 0.
+ * Calls that use the resident payload fail with TV_ERR_STATE while a stream is active;
+ * tv_set_layout / tv_set_digests / tv_stream_abort end it.  Replaces: the per-piece
+ * Storage.get + digest loop (storage.ts:50-65, make_torrent.ts:28-31) of a resume check.
+ */
+#define TV_STREAM_RING_SLOTS 3
+#define TV_STREAM_SLOT_BYTES (64ull << 20)
+typedef struct tv_stream_req {
+    uint64_t piece;   /* GLOBAL index of row 0's piece */
+    uint64_t rows;    /* pieces in this request; 0 = the stream is complete */
+    uint64_t offset;  /* byte offset inside each piece (the column) */
+    uint64_t width;   /* row pitch in `slot`; row q holds tv_row_bytes(q) <= width valid bytes */
+    uint8_t *slot;    /* library-owned page-locked staging memory, rows * width bytes */
+    uint64_t seq;     /* request number (tv_stream_commit checks it) */
+} tv_stream_req;
+int tv_stream_begin(tv_ctx *ctx, const uint8_t *avail_bits);
+int tv_stream_next(tv_ctx *ctx, tv_stream_req *req);
+int tv_stream_commit(tv_ctx *ctx, const tv_stream_req *req);
+/* Rows from caller memory: row q at src + q*src_pitch (row_bytes(q) bytes).  A page-locked src
+ * (tv_host_alloc / tv_host_register) is DMA'd directly and must stay unmodified until tv_stream_end /
+ * tv_stream_abort returns; pageable memory is copied into the request's slot before the call returns. */
+int tv_stream_commit_from(tv_ctx *ctx, const tv_stream_req *req, const uint8_t *src, uint64_t src_pitch);
+/* Piece `piece` (GLOBAL, inside the shard) is unreadable: its bit will be 0. */
+int tv_stream_unreadable(tv_ctx *ctx, uint64_t piece);
+int tv_stream_end(tv_ctx *ctx, uint8_t *bitfield_out);
+/* Drop an active stream (a reader failed part-way); the ctx is usable again.  No-op when idle. */
+int tv_stream_abort(tv_ctx *ctx);
+/* Benchmarks / tests: fill the outstanding request's slot with the synthetic payload of `seed` (the
+ * bytes tv_fill_synthetic writes), generated on the host by TV_OPT_FILE_THREADS threads. */
+int tv_stream_fill_synthetic(tv_ctx *ctx, const tv_stream_req *req, uint64_t seed);
+
 /* Page-locked host memory for tv_verify_host / tv_stage sources.  A pinned source is read by
  * DMA directly (no staging memcpy); pageable memory goes through the library's pinned ring.
  * tv_host_register pins an existing range (e.g. a caller's buffer), tv_host_unregister undoes it. */
@@ -187,6 +239,11 @@ int tv_host_unregister(void *ptr);
 #define TV_OPT_FILE_THREADS 8    /* host threads (default 16): tv_stage_files' readers, and the copies of pageable
                                     tv_stage sources into the pinned ring (25.8 -> 55.8 GB/s) */
 #define TV_OPT_FILE_CONCURRENT 9 /* tv_stage_files: 1 (default) = long segments on two staging lanes, 0 = one */
+#define TV_OPT_RESIDENT 10       /* 1 (default): tv_set_layout allocates the resident payload; 0: it does not (a
+                                    streamed-only ctx, tv_stream_*; the resident calls then fail with TV_ERR_STATE).
+                                    Takes effect at the next tv_set_layout */
+#define TV_OPT_DEBUG_REBOUNCE 11 /* tests: 1 = bounce ring-resident sources through the ring again (the staging
+                                    path that once raced); slot leases must keep it exact.  Default 0 */
 int tv_set_option(tv_ctx *ctx, int key, int64_t value);
 int tv_get_option(tv_ctx *ctx, int key, int64_t *value);
 

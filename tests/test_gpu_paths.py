@@ -664,3 +664,80 @@ def test_verify_files_read_faults_are_unreadable_pieces(native, tmp_path):
         ctx.set_layout(total, L, P)
         st = ctx.stage_files([str(tmp_path / f"f{k}") for k in range(5)], [0] * 5, starts[:5], sizes)
         assert st == [0, native.TV_ERR_IO, native.TV_ERR_IO, native.TV_ERR_IO, 0]
+
+
+@pytest.mark.parametrize("concurrent", [1, 0])
+def test_ring_leases_keep_rebounced_ring_sources_exact(native, oracle, tmp_path, concurrent):
+    """The staging ring's invariant, checked deterministically: a slot stays LENT from take_slot until the
+    event after its last queued copy is recorded, and take_slot never hands out a lent slot.
+    TV_OPT_DEBUG_REBOUNCE puts back the bounce of ring-resident sources that once raced (the bounce took the
+    ring's next slots, and the third take was the slot being read, overwriting bytes still to be DMA'd).
+    With leases the bounce skips the source slot, so every byte reads back exact whatever the DMA timing:
+    an odd piece length (no staged fragment is dword-congruent, so every fragment bounces), 300 ragged
+    segments through the reader pool's packed slots on lane 0 and windowed preads on lane 1."""
+    import random
+    rnd = random.Random(13)
+    L, P = 65539, 300
+    total = L * P - 91
+    payload = oracle.synth_fill(29, 0, total)
+    bounds = [0] + sorted(rnd.sample(range(1, total), 299)) + [total]
+    paths, fos, lins, lens = [], [], [], []
+    for k in range(300):
+        a, b = bounds[k], bounds[k + 1]
+        pre = rnd.randrange(4)
+        path = tmp_path / f"r{k:03d}.bin"
+        path.write_bytes(bytes(pre) + bytes(payload[a:b]))
+        paths.append(str(path)); fos.append(pre); lins.append(a); lens.append(b - a)
+    with native.Context(0) as ctx:
+        ctx.set_option(native.TV_OPT_DEBUG_REBOUNCE, 1)
+        assert ctx.get_option(native.TV_OPT_DEBUG_REBOUNCE) == 1
+        ctx.set_option(native.TV_OPT_FILE_DIRECT, 0)
+        ctx.set_option(native.TV_OPT_FILE_CHUNK, 64 << 10)
+        ctx.set_option(native.TV_OPT_FILE_DIRECT_MIN, sorted(lens)[150])  # half the segments on lane 1
+        ctx.set_option(native.TV_OPT_FILE_CONCURRENT, concurrent)
+        ctx.set_layout(total, L, P)
+        ctx.set_digests(oracle.hash_pieces(payload, total, L, P))
+        ctx.fill_synthetic(77)
+        assert ctx.stage_files(paths, fos, lins, lens) == [0] * 300
+        out = bytearray(total)
+        ctx.read(0, out)
+        assert out == payload
+        bf = ctx.verify()
+        assert all(bf[i >> 3] >> (7 - (i & 7)) & 1 for i in range(P))
+        # pageable tv_stage through the ring with the bounce on, at an odd source alignment
+        ctx.fill_synthetic(78)
+        src = bytearray(3) + payload
+        ctx.stage(0, memoryview(src)[3:])
+        ctx.read(0, out)
+        assert out == payload
+
+
+def test_set_layout_reuses_allocations_across_geometries(native, oracle):
+    """One context through a sequence of geometries (verify_piece-sized, bigger, smaller, empty, a shard,
+    the stream path between them): tv_set_layout keeps the allocations that fit, and no stale digest,
+    availability bit or payload byte of an earlier geometry leaks into a later result."""
+    cases = [(262144, 1, 262144, 0, 1), (262144, 1, 1000, 0, 1), (4096, 300, 17, 8, 200), (4096, 10, 4096, 0, 10),
+             (65536, 3, 100, 0, 3), (1 << 20, 0, 0, 0, 0), (262144, 1, 262144, 0, 1), (8192, 600, 8192, 0, 600),
+             (4096, 2, 5, 0, 2)]
+    with native.Context(0) as ctx:
+        for n, (L, P, last, first, count) in enumerate(cases):
+            total = L * (P - 1) + last if P else 0
+            payload = oracle.synth_fill(200 + n, 0, total)
+            pieces = bytearray(oracle.hash_pieces(payload, total, L, P)) if P else bytearray()
+            if P:
+                pieces[20 * (P // 2) + 1] ^= 4
+            exp = oracle.verify_linear(payload, total, L, bytes(pieces)) if P else b""
+            want = bytearray((count + 7) // 8)
+            for j in range(count):
+                i = first + j
+                if (exp[i >> 3] >> (7 - (i & 7))) & 1:
+                    want[j >> 3] |= 0x80 >> (j & 7)
+            ctx.set_layout(total, L, P, first, count)
+            ctx.set_digests(bytes(pieces))
+            if total:
+                ctx.stage(0, payload)
+            assert ctx.verify() == bytes(want), n
+            assert ctx.verify_host(memoryview(payload)[first * L:]) == bytes(want), n
+            if count:
+                assert ctx.verify_list(list(range(first, first + count))) == bytes(
+                    (want[j >> 3] >> (7 - (j & 7))) & 1 for j in range(count)), n

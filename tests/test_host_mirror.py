@@ -379,3 +379,50 @@ def test_cli_usage_without_a_gpu(capsys):
     from torrent_amd.make_torrent import main as make_main
     assert verify_main([]) == 2 and "python -m torrent_amd verify" in capsys.readouterr().out
     assert make_main(["--help"]) == 0 and "make_torrent [-c <comment>] -t <tracker url> <target>" in capsys.readouterr().out
+
+
+def test_files_shard_zero_length_segments_match_fs_storage(tmp_path, monkeypatch):
+    """Zero-length segments (storage.ts:109-110 `fileEnd >= offset`; zero-length files) are still opened by
+    fsStorage.get (storage.ts:158): a directory in a zero-length file's place, or a zero-length file in a
+    missing directory, makes the piece null; a missing zero-length file in an existing directory is
+    created there and reads fine.  verify_files' plan gives the same bits as Storage(fs_storage).get per
+    piece (run on a copy of the tree, since that get creates files), without creating any file itself."""
+    import shutil
+    from torrent_amd import verify
+    from torrent_amd.storage import Storage, fs_storage
+
+    L = 4096
+    names = [("a",), ("z_dir",), ("b",), ("nodir", "z"), ("c",), ("z_missing",), ("d",), ("z_ok",), ("e",)]
+    sizes = [3 * L, 0, 2 * L + 100, 0, L - 100, 0, 2 * L, 0, L + 7]   # a, b end exactly on piece starts
+    payload = bytes((k * 13 + 1) & 0xFF for k in range(sum(sizes)))
+    P = -(-len(payload) // L)
+    info = make_info(L, bytes(20 * P), "t", files=[FileInfo(n, list(p)) for n, p in zip(sizes, names)])
+    root = tmp_path / "t0"
+    off = 0
+    for n, p in zip(sizes, names):
+        q = root.joinpath(*p)
+        if p == ("z_dir",):
+            q.mkdir(parents=True)
+        elif p in (("nodir", "z"), ("z_missing",)):
+            pass                                                   # missing (nodir/ does not exist)
+        else:
+            q.parent.mkdir(parents=True, exist_ok=True)
+            q.write_bytes(payload[off:off + n])
+        off += n
+    ref_root = tmp_path / "t1"
+    shutil.copytree(root, ref_root)
+    monkeypatch.chdir(tmp_path)
+    ref = Storage(fs_storage, info, str(ref_root))
+    expect = [ref.get(i * L, piece_length(i, info)) is not None for i in range(P)]
+    assert not all(expect) and any(expect)
+    before = sorted(str(x) for x in root.rglob("*"))
+    st = Storage(fs_storage, info, str(root))
+    got = []
+    for first, count in verify.shard_ranges(P, 2):
+        if not count:
+            continue
+        hi = (first + count - 1) * L + piece_length(first + count - 1, info)
+        avail = verify._files_shard(_ImageCtx(info.length, first * L, hi), info, st, first, count, threads=2)
+        got += [bool((avail[j >> 3] >> (7 - (j & 7))) & 1) for j in range(count)]
+    assert got == expect
+    assert sorted(str(x) for x in root.rglob("*")) == before      # nothing created

@@ -16,7 +16,9 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libtorrent_verify.so")
 SOURCES = ["tv_kernels.hip", "tv_api.hip"]
+HOST_SOURCES = ["tv_host.cpp"]          # host-only C++ (no device code): the host compiler
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CXX = os.environ.get("CXX", "g++")
 ARCH = os.environ.get("TV_OFFLOAD_ARCH", "gfx950")
 
 
@@ -33,8 +35,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if force or _newer(header, [gen]):
         subprocess.check_call([sys.executable, gen, "--out", header])
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
-    deps = srcs + [header, os.path.join(CSRC, "tv_internal.h"),
-                   os.path.join(ROOT, "include", "torrent_verify.h")]
+    host_srcs = [os.path.join(CSRC, s) for s in HOST_SOURCES]
+    deps = srcs + host_srcs + [header, os.path.join(CSRC, "tv_internal.h"), os.path.join(CSRC, "tv_host.h"),
+                               os.path.join(ROOT, "include", "torrent_verify.h")]
     if not (force or _newer(LIB, deps)):
         return LIB
     objs = []
@@ -42,6 +45,13 @@ def build(force: bool = False, verbose: bool = False) -> str:
         o = os.path.join(CSRC, os.path.basename(s) + ".o")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
                "-I", os.path.join(ROOT, "include"), "-c", s, "-o", o]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd)
+        objs.append(o)
+    for s in host_srcs:
+        o = os.path.join(CSRC, os.path.basename(s) + ".o")
+        cmd = [CXX, "-O3", "-std=c++17", "-fPIC", "-Wall", "-c", s, "-o", o]
         if verbose:
             print(" ".join(cmd))
         subprocess.check_call(cmd)

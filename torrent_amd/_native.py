@@ -29,11 +29,25 @@ TV_OPT_FILE_CHUNK = 6
 TV_OPT_FILE_DIRECT_MIN = 7
 TV_OPT_FILE_THREADS = 8
 TV_OPT_FILE_CONCURRENT = 9
+TV_OPT_RESIDENT = 10
+TV_OPT_DEBUG_REBOUNCE = 11
+
+TV_STREAM_RING_SLOTS = 3
+TV_STREAM_SLOT_BYTES = 64 << 20
 
 KERNEL_AUTO, KERNEL_LANE, KERNEL_SPLIT = 0, 1, 2
 
-# every symbol include/torrent_verify.h declares: (name, restype, argtypes)
 _u64, _i64, _int, _p = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p
+
+
+class StreamReq(ctypes.Structure):
+    """tv_stream_req (include/torrent_verify.h): rows [piece, piece+rows) x bytes [offset, offset+width)."""
+    _fields_ = [("piece", _u64), ("rows", _u64), ("offset", _u64), ("width", _u64), ("slot", _p), ("seq", _u64)]
+
+
+_REQ = ctypes.POINTER(StreamReq)
+
+# every symbol include/torrent_verify.h declares: (name, restype, argtypes)
 SYMBOLS = [
     ("tv_abi_version", _int, []),
     ("tv_device_count", _int, [ctypes.POINTER(_int)]),
@@ -51,6 +65,14 @@ SYMBOLS = [
     ("tv_verify_host", _int, [_p, _p, _u64, _p, _p]),
     ("tv_verify_list", _int, [_p, _p, _u64, _p]),
     ("tv_hash", _int, [_p, _p]),
+    ("tv_stream_begin", _int, [_p, _p]),
+    ("tv_stream_next", _int, [_p, _REQ]),
+    ("tv_stream_commit", _int, [_p, _REQ]),
+    ("tv_stream_commit_from", _int, [_p, _REQ, _p, _u64]),
+    ("tv_stream_unreadable", _int, [_p, _u64]),
+    ("tv_stream_end", _int, [_p, _p]),
+    ("tv_stream_abort", _int, [_p]),
+    ("tv_stream_fill_synthetic", _int, [_p, _REQ, _u64]),
     ("tv_set_option", _int, [_p, _int, _i64]),
     ("tv_get_option", _int, [_p, _int, ctypes.POINTER(_i64)]),
     ("tv_last_timing", _int, [_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
@@ -207,6 +229,7 @@ class Context:
             shard_count = n_pieces - shard_first
         self._check(self._L.tv_set_layout(self._h, total_length, piece_length, n_pieces, shard_first, shard_count))
         self.shard_first, self.shard_count = shard_first, shard_count
+        self.total_length, self.piece_length, self.n_pieces = total_length, piece_length, n_pieces
 
     def set_digests(self, pieces_raw: bytes) -> None:
         a, keep = _addr(pieces_raw)
@@ -295,6 +318,61 @@ class Context:
         out = ctypes.create_string_buffer(n)
         self._check(self._L.tv_verify_list(self._h, ctypes.cast(arr, _p), n, out))
         return out.raw[:n]
+
+    # -- streamed verify (tv_stream_*): bounded pinned ring, end-to-end resume check ----
+    def stream_begin(self, avail_bits=None) -> None:
+        a, keep = _addr(avail_bits)
+        self._check(self._L.tv_stream_begin(self._h, a))
+        del keep
+
+    def stream_next(self) -> StreamReq:
+        """The next request (req.rows == 0: every byte has been requested)."""
+        req = StreamReq()
+        self._check(self._L.tv_stream_next(self._h, ctypes.byref(req)))
+        return req
+
+    def row_bytes(self, req: StreamReq, q: int) -> int:
+        """Valid bytes of row q: min(width, piece_len - offset) (piece.ts:16-19)."""
+        i = req.piece + q
+        L, P, total = self.piece_length, self.n_pieces, self.total_length
+        plen = total % L if (i == P - 1 and total % L) else L
+        return max(0, min(req.width, plen - req.offset))
+
+    def stream_slot(self, req: StreamReq) -> memoryview:
+        """Writable view of the request's pinned slot: row q at [q*width, q*width + row_bytes(q))."""
+        n = req.rows * req.width
+        return memoryview((ctypes.c_char * n).from_address(req.slot)).cast("B")
+
+    def stream_commit(self, req: StreamReq) -> None:
+        self._check(self._L.tv_stream_commit(self._h, ctypes.byref(req)))
+
+    def stream_commit_from(self, req: StreamReq, src, pitch: int, src_offset: int = 0) -> None:
+        """Rows from caller memory: row q at src[src_offset + q*pitch:][:row_bytes(q)] (bounds-checked)."""
+        mv = memoryview(src).cast("B")
+        need = 0   # end of the last row that has bytes (only the short last piece's row can have fewer)
+        for q in (req.rows - 1, req.rows - 2):
+            if q >= 0 and self.row_bytes(req, q):
+                need = src_offset + q * pitch + self.row_bytes(req, q)
+                break
+        if need > mv.nbytes or src_offset < 0:
+            raise ValueError(f"stream_commit_from: the rows need {need} bytes of src, it has {mv.nbytes}")
+        a, keep = _addr(src)
+        self._check(self._L.tv_stream_commit_from(self._h, ctypes.byref(req), (a or 0) + src_offset, pitch))
+        del keep
+
+    def stream_unreadable(self, piece: int) -> None:
+        self._check(self._L.tv_stream_unreadable(self._h, piece))
+
+    def stream_fill_synthetic(self, req: StreamReq, seed: int) -> None:
+        self._check(self._L.tv_stream_fill_synthetic(self._h, ctypes.byref(req), seed))
+
+    def stream_end(self) -> bytes:
+        out = ctypes.create_string_buffer(max(1, self._nbits()))
+        self._check(self._L.tv_stream_end(self._h, out))
+        return out.raw[: self._nbits()]
+
+    def stream_abort(self) -> None:
+        self._check(self._L.tv_stream_abort(self._h))
 
     def hash(self) -> bytes:
         out = ctypes.create_string_buffer(max(1, 20 * self.shard_count))

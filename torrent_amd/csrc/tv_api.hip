@@ -13,24 +13,105 @@
 #include <algorithm>
 #include <atomic>
 #include <cerrno>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "../../include/torrent_verify.h"
+#include "tv_host.h"
 #include "tv_internal.h"
 
 namespace {
 
 thread_local std::string g_thread_error;
 
-constexpr uint64_t kSlack = 256;               // bytes past the last resident piece (tail over-read)
-constexpr int kRingSlots = 3;                  // pinned staging buffers
-constexpr size_t kRingSlotBytes = 64ull << 20;
+constexpr uint64_t kSlack = 256;                          // bytes past the last resident piece (tail over-read)
+constexpr int kRingSlots = TV_STREAM_RING_SLOTS;          // pinned staging buffers per lane
+constexpr size_t kRingSlotBytes = TV_STREAM_SLOT_BYTES;
+
+// Persistent host workers (one pool per staging lane): run(threads, tasks, fn) calls fn(0..tasks-1) on up
+// to `threads` threads, the caller included, and returns when every task is done.  Spawning threads for
+// every 64 MiB staging slot cost ~0.3 ms a slot, a quarter of the slot's PCIe time.
+class Pool {
+  public:
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    void run(int threads, uint64_t tasks, const std::function<void(uint64_t)>& fn) {
+        const uint64_t t = std::min<uint64_t>((uint64_t)std::max(1, threads), tasks);
+        if (t <= 1) {
+            for (uint64_t q = 0; q < tasks; q++) fn(q);
+            return;
+        }
+        std::unique_lock<std::mutex> lk(mu_);
+        while (th_.size() < t - 1) th_.emplace_back([this] { loop(); });
+        fn_ = &fn;
+        tasks_ = tasks;
+        next_ = 0;
+        open_ = (int)t - 1;
+        gen_++;
+        lk.unlock();
+        cv_.notify_all();
+        work();
+        lk.lock();
+        open_ = 0;  // no late joiner may start on this run once the caller has seen every task claimed
+        done_.wait(lk, [&] { return running_ == 0; });
+    }
+
+  private:
+    void work() {
+        for (uint64_t q = next_++; q < tasks_; q = next_++) (*fn_)(q);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return stop_ || (gen_ != seen && open_ > 0); });
+            if (stop_) return;
+            seen = gen_;
+            open_--;
+            running_++;
+            lk.unlock();
+            work();
+            lk.lock();
+            if (--running_ == 0) done_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(uint64_t)>* fn_ = nullptr;
+    uint64_t tasks_ = 0;
+    std::atomic<uint64_t> next_{0};
+    int open_ = 0, running_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+// One streamed verify (tv_stream_*): columns of C bytes of every shard piece flow host -> pinned ring
+// slot -> device chunk buffer (two, ping-pong) -> one kernel launch per column.
+struct StreamState {
+    bool active = false;
+    bool outstanding = false;  // a request (and its ring slot) is lent to the caller
+    int slot = -1;             // the lent ring slot (lane 0)
+    tv_stream_req req{};
+    uint64_t C = 0, row_pitch = 0, ncol = 0, col = 0, row = 0, rows_per_req = 0, seq = 0;
+    int kernel = 0;
+    bool k0 = false;           // ev_k0 recorded (first launch queued)
+    TvPieces p{};
+    std::vector<uint8_t> av;   // shard-relative availability bits, applied to the bitfield at the end
+};
 
 }  // namespace
 
@@ -58,6 +139,13 @@ struct tv_ctx {
     bool file_concurrent = true;         // tv_stage_files: long segments on two staging lanes
     uint64_t file_direct_min = 32ull << 20;  // tv_stage_files: segments >= this take the tv_stage_file path
     int file_threads = 16;                   // tv_stage_files: reader threads
+    bool resident = true;                    // TV_OPT_RESIDENT
+    bool debug_rebounce = false;             // TV_OPT_DEBUG_REBOUNCE
+
+    // allocation capacities (tv_set_layout reuses what fits)
+    uint64_t cap_payload = 0;   // bytes of d_payload
+    uint64_t cap_count = 0;     // pieces of d_digests / d_state / d_hash
+    uint64_t cap_words = 0;     // 64-bit words of d_avail / d_base_avail / h_avail / d_out
 
     // device memory
     uint8_t* d_payload = nullptr;
@@ -80,17 +168,27 @@ struct tv_ctx {
     std::vector<uint8_t> digest_ok;   // shard-relative MSB-first bits: digest slice is 20 bytes
     std::vector<uint8_t> base_avail;  // host copy of d_base_avail (bit_words * 8 bytes)
 
-    // pinned staging ring
+    // pinned staging ring.  A slot is LENT from take_slot until release_slot records its event after the
+    // last copy queued from it; take_slot never hands out a lent slot (it takes the next free one), so a
+    // copy can never be overwritten by a later take of the same lane, whatever the DMA timing.
     uint8_t* ring[kRingSlots] = {nullptr, nullptr, nullptr};
     hipEvent_t ring_ev[kRingSlots] = {nullptr, nullptr, nullptr};
+    bool ring_lent[kRingSlots] = {false, false, false};
     int ring_next = 0;
     // lane 1 (copy_stream2 + ring2): tv_stage_files runs its long segments on it beside the reader pool
     uint8_t* ring2[kRingSlots] = {nullptr, nullptr, nullptr};
     hipEvent_t ring2_ev[kRingSlots] = {nullptr, nullptr, nullptr};
+    bool ring2_lent[kRingSlots] = {false, false, false};
     int ring2_next = 0;
+    Pool pool[2];                     // host workers of lane 0 / lane 1
     std::mutex err_mu;                // fail() may run on a tv_stage_files helper thread
     uint8_t* h_bits = nullptr;        // pinned bitfield bounce buffer
     size_t h_bits_cap = 0;
+
+    // streamed verify (tv_stream_*)
+    StreamState st;
+    hipEvent_t col_ev[2] = {nullptr, nullptr};   // copies of the column into chunk buffer k queued before it
+    hipEvent_t done_ev[2] = {nullptr, nullptr};  // the kernel that last read chunk buffer k
 
     // last call
     float kernel_ms = 0.f, total_ms = 0.f;
@@ -129,16 +227,31 @@ uint64_t piece_len(const tv_ctx* c, uint64_t i) {  // piece.ts:16-19
 inline void set_bit(uint8_t* bf, uint64_t i) { bf[i >> 3] |= (uint8_t)(0x80u >> (i & 7)); }
 inline bool get_bit(const uint8_t* bf, uint64_t i) { return (bf[i >> 3] >> (7 - (i & 7))) & 1; }
 
-void free_device(tv_ctx* c) {
+void free_payload(tv_ctx* c) {
     (void)hipFree(c->d_payload); c->d_payload = nullptr;
+    c->cap_payload = 0;
+}
+
+void free_per_piece(tv_ctx* c) {
     (void)hipFree(c->d_digests); c->d_digests = nullptr;
+    (void)hipFree(c->d_state); c->d_state = nullptr;
+    (void)hipFree(c->d_hash); c->d_hash = nullptr;
+    c->cap_count = 0;
+}
+
+void free_words(tv_ctx* c) {
     (void)hipFree(c->d_avail); c->d_avail = nullptr;
     (void)hipFree(c->d_base_avail); c->d_base_avail = nullptr;
     if (c->ev_avail) (void)hipEventSynchronize(c->ev_avail);
     (void)hipHostFree(c->h_avail); c->h_avail = nullptr;
     (void)hipFree(c->d_out); c->d_out = nullptr;
-    (void)hipFree(c->d_state); c->d_state = nullptr;
-    (void)hipFree(c->d_hash); c->d_hash = nullptr;
+    c->cap_words = 0;
+}
+
+void free_device(tv_ctx* c) {
+    free_payload(c);
+    free_per_piece(c);
+    free_words(c);
     for (auto& p : c->d_chunk) { (void)hipFree(p); p = nullptr; }
     c->chunk_bytes = 0;
     (void)hipFree(c->d_list); c->d_list = nullptr;
@@ -146,15 +259,23 @@ void free_device(tv_ctx* c) {
     c->list_cap = 0;
 }
 
+// An allocation of `cap` units is reused for `need` units when it holds them and is not more than twice
+// (or 64 Mi units) larger: a stream of small layouts after a big one must not pin the big one forever.
+bool reuse_fits(uint64_t need, uint64_t cap) {
+    return need <= cap && (cap <= (64ull << 20) || need >= cap / 2);
+}
+
 // Staging lane `which`: 0 = copy_stream + ring, 1 = copy_stream2 + ring2.  Lane 1 is used only by
 // tv_stage_files' helper thread, so the two lanes never share a ring slot or a stream.
 struct RingRef {
     uint8_t** buf;
     hipEvent_t* ev;
+    bool* lent;
     int* next;
 };
 RingRef ring_ref(tv_ctx* c, int which) {
-    return which ? RingRef{c->ring2, c->ring2_ev, &c->ring2_next} : RingRef{c->ring, c->ring_ev, &c->ring_next};
+    return which ? RingRef{c->ring2, c->ring2_ev, c->ring2_lent, &c->ring2_next}
+                 : RingRef{c->ring, c->ring_ev, c->ring_lent, &c->ring_next};
 }
 
 hipStream_t lane_stream(const tv_ctx* c, int which) { return which ? c->copy_stream2 : c->copy_stream; }
@@ -178,17 +299,54 @@ int ensure_hbits(tv_ctx* c, size_t bytes) {
     return TV_OK;
 }
 
-// Take the next pinned ring slot (waiting for its previous copy to finish).
+// Lend the next free pinned ring slot of lane `which` (waiting for the copies queued from it before its
+// last release).  A slot that is still lent -- the source of copies that are being queued right now -- is
+// never handed out: the next free one is taken instead.  All lent: TV_ERR_STATE (a caller bug, never a
+// silent overwrite).
 int take_slot(tv_ctx* c, int* slot, int which = 0) {
     int rc = ensure_ring(c, which);
     if (rc) return rc;
     RingRef r = ring_ref(c, which);
-    int s = *r.next;
-    *r.next = (s + 1) % kRingSlots;
-    TV_HIP(c, hipEventSynchronize(r.ev[s]));
-    *slot = s;
+    for (int k = 0; k < kRingSlots; k++) {
+        const int s = (*r.next + k) % kRingSlots;
+        if (r.lent[s]) continue;
+        *r.next = (s + 1) % kRingSlots;
+        TV_HIP(c, hipEventSynchronize(r.ev[s]));
+        r.lent[s] = true;
+        *slot = s;
+        return TV_OK;
+    }
+    return fail(c, TV_ERR_STATE, "every staging slot of lane %d is lent out", which);
+}
+
+// Return a lent slot: its event is recorded on the lane's copy stream, after every copy queued from it.
+int release_slot(tv_ctx* c, int slot, int which = 0) {
+    RingRef r = ring_ref(c, which);
+    r.lent[slot] = false;
+    TV_HIP(c, hipEventRecord(r.ev[slot], lane_stream(c, which)));
     return TV_OK;
 }
+
+// A lent slot that goes back to the ring on every exit of its scope (error paths included).
+struct SlotLease {
+    tv_ctx* c;
+    int lane;
+    int s = -1;
+    SlotLease(tv_ctx* ctx, int l) : c(ctx), lane(l) {}
+    ~SlotLease() {
+        if (s >= 0) (void)release_slot(c, s, lane);
+        (void)hipGetLastError();
+    }
+    SlotLease(const SlotLease&) = delete;
+    SlotLease& operator=(const SlotLease&) = delete;
+    int take() { return take_slot(c, &s, lane); }
+    int release() {
+        const int k = s;
+        s = -1;
+        return k >= 0 ? release_slot(c, k, lane) : TV_OK;
+    }
+    uint8_t* ptr() const { return ring_ref(c, lane).buf[s]; }
+};
 
 // Base availability of every shard piece, computed once per tv_set_digests and kept in HBM: the
 // digest slice is complete (metainfo.ts:111) and the piece's bytes lie inside the torrent (piece.ts:16-19
@@ -256,9 +414,14 @@ TvPieces resident_launch(const tv_ctx* c) {
     return p;
 }
 
-int require_layout(tv_ctx* c, bool need_digests) {
+// The state every non-stream call needs.  need_resident: the call reads or writes the resident payload
+// (absent with TV_OPT_RESIDENT = 0).  Calls sharing the output / chunk buffers wait for a stream to end.
+int require_layout(tv_ctx* c, bool need_digests, bool need_resident = false) {
     if (!c->has_layout) return fail(c, TV_ERR_STATE, "tv_set_layout has not been called");
     if (need_digests && !c->digests_set) return fail(c, TV_ERR_STATE, "tv_set_digests has not been called");
+    if (c->st.active) return fail(c, TV_ERR_STATE, "a stream is active (finish it with tv_stream_end or tv_stream_abort)");
+    if (need_resident && c->count && !c->d_payload)
+        return fail(c, TV_ERR_STATE, "no resident payload (the layout was set with TV_OPT_RESIDENT = 0): use tv_stream_*");
     return TV_OK;
 }
 
@@ -282,41 +445,24 @@ int finish_timing(tv_ctx* c) {
 
 // Host memcpy into a pinned ring slot, split over up to `threads` threads in 4 MiB parts when it is
 // long (one core copies pageable memory at well under the PCIe rate).
-void copy_into_ring(uint8_t* dst, const uint8_t* src, uint64_t n, int threads) {
+void copy_into_ring(Pool& pool, uint8_t* dst, const uint8_t* src, uint64_t n, int threads) {
     constexpr uint64_t kPart = 4ull << 20;
     const uint64_t parts = (n + kPart - 1) / kPart;
-    const int t = (int)std::min<uint64_t>((uint64_t)std::max(1, threads), parts);
-    if (t <= 1) {
-        memcpy(dst, src, n);
-        return;
-    }
-    std::atomic<uint64_t> next{0};
-    auto work = [&]() {
-        for (uint64_t q = next++; q < parts; q = next++) {
-            const uint64_t o = q * kPart;
-            memcpy(dst + o, src + o, std::min(kPart, n - o));
-        }
-    };
-    std::vector<std::thread> th;
-    for (int i = 1; i < t; i++) th.emplace_back(work);
-    work();
-    for (auto& x : th) x.join();
+    pool.run(threads, parts, [&](uint64_t q) {
+        const uint64_t o = q * kPart;
+        memcpy(dst + o, src + o, std::min(kPart, n - o));
+    });
 }
 
-// Gather k rows of `width` bytes at pitch `pitch` from src into dst (packed), on up to `threads` threads.
-void gather_rows(uint8_t* dst, const uint8_t* src, uint64_t width, uint64_t pitch, uint64_t k, int threads) {
+// Gather k rows of `width` bytes at pitch `pitch` from src into dst (packed at pitch width), on up to
+// `threads` threads.
+void gather_rows(Pool& pool, uint8_t* dst, const uint8_t* src, uint64_t width, uint64_t pitch, uint64_t k,
+                 int threads) {
     const uint64_t per = std::max<uint64_t>(1, (4ull << 20) / std::max<uint64_t>(1, width));  // rows per task
     const uint64_t tasks = (k + per - 1) / per;
-    const int t = (int)std::min<uint64_t>((uint64_t)std::max(1, threads), tasks);
-    std::atomic<uint64_t> next{0};
-    auto work = [&]() {
-        for (uint64_t q = next++; q < tasks; q = next++)
-            for (uint64_t r = q * per; r < std::min(k, (q + 1) * per); r++) memcpy(dst + r * width, src + r * pitch, width);
-    };
-    std::vector<std::thread> th;
-    for (int i = 1; i < t; i++) th.emplace_back(work);
-    work();
-    for (auto& x : th) x.join();
+    pool.run(threads, tasks, [&](uint64_t q) {
+        for (uint64_t r = q * per; r < std::min(k, (q + 1) * per); r++) memcpy(dst + r * width, src + r * pitch, width);
+    });
 }
 
 // One host -> device copy on the lane's copy stream, dword-aligned.  The DMA engine moves 1-byte-aligned
@@ -348,7 +494,6 @@ int dma_h2d(tv_ctx* c, uint8_t* dst, const uint8_t* src, uint64_t n, int lane = 
 int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n, bool pinned, int lane = 0,
                bool src_in_ring = false) {
     hipStream_t cs = lane_stream(c, lane);
-    RingRef ring = ring_ref(c, lane);
     while (n) {
         const uint64_t i = pos / c->L, within = pos % c->L;
         const uint64_t plen = piece_len(c, i);
@@ -356,13 +501,15 @@ int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n, bool pin
         const bool whole = within == 0 && plen == c->L && n >= c->L;
         // A pinned source whose alignment cannot match the destination's (mod 4; whole-piece rows need
         // it at 0 mod 4 and L % 4 == 0) goes through the ring instead: one memcpy, then aligned DMA.
-        const bool via_ring = !src_in_ring &&
+        // (TV_OPT_DEBUG_REBOUNCE re-enables the bounce for ring-resident sources: the slot lease then
+        // keeps the source slot out of the bounce's reach.)
+        const bool via_ring = (!src_in_ring || c->debug_rebounce) &&
                               (!pinned || (whole ? (((uintptr_t)src & 3) != 0 && c->L % 4 == 0)
                                                  : (((uintptr_t)src ^ (uintptr_t)dst) & 3) != 0));
         const uint64_t cap = via_ring ? (uint64_t)kRingSlotBytes - 4 : UINT64_MAX;
-        int slot = -1;
+        SlotLease slot(c, lane);
         if (via_ring) {
-            int rc = take_slot(c, &slot, lane);
+            int rc = slot.take();
             if (rc) return rc;
         }
         uint64_t bytes;
@@ -372,8 +519,8 @@ int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n, bool pin
             const uint64_t last_full = (c->total % c->L) ? c->P - 1 : c->P;  // first index that is not full
             k = std::min<uint64_t>(k, (last_full > i) ? last_full - i : 1);
             bytes = k * c->L;
-            const uint8_t* from = via_ring ? ring.buf[slot] : src;
-            if (via_ring) copy_into_ring(ring.buf[slot], src, bytes, c->file_threads);
+            const uint8_t* from = via_ring ? slot.ptr() : src;
+            if (via_ring) copy_into_ring(c->pool[lane], slot.ptr(), src, bytes, c->file_threads);
             TV_HIP(c, hipMemcpy2DAsync(dst, c->stride, from, c->L, c->L, k, hipMemcpyHostToDevice, cs));
         } else {
             bytes = std::min<uint64_t>({n, plen > within ? plen - within : 0, cap});
@@ -381,14 +528,17 @@ int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n, bool pin
                                         (unsigned long long)i);
             const uint8_t* from = src;
             if (via_ring) {  // place the bytes at the destination's alignment inside the slot
-                uint8_t* r = ring.buf[slot] + ((uintptr_t)dst & 3);
-                copy_into_ring(r, src, bytes, c->file_threads);
+                uint8_t* r = slot.ptr() + ((uintptr_t)dst & 3);
+                copy_into_ring(c->pool[lane], r, src, bytes, c->file_threads);
                 from = r;
             }
             int rc = dma_h2d(c, dst, from, bytes, lane);
             if (rc) return rc;
         }
-        if (via_ring) TV_HIP(c, hipEventRecord(ring.ev[slot], cs));
+        if (via_ring) {
+            int rc = slot.release();
+            if (rc) return rc;
+        }
         pos += bytes;
         src += bytes;
         n -= bytes;
@@ -537,6 +687,188 @@ struct FileWindows {
     }
 };
 
+// ---- streamed verify (tv_stream_*; tv_verify_host runs on it too) ------------------------------------
+//
+// Column `col` carries bytes [col*C, col*C + C) of every shard piece.  Its rows arrive as requests of up to
+// one ring slot (64 MiB) each, filled by the caller, and are DMA'd from the slot into device chunk buffer
+// col & 1 (row pitch C + 256).  When a column's last request is committed, one kernel launch hashes it on the
+// compute stream (chaining values persist in d_state; the last column pads, compares and writes the
+// bitfield) while the next column's requests fill the other buffer.  Host memory in flight: the ring.
+
+uint64_t row_bytes(const tv_ctx* c, uint64_t piece, uint64_t offset, uint64_t width) {  // piece.ts:16-19
+    const uint64_t plen = piece_len(c, piece);
+    return plen > offset ? std::min(width, plen - offset) : 0;
+}
+
+// Drop an active stream: give its lent slot back and let the queued copies and kernels drain.
+void stream_abort_locked(tv_ctx* c) {
+    StreamState& st = c->st;
+    if (!st.active) return;
+    if (st.outstanding && st.slot >= 0) (void)release_slot(c, st.slot, 0);
+    (void)hipStreamSynchronize(c->copy_stream);
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipGetLastError();
+    st = StreamState{};
+}
+
+// Column width: TV_OPT_STREAM_CHUNK, or ~512 MiB columns (64 KiB .. L); a multiple of 64, at most one slot.
+uint64_t stream_column(const tv_ctx* c) {
+    uint64_t C = c->stream_chunk;
+    if (!C) {
+        C = 64ull << 10;
+        while (C * 2 <= c->L && C * 2 * c->count <= (512ull << 20)) C *= 2;
+    }
+    C = std::min<uint64_t>((C / 64) * 64, ((c->L + 63) / 64) * 64);
+    return std::max<uint64_t>(64, std::min<uint64_t>(C, kRingSlotBytes));
+}
+
+int stream_begin_locked(tv_ctx* c, const uint8_t* avail_bits) {
+    StreamState& st = c->st;
+    st = StreamState{};
+    st.av.assign((c->count + 7) / 8, 0xFF);
+    if (avail_bits) memcpy(st.av.data(), avail_bits, st.av.size());
+    if (c->count == 0) {  // nothing to hash: the first tv_stream_next reports completion
+        st.active = true;
+        return TV_OK;
+    }
+    st.C = stream_column(c);
+    st.row_pitch = st.C + 256;  // (tail over-read slack per row)
+    const uint64_t need = st.row_pitch * c->count + kSlack;
+    if (c->chunk_bytes < need) {
+        for (auto& p : c->d_chunk) { (void)hipFree(p); p = nullptr; }
+        c->chunk_bytes = 0;
+        for (auto& p : c->d_chunk) TV_HIP(c, hipMalloc((void**)&p, need));
+        c->chunk_bytes = need;
+    }
+    st.ncol = (c->L + st.C - 1) / st.C;
+    st.rows_per_req = std::max<uint64_t>(1, kRingSlotBytes / st.C);
+    st.kernel = choose_kernel(c);
+    st.p = resident_launch(c);
+    st.p.stride = st.row_pitch;
+    TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
+    TV_HIP(c, hipMemsetAsync(c->d_out, 0, c->bit_words * 8, c->stream));  // fail closed, as tv_verify
+    TV_HIP(c, hipEventRecord(c->done_ev[0], c->stream));
+    TV_HIP(c, hipEventRecord(c->done_ev[1], c->stream));
+    st.active = true;
+    return TV_OK;
+}
+
+int stream_next_locked(tv_ctx* c, tv_stream_req* req) {
+    StreamState& st = c->st;
+    if (!st.active) return fail(c, TV_ERR_STATE, "tv_stream_begin has not been called");
+    if (st.outstanding)
+        return fail(c, TV_ERR_STATE, "request %llu is still outstanding (commit it first)", (unsigned long long)st.req.seq);
+    *req = tv_stream_req{};
+    if (st.col >= st.ncol) return TV_OK;  // rows == 0: every byte has been requested
+    const int buf = (int)(st.col & 1);
+    // the first copy into chunk buffer `buf` waits for the kernel that last read it
+    if (st.row == 0) TV_HIP(c, hipStreamWaitEvent(c->copy_stream, c->done_ev[buf], 0));
+    int rc = take_slot(c, &st.slot, 0);
+    if (rc) return rc;
+    req->piece = c->first + st.row;
+    req->rows = std::min<uint64_t>(st.rows_per_req, c->count - st.row);
+    req->offset = st.col * st.C;
+    req->width = std::min<uint64_t>(st.C, c->L - req->offset);
+    req->slot = c->ring[st.slot];
+    req->seq = ++st.seq;
+    st.req = *req;
+    st.outstanding = true;
+    return TV_OK;
+}
+
+// Queue the outstanding request's rows [0, rows_copy) (the others are unreadable and not copied).  Source:
+// the request's slot (src == nullptr), or caller memory at src (row q at src + q*pitch), DMA'd directly when
+// page-locked and gathered into the slot otherwise.  Completes the column: one kernel launch.
+int stream_commit_locked(tv_ctx* c, const tv_stream_req* req, const uint8_t* src, uint64_t pitch, bool pinned,
+                         uint64_t rows_copy) {
+    StreamState& st = c->st;
+    if (!st.active) return fail(c, TV_ERR_STATE, "tv_stream_begin has not been called");
+    if (!st.outstanding) return fail(c, TV_ERR_STATE, "no outstanding request (call tv_stream_next)");
+    if (!req || req->seq != st.req.seq || req->piece != st.req.piece || req->rows != st.req.rows)
+        return fail(c, TV_ERR_ARG, "the request does not match outstanding request %llu", (unsigned long long)st.req.seq);
+    const tv_stream_req r = st.req;
+    const int buf = (int)(st.col & 1);
+    uint8_t* dst = c->d_chunk[buf] + st.row * st.row_pitch;
+    uint8_t* slot = c->ring[st.slot];
+    const uint64_t n = std::min(rows_copy, r.rows);
+    uint64_t full = n;  // rows [0, full) carry `width` bytes; only the torrent's short last piece has fewer
+    if (full && row_bytes(c, r.piece + full - 1, r.offset, r.width) < r.width) full--;
+    const uint64_t tail = full < n ? row_bytes(c, r.piece + full, r.offset, r.width) : 0;
+    const uint8_t* from = slot;
+    uint64_t from_pitch = r.width;
+    if (src) {
+        if (pinned) {
+            from = src;
+            from_pitch = pitch;
+        } else {
+            gather_rows(c->pool[0], slot, src, r.width, pitch, full, c->file_threads);
+            if (tail) memcpy(slot + full * r.width, src + full * pitch, tail);
+        }
+    }
+    if (full)
+        TV_HIP(c, hipMemcpy2DAsync(dst, st.row_pitch, from, from_pitch, r.width, full, hipMemcpyHostToDevice,
+                                   c->copy_stream));
+    if (tail)
+        TV_HIP(c, hipMemcpyAsync(dst + full * st.row_pitch, from + full * from_pitch, tail, hipMemcpyHostToDevice,
+                                 c->copy_stream));
+    st.outstanding = false;
+    const int s = st.slot;
+    st.slot = -1;
+    int rc = release_slot(c, s, 0);  // its event follows the copies just queued
+    if (rc) return rc;
+    st.row += r.rows;
+    if (st.row < c->count) return TV_OK;
+    // the column is complete: hash it while the caller fills the next one
+    TV_HIP(c, hipEventRecord(c->col_ev[buf], c->copy_stream));
+    TV_HIP(c, hipStreamWaitEvent(c->stream, c->col_ev[buf], 0));
+    if (!st.k0) {
+        TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
+        st.k0 = true;
+    }
+    const bool last = st.col + 1 == st.ncol;
+    TvPieces p = st.p;
+    p.data = c->d_chunk[buf];
+    p.data_off = r.offset;
+    p.blk_begin = r.offset / 64;
+    p.blk_end = last ? UINT64_MAX : (r.offset + st.C) / 64;
+    p.finalize = last ? 1 : 0;
+    TV_HIP(c, tv_launch_verify(p, st.kernel, false, c->stream, c->split_pairs));
+    TV_HIP(c, hipEventRecord(c->done_ev[buf], c->stream));
+    st.col++;
+    st.row = 0;
+    return TV_OK;
+}
+
+int stream_end_locked(tv_ctx* c, uint8_t* bitfield_out) {
+    StreamState& st = c->st;
+    if (!st.active) return fail(c, TV_ERR_STATE, "tv_stream_begin has not been called");
+    if (st.outstanding || st.col < st.ncol) {
+        const unsigned long long done = st.col, all = st.ncol;
+        stream_abort_locked(c);
+        return fail(c, TV_ERR_STATE, "stream ended before its last column (%llu of %llu hashed); aborted", done, all);
+    }
+    if (c->count) {
+        if (!bitfield_out) {
+            stream_abort_locked(c);
+            return fail(c, TV_ERR_ARG, "bitfield_out is NULL");
+        }
+        TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
+        int rc = read_bits(c, bitfield_out);
+        if (rc) {
+            stream_abort_locked(c);
+            return rc;
+        }
+        for (size_t k = 0; k < st.av.size(); k++) bitfield_out[k] &= st.av[k];  // unreadable pieces: bit 0
+        c->last_kernel = st.kernel;
+        c->last_launches = (int)st.ncol;
+        rc = finish_timing(c);
+        st = StreamState{};
+        return rc;
+    }
+    st = StreamState{};
+    return TV_OK;
+}
+
 }  // namespace
 
 // ============================================================================================
@@ -572,6 +904,10 @@ int tv_create(tv_ctx** out, int device) {
     if (e == hipSuccess) e = hipEventCreate(&c->ev_k1);
     if (e == hipSuccess) e = hipEventCreate(&c->ev_call1);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_avail, hipEventDisableTiming);
+    for (int k = 0; k < 2; k++) {
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->col_ev[k], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done_ev[k], hipEventDisableTiming);
+    }
     if (e != hipSuccess) {
         fail(nullptr, TV_ERR_HIP, "tv_create: %s", hipGetErrorString(e));
         tv_destroy(c);
@@ -595,7 +931,8 @@ void tv_destroy(tv_ctx* c) {
         if (c->ring2_ev[s]) (void)hipEventDestroy(c->ring2_ev[s]);
     }
     if (c->h_bits) (void)hipHostFree(c->h_bits);
-    for (hipEvent_t ev : {c->ev_call0, c->ev_k0, c->ev_k1, c->ev_call1, c->ev_avail})
+    for (hipEvent_t ev : {c->ev_call0, c->ev_k0, c->ev_k1, c->ev_call1, c->ev_avail, c->col_ev[0], c->col_ev[1],
+                          c->done_ev[0], c->done_ev[1]})
         if (ev) (void)hipEventDestroy(ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -660,6 +997,14 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
             if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_FILE_CONCURRENT must be 0 or 1");
             c->file_concurrent = value != 0;
             return TV_OK;
+        case TV_OPT_RESIDENT:
+            if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_RESIDENT must be 0 or 1");
+            c->resident = value != 0;  // takes effect at the next tv_set_layout
+            return TV_OK;
+        case TV_OPT_DEBUG_REBOUNCE:
+            if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_DEBUG_REBOUNCE must be 0 or 1");
+            c->debug_rebounce = value != 0;
+            return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
@@ -677,6 +1022,8 @@ int tv_get_option(tv_ctx* c, int key, int64_t* value) {
         case TV_OPT_FILE_DIRECT_MIN: *value = (int64_t)c->file_direct_min; return TV_OK;
         case TV_OPT_FILE_THREADS: *value = c->file_threads; return TV_OK;
         case TV_OPT_FILE_CONCURRENT: *value = c->file_concurrent ? 1 : 0; return TV_OK;
+        case TV_OPT_RESIDENT: *value = c->resident ? 1 : 0; return TV_OK;
+        case TV_OPT_DEBUG_REBOUNCE: *value = c->debug_rebounce ? 1 : 0; return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
@@ -689,7 +1036,10 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
     if (shard_first > n_pieces || shard_count > n_pieces - shard_first)
         return fail(c, TV_ERR_ARG, "shard [%llu, +%llu) outside %llu pieces", (unsigned long long)shard_first,
                     (unsigned long long)shard_count, (unsigned long long)n_pieces);
-    if (shard_first % 8) return fail(c, TV_ERR_ARG, "shard_first must be a multiple of 8 (whole bitfield bytes)");
+    // (an empty shard has no bitfield slice, so it may start anywhere: a trailing empty shard of
+    // shard_ranges starts at P, which need not be a multiple of 8)
+    if (shard_first % 8 && shard_count)
+        return fail(c, TV_ERR_ARG, "shard_first must be a multiple of 8 (whole bitfield bytes)");
     if (shard_count >= 0xFFFFFFFFull) return fail(c, TV_ERR_ARG, "shard_count too large");
     if (piece_length > (1ull << 36)) return fail(c, TV_ERR_ARG, "piece_length must be <= 64 GiB");
     // every linear offset i*L (+L) and digest offset 20*i (+20) of the torrent must fit in 64 bits, and so
@@ -700,10 +1050,10 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
         return fail(c, TV_ERR_ARG, "geometry overflows 64-bit offsets (%llu pieces of %llu bytes)",
                     (unsigned long long)n_pieces, (unsigned long long)piece_length);
     TV_HIP(c, hipSetDevice(c->device));
+    stream_abort_locked(c);
     TV_HIP(c, hipStreamSynchronize(c->stream));
     TV_HIP(c, hipStreamSynchronize(c->copy_stream));
     TV_HIP(c, hipStreamSynchronize(c->copy_stream2));
-    free_device(c);
     c->has_layout = false;
     c->digests_set = false;
     c->total = total_length;
@@ -714,15 +1064,31 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
     c->stride = stride;
     c->bit_words = ((shard_count + 255) / 256) * 4;
     c->digest_ok.assign((shard_count + 7) / 8 + 8, 0);
-    if (shard_count) {
-        TV_HIP(c, hipMalloc((void**)&c->d_payload, shard_count * c->stride + kSlack));
+    // Keep every allocation the new geometry fits (reuse_fits): a run of small layouts (verify_piece,
+    // a flush of tv_verify_list) allocates once.  Everything else is released first, so a big payload
+    // is never held beside its replacement.
+    const uint64_t need_payload = (shard_count && c->resident) ? shard_count * c->stride + kSlack : 0;
+    if (!reuse_fits(need_payload, c->cap_payload)) free_payload(c);
+    if (!reuse_fits(shard_count, c->cap_count)) free_per_piece(c);
+    if (!reuse_fits(c->bit_words, c->cap_words)) free_words(c);
+    if (need_payload && !c->d_payload) {
+        TV_HIP(c, hipMalloc((void**)&c->d_payload, need_payload));
+        c->cap_payload = need_payload;
+    }
+    if (shard_count && !c->d_digests) {
         TV_HIP(c, hipMalloc((void**)&c->d_digests, 5 * shard_count * sizeof(uint32_t)));
         TV_HIP(c, hipMalloc((void**)&c->d_state, 5 * shard_count * sizeof(uint32_t)));
         TV_HIP(c, hipMalloc((void**)&c->d_hash, 5 * shard_count * sizeof(uint32_t)));
+        c->cap_count = shard_count;
+    }
+    if (shard_count && !c->d_out) {
         TV_HIP(c, hipMalloc((void**)&c->d_avail, c->bit_words * 8));
         TV_HIP(c, hipMalloc((void**)&c->d_base_avail, c->bit_words * 8));
         TV_HIP(c, hipHostMalloc((void**)&c->h_avail, c->bit_words * 8, hipHostMallocDefault));
         TV_HIP(c, hipMalloc((void**)&c->d_out, c->bit_words * 8));
+        c->cap_words = c->bit_words;
+    }
+    if (need_payload) {  // the tail over-read slack past the last piece reads zeros
         TV_HIP(c, hipMemsetAsync(c->d_payload + shard_count * c->stride, 0, kSlack, c->stream));
         TV_HIP(c, hipStreamSynchronize(c->stream));
     }
@@ -733,6 +1099,10 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
 int tv_set_digests(tv_ctx* c, const uint8_t* pieces, uint64_t pieces_len) {
     if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
     std::lock_guard<std::mutex> g(c->mu);
+    if (c->st.active) {
+        TV_HIP(c, hipSetDevice(c->device));
+        stream_abort_locked(c);
+    }
     int rc = require_layout(c, false);
     if (rc) return rc;
     if (!pieces && pieces_len) return fail(c, TV_ERR_ARG, "pieces is NULL");
@@ -765,7 +1135,7 @@ int tv_set_digests(tv_ctx* c, const uint8_t* pieces, uint64_t pieces_len) {
 int tv_stage(tv_ctx* c, uint64_t linear_offset, const uint8_t* src, uint64_t len) {
     if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
     std::lock_guard<std::mutex> g(c->mu);
-    int rc = require_layout(c, false);
+    int rc = require_layout(c, false, true);
     if (rc) return rc;
     if (!src && len) return fail(c, TV_ERR_ARG, "src is NULL");
     if (linear_offset + len < linear_offset) return fail(c, TV_ERR_ARG, "offset + len overflows");
@@ -838,16 +1208,16 @@ int stage_file_locked(tv_ctx* c, const char* path, uint64_t file_offset, uint64_
             win.release(k);
             for (uint64_t q = 0; q < n; q += kRingSlotBytes - 4) {
                 const uint64_t kq = std::min<uint64_t>(kRingSlotBytes - 4, n - q);
-                int slot;
-                rc = take_slot(c, &slot, lane);
+                SlotLease slot(c, lane);  // lent until every copy out of it is queued
+                rc = slot.take();
                 if (rc) return rc;
-                RingRef ring = ring_ref(c, lane);
-                uint8_t* at = ring.buf[slot] + ((p + q) & 3);  // at the resident bytes' alignment mod 4
+                uint8_t* at = slot.ptr() + ((p + q) & 3);  // at the resident bytes' alignment mod 4
                 const int e = pread_parallel(win.fd, at, fo + q, kq, c->file_threads);
                 if (e) return fail(c, TV_ERR_IO, "read %s at %llu: %s", path, (unsigned long long)(fo + q), strerror(e));
                 rc = stage_range(c, p + q, p + q + kq, at, p + q, true, lane, /*src_in_ring=*/true);
                 if (rc) return rc;
-                TV_HIP(c, hipEventRecord(ring.ev[slot], cs));
+                rc = slot.release();
+                if (rc) return rc;
             }
         }
         TV_HIP(c, hipEventRecord(drain.ev[k], cs));
@@ -911,7 +1281,7 @@ void read_segments(const std::vector<SmallSeg>& segs, size_t lo, size_t hi, cons
 int tv_stage_file(tv_ctx* c, const char* path, uint64_t file_offset, uint64_t linear_offset, uint64_t len) {
     if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
     std::lock_guard<std::mutex> g(c->mu);
-    int rc = require_layout(c, false);
+    int rc = require_layout(c, false, true);
     if (rc) return rc;
     if (!path) return fail(c, TV_ERR_ARG, "path is NULL");
     if (linear_offset + len < linear_offset || file_offset + len < file_offset)
@@ -923,7 +1293,7 @@ int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64
                    const uint64_t* linear_offsets, const uint64_t* lens, int32_t* status_out) {
     if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
     std::lock_guard<std::mutex> g(c->mu);
-    int rc = require_layout(c, false);
+    int rc = require_layout(c, false, true);
     if (rc) return rc;
     if (n == 0) return TV_OK;
     if (!paths || !file_offsets || !linear_offsets || !lens || !status_out)
@@ -1021,21 +1391,22 @@ int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64
             used = at + small[j].len;
             j++;
         }
-        int slot;
-        rc = take_slot(c, &slot);
+        SlotLease slot(c, 0);  // lent until every copy out of it is queued
+        rc = slot.take();
         if (rc) return rc;
-        read_segments(small, i, j, paths, c->ring[slot], status_out, c->file_threads, &first_err, &err_mu);
+        read_segments(small, i, j, paths, slot.ptr(), status_out, c->file_threads, &first_err, &err_mu);
         for (size_t q = i; q < j;) {  // one copy per run of readable, linear-contiguous segments
             if (status_out[small[q].k] != TV_OK) { q++; continue; }
             size_t r = q + 1;
             while (r < j && status_out[small[r].k] == TV_OK && small[r].linear == small[r - 1].linear + small[r - 1].len)
                 r++;
             const uint64_t lin_a = small[q].linear, lin_b = small[r - 1].linear + small[r - 1].len;
-            rc = stage_range(c, lin_a, lin_b, c->ring[slot] + small[q].packed, lin_a, true, 0, /*src_in_ring=*/true);
+            rc = stage_range(c, lin_a, lin_b, slot.ptr() + small[q].packed, lin_a, true, 0, /*src_in_ring=*/true);
             if (rc) return rc;
             q = r;
         }
-        TV_HIP(c, hipEventRecord(c->ring_ev[slot], c->copy_stream));
+        rc = slot.release();
+        if (rc) return rc;
         i = j;
     }
     TV_HIP(c, hipStreamSynchronize(c->copy_stream));
@@ -1048,7 +1419,7 @@ int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64
 int tv_read(tv_ctx* c, uint64_t linear_offset, uint8_t* dst, uint64_t len) {
     if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
     std::lock_guard<std::mutex> g(c->mu);
-    int rc = require_layout(c, false);
+    int rc = require_layout(c, false, true);
     if (rc) return rc;
     if (!dst && len) return fail(c, TV_ERR_ARG, "dst is NULL");
     if (linear_offset + len < linear_offset) return fail(c, TV_ERR_ARG, "offset + len overflows");
@@ -1085,7 +1456,7 @@ int tv_read(tv_ctx* c, uint64_t linear_offset, uint8_t* dst, uint64_t len) {
 int tv_fill_synthetic(tv_ctx* c, uint64_t seed) {
     if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
     std::lock_guard<std::mutex> g(c->mu);
-    int rc = require_layout(c, false);
+    int rc = require_layout(c, false, true);
     if (rc) return rc;
     if (!c->count) return TV_OK;
     TV_HIP(c, hipSetDevice(c->device));
@@ -1097,7 +1468,7 @@ int tv_fill_synthetic(tv_ctx* c, uint64_t seed) {
 int tv_verify(tv_ctx* c, const uint8_t* avail_bits, uint8_t* bitfield_out) {
     if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
     std::lock_guard<std::mutex> g(c->mu);
-    int rc = require_layout(c, true);
+    int rc = require_layout(c, true, true);
     if (rc) return rc;
     if (!bitfield_out && c->count) return fail(c, TV_ERR_ARG, "bitfield_out is NULL");
     if (!c->count) return TV_OK;
@@ -1124,7 +1495,7 @@ int tv_verify(tv_ctx* c, const uint8_t* avail_bits, uint8_t* bitfield_out) {
 int tv_verify_list(tv_ctx* c, const uint64_t* pieces, uint64_t n, uint8_t* ok_out) {
     if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
     std::lock_guard<std::mutex> g(c->mu);
-    int rc = require_layout(c, true);
+    int rc = require_layout(c, true, true);
     if (rc) return rc;
     if (n == 0) return TV_OK;
     if (!pieces || !ok_out) return fail(c, TV_ERR_ARG, "NULL argument");
@@ -1199,7 +1570,7 @@ int tv_verify_list(tv_ctx* c, const uint64_t* pieces, uint64_t n, uint8_t* ok_ou
 int tv_hash(tv_ctx* c, uint8_t* digests_out) {
     if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
     std::lock_guard<std::mutex> g(c->mu);
-    int rc = require_layout(c, false);
+    int rc = require_layout(c, false, true);
     if (rc) return rc;
     if (!digests_out && c->count) return fail(c, TV_ERR_ARG, "digests_out is NULL");
     if (!c->count) return TV_OK;
@@ -1227,10 +1598,10 @@ int tv_hash(tv_ctx* c, uint8_t* digests_out) {
     return finish_timing(c);
 }
 
-// End-to-end verification from host memory: column-chunked streaming.  Column c carries bytes
-// [c*C, (c+1)*C) of every shard piece; it is copied (one 2D DMA, src pitch L) into one of two
-// device chunk buffers while the kernel hashes the previous column.  Chaining values persist in
-// d_state between columns; the last column finalises (padding block, compare).
+// End-to-end verification from a host buffer holding the whole shard (tv_verify_host): the stream engine
+// with the caller's buffer as the producer.  Each request's rows are one 2D DMA straight from a page-locked
+// source (src pitch L) or are gathered into the request's ring slot first.  Rows past src_len are not
+// copied; their pieces are unreadable.
 int tv_verify_host(tv_ctx* c, const uint8_t* src, uint64_t src_len, const uint8_t* avail_bits,
                    uint8_t* bitfield_out) {
     if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
@@ -1241,114 +1612,121 @@ int tv_verify_host(tv_ctx* c, const uint8_t* src, uint64_t src_len, const uint8_
     if (!src && src_len) return fail(c, TV_ERR_ARG, "src is NULL");
     if (!c->count) return TV_OK;
     TV_HIP(c, hipSetDevice(c->device));
-
     // pieces whose bytes extend past src_len are unreadable
-    std::vector<uint8_t> av((c->count + 7) / 8 + 8, 0);
+    std::vector<uint8_t> av((c->count + 7) / 8, 0);
     for (uint64_t j = 0; j < c->count; j++) {
-        const uint64_t i = c->first + j;
-        const uint64_t end = (j * c->L) + piece_len(c, i);
+        const uint64_t end = j * c->L + piece_len(c, c->first + j);
         if (end <= src_len && (!avail_bits || get_bit(avail_bits, j))) set_bit(av.data(), j);
     }
-    TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
-    const uint64_t* av_dev = nullptr;
-    rc = launch_avail(c, av.data(), &av_dev);
-    if (rc) return rc;
-
-    const uint64_t n = c->count;
-    uint64_t C = c->stream_chunk;
-    if (!C) {  // ~512 MiB columns, 64 KiB .. L
-        C = 64ull << 10;
-        while (C * 2 <= c->L && C * 2 * n <= (512ull << 20)) C *= 2;
-    }
-    C = std::max<uint64_t>(64, std::min<uint64_t>((C / 64) * 64, ((c->L + 63) / 64) * 64));
-    const uint64_t row = C + 256;  // device row pitch (tail over-read slack)
-    if (c->chunk_bytes < row * n + kSlack) {
-        for (auto& p : c->d_chunk) { (void)hipFree(p); p = nullptr; }
-        c->chunk_bytes = 0;
-        for (auto& p : c->d_chunk) TV_HIP(c, hipMalloc((void**)&p, row * n + kSlack));
-        c->chunk_bytes = row * n + kSlack;
-    }
-    // DMA straight from the caller's buffer only when it is page-locked (hipHostMalloc or
-    // hipHostRegister): such memory has a device mapping.  Pageable memory goes through the ring.
     const bool pinned = is_pinned(src);
-
-    const uint64_t ncol = (c->L + C - 1) / C;
-    const int kernel = choose_kernel(c);
-    TvPieces p = resident_launch(c);
-    p.stride = row;
-    p.avail64 = av_dev;
-    DrainGuard drain(c);
-    TV_HIP(c, hipMemsetAsync(c->d_out, 0, c->bit_words * 8, c->stream));  // fail closed, as tv_verify
-    hipEvent_t* col_ev = drain.ev;       // copy of column -> buffer k done
-    hipEvent_t* done_ev = drain.ev + 2;  // kernel that read buffer k done
-    for (int k = 0; k < 4; k++) TV_HIP(c, hipEventCreateWithFlags(&drain.ev[k], hipEventDisableTiming));
-    TV_HIP(c, hipEventRecord(done_ev[0], c->stream));
-    TV_HIP(c, hipEventRecord(done_ev[1], c->stream));
-    bool k0_recorded = false;
-    for (uint64_t col = 0; col < ncol; col++) {
-        const int buf = (int)(col & 1);
-        const uint64_t off = col * C;
-        const uint64_t width = std::min(C, c->L - off);
-        // the copy into buf must wait until the kernel that last read buf is done
-        TV_HIP(c, hipStreamWaitEvent(c->copy_stream, done_ev[buf], 0));
-        // rows whose piece holds all `width` bytes inside src: 2D copy; the others one by one
-        uint64_t full_rows = 0;
-        while (full_rows < n && full_rows * c->L + off + width <= src_len &&
-               (c->first + full_rows != c->P - 1 || piece_len(c, c->P - 1) >= off + width))
-            full_rows++;
-        if (pinned) {
-            if (full_rows)
-                TV_HIP(c, hipMemcpy2DAsync(c->d_chunk[buf], row, src + off, c->L, width, full_rows,
-                                           hipMemcpyHostToDevice, c->copy_stream));
-        } else {
-            // pageable source: gather rows through the pinned ring
-            uint64_t r = 0;
-            while (r < full_rows) {
-                int slot;
-                rc = take_slot(c, &slot);
-                if (rc) return rc;
-                const uint64_t k = std::min<uint64_t>(full_rows - r, std::max<uint64_t>(1, kRingSlotBytes / width));
-                gather_rows(c->ring[slot], src + r * c->L + off, width, c->L, k, c->file_threads);
-                TV_HIP(c, hipMemcpy2DAsync(c->d_chunk[buf] + r * row, row, c->ring[slot], width, width, k,
-                                           hipMemcpyHostToDevice, c->copy_stream));
-                TV_HIP(c, hipEventRecord(c->ring_ev[slot], c->copy_stream));
-                r += k;
-            }
-        }
-        for (uint64_t r = full_rows; r < n; r++) {  // short / truncated rows
-            const uint64_t start = r * c->L + off;
-            const uint64_t plen = piece_len(c, c->first + r);
-            uint64_t have = 0;
-            if (start < src_len && off < plen) have = std::min({width, src_len - start, plen - off});
-            if (!have) continue;
-            int slot;
-            rc = take_slot(c, &slot);
-            if (rc) return rc;
-            memcpy(c->ring[slot], src + start, have);
-            TV_HIP(c, hipMemcpyAsync(c->d_chunk[buf] + r * row, c->ring[slot], have, hipMemcpyHostToDevice, c->copy_stream));
-            TV_HIP(c, hipEventRecord(c->ring_ev[slot], c->copy_stream));
-        }
-        TV_HIP(c, hipEventRecord(col_ev[buf], c->copy_stream));
-        TV_HIP(c, hipStreamWaitEvent(c->stream, col_ev[buf], 0));
-        if (!k0_recorded) {
-            TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
-            k0_recorded = true;
-        }
-        p.data = c->d_chunk[buf];
-        p.data_off = off;
-        p.blk_begin = off / 64;
-        const bool last_col = col + 1 == ncol;
-        p.blk_end = last_col ? UINT64_MAX : (off + C) / 64;
-        p.finalize = last_col ? 1 : 0;
-        TV_HIP(c, tv_launch_verify(p, kernel, false, c->stream, c->split_pairs));
-        TV_HIP(c, hipEventRecord(done_ev[buf], c->stream));
+    DrainGuard drain(c);  // no DMA reads the caller's buffer after the call returns, also on error paths
+    rc = stream_begin_locked(c, av.data());
+    if (rc) {
+        stream_abort_locked(c);
+        return rc;
     }
-    TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
-    rc = read_bits(c, bitfield_out);
+    for (;;) {
+        tv_stream_req req;
+        rc = stream_next_locked(c, &req);
+        if (rc || !req.rows) break;
+        // rows wholly inside src: a prefix of the request (its rows ascend in linear offset)
+        const uint64_t base = (req.piece - c->first) * c->L + req.offset;
+        uint64_t k = 0;
+        while (k < req.rows && base + k * c->L + row_bytes(c, req.piece + k, req.offset, req.width) <= src_len) k++;
+        rc = stream_commit_locked(c, &req, k ? src + base : nullptr, c->L, pinned, k);
+        if (rc) break;
+    }
+    if (rc) {
+        stream_abort_locked(c);
+        return rc;
+    }
+    return stream_end_locked(c, bitfield_out);
+}
+
+namespace {
+
+// Public stream calls: a HIP failure leaves the stream unusable, so it is aborted (the ctx stays usable).
+int stream_result(tv_ctx* c, int rc) {
+    if (rc == TV_ERR_HIP || rc == TV_ERR_NOMEM) stream_abort_locked(c);
+    return rc;
+}
+
+}  // namespace
+
+int tv_stream_begin(tv_ctx* c, const uint8_t* avail_bits) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = require_layout(c, true);
     if (rc) return rc;
-    c->last_kernel = kernel;
-    c->last_launches = (int)ncol;
-    return finish_timing(c);
+    TV_HIP(c, hipSetDevice(c->device));
+    return stream_result(c, stream_begin_locked(c, avail_bits));
+}
+
+int tv_stream_next(tv_ctx* c, tv_stream_req* req) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    if (!req) return fail(c, TV_ERR_ARG, "req is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    TV_HIP(c, hipSetDevice(c->device));
+    return stream_result(c, stream_next_locked(c, req));
+}
+
+int tv_stream_commit(tv_ctx* c, const tv_stream_req* req) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    TV_HIP(c, hipSetDevice(c->device));
+    return stream_result(c, stream_commit_locked(c, req, nullptr, 0, true, req ? req->rows : 0));
+}
+
+int tv_stream_commit_from(tv_ctx* c, const tv_stream_req* req, const uint8_t* src, uint64_t src_pitch) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    if (!src) return fail(c, TV_ERR_ARG, "src is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (req && req->rows > 1 && src_pitch < req->width)
+        return fail(c, TV_ERR_ARG, "src_pitch %llu is shorter than the row width %llu", (unsigned long long)src_pitch,
+                    (unsigned long long)req->width);
+    TV_HIP(c, hipSetDevice(c->device));
+    return stream_result(c, stream_commit_locked(c, req, src, src_pitch, is_pinned(src), req ? req->rows : 0));
+}
+
+int tv_stream_unreadable(tv_ctx* c, uint64_t piece) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->st.active) return fail(c, TV_ERR_STATE, "tv_stream_begin has not been called");
+    if (piece < c->first || piece >= c->first + c->count)
+        return fail(c, TV_ERR_ARG, "piece %llu is not in this context's shard", (unsigned long long)piece);
+    const uint64_t j = piece - c->first;
+    c->st.av[j >> 3] &= (uint8_t)~(0x80u >> (j & 7));
+    return TV_OK;
+}
+
+int tv_stream_end(tv_ctx* c, uint8_t* bitfield_out) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    TV_HIP(c, hipSetDevice(c->device));
+    return stream_end_locked(c, bitfield_out);
+}
+
+int tv_stream_abort(tv_ctx* c) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    TV_HIP(c, hipSetDevice(c->device));
+    stream_abort_locked(c);
+    return TV_OK;
+}
+
+int tv_stream_fill_synthetic(tv_ctx* c, const tv_stream_req* req, uint64_t seed) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    const StreamState& st = c->st;
+    if (!st.active || !st.outstanding) return fail(c, TV_ERR_STATE, "no outstanding request (call tv_stream_next)");
+    if (!req || req->seq != st.req.seq) return fail(c, TV_ERR_ARG, "the request does not match the outstanding one");
+    const tv_stream_req r = st.req;
+    uint8_t* slot = c->ring[st.slot];
+    c->pool[0].run(c->file_threads, r.rows, [&](uint64_t q) {
+        const uint64_t i = r.piece + q;
+        tv_synth_fill_host(seed, i * c->L + r.offset, row_bytes(c, i, r.offset, r.width), slot + q * r.width);
+    });
+    return TV_OK;
 }
 
 int tv_host_alloc(uint64_t bytes, void** out) {

@@ -37,6 +37,7 @@ class IncrementalVerifier:
         self._bufs: Dict[int, bytearray] = {}
         self._have_blocks: Dict[int, set] = {}
         self._pending: List[int] = []
+        self._pending_set: set = set()
 
     def _blocks_in(self, index: int) -> int:
         return -(-piece_length(index, self.info) // BLOCK_SIZE)
@@ -52,17 +53,24 @@ class IncrementalVerifier:
             self.storage.set(i * self.info.piece_length + msg.offset, msg.block)
         if self.bitfield[i >> 3] & (0x80 >> (i & 7)):
             return False                                  # already verified
+        if i in self._pending_set:
+            return False                                  # complete and staged, waiting for flush()
+        plen = piece_length(i, self.info)
+        if msg.offset >= plen:
+            return False
+        block = memoryview(msg.block)[:plen - msg.offset]  # never past the piece (L % BLOCK_SIZE != 0)
         buf = self._bufs.get(i)
         if buf is None:
-            buf = self._bufs[i] = bytearray(piece_length(i, self.info))
+            buf = self._bufs[i] = bytearray(plen)
             self._have_blocks[i] = set()
-        buf[msg.offset:msg.offset + len(msg.block)] = msg.block
+        buf[msg.offset:msg.offset + len(block)] = block
         blocks = self._have_blocks[i]
         blocks.add(msg.offset // BLOCK_SIZE)
         if len(blocks) == self._blocks_in(i):
             self.ctx.stage(i * self.info.piece_length, buf)
             del self._bufs[i], self._have_blocks[i]
             self._pending.append(i)
+            self._pending_set.add(i)
             return True
         return False
 
@@ -71,6 +79,7 @@ class IncrementalVerifier:
         if not self._pending:
             return []
         pending, self._pending = self._pending, []
+        self._pending_set.clear()
         ok = self.ctx.verify_list(pending)
         out = []
         for i, r in zip(pending, ok):

@@ -18,12 +18,15 @@ Public API (names follow the reference's camelCase surface, snake_cased):
     verify_pieces(info, storage, devices=None) -> bytearray         (verifyPieces)
     verify_piece(info, index, data) -> bool                         (verifyPiece)
     verify_payload(info, payload, devices=None, resident=True) -> bytearray
+    verify_stream(info, read, devices=None) -> bytearray             (bounded-ring resume check)
     hash_pieces(payload, piece_length, devices=None) -> bytes       (creation mode, make_torrent.ts)
 and asyncio wrappers verify_pieces_async / verify_piece_async (the reference API is Promise-based).
 """
 from __future__ import annotations
 
 import asyncio
+import os
+import stat
 import threading
 from concurrent.futures import ThreadPoolExecutor
 from contextlib import contextmanager
@@ -111,6 +114,8 @@ def _run_shards(devs: List[int], n_pieces: int, fn):
     ranges = shard_ranges(n_pieces, len(devs))
 
     def run(slot: int, first: int, count: int):
+        if count == 0:       # a trailing empty shard (P < 8 x devices): no context, no bits
+            return b""
         with _context(devs[slot], slot) as ctx:
             return fn(ctx, first, count)
 
@@ -171,13 +176,7 @@ def verify_payload(info: InfoDict, payload, devices=None, resident: bool = True,
     def shard(ctx, first: int, count: int) -> bytes:
         ctx.set_layout(info.length, L, P, first, count)
         ctx.set_digests(info.pieces_raw)
-        av = None
-        if avail is not None:
-            av = bytearray((count + 7) // 8)
-            for j in range(count):
-                i = first + j
-                if (avail[i >> 3] >> (7 - (i & 7))) & 1:
-                    _set_bit(av, j)
+        av = _shard_avail(avail, first, count)
         lo = min(first * L, len(mv))
         hi = min((first + count) * L, len(mv))
         if resident:
@@ -198,6 +197,115 @@ def verify_payload(info: InfoDict, payload, devices=None, resident: bool = True,
         return bytearray()
     ranges, slices = _run_shards(_devices(devices), P, shard)
     return _concat(slices, ranges, P)
+
+
+def _shard_avail(avail: Optional[bytes], first: int, count: int) -> Optional[bytearray]:
+    """Shard-relative slice of a torrent-wide MSB-first availability bitfield (None = all readable)."""
+    if avail is None:
+        return None
+    av = bytearray((count + 7) // 8)
+    for j in range(count):
+        i = first + j
+        if (avail[i >> 3] >> (7 - (i & 7))) & 1:
+            _set_bit(av, j)
+    return av
+
+
+def verify_stream(info: InfoDict, read, devices=None, avail: Optional[bytes] = None, chunk: int = 0) -> bytearray:
+    """End-to-end resume check through the library's BOUNDED pinned ring (tv_stream_*; SURVEY 8d config 5:
+    the resume flow Client.add -> verify -> Torrent.bitfield -> sendBitfield, client.ts:53-67,
+    torrent.ts:56-60,101).  No resident payload and no whole-shard host buffer: the library asks for the
+    shard column by column (bytes [c*C, c*C + C) of every piece, C = `chunk` or automatic), and each row
+    is one read(linear_offset, length) -> bytes | None -- Storage.get's shape (storage.ts:50-65), so a
+    Storage's bound .get can be passed.  None makes that piece unreadable (bit 0); a piece is readable
+    iff every slice of it reads.  Host memory in flight: 3 x 64 MiB per device, whatever the size."""
+    P, L = info.n_pieces, info.piece_length
+
+    def shard(ctx, first: int, count: int) -> bytes:
+        ctx.set_option(_native.TV_OPT_RESIDENT, 0)       # no resident payload for a streamed check
+        try:
+            ctx.set_option(_native.TV_OPT_STREAM_CHUNK, chunk)
+            ctx.set_layout(info.length, L, P, first, count)
+            ctx.set_digests(info.pieces_raw)
+        finally:
+            ctx.set_option(_native.TV_OPT_RESIDENT, 1)
+        ctx.stream_begin(_shard_avail(avail, first, count))
+        try:
+            while True:
+                req = ctx.stream_next()
+                if not req.rows:
+                    break
+                slot = ctx.stream_slot(req)
+                for q in range(req.rows):
+                    n = ctx.row_bytes(req, q)
+                    if n == 0:
+                        continue
+                    i = req.piece + q
+                    data = read(i * L + req.offset, n)
+                    if data is None or len(data) != n:
+                        ctx.stream_unreadable(i)
+                        continue
+                    slot[q * req.width:q * req.width + n] = data
+                slot.release()
+                ctx.stream_commit(req)
+            return ctx.stream_end()
+        except BaseException:
+            ctx.stream_abort()
+            raise
+        finally:
+            ctx.set_option(_native.TV_OPT_STREAM_CHUNK, 0)
+
+    if P == 0:
+        return bytearray()
+    ranges, slices = _run_shards(_devices(devices), P, shard)
+    return _concat(slices, ranges, P)
+
+
+def _openable(path: str) -> bool:
+    """Would fsStorage.get's Deno.open(path, {read, write, create}) succeed (storage.ts:149-160)?  Checked
+    without creating the file: an existing non-directory, or a missing file in an existing directory."""
+    try:
+        st = os.stat(path)
+    except FileNotFoundError:
+        parent = os.path.dirname(path) or "."
+        return os.path.isdir(parent) and os.access(parent, os.W_OK | os.X_OK)
+    except OSError:
+        return False
+    return not stat.S_ISDIR(st.st_mode) and os.access(path, os.R_OK | os.W_OK)
+
+
+def _zero_length_faults(info: InfoDict, storage, first: int, count: int, clear) -> None:
+    """The zero-length segments of Storage.get's walk (storage.ts:105-128): a file ending exactly where a
+    piece starts (`fileEnd >= offset`), and zero-length files inside a piece.  fsStorage.get still opens
+    them (storage.ts:158), so a path that cannot be opened -- a directory, a missing parent directory --
+    makes the piece null.  segment_arrays drops these segments, so they are checked here, only for the
+    pieces whose range holds such a boundary."""
+    import numpy as np
+
+    if info.files is None or count == 0:
+        return
+    L = info.piece_length
+    lens = np.fromiter((f.length for f in info.files), dtype=np.int64, count=len(info.files))
+    ends = np.cumsum(lens)
+    starts = ends - lens
+    lo, hi = first * L, (first + count) * L
+    cand = set()
+    on_start = ends[(ends >= lo) & (ends < hi) & (ends % L == 0)]              # a file ends where a piece starts
+    cand.update(((on_start // L) - first).tolist())
+    zs = starts[(lens == 0) & (starts >= lo) & (starts < hi)]                  # zero-length files
+    cand.update(((zs // L) - first).tolist())
+    cache = {}
+    for j in sorted(cand):
+        i = first + j
+        segs = storage.segments(i * L, piece_length(i, info))
+        for path, _, n, _ in segs or ():
+            if n == 0:
+                p = os.path.join(*path)
+                if p not in cache:
+                    cache[p] = _openable(p)
+                if not cache[p]:
+                    clear(j, j)
+                    break
 
 
 def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: int = 16,
@@ -232,6 +340,7 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
     segs = storage.segment_arrays(lo, span) if span else None
     if span and segs is None:         # unmappable (Storage.get -> null for every piece)
         clear(0, count - 1)
+    _zero_length_faults(info, storage, first, count, clear)
     if segs is None or len(segs[0]) == 0:
         return avail
     k, foff, nbytes, start = segs

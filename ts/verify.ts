@@ -38,6 +38,14 @@ const SYMBOLS = {
   },
   tv_verify_list: { parameters: ["pointer", "pointer", "u64", "pointer"], result: "i32", nonblocking: true },
   tv_hash: { parameters: ["pointer", "pointer"], result: "i32", nonblocking: true },
+  tv_stream_begin: { parameters: ["pointer", "pointer"], result: "i32" },
+  tv_stream_next: { parameters: ["pointer", "pointer"], result: "i32", nonblocking: true },
+  tv_stream_commit: { parameters: ["pointer", "pointer"], result: "i32", nonblocking: true },
+  tv_stream_commit_from: { parameters: ["pointer", "pointer", "pointer", "u64"], result: "i32", nonblocking: true },
+  tv_stream_unreadable: { parameters: ["pointer", "u64"], result: "i32" },
+  tv_stream_end: { parameters: ["pointer", "pointer"], result: "i32", nonblocking: true },
+  tv_stream_abort: { parameters: ["pointer"], result: "i32" },
+  tv_stream_fill_synthetic: { parameters: ["pointer", "pointer", "u64"], result: "i32", nonblocking: true },
   tv_set_option: { parameters: ["pointer", "i32", "i64"], result: "i32" },
   tv_get_option: { parameters: ["pointer", "i32", "pointer"], result: "i32" },
   tv_last_timing: { parameters: ["pointer", "pointer", "pointer"], result: "i32" },
@@ -78,6 +86,40 @@ function check(l: Lib, ctx: Deno.PointerValue, rc: number): void {
     const buf = new Uint8Array(1024);
     const n = l.symbols.tv_last_error(ctx, ptr(buf), BigInt(buf.length));
     throw new Error(`torrent_verify error ${rc}: ${new TextDecoder().decode(buf.subarray(0, Math.min(n, 1023)))}`);
+  }
+}
+
+/**
+ * One cached context per (device, shard slot), held exclusively for a whole job: device memory and the
+ * pinned staging ring are reused across calls (tv_set_layout keeps allocations that fit), so a
+ * verifyPiece does not pay tv_create + stream/event creation + a 192 MiB pinned ring each time.  Jobs on
+ * one context take turns (a promise chain), so a job's set_layout -> stage -> verify sequence is never
+ * interleaved with another's.  Same policy as torrent_amd/verify.py _context.
+ */
+const contexts = new Map<string, { ctx: Deno.PointerValue; tail: Promise<void> }>();
+
+async function withContext<T>(l: Lib, device: number, slot: number, job: (ctx: Deno.PointerValue) => Promise<T>): Promise<T> {
+  const key = `${device}:${slot}`;
+  let e = contexts.get(key);
+  if (!e) {
+    const h = new BigUint64Array(1);
+    check(l, null, l.symbols.tv_create(ptr(new Uint8Array(h.buffer)), device));
+    e = { ctx: Deno.UnsafePointer.create(h[0]), tail: Promise.resolve() };
+    contexts.set(key, e);
+  }
+  const entry = e;
+  const run = entry.tail.then(() => job(entry.ctx));
+  entry.tail = run.then(() => {}, () => {});
+  return await run;
+}
+
+/** Free every cached context (device payload, pinned ring); the next call creates new ones. */
+export async function releaseContexts(): Promise<void> {
+  const all = [...contexts.values()];
+  contexts.clear();
+  for (const e of all) {
+    await e.tail;
+    lib?.symbols.tv_destroy(e.ctx);
   }
 }
 
@@ -131,10 +173,7 @@ export async function verifyPieces(
 
   await Promise.all(shardRanges(P, devices.length).map(async ([first, count], s) => {
     if (count === 0) return;
-    const h = new BigUint64Array(1);
-    check(l, null, l.symbols.tv_create(ptr(new Uint8Array(h.buffer)), devices[s]));
-    const ctx = Deno.UnsafePointer.create(h[0]);
-    try {
+    await withContext(l, devices[s], s, async (ctx) => {
       check(l, ctx, l.symbols.tv_set_layout(ctx, BigInt(info.length), BigInt(L), BigInt(P), BigInt(first), BigInt(count)));
       check(l, ctx, l.symbols.tv_set_digests(ctx, ptr(raw), BigInt(raw.length)));
       const avail = new Uint8Array(Math.ceil(count / 8));
@@ -157,14 +196,77 @@ export async function verifyPieces(
       const out = new Uint8Array(Math.ceil(count / 8));
       check(l, ctx, await l.symbols.tv_verify(ctx, ptr(avail), ptr(out)));
       bitfield.set(out, first / 8);
-    } finally {
-      l.symbols.tv_destroy(ctx);
-    }
+    });
   }));
   return bitfield;
 }
 
 const TV_ERR_IO = -5;
+const TV_OPT_STREAM_CHUNK = 3;
+const TV_OPT_RESIDENT = 10;
+
+/**
+ * verifyStream(info, storage) -> have-bitfield: the end-to-end resume check through the library's
+ * BOUNDED pinned ring (tv_stream_*; SURVEY 8d config 5; the resume flow Client.add -> verify ->
+ * Torrent.bitfield -> sendBitfield, client.ts:53-67, torrent.ts:56-60,101).  No resident payload and no
+ * whole-shard buffer: the library requests the shard column by column (bytes [c*C, c*C + C) of every
+ * piece), each row is one storage.get(offset, length) written straight into the library's pinned slot,
+ * and the library DMAs the slot to HBM while the GPU hashes the previous column.  Host memory in flight:
+ * 3 x 64 MiB per device.  null from storage.get makes that piece 0 (a piece is readable iff every slice
+ * of it reads).  Same behaviour as torrent_amd.verify_stream.
+ */
+export async function verifyStream(info: InfoDict, storage: Storage, opts: VerifyOptions & { chunk?: number } = {}): Promise<Uint8Array> {
+  const l = load(opts.libPath);
+  const P = info.pieces.length;
+  const L = info.pieceLength;
+  const devices = opts.devices ?? [0];
+  const raw = piecesRaw(info);
+  const bitfield = new Uint8Array(Math.ceil(P / 8));
+  await Promise.all(shardRanges(P, devices.length).map(async ([first, count], s) => {
+    if (count === 0) return;
+    await withContext(l, devices[s], s, async (ctx) => {
+      check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_RESIDENT, 0n));
+      check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_STREAM_CHUNK, BigInt(opts.chunk ?? 0)));
+      try {
+        check(l, ctx, l.symbols.tv_set_layout(ctx, BigInt(info.length), BigInt(L), BigInt(P), BigInt(first), BigInt(count)));
+      } finally {
+        l.symbols.tv_set_option(ctx, TV_OPT_RESIDENT, 1n);
+      }
+      check(l, ctx, l.symbols.tv_set_digests(ctx, ptr(raw), BigInt(raw.length)));
+      check(l, ctx, l.symbols.tv_stream_begin(ctx, null));
+      const req = new BigUint64Array(6); // tv_stream_req: piece, rows, offset, width, slot, seq
+      const reqp = ptr(new Uint8Array(req.buffer));
+      try {
+        for (;;) {
+          check(l, ctx, await l.symbols.tv_stream_next(ctx, reqp));
+          const rows = Number(req[1]);
+          if (rows === 0) break;
+          const piece = Number(req[0]), offset = Number(req[2]), width = Number(req[3]);
+          const slot = new Uint8Array(Deno.UnsafePointerView.getArrayBuffer(Deno.UnsafePointer.create(req[4])!, rows * width));
+          // every read of the request outstanding at once (make_torrent.ts:96,111 keeps its digests in flight)
+          const got = await Promise.all(Array.from({ length: rows }, (_, q) => {
+            const n = Math.max(0, Math.min(width, pieceLength(piece + q, info) - offset));
+            return n ? storage.get((piece + q) * L + offset, n) : Promise.resolve(new Uint8Array(0));
+          }));
+          got.forEach((bytes, q) => {
+            if (bytes) slot.set(bytes, q * width);
+            else check(l, ctx, l.symbols.tv_stream_unreadable(ctx, BigInt(piece + q)));
+          });
+          check(l, ctx, await l.symbols.tv_stream_commit(ctx, reqp));
+        }
+        const out = new Uint8Array(Math.ceil(count / 8));
+        check(l, ctx, await l.symbols.tv_stream_end(ctx, ptr(out)));
+        bitfield.set(out, first / 8);
+      } catch (err) {
+        l.symbols.tv_stream_abort(ctx);
+        throw err;
+      } finally {
+        l.symbols.tv_set_option(ctx, TV_OPT_STREAM_CHUNK, 0n);
+      }
+    });
+  }));
+  return bitfield;
+}
 
 /**
  * verifyFiles(info, dir) -> have-bitfield of the files under `dir` (resume from disk, SURVEY 8f
@@ -189,10 +291,7 @@ export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptio
 
   await Promise.all(shardRanges(P, devices.length).map(async ([first, count], s) => {
     if (count === 0) return;
-    const h = new BigUint64Array(1);
-    check(l, null, l.symbols.tv_create(ptr(new Uint8Array(h.buffer)), devices[s]));
-    const ctx = Deno.UnsafePointer.create(h[0]);
-    try {
+    await withContext(l, devices[s], s, async (ctx) => {
       check(l, ctx, l.symbols.tv_set_layout(ctx, BigInt(info.length), BigInt(L), BigInt(P), BigInt(first), BigInt(count)));
       check(l, ctx, l.symbols.tv_set_digests(ctx, ptr(raw), BigInt(raw.length)));
       const avail = new Uint8Array(Math.ceil(count / 8)).fill(0xff);
@@ -238,9 +337,7 @@ export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptio
       const out = new Uint8Array(Math.ceil(count / 8));
       check(l, ctx, await l.symbols.tv_verify(ctx, ptr(avail), ptr(out)));
       bitfield.set(out, first / 8);
-    } finally {
-      l.symbols.tv_destroy(ctx);
-    }
+    });
   }));
   return bitfield;
 }
@@ -250,20 +347,15 @@ export async function verifyPiece(info: InfoDict, index: number, bytes: Uint8Arr
   if (index >= info.pieces.length) throw new Error(`verifyPiece: invalid piece index ${index}`);
   if (bytes.length !== pieceLength(index, info) || info.pieces[index].length !== 20) return false;
   const l = load(opts.libPath);
-  const h = new BigUint64Array(1);
-  check(l, null, l.symbols.tv_create(ptr(new Uint8Array(h.buffer)), (opts.devices ?? [0])[0]));
-  const ctx = Deno.UnsafePointer.create(h[0]);
-  try {
+  return await withContext(l, (opts.devices ?? [0])[0], 0, async (ctx) => {
     const n = BigInt(bytes.length);
-    check(l, ctx, l.symbols.tv_set_layout(ctx, n, n, 1n, 0n, 1n));
+    check(l, ctx, l.symbols.tv_set_layout(ctx, n, n, 1n, 0n, 1n)); // reuses the context's allocations
     check(l, ctx, l.symbols.tv_set_digests(ctx, ptr(info.pieces[index]), 20n));
     check(l, ctx, await l.symbols.tv_stage(ctx, 0n, ptr(bytes), n));
     const out = new Uint8Array(1);
     check(l, ctx, await l.symbols.tv_verify(ctx, null, ptr(out)));
     return (out[0] & 0x80) !== 0;
-  } finally {
-    l.symbols.tv_destroy(ctx);
-  }
+  });
 }
 
 /**
@@ -275,19 +367,14 @@ export async function hashPieces(payload: Uint8Array, pieceLength: number, opts:
   const P = Math.ceil(payload.length / pieceLength);
   if (P === 0) return new Uint8Array(0);
   const l = load(opts.libPath);
-  const h = new BigUint64Array(1);
-  check(l, null, l.symbols.tv_create(ptr(new Uint8Array(h.buffer)), (opts.devices ?? [0])[0]));
-  const ctx = Deno.UnsafePointer.create(h[0]);
-  try {
+  return await withContext(l, (opts.devices ?? [0])[0], 0, async (ctx) => {
     check(l, ctx, l.symbols.tv_set_layout(ctx, BigInt(payload.length), BigInt(pieceLength), BigInt(P), 0n, BigInt(P)));
     check(l, ctx, l.symbols.tv_set_digests(ctx, null, 0n));
     check(l, ctx, await l.symbols.tv_stage(ctx, 0n, ptr(payload), BigInt(payload.length)));
     const out = new Uint8Array(20 * P);
     check(l, ctx, await l.symbols.tv_hash(ctx, ptr(out)));
     return out;
-  } finally {
-    l.symbols.tv_destroy(ctx);
-  }
+  });
 }
 
 /**
@@ -318,7 +405,10 @@ export class PieceVerifier {
   /** One received block (already validated); true when it completed its piece. */
   async onBlock(index: number, offset: number, block: Uint8Array): Promise<boolean> {
     if (this.bitfield[index >> 3] & (128 >> (index % 8))) return false;
+    if (this.#pending.includes(index)) return false; // complete, waiting for flush(): ignore re-sends
     const len = pieceLength(index, this.info);
+    if (offset >= len) return false;
+    if (offset + block.length > len) block = block.subarray(0, len - offset); // never into the next piece
     let e = this.#bufs.get(index);
     if (!e) this.#bufs.set(index, e = { bytes: new Uint8Array(len), blocks: new Set() });
     e.bytes.set(block, offset);
