@@ -1,28 +1,41 @@
 #!/usr/bin/env python3
 """Benchmark: verified GB/s of SHA-1 piece verification, HBM-resident (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg2|suppl|cfg4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg2|cfg4|suppl|p262k] [--weak|--strong]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (default cfg2 = BASELINE.json configs[1]): a synthetic single-file torrent, 16 GiB per
-GPU, 1 MiB pieces (16,384 pieces per GPU).  Weak scaling: the torrent has N x 16,384 pieces and
-rank r verifies the contiguous shard [r*16384, (r+1)*16384) of it (shard start a multiple of 8 so
-its bitfield slice is whole bytes; no data-path collective exists).  The payload is generated in
-HBM by the device fill kernel (counter PRNG, the oracle's definition); expected digests are the
-GPU's own creation-mode digests, with 1 % of them corrupted so the expected bitfield is known, and
-a sample of them is checked against the CPU oracle.
+`value` (the timed workload):
+  * N = 1: BASELINE configs[1] = cfg2, a 16 GiB synthetic single-file torrent in 16,384 pieces of 1 MiB,
+    HBM-resident on one MI355X.
+  * N > 1: BASELINE configs[3] = cfg4, ONE 200 GiB torrent in 51,200 pieces of 4 MiB, strong-scaled: rank
+    r verifies the contiguous 8-aligned shard shard_ranges(51200, N)[r] (no data-path collective; the
+    bitfield slices are whole bytes and concatenate).  `--weak` runs cfg2 per GPU instead.
+  One step = one tv_verify of the rank's whole resident shard (availability bits up, the verify kernel,
+  the bitfield slice down).  W untimed steps, then exactly K steps between a barrier + device synchronize
+  on both sides; time = max over ranks; value = bytes of all ranks' shards x K / time.
 
-One step = one tv_verify of the rank's whole resident shard (upload availability bits, the verify
-kernel, bitfield download).  W untimed steps, then exactly K steps between a barrier +
-device synchronize on both sides; the time is the max over ranks.  value = total payload bytes
-of all ranks x K / time.
+Expected values are the CPU ORACLE's (oracle/sha1_oracle.c, pinned by the reference's own test_data
+digests): the rank's whole shard is hashed on the host's cores before the timed region and 1 % of the
+digests are corrupted, so `bitfield_exact` means "equal, on every piece, to the oracle's bitfield".
 
-The roofline object is for the verify kernel: algorithmic bytes per launch (the shard's payload
-bytes, SURVEY.md 8d: one byte read per payload byte) / the average kernel duration from HIP events
-recorded on the library's compute stream around each launch.  The cpu_baseline leg (rank 0, N=1)
-times the CPU oracle (a port of the reference's per-piece SHA-1 path) on a bounded sample of the
-same workload.
+Legs reported beside `value` (never as it):
+  * cfg4 (N = 1): the whole 200 GiB torrent on one GPU -- the same-config anchor of the 1 -> 8 GPU curve.
+  * e2e_cfg5: BASELINE configs[4], the end-to-end resume check: the cfg4 torrent streamed from host memory
+    over PCIe through the library's BOUNDED pinned ring (tv_stream_*; 3 x 64 MiB per GPU, no resident
+    payload, no whole-shard host buffer), each rank its shard.  `generated`: the bytes are produced by the
+    host generator into the ring slots inside the timed region; `pinned_pool`: rows are DMA'd straight
+    from a 1 GiB page-locked pool of pre-generated pieces (the torrent is that pool repeated), i.e. the
+    PCIe path without the producer.
+  * piece_saturated (N = 1): 65,536 x 256 KiB pieces (SURVEY 8d suppl.) against the VALU roofline.
+  * cfg2_weak (N > 1): cfg2 per GPU, weak scaling.
+  * cpu_baseline (rank 0, N = 1): the oracle (C port of the per-piece SHA-1 path, SHA-NI) on the host's
+    allowed cores: a bounded sample of the cfg2 workload, BASELINE configs[0] (cfg1) as its own entry, the
+    1-core figure, and the full-shard ground-truth pass.
+
+The roofline object is for the verify kernel: algorithmic bytes per launch (the shard's payload bytes,
+SURVEY.md 8d: each payload byte read once) / the average kernel duration from HIP events recorded on the
+library's compute stream around each launch, against min(HBM peak, the measured SHA-1 VALU roofline).
 """
 from __future__ import annotations
 
@@ -36,6 +49,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from torrent_amd import _native  # noqa: E402  (load the HIP library before torch)
+from torrent_amd.verify import shard_ranges  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # SHA-1 VALU roofline from the measured SIMD cost per wave64 instruction (tools/ubench_simd.hip,
@@ -45,19 +59,32 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level par
 CLOCK_HZ = 2.4e9
 SIMD_CYC_PER_BLOCK = 400 * 4 + 213 * 2
 VALU_PEAK_GBPS = 1024 * 64 * 64 * CLOCK_HZ / SIMD_CYC_PER_BLOCK / 1e9
+ROOF_PEAK_GBPS = min(HBM_PEAK_GBPS, VALU_PEAK_GBPS)
+VALU_DERIVATION = (
+    "R_valu = 1024 SIMDs x 64 lanes x 64 B x 2.4 GHz / 2,026 SIMD cycles per block. 2,026 = the minimal "
+    "gfx950 SHA-1 mix per 64-B block at the per-op SIMD costs measured by tools/ubench_simd.hip "
+    "(profiles/r01/ubench_simd.log): 400 half-rate ops x 4 cyc (224 v_alignbit_b32 rotates, 160 v_add3_u32, "
+    "16 v_perm_b32 byte swaps) + 213 full-rate ops x 2 cyc (144 v_bitop3_b32, 64 v_xor_b32, 5 v_add_u32). "
+    "MI355X_MICROARCH.md gives 2-cycle full-rate wave64 VALU for every op, which would make it 1,226 cycles "
+    "and R_valu 8.2 TB/s (> HBM); the ubench measures v_alignbit/v_add3/v_perm at 4.06-4.25 cycles, half "
+    "rate, so the binding roofline is R_valu, not HBM")
 # Cycles per VALU instruction of a lone wave: 4.07 for 8-byte VOP3 ops in a long loop body, 4.09 for the
 # SHA-1 round mix (tools/ubench_fetch.hip, profiles/r01/ubench_fetch.log); the wave64 cadence is 4.
 LONE_WAVE_CYC = 4.07
 SERIAL_INSTR = {1: 613, 2: 405}  # per-block serial stream: lane kernel / split rounds wave
 
+MiB = 1 << 20
 WORKLOADS = {
-    # name: (piece_length, pieces per GPU, description)
-    "cfg2": (1 << 20, 16384, "cfg2: 16 GiB synthetic single-file torrent per GPU, 1 MiB pieces (16384 pieces), HBM-resident"),
-    "suppl": (256 << 10, 65536, "suppl: 16 GiB per GPU, 256 KiB pieces (65536 pieces), HBM-resident"),
-    "cfg4": (4 << 20, 51200, "cfg4: 200 GiB single-file torrent, 4 MiB pieces (51200 pieces per GPU at N=1), HBM-resident"),
-    "p262k": (64 << 10, 262144, "p262k: 16 GiB per GPU, 64 KiB pieces (262144 pieces), HBM-resident (VALU-saturating)"),
+    # name: (piece_length, pieces (per GPU for weak, whole torrent for strong), seed, description)
+    "cfg1": (256 << 10, 256, 1, "cfg1: 64 MiB synthetic single file, 256 KiB pieces (256 pieces)"),
+    "cfg2": (MiB, 16384, 2, "cfg2: 16 GiB synthetic single-file torrent, 1 MiB pieces (16384 pieces), HBM-resident"),
+    "cfg4": (4 * MiB, 51200, 4, "cfg4: 200 GiB synthetic single-file torrent, 4 MiB pieces (51200 pieces), HBM-resident"),
+    "suppl": (256 << 10, 65536, 6, "suppl: 16 GiB, 256 KiB pieces (65536 pieces), HBM-resident"),
+    "p262k": (64 << 10, 262144, 7, "p262k: 16 GiB, 64 KiB pieces (262144 pieces), HBM-resident (VALU-saturating)"),
+    "tiny": (64 << 10, 1000, 9, "tiny: 62.5 MiB, 64 KiB pieces (1000 pieces) -- multi-rank rehearsals and tests only"),
 }
-SEED = 2
+POOL_PIECES = 256          # e2e pinned_pool: 256 x 4 MiB = 1 GiB page-locked pool
+E2E_CHUNK = 256 << 10      # e2e column width: one 64 MiB ring request = 256 rows = the whole pool
 
 
 def _dist():
@@ -115,72 +142,256 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(L: int, total: int, P: int, first: int, gpu_digests: bytes, target_s: float = 10.0):
-    """Time the CPU oracle (C port of the per-piece SHA-1 path, SHA-NI where the host has it: the
-    reference's WebCrypto SHA-1 is native code of that class) on a bounded sample:
-    the first `n` pieces of this shard, generated once (not timed), hashed repeatedly for
-    ~target_s on all `cores` threads, then ~target_s/5 on one thread (the 1-core figure).  Also
-    checks the sample's digests against the GPU's (parity inside the bench)."""
+def cpu_share() -> dict:
+    """The host cores this process may use: the cgroup CPU quota (cpu.max, v2; cfs_quota_us, v1) when one
+    is set, else the box's CPU share as its environment states it (OMP_NUM_THREADS; 16 per GPU on the
+    GPU boxes), else the affinity mask.  Everything it looked at is reported."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if quota:
+        cores, src = max(1, min(aff, int(quota))), "cgroup CPU quota"
+    elif omp and omp.isdigit() and int(omp) > 0:
+        cores, src = min(aff, int(omp)), "OMP_NUM_THREADS (the box's stated CPU share; no cgroup quota)"
+    else:
+        cores, src = aff, "sched_getaffinity (no cgroup quota, no stated share)"
+    return {"cores": cores, "source": src, "nproc": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota,
+            "omp_num_threads": omp}
+
+
+def _corrupt(dig: bytearray, count: int, salt: int) -> set:
+    """Corrupt 1 % of a shard's digests (every 100th piece, plus its last) -> the pieces expected to fail."""
+    bad = set(range(salt % 100, count, 100)) | {count - 1}
+    for j in bad:
+        dig[20 * j + 7] ^= 0x10
+    return bad
+
+
+def _expected_bits(count: int, bad: set) -> bytes:
+    out = bytearray(b"\xff" * ((count + 7) // 8))
+    if count % 8:
+        out[-1] = (0xFF00 >> (count % 8)) & 0xFF
+    for j in bad:
+        out[j >> 3] &= ~(0x80 >> (j & 7)) & 0xFF
+    return bytes(out)
+
+
+def ground_truth(seed: int, total: int, L: int, P: int, first: int, count: int, threads: int) -> tuple:
+    """The oracle's digests of the shard's synthetic pieces (generated and hashed on `threads` host cores;
+    outside every timed region) and the seconds it took."""
     from oracle import oracle as O
     O.set_impl("best")
-    n = max(1, min(256, (256 << 20) // L))
-    cores = min(16, len(os.sched_getaffinity(0)))
-    buf = O.synth_fill(SEED, first * L, n * L)
-    # digests of the sample (piece-relative: a sub-torrent of n pieces of length L)
-    d = O.hash_pieces(buf, n * L, L, n, 0, n, threads=cores)
-    parity_ok = d == gpu_digests[: 20 * n]
-
-    def timed(threads: int, pieces: int, seconds: float):
-        reps, t0 = 0, time.perf_counter()
-        while True:
-            O.hash_pieces(buf, pieces * L, L, pieces, 0, pieces, threads=threads)
-            reps += 1
-            el = time.perf_counter() - t0
-            if el >= seconds:
-                return reps * pieces * L / el / 1e9, reps, el
-
-    gbps, reps, el = timed(cores, n, target_s)
-    one, _, _ = timed(1, min(n, 16), max(1.0, target_s / 5))
-    return {"value": round(gbps, 3), "unit": "GB/s", "cores": cores, "kind": "port",
-            "sample": f"{n} pieces x {L >> 10} KiB of the same synthetic payload hashed {reps} times "
-                      f"({el:.1f} s) by oracle/sha1_oracle.c ({O.impl()} SHA-1, one piece per task, "
-                      f"{cores} threads)",
-            "impl": O.impl(), "per_core": round(one, 3), "cpu_model": _cpu_model(),
-            "host_cpus_visible": os.cpu_count(), "parity_vs_gpu": parity_ok}
+    t0 = time.perf_counter()
+    d = O.synth_piece_digests(seed, total, L, P, first, count, threads=threads)
+    return d, time.perf_counter() - t0
 
 
-def saturating_leg(device: int, steps: int = 5) -> dict:
-    """The piece-saturated configuration (SURVEY 8d "suppl": 16 GiB, 65,536 x 256 KiB pieces, one
-    lane-kernel wave per SIMD) on the same GPU, reported beside `value` (never as it): with enough
-    pieces the per-piece serial limit of cfg2 is gone and the kernel runs against the VALU roofline,
-    the one the north-star's >= 60 % target is stated for.  1 % corrupted digests; bitfield checked."""
-    L, per, desc = WORKLOADS["suppl"]
+def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: bool, steps: int, warmup: int,
+                 kernel_opt: int, threads: int, want_digests: bool = False) -> dict:
+    """One resident workload on every rank: synthetic payload filled in HBM by the device generator, oracle
+    digests with 1 % corrupted, W + K timed verify steps.  Every rank runs it (barriers inside)."""
+    L, n, seed, desc = WORKLOADS[workload]
+    if strong:
+        P = n
+        first, count = shard_ranges(P, ws)[rank]
+    else:
+        P = n * ws
+        first, count = rank * n, n
+    total = L * P
+    dig, gt_s = ground_truth(seed, total, L, P, first, count, threads)
     ctx = _native.Context(device)
     try:
-        ctx.set_layout(L * per, L, per)
-        ctx.fill_synthetic(SEED + 4)
-        dig = bytearray(ctx.hash())
-        bad = set(range(0, per, 100)) | {per - 1}
-        for j in bad:
-            dig[20 * j + 3] ^= 0x01
-        ctx.set_digests(bytes(dig))
-        expect = bytearray(b"\xff" * (per // 8))
-        for j in bad:
-            expect[j >> 3] &= ~(0x80 >> (j & 7)) & 0xFF
-        bf = ctx.verify()
-        ms = []
+        ctx.set_option(_native.TV_OPT_KERNEL, kernel_opt)
+        ctx.set_layout(total, L, P, first, count)
+        ctx.fill_synthetic(seed)
+        creation_exact = ctx.hash() == dig            # creation mode (make_torrent.ts:28-31) at full size
+        d2 = bytearray(dig)
+        bad = _corrupt(d2, count, seed)
+        pieces = bytearray(20 * P)
+        pieces[20 * first:20 * (first + count)] = d2
+        ctx.set_digests(bytes(pieces))
+        expect = _expected_bits(count, bad)
+        for _ in range(warmup):
+            ctx.verify()
+        _device_sync(ctx, device)
+        _barrier(dist)
+        kernel_ms = []
+        t0 = time.perf_counter()
         for _ in range(steps):
             bf = ctx.verify()
-            ms.append(ctx.last_timing()[0])
+            kernel_ms.append(ctx.last_timing()[0])
+        _device_sync(ctx, device)
+        t1 = time.perf_counter()
+        _barrier(dist)
         kernel, _ = ctx.last_kernel()
     finally:
         ctx.close()
-    avg = sum(ms) / len(ms)
-    gbps = L * per / (avg / 1e3) / 1e9
-    return {"workload": desc, "kernel": {1: "lane", 2: "split"}.get(kernel, str(kernel)), "steps": steps,
-            "kernel_ms_avg": round(avg, 3), "achieved": round(gbps, 1), "unit": "GB/s",
-            "valu_peak": round(VALU_PEAK_GBPS, 1), "frac_of_valu_peak": round(gbps / VALU_PEAK_GBPS, 4),
-            "bitfield_exact": bf == bytes(expect)}
+    elapsed = _max(dist, t1 - t0)
+    exact = _sum(dist, 1.0 if (bf == expect and creation_exact) else 0.0) == ws
+    avg = sum(kernel_ms) / len(kernel_ms)
+    bytes_rank = L * count
+    bytes_all = _sum(dist, float(bytes_rank))
+    achieved = bytes_rank / (avg / 1e3) / 1e9
+    ceiling = min(VALU_PEAK_GBPS, count * 64 * CLOCK_HZ / (SERIAL_INSTR.get(kernel, 613) * LONE_WAVE_CYC) / 1e9)
+    out = {"workload": desc if not strong else desc.split(" (")[0] + f" ({P} pieces in all, {ws} shard(s), strong scaling)",
+           "piece_length": L, "total_pieces": P, "pieces_per_gpu": count, "bytes_per_gpu": bytes_rank,
+           "value": round(bytes_all * steps / elapsed / 1e9, 2), "unit": "GB/s", "steps": steps, "warmup": warmup,
+           "ms_per_step": round(elapsed * 1e3 / steps, 3), "scaling": "strong" if strong else "weak",
+           "kernel": {1: "lane", 2: "split"}.get(kernel, str(kernel)), "kernel_ms_avg": round(avg, 3),
+           "kernel_ms_max_over_ranks": round(_max(dist, avg), 3), "achieved": round(achieved, 1),
+           "piece_parallelism_ceiling": round(ceiling, 1), "frac_of_piece_ceiling": round(achieved / ceiling, 4),
+           "frac_of_valu_peak": round(achieved / VALU_PEAK_GBPS, 4),
+           "bitfield_exact": exact, "expected": "oracle digests of every piece, 1 % corrupted",
+           "ground_truth_s": round(gt_s, 2), "ground_truth_threads": threads}
+    if want_digests:
+        out["_digests"] = dig
+        out["_first"] = first
+    return out
+
+
+def e2e_cfg5(dist, ws: int, rank: int, device: int, steps: int, threads: int, shard_digests=None) -> dict:
+    """BASELINE configs[4]: the cfg4 torrent (200 GiB, 51,200 x 4 MiB) streamed host -> PCIe -> HBM through the
+    library's bounded pinned ring (tv_stream_*), each rank its shard_ranges shard, no resident payload."""
+    from oracle import oracle as O
+    L, P, seed, _ = WORKLOADS["cfg4"]
+    total = L * P
+    first, count = shard_ranges(P, ws)[rank]
+    if shard_digests is None:
+        shard_digests, _ = ground_truth(seed, total, L, P, first, count, threads)
+    d2 = bytearray(shard_digests)
+    bad = _corrupt(d2, count, 5)
+    pieces = bytearray(20 * P)
+    pieces[20 * first:20 * (first + count)] = d2
+    expect = _expected_bits(count, bad)
+    out = {"workload": "cfg5: the cfg4 torrent (200 GiB, 51200 x 4 MiB) streamed from host memory over PCIe "
+                       "through the bounded pinned ring, copy/compute overlapped, no resident payload",
+           "piece_length": L, "total_pieces": P, "pieces_per_gpu": count, "bytes_per_gpu": L * count, "ranks": ws,
+           "ring_bytes_per_gpu": _native.TV_STREAM_RING_SLOTS * _native.TV_STREAM_SLOT_BYTES,
+           "column_bytes": E2E_CHUNK, "unit": "GB/s", "steps": steps}
+    ctx = _native.Context(device)
+    pool = None
+    try:
+        ctx.set_option(_native.TV_OPT_RESIDENT, 0)
+        ctx.set_option(_native.TV_OPT_STREAM_CHUNK, E2E_CHUNK)
+        ctx.set_option(_native.TV_OPT_FILE_THREADS, threads)
+        ctx.set_layout(total, L, P, first, count)
+        ctx.set_digests(bytes(pieces))
+
+        def run(fill) -> tuple:
+            ctx.stream_begin()
+            reqs = 0
+            while True:
+                req = ctx.stream_next()
+                if not req.rows:
+                    break
+                fill(req)
+                reqs += 1
+            return ctx.stream_end(), reqs
+
+        def gen(req):
+            ctx.stream_fill_synthetic(req, seed)
+            ctx.stream_commit(req)
+
+        # warm the ring and the chunk buffers (first allocation) outside the timed region
+        ctx.stream_begin()
+        for _ in range(2):
+            gen(ctx.stream_next())
+        ctx.stream_abort()
+
+        def timed(fill):
+            _barrier(dist)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                bf, reqs = run(fill)
+            t1 = time.perf_counter()
+            _barrier(dist)
+            return bf, reqs, _max(dist, t1 - t0)
+
+        bf, reqs, el = timed(gen)
+        ok = _sum(dist, 1.0 if bf == expect else 0.0) == ws
+        out["generated"] = {"value": round(total * steps / el / 1e9, 2), "ms_per_step": round(el * 1e3 / steps, 1),
+                            "bitfield_exact": ok, "requests_per_step": reqs,
+                            "producer": f"host generator (tv_stream_fill_synthetic, {threads} threads) writing "
+                                        "the bytes into the ring slots inside the timed region"}
+        # pinned_pool: the torrent is a 1 GiB page-locked pool of 256 pieces repeated; rows DMA'd from it
+        pool = _native.PinnedBuffer(POOL_PIECES * L)
+        pool.mv[:] = O.synth_fill(seed + 100, 0, POOL_PIECES * L)
+        pool_dig = O.hash_pieces(pool.mv, POOL_PIECES * L, L, POOL_PIECES, threads=threads)
+        dp = bytearray(20 * P)
+        for j in range(count):
+            k = j % POOL_PIECES
+            dp[20 * (first + j):20 * (first + j + 1)] = pool_dig[20 * k:20 * k + 20]
+        bad2 = _corrupt(memoryview(dp)[20 * first:20 * (first + count)], count, 7)
+        ctx.set_digests(bytes(dp))
+
+        def from_pool(req):
+            ctx.stream_commit_from(req, pool.mv, L, ((req.piece - first) % POOL_PIECES) * L + req.offset)
+
+        bf, reqs, el = timed(from_pool)
+        ok = _sum(dist, 1.0 if bf == _expected_bits(count, bad2) else 0.0) == ws
+        out["pinned_pool"] = {"value": round(total * steps / el / 1e9, 2), "ms_per_step": round(el * 1e3 / steps, 1),
+                              "bitfield_exact": ok, "requests_per_step": reqs,
+                              "producer": f"rows DMA'd straight from a {POOL_PIECES * L >> 20} MiB page-locked pool "
+                                          f"(piece first+j = pool piece j % {POOL_PIECES})"}
+        out["value"] = out["generated"]["value"]
+        out["bitfield_exact"] = out["generated"]["bitfield_exact"] and ok
+        out["kernel"] = {1: "lane", 2: "split"}.get(ctx.last_kernel()[0], "?")
+    finally:
+        if pool is not None:
+            pool.close()
+        ctx.close()
+    return out
+
+
+def cpu_baseline(share: dict, target_s: float = 10.0) -> dict:
+    """The CPU oracle (C port of the per-piece SHA-1 path; SHA-NI where the host has it: the reference's
+    WebCrypto SHA-1 is native code of that class) on the allowed cores, one piece per task:
+    a bounded sample of cfg2 (4 GiB of its pieces, generated once, hashed repeatedly for ~target_s),
+    BASELINE configs[0] = cfg1 (64 MiB, 256 x 256 KiB) as its own entry, and the 1-core figures."""
+    from oracle import oracle as O
+    O.set_impl("best")
+    cores = share["cores"]
+
+    def timed(buf, L, n, threads, seconds):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            O.hash_pieces(buf, n * L, L, n, 0, n, threads=threads)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                return n * L * reps / el / 1e9, reps, el
+
+    L2, _, seed2, _ = WORKLOADS["cfg2"]
+    n2 = 4096
+    buf = O.synth_fill(seed2, 0, n2 * L2)
+    gbps, reps, el = timed(buf, L2, n2, cores, target_s)
+    one, _, _ = timed(buf, L2, 64, 1, max(1.0, target_s / 5))
+    del buf
+    L1, n1, seed1, desc1 = WORKLOADS["cfg1"]
+    b1 = O.synth_fill(seed1, 0, n1 * L1)
+    c1, r1, e1 = timed(b1, L1, n1, cores, max(1.0, target_s / 4))
+    c1one, _, _ = timed(b1, L1, n1, 1, max(1.0, target_s / 5))
+    return {"value": round(gbps, 3), "unit": "GB/s", "cores": cores, "kind": "port",
+            "sample": f"{n2} of cfg2's 1 MiB pieces (4 GiB of the same synthetic payload) hashed {reps} times "
+                      f"({el:.1f} s) by oracle/sha1_oracle.c ({O.impl()} SHA-1, one piece per task, {cores} threads)",
+            "impl": O.impl(), "per_core": round(one, 3), "cpu_model": _cpu_model(),
+            "cores_source": share["source"], "nproc": share["nproc"], "affinity_cpus": share["affinity"],
+            "cgroup_quota_cpus": share["cgroup_quota_cpus"], "omp_num_threads": share["omp_num_threads"],
+            "cfg1": {"workload": desc1 + ", the reference's CPU SHA-1 path restated (oracle)",
+                     "value": round(c1, 3), "unit": "GB/s", "ms_per_verify": round(n1 * L1 / c1 / 1e6, 2),
+                     "cores": cores, "reps": r1, "per_core": round(c1one, 3)}}
 
 
 def main() -> int:
@@ -188,120 +399,57 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
+                    help="timed workload (default: cfg2 at N=1, cfg4 strong at N>1)")
+    sc = ap.add_mutually_exclusive_group()
+    sc.add_argument("--strong", action="store_true", help="the workload's pieces are the WHOLE torrent, sharded")
+    sc.add_argument("--weak", action="store_true", help="the workload's pieces are per GPU")
     ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 lane, 2 split")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--no-saturating", action="store_true",
-                    help="skip the piece-saturated leg (N=1 only: 65,536 x 256 KiB pieces against R_valu)")
-    ap.add_argument("--strong", action="store_true",
-                    help="strong scaling: the workload's piece count is the WHOLE torrent, split into N contiguous "
-                         "8-aligned shards (BASELINE config 4: 200 GiB over 2/4/8 GPUs); default is weak scaling")
-    ap.add_argument("--e2e-steps", type=int, default=3,
-                    help="timed end-to-end passes from pinned host memory over PCIe (0 = skip)")
+    ap.add_argument("--no-saturating", action="store_true", help="skip the piece_saturated leg (N=1)")
+    ap.add_argument("--no-cfg4", action="store_true", help="skip the cfg4 anchor leg (N=1) / cfg2_weak leg (N>1)")
+    ap.add_argument("--e2e-steps", type=int, default=1, help="timed e2e_cfg5 passes (0 = skip the leg)")
+    ap.add_argument("--leg-steps", type=int, default=5, help="timed steps of the cfg4 / cfg2_weak / suppl legs")
     a = ap.parse_args()
 
     dist, rank, ws, local = _dist()
-    L, per_gpu, desc = WORKLOADS[a.workload]
-    if a.strong:
-        from torrent_amd.verify import shard_ranges
-        P = per_gpu
-        first, per_gpu = shard_ranges(P, ws)[rank]
-        desc = desc.split(" per GPU")[0].split(" (")[0] + f" ({P} pieces in all, {ws} shard(s), strong scaling)"
-    else:
-        P = per_gpu * ws
-        first = rank * per_gpu
-    total = L * P
-
     device = local % max(1, _native.device_count())
-    ctx = _native.Context(device)
-    ctx.set_option(_native.TV_OPT_KERNEL, a.kernel)
-    ctx.set_layout(total, L, P, first, per_gpu)
-    ctx.fill_synthetic(SEED)
-    shard_digests = ctx.hash()                     # creation mode on the resident shard
-    # 1 % corrupted digests (every 100th piece, plus the shard's last) -> known expected bitfield
-    bad = set(range(0, per_gpu, 100)) | {per_gpu - 1}
-    dig = bytearray(shard_digests)
-    for j in bad:
-        dig[20 * j + 7] ^= 0x10
-    pieces = bytearray(20 * P)
-    pieces[20 * first:20 * (first + per_gpu)] = dig
-    ctx.set_digests(bytes(pieces))
-    expect = bytearray(b"\xff" * ((per_gpu + 7) // 8))
-    if per_gpu % 8:
-        expect[-1] = (0xFF00 >> (per_gpu % 8)) & 0xFF
-    for j in bad:
-        expect[j >> 3] &= ~(0x80 >> (j & 7)) & 0xFF
+    share = cpu_share()
+    threads = share["cores"]
+    workload = a.workload or ("cfg2" if ws == 1 else "cfg4")
+    strong = a.strong or (not a.weak and a.workload is None and ws > 1)
 
-    for _ in range(a.warmup):
-        bf = ctx.verify()
-    _device_sync(ctx, device)
-    _barrier(dist)
-    kernel_ms = []
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        bf = ctx.verify()
-        kernel_ms.append(ctx.last_timing()[0])
-    _device_sync(ctx, device)
-    t1 = time.perf_counter()
-    _barrier(dist)
-    elapsed = _max(dist, t1 - t0)
-    correct = bf == bytes(expect)
-    all_correct = _sum(dist, 1.0 if correct else 0.0) == ws
-    kernel, _ = ctx.last_kernel()
-    avg_kernel_ms = sum(kernel_ms) / len(kernel_ms)
-    worst_kernel_ms = _max(dist, avg_kernel_ms)
-
-    bytes_per_gpu = L * per_gpu
-
-    # End-to-end leg (reported beside `value`, never as it): the same shard streamed from a pinned
-    # host copy over PCIe with copy/compute overlap (tv_verify_host; SURVEY 8d config 5 form).
-    e2e = None
-    host = None
+    main_leg = resident_leg(dist, ws, rank, device, workload, strong, a.steps, a.warmup, a.kernel, threads,
+                            want_digests=(workload == "cfg4" and strong))
+    legs = {}
+    cfg4_digests = None
+    if workload == "cfg4" and strong:
+        cfg4_digests = main_leg.pop("_digests")
+        main_leg.pop("_first")
+    elif ws == 1 and not a.no_cfg4:
+        legs["cfg4"] = resident_leg(dist, 1, 0, device, "cfg4", True, a.leg_steps, 1, a.kernel, threads,
+                                    want_digests=True)
+        cfg4_digests = legs["cfg4"].pop("_digests")
+        legs["cfg4"].pop("_first")
+    if ws > 1 and not a.no_cfg4 and not (workload == "cfg2" and not strong):
+        legs["cfg2_weak"] = resident_leg(dist, ws, rank, device, "cfg2", False, a.leg_steps, 1, a.kernel, threads)
     if a.e2e_steps > 0:
         try:
-            host = _native.PinnedBuffer(bytes_per_gpu)
-        except Exception as exc:  # e.g. not enough page-lockable host memory on this node
-            e2e = {"skipped": f"pinned host allocation of {bytes_per_gpu} B failed: {exc}"}
-        # collective decision: every rank runs the leg (and its barriers) or none does
-        if _sum(dist, 1.0 if host is not None else 0.0) < ws:
-            if host is not None:
-                host.close()
-                host = None
-            e2e = e2e or {"skipped": "pinned host allocation failed on another rank"}
-    if host is not None:
-        ctx.read(first * L, host.mv)            # host copy of the resident synthetic payload
-        bf2 = ctx.verify_host(host.mv)          # warmup
-        _device_sync(ctx, device)
-        _barrier(dist)
-        e0 = time.perf_counter()
-        for _ in range(a.e2e_steps):
-            bf2 = ctx.verify_host(host.mv)
-        _device_sync(ctx, device)
-        e1 = time.perf_counter()
-        _barrier(dist)
-        e_el = _max(dist, e1 - e0)
-        e_ok = _sum(dist, 1.0 if bf2 == bytes(expect) else 0.0) == ws
-        e2e = {"value": round(total * a.e2e_steps / e_el / 1e9, 2), "unit": "GB/s",
-               "steps": a.e2e_steps, "ms_per_step": round(e_el * 1e3 / a.e2e_steps, 2), "bitfield_exact": e_ok,
-               "launches_per_step": ctx.last_kernel()[1],
-               "mode": "pinned host -> HBM column stream (2D DMA) overlapped with the verify kernel; PCIe-inclusive"}
-        host.close()
-
-    sat = None
-    if ws == 1 and a.workload == "cfg2" and not a.no_saturating:
-        try:
-            sat = saturating_leg(device)
+            legs["e2e_cfg5"] = e2e_cfg5(dist, ws, rank, device, a.e2e_steps, threads, cfg4_digests)
         except Exception as exc:  # reported, never fatal to the bench line
-            sat = {"skipped": f"{type(exc).__name__}: {exc}"}
-
-    value = total * a.steps / elapsed / 1e9      # every rank's shard: weak N x per-GPU bytes, strong the whole torrent
-    achieved = bytes_per_gpu / (avg_kernel_ms / 1e3) / 1e9
-    piece_ceiling = min(VALU_PEAK_GBPS, per_gpu * 64 * CLOCK_HZ / (SERIAL_INSTR.get(kernel, 613) * LONE_WAVE_CYC) / 1e9)
+            legs["e2e_cfg5"] = {"skipped": f"{type(exc).__name__}: {exc}"}
+    cfg4_digests = None
+    if ws == 1 and workload == "cfg2" and not a.no_saturating:
+        try:
+            legs["piece_saturated"] = resident_leg(dist, 1, 0, device, "suppl", False, a.leg_steps, 1, a.kernel, threads)
+        except Exception as exc:
+            legs["piece_saturated"] = {"skipped": f"{type(exc).__name__}: {exc}"}
 
     if rank == 0:
+        bytes_per_gpu = main_leg["bytes_per_gpu"]
         traffic = None
-        tpath = os.path.join(ROOT, "profiles", f"traffic_{a.workload}.json")
+        tpath = os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
         if os.path.exists(tpath):
             try:
                 rec = json.load(open(tpath))
@@ -310,47 +458,50 @@ def main() -> int:
                     traffic = rec.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        achieved = main_leg["achieved"]
         out = {
             "metric": "verified GB/s (SHA-1 pieces, HBM-resident)",
-            "value": round(value, 2),
+            "value": main_leg["value"],
             "unit": "GB/s",
             "n_gpus": ws,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": round(elapsed * 1e3 / a.steps, 3),
+            "ms_per_step": main_leg["ms_per_step"],
             "higher_is_better": True,
-            "scaling": "strong" if a.strong else "weak",
+            "scaling": main_leg["scaling"],
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (device counter-PRNG payload; 1% corrupted digests)",
-            "config": {"workload": desc, "piece_length": L, "pieces_per_gpu": per_gpu,
-                       "total_pieces": P, "bytes_per_gpu": bytes_per_gpu,
-                       "kernel": {1: "lane", 2: "split"}.get(kernel, str(kernel)),
+            "data": "synthetic (device counter-PRNG payload; expected digests from the CPU oracle, 1% corrupted)",
+            "config": {"workload": main_leg["workload"], "piece_length": main_leg["piece_length"],
+                       "pieces_per_gpu": main_leg["pieces_per_gpu"], "total_pieces": main_leg["total_pieces"],
+                       "bytes_per_gpu": bytes_per_gpu, "kernel": main_leg["kernel"],
                        "parallelism": f"piece shards x{ws}, no collective"},
-            "bitfield_exact": all_correct,
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel_ms_avg": round(avg_kernel_ms, 3), "kernel_ms_max_over_ranks": round(worst_kernel_ms, 3),
+            "bitfield_exact": main_leg["bitfield_exact"],
+            "expected": main_leg["expected"],
+            "roofline": {"bound": "valu", "achieved": achieved, "peak": round(ROOF_PEAK_GBPS, 1), "unit": "GB/s",
+                         "frac": round(achieved / ROOF_PEAK_GBPS, 4), "traffic": traffic,
+                         "kernel_ms_avg": main_leg["kernel_ms_avg"],
+                         "kernel_ms_max_over_ranks": main_leg["kernel_ms_max_over_ranks"],
                          "algorithmic_bytes_per_launch": bytes_per_gpu,
-                         "valu_peak": round(VALU_PEAK_GBPS, 1),
-                         "frac_of_valu_peak": round(achieved / VALU_PEAK_GBPS, 4),
-                         "piece_parallelism_ceiling": round(piece_ceiling, 1),
-                         "frac_of_piece_ceiling": round(achieved / piece_ceiling, 4),
-                         "note": "SHA-1 is VALU-bound on MI355X (valu_peak from measured per-op SIMD costs), not "
-                                 "HBM-bound; it is serial per piece, so P pieces cap the rate at P x 64 B / "
-                                 "(serial VALU instr x 4.07 cyc) per GPU (piece_parallelism_ceiling)"},
+                         "peak_is": "min(HBM 8000 GB/s, R_valu)", "valu_peak": round(VALU_PEAK_GBPS, 1),
+                         "hbm_peak": HBM_PEAK_GBPS, "frac_hbm": round(achieved / HBM_PEAK_GBPS, 4),
+                         "piece_parallelism_ceiling": main_leg["piece_parallelism_ceiling"],
+                         "frac_of_piece_ceiling": main_leg["frac_of_piece_ceiling"],
+                         "valu_peak_derivation": VALU_DERIVATION,
+                         "note": "SHA-1 is serial per piece, so P pieces per GPU cap the rate at P x 64 B / "
+                                 "(serial VALU instr x 4.07 cyc) (piece_parallelism_ceiling; 405 instr for the "
+                                 "split rounds wave, 613 for the lane kernel); full R_valu needs >= 65,536 "
+                                 "pieces per GPU (piece_saturated)"},
+            "ground_truth_s": main_leg["ground_truth_s"],
         }
-        if sat is not None:
-            out["piece_saturated"] = sat
-        if e2e is not None:
-            out["e2e_pinned_host"] = e2e
+        out.update(legs)
         if ws == 1 and not a.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(L, total, P, first, shard_digests, a.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(share, a.cpu_seconds)
         print(json.dumps(out), flush=True)
-    ctx.close()
+    ok = main_leg["bitfield_exact"] and all(v.get("bitfield_exact", True) for v in legs.values())
     if dist is not None:
         dist.destroy_process_group()
-    return 0 if all_correct and (e2e is None or e2e.get("bitfield_exact", True)) else 1
+    return 0 if ok else 1
 
 
 if __name__ == "__main__":
