@@ -93,7 +93,17 @@ def _dist():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if ws > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo", init_method="env://")
+        # gloo prints its "connected to N peer ranks" banner on fd 1 from C++: send it to stderr, so the
+        # bench's stdout carries exactly one JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", init_method="env://")
+            dist.barrier()
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
         return dist, rank, ws, local
     return None, 0, 1, 0
 
