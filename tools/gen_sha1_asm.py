@@ -6,7 +6,7 @@ compression compiles to ~790 VALU instead of ~613), and it pads every inline-asm
 with `s_nop 0`, which costs a full issue slot for a lone wave.  So each compression is ONE
 asm statement, and this script emits it.  The emitted instruction stream is executed by the
 emulator below against hashlib before the header is written (`--check`, also run by
-tests/test_asm_gen.py), so a wrong register rotation can never reach the GPU.
+tests/test_abi.py::test_asm_generator_emulator), so a wrong register rotation can never reach the GPU.
 
 Blocks emitted
 --------------
@@ -14,8 +14,12 @@ SHA1_FULL   one 64-byte block, message schedule computed in-asm (16-word rolling
             5 VALU per round + 3 per scheduled word = 400 + 192 = 592 (+16 v_perm bswap and
             5 feed-forward adds by the compiler outside) = 613 per block.
 SHA1_LDS    the 80 rounds only (400 VALU); W[0..79] comes from LDS as 20 ds_read_b128
-            (layout [t/4][lane][4 words], conflict-free), kept 15 quads ahead in a 64-VGPR
+            (layout [t/4][lane][4 words], conflict-free), kept 15 quads ahead in an 80-VGPR
             ring of PHYSICAL registers (a 128-bit asm operand cannot be split in AMDGPU asm).
+            The split kernel's rounds loop is one pipelined stream over its blocks: the reads
+            run 15 quads ahead across block boundaries (gen_rounds_block; 3 LDS buffers, the
+            helper two blocks ahead), checked by check_rounds_stream against the helper's
+            protocol.
 
 Round (roles rotate statically; the new `a` is written into the old `e` register):
     E  = v_add3_u32(E, K, W[t])          # off the critical path
@@ -43,9 +47,19 @@ M32 = 0xFFFFFFFF
 # long: 15 quads in flight (60 rounds ahead, lgkmcnt's 4-bit maximum) run the 80-round block in
 # 1,794 cycles against 1,894 with 7 in flight (tools/gen_ubench_rounds.py, profiles/r01/ubench_rounds.log).
 RING_BASE = 64
-RING_QUADS = 16
-READ_AHEAD = 15     # quads in flight ahead of the one being consumed
-WAIT_EVERY = 4      # one s_waitcnt per 4 quads (16 rounds)
+# (the TV_GEN_* environment variables select build variants for A/B measurements; the defaults are
+# the shipped configuration)
+RING_QUADS = int(os.environ.get("TV_GEN_RING", "16"))   # register quads of the K+W ring
+READ_AHEAD = int(os.environ.get("TV_GEN_RA", "15"))   # quads in flight ahead of the one being consumed
+WAIT_EVERY = int(os.environ.get("TV_GEN_WAIT", "4"))    # one s_waitcnt per WAIT_EVERY quads
+LDS_BUFS = int(os.environ.get("TV_GEN_BUFS", "3"))      # K+W buffers per pair; the helper runs LDS_BUFS-1 blocks ahead
+# PIPELINED = 1: the rounds reads run 15 quads ahead ACROSS block boundaries (gen_rounds_block).  Measured
+# 4 % slower than a burst of 15 reads at each block's start (13.69 vs 12.95 ms at cfg2,
+# profiles/r02/split_variants.jsonl): LDS data returning under the VALU stream costs more issue cycles
+# than a burst landing while the wave waits.  Kept as a checked option; the shipped build is 0.
+PIPELINED = os.environ.get("TV_GEN_PIPE", "0") == "1"
+HELPER_AHEAD = LDS_BUFS - 1
+assert not PIPELINED or (LDS_BUFS >= 3 and RING_QUADS == 20), "the pipelined stream needs 3 buffers and a 20-quad ring"
 # physical VGPRs of the helper (schedule) block: 16-word W window, xor3 temp, 3 output quads
 HW_BASE = 80
 HT = 96
@@ -132,7 +146,7 @@ def gen_lds(off_base: int = 0, lead_wait: bool = True):
         g = t // 4
         if t % 4 == 0 and g % WAIT_EVERY == 0:
             need = min(g + WAIT_EVERY - 1, 19)          # quads consumed before the next wait
-            ins.append(("s_waitcnt_lgkm", max(0, issued - need)))
+            ins.append(("s_waitcnt_lgkm", min(15, max(0, issued - need))))   # (lgkmcnt is 4 bits)
         A, B, C, D, E = roles(t)
         e_src = R.rd(E)
         ins.append(("v_add_u32", R.wr(E), ring_reg(g, t % 4), e_src))
@@ -146,6 +160,43 @@ def gen_lds(off_base: int = 0, lead_wait: bool = True):
         ins.append(("v_add3_u32", R.rd(E), R.rd(E), "t0", "t1"))
     assert R.cur == [f"r{i}" for i in range(5)]
     return ins
+
+
+def gen_rounds_block(off_cur: int, off_next: int):
+    """One block of the split kernel's PIPELINED rounds stream.  On entry quads 0..14 of this block are in
+    flight (issued by the previous block, or the loop prologue); after consuming quad g the read of quad
+    g + 15 is issued -- past quad 19 that is quad g - 5 of the NEXT block, from its buffer at off_next -- so
+    READ_AHEAD quads stay in flight across block boundaries and no block starts on an LDS latency bubble.
+    Then h += r and the workgroup barrier.  Needs the helper two blocks ahead (LDS_BUFS = 3): the next
+    block was written before the barrier that started this one."""
+    ins = []
+    R = Regs()
+    allowed = READ_AHEAD - WAIT_EVERY   # reads still in flight once quads g .. g+WAIT_EVERY-1 retired
+    for t in range(80):
+        g = t // 4
+        if t % 4 == 0 and g % WAIT_EVERY == 0:
+            ins.append(("s_waitcnt_lgkm", allowed))
+        A, B, C, D, E = roles(t)
+        e_src = R.rd(E)
+        ins.append(("v_add_u32", R.wr(E), ring_reg(g, t % 4), e_src))
+        if t % 4 == 3:
+            q = g + READ_AHEAD
+            ins.append(("ds_read_b128", q % 20, off_cur + q * 1024 if q < 20 else off_next + (q - 20) * 1024))
+        ins.append(("v_alignbit_b32", "t0", R.rd(A), R.rd(A), 27))
+        ins.append(_fop(t, "t1", R.rd(B), R.rd(C), R.rd(D)))
+        b_src = R.rd(B)
+        ins.append(("v_alignbit_b32", R.wr(B), b_src, b_src, 2))
+        ins.append(("v_add3_u32", R.rd(E), R.rd(E), "t0", "t1"))
+    assert R.cur == [f"r{i}" for i in range(5)]
+    for i in range(5):
+        ins.append(("v_add_u32", f"h{i}", f"h{i}", f"r{i}"))
+    ins.append(("s_barrier",))
+    return ins
+
+
+def rounds_prologue(off: int = 0):
+    """Issue quads 0 .. READ_AHEAD-1 of the first block (buffer at off)."""
+    return [("ds_read_b128", g, off + g * 1024) for g in range(READ_AHEAD)]
 
 
 def hw(t: int) -> str:
@@ -177,21 +228,25 @@ def gen_helper(src=None, off_base: int = 0):
 
 
 def rounds_loop_text() -> str:
-    """The split kernel's rounds wave over nsteps (>= 1) blocks in which every lane updates: per
-    block the 80 rounds from K+W in LDS (buffer (step & 1)), h += r, barrier.  One asm statement,
-    so no compiler bookkeeping or asm-boundary s_nop between blocks."""
-    L = ["s_waitcnt lgkmcnt(0)", "s_mov_b32 %[cnt], %[nsteps]", "L_rloop_%=:"]
-
-    def step(off):
-        L.extend(_emit_lines(gen_lds(off, lead_wait=False)))
-        for i in range(5):
-            L.append(f"v_add_u32 %[h{i}], %[h{i}], %[r{i}]")
-        L.append("s_barrier")
-
-    step(0)
-    L += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_eq_u32 %[cnt], 0", "s_cbranch_scc1 L_rdone_%="]
-    step(RING_BYTES)
-    L += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_lg_u32 %[cnt], 0", "s_cbranch_scc1 L_rloop_%=", "L_rdone_%=:"]
+    """The split kernel's rounds wave over nsteps (>= 1) blocks in which every lane updates, starting
+    at ring buffer 0: one pipelined stream (gen_rounds_block) over buffers 0, 1, 2, 0, ... -- 80 rounds
+    from K+W in LDS, h += r, barrier per block.  One asm statement, so no compiler bookkeeping or
+    asm-boundary s_nop between blocks.  The reads issued ahead for the block after the last one are
+    drained before it returns."""
+    L = ["s_waitcnt lgkmcnt(0)", "s_mov_b32 %[cnt], %[nsteps]"]
+    if PIPELINED:
+        L.extend(_emit_lines(rounds_prologue(0)))
+    L.append("L_rloop_%=:")
+    for k in range(LDS_BUFS):
+        if PIPELINED:
+            L.extend(_emit_lines(gen_rounds_block(k * RING_BYTES, ((k + 1) % LDS_BUFS) * RING_BYTES)))
+        else:   # per-block stream: its 15 reads issued at the block's start
+            L.extend(_emit_lines(gen_lds(k * RING_BYTES, lead_wait=False)))
+            L.extend(f"v_add_u32 %[h{i}], %[h{i}], %[r{i}]" for i in range(5))
+            L.append("s_barrier")
+        L += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_eq_u32 %[cnt], 0",
+              "s_cbranch_scc1 L_rdone_%=" if k < LDS_BUFS - 1 else "s_cbranch_scc0 L_rloop_%="]
+    L += ["L_rdone_%=:", "s_waitcnt lgkmcnt(0)"]
     return "\n".join(f'    "{l}\\n"' for l in L)
 
 
@@ -217,7 +272,7 @@ def helper_loop_text() -> str:
         L.append("s_subb_u32 %[adv], %[adv], 0")
         L.append(f"v_lshl_add_u64 v[{VL}:{VL + 1}], v[{VL}:{VL + 1}], 0, %[inc]")
 
-    def step(pbase, off_base):
+    def step(pbase, off_base, barrier=True):
         L.append("s_waitcnt vmcnt(4)")
         body = gen_helper([f"v{pbase + i}" for i in range(16)], off_base)
         perms, rest = body[:16], body[16:]
@@ -225,8 +280,9 @@ def helper_loop_text() -> str:
         loads(pbase)        # the perms have read pbase: refill it with the block 2 ahead
         advance()
         L.extend(_emit_lines(rest))
-        L.append("s_waitcnt lgkmcnt(0)")
-        L.append("s_barrier")
+        if barrier:
+            L.append("s_waitcnt lgkmcnt(0)")
+            L.append("s_barrier")
 
     L.append("s_sub_u32 %[adv], %[nraw], 1")
     L.append(f"v_mov_b64 v[{VL}:{VL + 1}], %[va]")
@@ -234,16 +290,20 @@ def helper_loop_text() -> str:
     advance()
     loads(P1_BASE)
     advance()
-    L.append("s_mov_b32 %[cnt], %[nraw]")
-    L.append("L_hloop_%=:")
-    step(P0_BASE, 0)
-    L.append("s_sub_u32 %[cnt], %[cnt], 1")
+    # block 0 into buffer 0; with the helper two blocks ahead (HELPER_AHEAD = 2) no barrier follows it:
+    # its first barrier (the rounds wave's starting one) follows the write of block 1
+    step(P0_BASE, 0, barrier=HELPER_AHEAD == 1)
+    L.append("s_sub_u32 %[cnt], %[nraw], 1")
     L.append("s_cmp_eq_u32 %[cnt], 0")
     L.append("s_cbranch_scc1 L_hdone_%=")
-    step(P1_BASE, RING_BYTES)
-    L.append("s_sub_u32 %[cnt], %[cnt], 1")
-    L.append("s_cmp_lg_u32 %[cnt], 0")
-    L.append("s_cbranch_scc1 L_hloop_%=")
+    L.append("L_hloop_%=:")
+    period = 2 * LDS_BUFS // (2 if LDS_BUFS % 2 == 0 else 1)   # lcm(prefetch register sets 2, LDS buffers)
+    for k in range(period):
+        blk = k + 1                  # block index (mod period) of this step
+        step((P0_BASE, P1_BASE)[blk % 2], (blk % LDS_BUFS) * RING_BYTES)
+        L.append("s_sub_u32 %[cnt], %[cnt], 1")
+        L.append("s_cmp_eq_u32 %[cnt], 0")
+        L.append("s_cbranch_scc1 L_hdone_%=" if k < period - 1 else "s_cbranch_scc0 L_hloop_%=")
     L.append("L_hdone_%=:")
     L.append("s_waitcnt vmcnt(0)")
     return "\n".join(f'    "{l}\\n"' for l in L)
@@ -251,22 +311,22 @@ def helper_loop_text() -> str:
 
 # ---------------------------------------------------------------- emulator -------------
 
-def emulate(ins, regs: dict, lds: dict | None = None, addr: int = 0):
+def emulate(ins, regs: dict, lds: dict | None = None, addr: int = 0, on_barrier=None, drain: bool = True):
     """Execute an instruction list on a dict of 32-bit registers (one lane).  ds_read results
     land only when an s_waitcnt lgkmcnt(N) retires them (in order); reading a register whose
     load is still in flight, or overwriting one, raises -- so the wait counts are checked too."""
-    pending = []  # [(regs, values)] oldest first
+    pending = []  # [(regs, values, lds addresses)] oldest first
 
     def v(x):
         if isinstance(x, str):
-            for rs, _ in pending:
+            for rs, _, _ in pending:
                 if x in rs:
                     raise AssertionError(f"read of {x} before its ds_read retired")
             return regs[x]
         return x
 
     def wr(x, val):
-        for rs, _ in pending:
+        for rs, _, _ in pending:
             if x in rs:
                 raise AssertionError(f"write of {x} while its ds_read is in flight")
         regs[x] = val
@@ -305,17 +365,23 @@ def emulate(ins, regs: dict, lds: dict | None = None, addr: int = 0):
             q, off = op[1], op[2]
             rs = [ring_reg(q, j) for j in range(4)]
             for x in rs:
-                for prs, _ in pending:
+                for prs, _, _ in pending:
                     assert x not in prs, f"ds_read into {x} while it is in flight"
-            pending.append((rs, [lds[addr + off + 4 * j] for j in range(4)]))
+            # (an address nothing wrote reads as garbage: a prefetch past the last block, never consumed)
+            pending.append((rs, [lds.get(addr + off + 4 * j, 0xBAD0BAD0) for j in range(4)],
+                            [addr + off + 4 * j for j in range(4)]))
         elif o == "s_waitcnt_lgkm":
             while len(pending) > op[1]:
-                rs, vals = pending.pop(0)
+                rs, vals, _ = pending.pop(0)
                 for x, val in zip(rs, vals):
                     regs[x] = val
+        elif o == "s_barrier":
+            if on_barrier is not None:
+                on_barrier({a for _, _, adrs in pending for a in adrs})
         else:
             raise ValueError(o)
-    assert not pending, "ds_read still in flight at the end of the block"
+    if drain:
+        assert not pending, "ds_read still in flight at the end of the block"
     return regs
 
 
@@ -363,6 +429,52 @@ def _check_block(block: bytes, h):
     return exp
 
 
+def _kw_words(block: bytes):
+    def rotl(x, n):
+        return ((x << n) | (x >> (32 - n))) & M32
+    ww = list(struct.unpack(">16I", block)) + [0] * 64
+    for t in range(16, 80):
+        ww[t] = rotl(ww[t - 3] ^ ww[t - 8] ^ ww[t - 14] ^ ww[t - 16], 1)
+    return [(ww[t] + K[t // 20]) & M32 for t in range(80)]
+
+
+def check_rounds_stream(blocks, h):
+    """The pipelined rounds stream over consecutive blocks, run exactly as rounds_loop_text lays it out
+    (prologue, blocks on buffers 0, 1, 2, 0, ...), against the helper's protocol: blocks 0 and 1 are in
+    LDS at the start; at the barrier that ends block k (B_{k+1}) block k+3's buffer is poisoned (the real
+    helper may be writing it from then on) and block k+2 is written (the latest moment the protocol
+    allows).  A read of a block too early, or of a buffer after it was handed back, returns wrong words."""
+    lds = {}
+
+    def put(m, words, in_flight=frozenset()):
+        base = (m % LDS_BUFS) * RING_BYTES
+        for t in range(80):
+            a = base + 1024 * (t // 4) + 4 * (t % 4)
+            assert a not in in_flight, f"LDS {a} rewritten while a ds_read of it is in flight"
+            lds[a] = words[t]
+
+    kws = [_kw_words(b) for b in blocks]
+    put(0, kws[0])
+    if len(blocks) > 1:
+        put(1, kws[1])
+    state = {"k": 0}
+
+    def on_barrier(in_flight):
+        k = state["k"]               # the block that just ended
+        state["k"] = k + 1
+        put(k + 3, [0xDEADBEEF ^ t for t in range(80)], in_flight)   # handed back to the helper
+        if k + 2 < len(blocks):
+            put(k + 2, kws[k + 2], in_flight)
+
+    regs = {f"h{i}": h[i] for i in range(5)}
+    ins = list(rounds_prologue(0))
+    for k in range(len(blocks)):
+        ins += gen_rounds_block((k % LDS_BUFS) * RING_BYTES, ((k + 1) % LDS_BUFS) * RING_BYTES)
+    ins.append(("s_waitcnt_lgkm", 0))
+    emulate(ins, regs, lds, 0, on_barrier=on_barrier)
+    return [regs[f"h{i}"] for i in range(5)]
+
+
 def self_check():
     """Hash several messages through the emulated instruction streams; compare with hashlib."""
     import random
@@ -375,6 +487,13 @@ def self_check():
         for i in range(0, len(padded), 64):
             h = _check_block(padded[i:i + 64], h)
         assert struct.pack(">5I", *h) == hashlib.sha1(msg).digest(), n
+    # the split kernel's pipelined rounds stream over 1 .. 7 consecutive blocks (every buffer phase)
+    for n in ([0, 55, 64, 119, 200, 310, 400] if PIPELINED else []):
+        msg = bytes(rng.randrange(256) for _ in range(n))
+        padded = msg + b"\x80" + b"\0" * ((55 - n) % 64) + struct.pack(">Q", 8 * n)
+        h0 = [0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0]
+        h = check_rounds_stream([padded[i:i + 64] for i in range(0, len(padded), 64)], h0)
+        assert struct.pack(">5I", *h) == hashlib.sha1(msg).digest(), ("stream", n)
     return True
 
 
@@ -409,6 +528,8 @@ def _emit_lines(ins, full: bool = False):
             lines.append(f"v_perm_b32 {_opnd(op[1], full)}, 0, {_opnd(op[3], full)}, {_opnd(op[4], full)}")
         elif o == "ds_write_b128":
             lines.append(f"ds_write_b128 %[addr], v[{op[1]}:{op[1] + 3}] offset:{op[2]}")
+        elif o == "s_barrier":
+            lines.append("s_barrier")
         else:
             lines.append(f"{o} " + ", ".join(_opnd(x, full) for x in op[1:]))
     return lines
@@ -421,12 +542,16 @@ def emit(ins, full: bool) -> str:
 HEADER = """// GENERATED by tools/gen_sha1_asm.py -- do not edit.  Regenerate with:
 //   python3 tools/gen_sha1_asm.py
 // The instruction streams below are checked against hashlib by the generator's emulator
-// (tests/test_asm_gen.py) before they are written.
+// (tests/test_abi.py::test_asm_generator_emulator) before they are written.
 #pragma once
 #include <stdint.h>
 
 #define TV_SHA1_RING_BASE {ring_base}
 #define TV_SHA1_RING_QUADS {ring_quads}
+// K+W buffers per split-kernel pair, and how many blocks the helper wave runs ahead of the rounds wave
+// (its first HELPER_AHEAD - 1 writes are not followed by a barrier; it ends with as many extra barriers)
+#define TV_SHA1_LDS_BUFS {lds_bufs}
+#define TV_SHA1_HELPER_AHEAD {helper_ahead}
 
 // One SHA-1 compression, schedule in-asm.  w[16] holds the big-endian message words and is
 // clobbered.  On return r = working state after round 79; caller does h += r.
@@ -512,7 +637,8 @@ def render() -> str:
     hregs = list(range(HW_BASE, HW_BASE + 16)) + [HT] + list(range(HOUT_BASE, HOUT_BASE + 4 * HOUT_QUADS))
     helper = ", ".join(f'"v{i}"' for i in hregs)
     loop = ", ".join(f'"v{i}"' for i in hregs + list(range(P0_BASE, VL + 2)))
-    return HEADER.format(ring_base=RING_BASE, ring_quads=RING_QUADS, full=emit(gen_full(), True),
+    return HEADER.format(ring_base=RING_BASE, ring_quads=RING_QUADS, lds_bufs=LDS_BUFS, helper_ahead=HELPER_AHEAD,
+                         full=emit(gen_full(), True),
                          lds=emit(gen_lds(), False), helper=emit(gen_helper(), False),
                          helper_loop=helper_loop_text(), rounds_loop=rounds_loop_text(),
                          ring_clobbers=ring, helper_clobbers=helper,

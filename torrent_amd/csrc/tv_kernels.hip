@@ -247,11 +247,16 @@ __global__ __launch_bounds__(256) void tv_lane_kernel(TvPieces p) {
 
 // ------------------------------------------------------------------------------------------
 // split kernel: wave 0 = rounds (80 rounds per block from LDS), wave 1 = helper (loads +
-// message schedule into a 2 x 20 KiB LDS ring).  One barrier per block.
+// message schedule into a 3 x 20 KiB LDS ring, two blocks ahead).  One barrier per block.
 // ------------------------------------------------------------------------------------------
 namespace {
 
 constexpr int kRingWords = 80 * 64;  // one buffer: [20 quads][64 lanes][4 words]
+// K+W buffers per pair.  The helper runs TWO blocks ahead (block j lives in buffer j % 3), so the rounds
+// wave can keep its 15 LDS reads in flight across block boundaries (tools/gen_sha1_asm.py
+// gen_rounds_block) instead of restarting them, and an LDS latency, at every block.
+constexpr uint32_t kBufs = TV_SHA1_LDS_BUFS;
+constexpr uint32_t kAhead = TV_SHA1_HELPER_AHEAD;
 
 __device__ __forceinline__ void lds_barrier() {
     // LDS writes of this wave complete, then the workgroup barrier.  Deliberately NOT
@@ -275,7 +280,7 @@ __global__ __launch_bounds__(128 * PAIRS) void tv_split_kernel(TvPieces p) {
     // with <= 1 workgroup per CU no rounds wave shares its SIMD.  Each pair has its own 2 x 20 KiB
     // K+W ring; the barrier is workgroup-wide, so both pairs run the same (workgroup) block range.
     static_assert(!LIST || PAIRS == 1, "list mode runs one pair per workgroup");
-    __shared__ __attribute__((aligned(16))) uint4 ring[2 * PAIRS * kRingWords / 4];
+    __shared__ __attribute__((aligned(16))) uint4 ring[kBufs * PAIRS * kRingWords / 4];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t pair = wave % PAIRS;
@@ -298,13 +303,16 @@ __global__ __launch_bounds__(128 * PAIRS) void tv_split_kernel(TvPieces p) {
     const uint32_t nb = (uint32_t)nblocks(len);
     const uint8_t* piece = p.data + (uint64_t)jj * p.stride - p.data_off;
     const uint32_t b0 = g.fast_begin, end = g.end, fast_end = g.fast_end;
-    uint4* const pring = ring + pair * 2 * (kRingWords / 4);
+    uint4* const pring = ring + pair * kBufs * (kRingWords / 4);
 
     if (role != 0) {
         // ---------------- helper wave ----------------
-        // Raw blocks [b0, fast_end): one asm loop (loads 2 blocks ahead into registers the compiler
-        // never allocates, schedule, K+W -> LDS, barrier per block).  Then the 1-2 padded tail blocks
-        // (and one spare block past `end` that the rounds wave never reads) in C++.
+        // Block j of the launch goes to buffer j % 3, and the helper's barrier k follows its write of
+        // block k + 1: it runs two blocks ahead.  Raw blocks [b0, fast_end): one asm loop (loads 2 blocks
+        // ahead into registers the compiler never allocates, schedule, K+W -> LDS, a barrier after every
+        // block but the first).  Then the 1-2 padded tail blocks and one spare block past `end` that the
+        // rounds wave never consumes, in C++, and the barrier that matches the rounds wave's last one
+        // (both waves execute end - b0 + 1 barriers).
         const uint32_t lds_lane = (uint32_t)(uintptr_t)(void*)pring + lane * 16u;
         uint32_t b = b0;
         if (fast_end > b0) {
@@ -316,9 +324,10 @@ __global__ __launch_bounds__(128 * PAIRS) void tv_split_kernel(TvPieces p) {
             build_tail_block(piece, len, b, w);
 #pragma unroll
             for (int i = 0; i < 16; i++) w[i] = bswap32(w[i]);  // the schedule block byte-swaps
-            tv_sha1_schedule_lds(w, lds_lane + ((b - b0) & 1u) * (kRingWords * 4u), TV_K0, TV_K1, TV_K2, TV_K3);
-            lds_barrier();
+            tv_sha1_schedule_lds(w, lds_lane + ((b - b0) % kBufs) * (kRingWords * 4u), TV_K0, TV_K1, TV_K2, TV_K3);
+            if (b - b0 + 1 >= kAhead) lds_barrier();
         }
+        for (uint32_t k = 1; k < kAhead; k++) lds_barrier();
         return;
     }
 
@@ -339,7 +348,7 @@ __global__ __launch_bounds__(128 * PAIRS) void tv_split_kernel(TvPieces p) {
     // the short last piece's wave: lanes past their final block keep their digest
     for (; b < end; b++) {
         uint32_t r[5];
-        tv_sha1_lds(h, r, ring_base + ((b - b0) & 1u) * (kRingWords * 4u));
+        tv_sha1_lds(h, r, ring_base + ((b - b0) % kBufs) * (kRingWords * 4u));
         if (b < nb) {
 #pragma unroll
             for (int i = 0; i < 5; i++) h[i] += r[i];
@@ -447,9 +456,10 @@ __global__ __launch_bounds__(256) void tv_fill_bytes_kernel(uint8_t* payload, ui
 hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_t s, int split_pairs) {
     if (p.n == 0) return hipSuccess;
     if (kernel == TV_KERNEL_SPLIT) {
-        // one pair per workgroup while that still gives <= 1 workgroup per CU (256 CUs); two pairs
-        // (4 waves on the CU's 4 SIMDs) up to 32768 pieces
-        const int pairs = (split_pairs == 1 || split_pairs == 2) ? split_pairs : (p.n <= 256 * 64 ? 1 : 2);
+        // one pair per workgroup: with its 60 KiB LDS ring at most two workgroups share a CU, and up to
+        // 32,768 pieces every rounds wave still gets a SIMD of its own; 1 pair beats 2 pairs (one 4-wave
+        // barrier couples more jitter) at every piece count up to there, by 1.7-3 % (profiles/r02/sweep_3buf.log)
+        const int pairs = (split_pairs == 1 || split_pairs == 2) ? split_pairs : 1;
         const unsigned grid = (p.n_main + 64 * pairs - 1) / (64 * pairs) + (p.n_main < p.n ? 1 : 0);
         if (pairs == 1) {
             if (hash) hipLaunchKernelGGL((tv_split_kernel<true, 1>), dim3(grid), dim3(128), 0, s, p);
