@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Write tools/ubench_rounds.hip: the split kernel's rounds block (gen_sha1_asm.gen_lds) in a loop
+"""Write tools/ubench_rounds.hip (generated on demand, not committed): the split kernel's rounds block (gen_sha1_asm.gen_lds) in a loop
 on one wave per CU, with variants of how K+W arrives from LDS.
 
 Question: the rounds wave runs 1,952 cyc per block, but 80 rounds of the same VALU mix in a loop
