@@ -295,18 +295,27 @@ def e2e_cfg5(dist, ws: int, rank: int, device: int, steps: int, threads: int, sh
     try:
         ctx.set_option(_native.TV_OPT_RESIDENT, 0)
         ctx.set_option(_native.TV_OPT_STREAM_CHUNK, E2E_CHUNK)
-        ctx.set_option(_native.TV_OPT_FILE_THREADS, threads)
+        # generator threads: half the allowed cores generate at ~100 GB/s (tools/pcie_probe.py), and more
+        # do not raise the streamed rate (tools/e2e_gen_probe.py: 8, 12, 16 threads all 40.5 GB/s)
+        gen_threads = max(1, threads // 2)
+        ctx.set_option(_native.TV_OPT_FILE_THREADS, gen_threads)
         ctx.set_layout(total, L, P, first, count)
         ctx.set_digests(bytes(pieces))
+
+        phase = {"next_s": 0.0, "fill_commit_s": 0.0}
 
         def run(fill) -> tuple:
             ctx.stream_begin()
             reqs = 0
             while True:
+                t0 = time.perf_counter()
                 req = ctx.stream_next()
+                t1 = time.perf_counter()
+                phase["next_s"] += t1 - t0
                 if not req.rows:
                     break
                 fill(req)
+                phase["fill_commit_s"] += time.perf_counter() - t1
                 reqs += 1
             return ctx.stream_end(), reqs
 
@@ -329,11 +338,13 @@ def e2e_cfg5(dist, ws: int, rank: int, device: int, steps: int, threads: int, sh
             _barrier(dist)
             return bf, reqs, _max(dist, t1 - t0)
 
+        phase.update(next_s=0.0, fill_commit_s=0.0)
         bf, reqs, el = timed(gen)
+        gen_phase = {k: round(v, 3) for k, v in phase.items()}
         ok = _sum(dist, 1.0 if bf == expect else 0.0) == ws
         out["generated"] = {"value": round(total * steps / el / 1e9, 2), "ms_per_step": round(el * 1e3 / steps, 1),
-                            "bitfield_exact": ok, "requests_per_step": reqs,
-                            "producer": f"host generator (tv_stream_fill_synthetic, {threads} threads) writing "
+                            "bitfield_exact": ok, "requests_per_step": reqs, "rank0_phase_s": gen_phase,
+                            "producer": f"host generator (tv_stream_fill_synthetic, {gen_threads} threads) writing "
                                         "the bytes into the ring slots inside the timed region"}
         # pinned_pool: the torrent is a 1 GiB page-locked pool of 256 pieces repeated; rows DMA'd from it
         pool = _native.PinnedBuffer(POOL_PIECES * L)
@@ -349,10 +360,12 @@ def e2e_cfg5(dist, ws: int, rank: int, device: int, steps: int, threads: int, sh
         def from_pool(req):
             ctx.stream_commit_from(req, pool.mv, L, ((req.piece - first) % POOL_PIECES) * L + req.offset)
 
+        phase.update(next_s=0.0, fill_commit_s=0.0)
         bf, reqs, el = timed(from_pool)
+        pool_phase = {k: round(v, 3) for k, v in phase.items()}
         ok = _sum(dist, 1.0 if bf == _expected_bits(count, bad2) else 0.0) == ws
         out["pinned_pool"] = {"value": round(total * steps / el / 1e9, 2), "ms_per_step": round(el * 1e3 / steps, 1),
-                              "bitfield_exact": ok, "requests_per_step": reqs,
+                              "bitfield_exact": ok, "requests_per_step": reqs, "rank0_phase_s": pool_phase,
                               "producer": f"rows DMA'd straight from a {POOL_PIECES * L >> 20} MiB page-locked pool "
                                           f"(piece first+j = pool piece j % {POOL_PIECES})"}
         out["value"] = out["generated"]["value"]
