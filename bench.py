@@ -439,7 +439,8 @@ def main() -> int:
     dist, rank, ws, local = _dist()
     device = local % max(1, _native.device_count())
     share = cpu_share()
-    threads = share["cores"]
+    # the node's allowed cores are shared by the ranks on it (ground truth, generators)
+    threads = max(1, share["cores"] // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1"))))
     workload = a.workload or ("cfg2" if ws == 1 else "cfg4")
     strong = a.strong or (not a.weak and a.workload is None and ws > 1)
 
