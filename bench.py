@@ -72,6 +72,23 @@ VALU_DERIVATION = (
 # SHA-1 round mix (tools/ubench_fetch.hip, profiles/r01/ubench_fetch.log); the wave64 cadence is 4.
 LONE_WAVE_CYC = 4.07
 SERIAL_INSTR = {1: 613, 2: 405}  # per-block serial stream: lane kernel / split rounds wave
+KERNEL_NAMES = {1: "lane", 2: "split", 3: "mix"}
+MIX_PAIRS, MIX_LANE_WAVES = 256, 512   # MIX workers on a 256-CU MI355X (tv_api.hip launch_resident)
+
+
+def piece_ceiling(kernel: int, count: int) -> float:
+    """GB/s if every piece (64-piece group for MIX) advanced at its serial SHA-1 stream's lone-wave rate:
+    lane / split = count pieces at that kernel's rate; MIX = its fastest ceil(count/64) workers busy
+    (split pairs first, then lane waves), 64 pieces each.  Capped at R_valu."""
+    rate = {k: 64 * CLOCK_HZ / (v * LONE_WAVE_CYC) for k, v in SERIAL_INSTR.items()}   # B/s per piece
+    if kernel == 3:
+        groups = (count + 63) // 64
+        pg = min(groups, MIX_PAIRS)
+        lg = min(groups - pg, MIX_LANE_WAVES)
+        bps = 64 * (pg * rate[2] + lg * rate[1])
+    else:
+        bps = count * rate.get(kernel, rate[1])
+    return min(VALU_PEAK_GBPS, bps / 1e9)
 
 MiB = 1 << 20
 WORKLOADS = {
@@ -254,12 +271,12 @@ def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: b
     bytes_rank = L * count
     bytes_all = _sum(dist, float(bytes_rank))
     achieved = bytes_rank / (avg / 1e3) / 1e9
-    ceiling = min(VALU_PEAK_GBPS, count * 64 * CLOCK_HZ / (SERIAL_INSTR.get(kernel, 613) * LONE_WAVE_CYC) / 1e9)
+    ceiling = piece_ceiling(kernel, count)
     out = {"workload": desc if not strong else desc.split(" (")[0] + f" ({P} pieces in all, {ws} shard(s), strong scaling)",
            "piece_length": L, "total_pieces": P, "pieces_per_gpu": count, "bytes_per_gpu": bytes_rank,
            "value": round(bytes_all * steps / elapsed / 1e9, 2), "unit": "GB/s", "steps": steps, "warmup": warmup,
            "ms_per_step": round(elapsed * 1e3 / steps, 3), "scaling": "strong" if strong else "weak",
-           "kernel": {1: "lane", 2: "split"}.get(kernel, str(kernel)), "kernel_ms_avg": round(avg, 3),
+           "kernel": KERNEL_NAMES.get(kernel, str(kernel)), "kernel_ms_avg": round(avg, 3),
            "kernel_ms_max_over_ranks": round(_max(dist, avg), 3), "achieved": round(achieved, 1),
            "piece_parallelism_ceiling": round(ceiling, 1), "frac_of_piece_ceiling": round(achieved / ceiling, 4),
            "frac_of_valu_peak": round(achieved / VALU_PEAK_GBPS, 4),
@@ -370,7 +387,7 @@ def e2e_cfg5(dist, ws: int, rank: int, device: int, steps: int, threads: int, sh
                                           f"(piece first+j = pool piece j % {POOL_PIECES})"}
         out["value"] = out["generated"]["value"]
         out["bitfield_exact"] = out["generated"]["bitfield_exact"] and ok
-        out["kernel"] = {1: "lane", 2: "split"}.get(ctx.last_kernel()[0], "?")
+        out["kernel"] = KERNEL_NAMES.get(ctx.last_kernel()[0], "?")
     finally:
         if pool is not None:
             pool.close()
@@ -427,7 +444,7 @@ def main() -> int:
     sc = ap.add_mutually_exclusive_group()
     sc.add_argument("--strong", action="store_true", help="the workload's pieces are the WHOLE torrent, sharded")
     sc.add_argument("--weak", action="store_true", help="the workload's pieces are per GPU")
-    ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 lane, 2 split")
+    ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 lane, 2 split, 3 mix")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-saturating", action="store_true", help="skip the piece_saturated leg (N=1)")

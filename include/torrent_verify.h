@@ -229,7 +229,7 @@ int tv_host_register(void *ptr, uint64_t bytes);
 int tv_host_unregister(void *ptr);
 
 /* Options (tv_set_option keys). */
-#define TV_OPT_KERNEL 1      /* 0 = auto, 1 = lane kernel, 2 = split (schedule-offload) kernel */
+#define TV_OPT_KERNEL 1      /* 0 = auto, 1 = lane, 2 = split (schedule offload), 3 = mix (work queue over split pairs + lane waves; resident calls only) */
 #define TV_OPT_STRIDE_PAD 2  /* bytes of padding between resident pieces (default 256) */
 #define TV_OPT_STREAM_CHUNK 3 /* tv_verify_host: bytes of each piece per streamed column chunk */
 #define TV_OPT_SPLIT_PAIRS 4  /* split kernel: (rounds, helper) wave pairs per workgroup, 0 = auto, 1, 2 */
@@ -251,7 +251,7 @@ int tv_get_option(tv_ctx *ctx, int key, int64_t *value);
  * library's compute stream: kernel_ms = the verify kernel(s) only; total_ms = whole call. */
 int tv_last_timing(tv_ctx *ctx, double *kernel_ms, double *total_ms);
 
-/* Kernel chosen for the last call (1 lane, 2 split) and launches it used. */
+/* Kernel chosen for the last call (1 lane, 2 split, 3 mix) and launches it used. */
 int tv_last_kernel(tv_ctx *ctx, int *kernel, int *launches);
 
 /* Block until all work queued by the ctx is complete. */

@@ -10,7 +10,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = [1, 2]  # lane, split
+KERNELS = [1, 2, 3]  # lane, split, mix (work queue; streamed calls run it as lane)
 
 
 def _ctx(native, kernel=0):
@@ -82,7 +82,7 @@ def test_kernels_agree_and_avail_mask(native, oracle):
             ctx.set_digests(pieces)
             ctx.stage(0, payload)
             outs.append(ctx.verify(bytes(avail)))
-    assert outs[0] == outs[1] == expect
+    assert all(o == expect for o in outs)
 
 
 def test_ragged_digest_string_and_extra_pieces(native, oracle):

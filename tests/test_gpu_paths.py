@@ -141,7 +141,7 @@ def test_full_size_cfg2_oracle_ground_truth(native, oracle):
     """BASELINE config 2 at full size (16 GiB, 16,384 x 1 MiB, HBM-resident) against the ORACLE on every
     piece: the CPU oracle hashes the whole synthetic torrent on the host's cores (the reference's SHA-1
     path, make_torrent.ts:28-31); the GPU's creation-mode digests equal it byte for byte, and verify with
-    the oracle's digests (1 % corrupted) gives exactly the oracle's bitfield with both kernels."""
+    the oracle's digests (1 % corrupted) gives exactly the oracle's bitfield with every kernel."""
     L, P = 1 << 20, 16384
     total = L * P
     truth = oracle.synth_piece_digests(2, total, L, P, threads=_threads())
@@ -154,7 +154,7 @@ def test_full_size_cfg2_oracle_ground_truth(native, oracle):
         ctx.fill_synthetic(2)
         assert ctx.hash() == truth
         ctx.set_digests(bytes(d2))
-        for k in (1, 2):
+        for k in (1, 2, 3):
             ctx.set_option(native.TV_OPT_KERNEL, k)
             bf = ctx.verify()
             assert ctx.last_kernel()[0] == k
@@ -172,7 +172,7 @@ def _threads():
 def test_full_size_cfg4_oracle_ground_truth(native, oracle):
     """BASELINE config 4 at its largest single-GPU size: 200 GiB, 51,200 x 4 MiB pieces resident in HBM
     (linear offsets to 214,748,364,800), against the ORACLE's digests of all 51,200 pieces: creation mode
-    equals them; verify with them (1 % corrupted) is exact with the lane and split kernels; and the 8-GPU
+    equals them; verify with them (1 % corrupted) is exact with the lane, split and MIX kernels; and the 8-GPU
     shard geometry of the same torrent (the last shard, pieces [44800, 51200), at linear offsets > 187 GB)
     hashes and verifies to the oracle's slice."""
     from torrent_amd import release_contexts, shard_ranges
@@ -188,8 +188,9 @@ def test_full_size_cfg4_oracle_ground_truth(native, oracle):
         ctx.set_layout(total, L, P)
         ctx.fill_synthetic(4)
         assert ctx.hash() == truth
+        assert ctx.last_kernel()[0] == 1      # auto at 51,200 pieces: lane
         ctx.set_digests(bytes(d2))
-        for k in (1, 2):
+        for k in (1, 2, 3):
             ctx.set_option(native.TV_OPT_KERNEL, k)
             bf = ctx.verify()
             assert ctx.last_kernel()[0] == k

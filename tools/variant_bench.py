@@ -3,6 +3,7 @@ piece count, every variant's verify kernel time (HIP events, best and median of 
 synthetic payload; each variant's digests must equal the first variant's and its bitfield be exact.
 
     python tools/variant_bench.py <pieces,...> <name> [<name> ...]      (libs in build/variants/)
+env: KERNEL (default 2 = split), REPS (5), GIB (payload GiB per point, 16)
 Each variant runs in its own process (one library per process); results as JSON lines."""
 import json
 import os
@@ -15,8 +16,8 @@ CHILD = r'''
 import json, os, sys, statistics
 sys.path.insert(0, os.environ["TV_ROOT"])
 from torrent_amd import _native as N
-P = int(sys.argv[1]); reps = int(sys.argv[2]); kernel = int(sys.argv[3])
-L = ((16 << 30) // P) // 64 * 64
+P = int(sys.argv[1]); reps = int(sys.argv[2]); kernel = int(sys.argv[3]); gib = int(sys.argv[4])
+L = ((gib << 30) // P) // 64 * 64
 ctx = N.Context(0)
 ctx.set_option(N.TV_OPT_KERNEL, kernel)
 ctx.set_layout(L * P, L, P)
@@ -43,13 +44,14 @@ def main():
     names = sys.argv[2:]
     reps = int(os.environ.get("REPS", "5"))
     kernel = int(os.environ.get("KERNEL", "2"))
+    gib = int(os.environ.get("GIB", "16"))       # payload per point (GIB=200 at 51,200 pieces = cfg4)
     for P in ps:
         ref = None
         for rnd in range(2):                     # two interleaved passes over the variants
             for name in names:
                 env = dict(os.environ, TV_ROOT=ROOT,
                            TORRENT_VERIFY_LIB=os.path.join(ROOT, "build", "variants", f"libtv_{name}.so"))
-                r = subprocess.run([sys.executable, "-c", CHILD, str(P), str(reps), str(kernel)], env=env,
+                r = subprocess.run([sys.executable, "-c", CHILD, str(P), str(reps), str(kernel), str(gib)], env=env,
                                    capture_output=True, text=True, timeout=300)
                 if r.returncode:
                     print(json.dumps({"variant": name, "P": P, "error": r.stderr[-800:]}), flush=True)

@@ -34,6 +34,10 @@ thread_local std::string g_thread_error;
 constexpr uint64_t kSlack = 256;                          // bytes past the last resident piece (tail over-read)
 constexpr int kRingSlots = TV_STREAM_RING_SLOTS;          // pinned staging buffers per lane
 constexpr size_t kRingSlotBytes = TV_STREAM_SLOT_BYTES;
+constexpr uint32_t kMixSegBlocks = 1024;    // MIX unit: 64 KiB of each of a group's 64 pieces
+
+// SHA-1 blocks of an n-byte message (data + 0x80 + 8-byte length, padded to 64)
+constexpr uint64_t nblocks_of(uint64_t n) { return (n + 8) / 64 + 1; }
 
 // Persistent host workers (one pool per staging lane): run(threads, tasks, fn) calls fn(0..tasks-1) on up
 // to `threads` threads, the caller included, and returns when every task is done.  Spawning threads for
@@ -123,6 +127,11 @@ struct tv_ctx {
     hipStream_t stream = nullptr;       // kernels
     hipStream_t copy_stream = nullptr;  // H2D staging
     hipStream_t copy_stream2 = nullptr; // H2D staging of the second lane (tv_stage_files' long segments)
+    // MIX launch (opt-in): pair workers on mix_pairs (CU mask: the low half of the CUs), lane workers on
+    // mix_lanes (the high half), created at the first MIX call; fork / join events
+    hipStream_t mix_pairs = nullptr, mix_lanes = nullptr;
+    hipEvent_t ev_mix0 = nullptr, ev_mix1 = nullptr, ev_mix2 = nullptr;
+    int cus = 256;                      // compute units of the device
     hipEvent_t ev_call0 = nullptr, ev_k0 = nullptr, ev_k1 = nullptr, ev_call1 = nullptr;
 
     // geometry
@@ -183,6 +192,9 @@ struct tv_ctx {
     Pool pool[2];                     // host workers of lane 0 / lane 1
     std::mutex err_mu;                // fail() may run on a tv_stage_files helper thread
     uint8_t* h_bits = nullptr;        // pinned bitfield bounce buffer
+    uint32_t* d_queue = nullptr;      // MIX work queue: head, tail, error, pad, then 64-bit slots
+    uint64_t queue_cap = 0;           // bytes of d_queue
+    uint32_t* h_qerr = nullptr;       // pinned copy of the queue's error word
     size_t h_bits_cap = 0;
 
     // streamed verify (tv_stream_*)
@@ -380,13 +392,91 @@ int launch_avail(tv_ctx* c, const uint8_t* avail_bits, const uint64_t** out) {
     return TV_OK;
 }
 
-int choose_kernel(const tv_ctx* c) {
+// Kernel of a launch over the whole shard.  resident: a one-launch call on the resident payload (MIX
+// needs it: its queue runs every segment of every piece in one launch); streamed columns fall back to
+// lane where MIX would be chosen.
+int choose_kernel(const tv_ctx* c, bool resident = true) {
+    // MIX (TV_OPT_KERNEL 3) is opt-in only: measured slower than lane wherever lane is chosen (DESIGN.md
+    // section 6, profiles/r02/mix_probe.log); its queue entries hold 16-bit group numbers
+    const bool mix_ok = resident && (c->count + 63) / 64 + 1 <= 0xFFFF;
+    if (c->kernel_opt == TV_KERNEL_MIX) return mix_ok ? TV_KERNEL_MIX : TV_KERNEL_LANE;
     if (c->kernel_opt == TV_KERNEL_LANE || c->kernel_opt == TV_KERNEL_SPLIT) return c->kernel_opt;
-    // Split (schedule offload) while every split workgroup (128 pieces, 4 waves on 4 SIMDs) has a
-    // CU to itself: <= 256 x 128 pieces.  Beyond that workgroups share CUs, a rounds wave shares
-    // its SIMD with another wave, and the lane kernel (about one wave per SIMD, VALU-bound) wins:
-    // measured 40,960 pieces split 1.62 vs lane 2.33 TB/s; 32,768 split 2.50 vs lane 1.87.
+    // Split (schedule offload) while every split pair (64 pieces, 2 waves) has SIMDs to itself:
+    // <= 32,768 pieces.  Beyond that rounds waves share SIMDs and the lane kernel wins
+    // (measured 40,960 pieces split 1.62 vs lane 2.33 TB/s; 32,768 split 2.50 vs lane 1.87).
     return c->count <= 32768 ? TV_KERNEL_SPLIT : TV_KERNEL_LANE;
+}
+
+// MIX workers, the shape measured best (profiles/r02/mix_probe.log): split pairs on the low half of the CUs,
+// two pair workgroups per CU (3 K+W buffers of LDS each); 4-wave lane workgroups, one per CU, on the high
+// half.  Without the CU masks the dispatcher puts lane waves on SIMDs that already hold a wave (up to 6x
+// slower units).  Streams created at the first MIX call.
+int mix_streams(tv_ctx* c) {
+    if (c->mix_pairs) return TV_OK;
+    std::vector<uint32_t> lo((c->cus + 31) / 32, 0), hi((c->cus + 31) / 32, 0);
+    for (int i = 0; i < c->cus; i++) (i < c->cus / 2 ? lo : hi)[i / 32] |= 1u << (i % 32);
+    TV_HIP(c, hipExtStreamCreateWithCUMask(&c->mix_pairs, (uint32_t)lo.size(), lo.data()));
+    TV_HIP(c, hipExtStreamCreateWithCUMask(&c->mix_lanes, (uint32_t)hi.size(), hi.data()));
+    return TV_OK;
+}
+
+TvMixShape mix_shape(const tv_ctx* c) {
+    TvMixShape m{};
+    m.pair_wgs = (unsigned)c->cus;          // 2 per CU on cus / 2 CUs
+    m.pair_lds_bufs = 3;
+    m.lane_wgs = (unsigned)(c->cus / 2);    // 1 per CU on cus / 2 CUs, 4 waves each
+    m.lane_waves_per_wg = 4;
+    m.lane_lds = 0;
+    return m;
+}
+
+// One launch over the resident shard with the chosen kernel.  MIX: the pair and lane workers run on the two
+// CU-masked streams, forked after everything queued on c->stream and joined back into it; the queue's error
+// word is copied to h_qerr for check_queue after the call's final sync.
+int launch_resident(tv_ctx* c, const TvPieces& p, int kernel, bool hash) {
+    if (kernel != TV_KERNEL_MIX) {
+        TV_HIP(c, tv_launch_verify(p, kernel, hash, c->stream, c->split_pairs));
+        return TV_OK;
+    }
+    TvQueue q{};
+    q.groups = (p.n_main + 63) / 64 + (p.n_main < p.n ? 1 : 0);
+    const uint64_t nb = nblocks_of(p.L);
+    q.seg_blocks = (uint32_t)std::max<uint64_t>(kMixSegBlocks, (nb + 0xFFFE) / 0xFFFF);   // segs < 65,536
+    q.segs = (uint32_t)((nb + q.seg_blocks - 1) / q.seg_blocks);
+    q.units = q.groups * q.segs;
+    q.ring = q.groups;
+    const uint64_t bytes = 16 + 8ull * q.ring;   // head, tail, error, pad, slots[ring]
+    if (c->queue_cap < bytes) {
+        (void)hipFree(c->d_queue); c->d_queue = nullptr; c->queue_cap = 0;
+        TV_HIP(c, hipMalloc((void**)&c->d_queue, bytes));
+        c->queue_cap = bytes;
+    }
+    if (!c->h_qerr) TV_HIP(c, hipHostMalloc((void**)&c->h_qerr, 64, hipHostMallocDefault));
+    q.head = c->d_queue;
+    q.tail = c->d_queue + 1;
+    q.error = c->d_queue + 2;
+    q.slots = reinterpret_cast<uint64_t*>(c->d_queue + 4);
+    q.trace = nullptr;
+    TV_HIP(c, hipMemsetAsync(c->d_queue, 0, bytes, c->stream));
+    int rc = mix_streams(c);
+    if (rc) return rc;
+    TV_HIP(c, hipEventRecord(c->ev_mix0, c->stream));
+    TV_HIP(c, hipStreamWaitEvent(c->mix_pairs, c->ev_mix0, 0));
+    TV_HIP(c, hipStreamWaitEvent(c->mix_lanes, c->ev_mix0, 0));
+    TV_HIP(c, tv_launch_mix(p, q, hash, c->mix_pairs, c->mix_lanes, mix_shape(c)));
+    TV_HIP(c, hipEventRecord(c->ev_mix1, c->mix_pairs));
+    TV_HIP(c, hipEventRecord(c->ev_mix2, c->mix_lanes));
+    TV_HIP(c, hipStreamWaitEvent(c->stream, c->ev_mix1, 0));
+    TV_HIP(c, hipStreamWaitEvent(c->stream, c->ev_mix2, 0));
+    TV_HIP(c, hipMemcpyAsync(c->h_qerr, q.error, 4, hipMemcpyDeviceToHost, c->stream));
+    return TV_OK;
+}
+
+// After the call's final sync: a MIX launch whose watchdog fired has no valid output.
+int check_queue(tv_ctx* c, int kernel) {
+    if (kernel == TV_KERNEL_MIX && *c->h_qerr)
+        return fail(c, TV_ERR_HIP, "work queue watchdog expired (a MIX worker waited > 4 s for a ready group)");
+    return TV_OK;
 }
 
 TvPieces resident_launch(const tv_ctx* c) {
@@ -742,7 +832,7 @@ int stream_begin_locked(tv_ctx* c, const uint8_t* avail_bits) {
     }
     st.ncol = (c->L + st.C - 1) / st.C;
     st.rows_per_req = std::max<uint64_t>(1, kRingSlotBytes / st.C);
-    st.kernel = choose_kernel(c);
+    st.kernel = choose_kernel(c, false);
     st.p = resident_launch(c);
     st.p.stride = st.row_pitch;
     TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
@@ -899,6 +989,10 @@ int tv_create(tv_ctx** out, int device) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy_stream2, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_mix0, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_mix1, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_mix2, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device);
     if (e == hipSuccess) e = hipEventCreate(&c->ev_call0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev_k0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev_k1);
@@ -923,7 +1017,11 @@ void tv_destroy(tv_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     if (c->copy_stream2) (void)hipStreamSynchronize(c->copy_stream2);
+    if (c->mix_pairs) (void)hipStreamSynchronize(c->mix_pairs);
+    if (c->mix_lanes) (void)hipStreamSynchronize(c->mix_lanes);
     free_device(c);
+    if (c->d_queue) (void)hipFree(c->d_queue);
+    if (c->h_qerr) (void)hipHostFree(c->h_qerr);
     for (int s = 0; s < kRingSlots; s++) {
         if (c->ring[s]) (void)hipHostFree(c->ring[s]);
         if (c->ring_ev[s]) (void)hipEventDestroy(c->ring_ev[s]);
@@ -932,11 +1030,14 @@ void tv_destroy(tv_ctx* c) {
     }
     if (c->h_bits) (void)hipHostFree(c->h_bits);
     for (hipEvent_t ev : {c->ev_call0, c->ev_k0, c->ev_k1, c->ev_call1, c->ev_avail, c->col_ev[0], c->col_ev[1],
-                          c->done_ev[0], c->done_ev[1]})
+                          c->done_ev[0], c->done_ev[1], c->ev_mix0, c->ev_mix1,
+                          c->ev_mix2})
         if (ev) (void)hipEventDestroy(ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->copy_stream2) (void)hipStreamDestroy(c->copy_stream2);
+    if (c->mix_pairs) (void)hipStreamDestroy(c->mix_pairs);
+    if (c->mix_lanes) (void)hipStreamDestroy(c->mix_lanes);
     delete c;
 }
 
@@ -961,7 +1062,7 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
     std::lock_guard<std::mutex> g(c->mu);
     switch (key) {
         case TV_OPT_KERNEL:
-            if (value < 0 || value > 2) return fail(c, TV_ERR_ARG, "TV_OPT_KERNEL must be 0, 1 or 2");
+            if (value < 0 || value > 3) return fail(c, TV_ERR_ARG, "TV_OPT_KERNEL must be 0, 1, 2 or 3");
             c->kernel_opt = (int)value;
             return TV_OK;
         case TV_OPT_STRIDE_PAD:
@@ -1483,9 +1584,12 @@ int tv_verify(tv_ctx* c, const uint8_t* avail_bits, uint8_t* bitfield_out) {
     // fail closed: a piece the launch does not write reads as 0, never as a stale 1
     TV_HIP(c, hipMemsetAsync(c->d_out, 0, c->bit_words * 8, c->stream));
     TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
-    TV_HIP(c, tv_launch_verify(p, kernel, false, c->stream, c->split_pairs));
+    rc = launch_resident(c, p, kernel, false);
+    if (rc) return rc;
     TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
     rc = read_bits(c, bitfield_out);
+    if (rc) return rc;
+    rc = check_queue(c, kernel);
     if (rc) return rc;
     c->last_kernel = kernel;
     c->last_launches = 1;
@@ -1580,13 +1684,16 @@ int tv_hash(tv_ctx* c, uint8_t* digests_out) {
     TvPieces p = resident_launch(c);
     p.avail64 = nullptr;
     TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
-    TV_HIP(c, tv_launch_verify(p, kernel, true, c->stream, c->split_pairs));
+    rc = launch_resident(c, p, kernel, true);
+    if (rc) return rc;
     TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
     std::vector<uint32_t> soa(5 * c->count);
     DrainGuard drain(c);  // declared after soa: drains before soa is freed, also on error paths
     TV_HIP(c, hipMemcpyAsync(soa.data(), c->d_hash, soa.size() * 4, hipMemcpyDeviceToHost, c->stream));
     TV_HIP(c, hipEventRecord(c->ev_call1, c->stream));
     TV_HIP(c, hipEventSynchronize(c->ev_call1));
+    rc = check_queue(c, kernel);
+    if (rc) return rc;
     for (uint64_t j = 0; j < c->count; j++)
         for (int k = 0; k < 5; k++) {
             const uint32_t v = soa[(uint64_t)k * c->count + j];

@@ -6,6 +6,7 @@
 #define TV_KERNEL_AUTO 0
 #define TV_KERNEL_LANE 1
 #define TV_KERNEL_SPLIT 2
+#define TV_KERNEL_MIX 3     // work queue: split pairs + lane waves share 64-piece groups segment by segment
 
 // One launch over a contiguous run of n pieces.  Piece j's byte k (piece-relative) is at
 // data + j*stride + k - data_off.  Blocks [blk_begin, min(blk_end, nb_j)) are processed.
@@ -32,7 +33,32 @@ struct TvPieces {
     uint8_t* out_bytes;      // list mode: out_bytes[j] = 1 iff piece idx[j] matches
 };
 
+// Work queue of the MIX launch (tv_launch_mix): a FIFO of ready 64-piece groups.  A unit is segment s
+// (blocks [s * seg_blocks, (s + 1) * seg_blocks); the last one runs to the end and finalises) of group g;
+// entries are (lap tag << 32 | s << 16 | g), so groups and segs are < 65,536.
+struct TvQueue {
+    uint32_t* head;      // pop tickets   (head, tail, error: zeroed before the launch)
+    uint32_t* tail;      // push tickets
+    uint32_t* error;     // nonzero: a worker's wait exceeded the watchdog; the launch's output is invalid
+    uint64_t* slots;     // [ring] entries (zeroed before the launch)
+    uint32_t ring;       // >= groups
+    uint32_t groups, segs, seg_blocks, units;  // units = groups * segs
+    uint64_t* trace;     // diagnostics (tools/mix_probe.cpp), null in the library: per unit (s * groups + g)
+                         // {pop, start, end} s_memrealtime ticks and the worker id
+};
+
+// Worker shape of a MIX launch: pair_wgs split-pair workgroups declaring pair_lds_bufs (3 or 5) K+W
+// buffers of LDS, lane_wgs lane workgroups of lane_waves_per_wg (1..4) waves each, lane_lds bytes of
+// (unused) dynamic LDS per lane workgroup.
+struct TvMixShape {
+    unsigned pair_wgs, pair_lds_bufs, lane_wgs, lane_waves_per_wg, lane_lds;
+};
+
 hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_t s, int split_pairs = 0);
+// The MIX launch: the pair workers on s_pairs and the lane workers on s_lanes, concurrently, over the
+// queue q (the short last piece, if any, is a group of its own like in tv_launch_verify).
+hipError_t tv_launch_mix(const TvPieces& p, const TvQueue& q, bool hash, hipStream_t s_pairs, hipStream_t s_lanes,
+                         const TvMixShape& m);
 hipError_t tv_launch_verify_list(const TvPieces& p, int kernel, hipStream_t s);
 hipError_t tv_launch_fill(uint8_t* payload, uint64_t stride, uint64_t first, uint32_t n, uint64_t L,
                           uint64_t seed, hipStream_t s);

@@ -154,7 +154,8 @@ __device__ __forceinline__ void finish(const TvPieces& p, bool writer, uint32_t 
     if (!p.finalize) {
         if (writer) {
 #pragma unroll
-            for (int k = 0; k < 5; k++) p.state[(uint64_t)k * p.dcount + jj] = h[k];
+            for (int k = 0; k < 5; k++)   // device-coherent (write-through) store: a MIX successor may read it
+                __hip_atomic_store(p.state + (uint64_t)k * p.dcount + jj, h[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         return;
     }
@@ -184,7 +185,8 @@ __device__ __forceinline__ void start_state(const TvPieces& p, uint32_t jj, uint
         sha1_iv(h);
     } else {
 #pragma unroll
-        for (int k = 0; k < 5; k++) h[k] = p.state[(uint64_t)k * p.dcount + jj];
+        for (int k = 0; k < 5; k++)       // device-coherent load (a MIX predecessor on another XCD wrote it)
+            h[k] = __hip_atomic_load(p.state + (uint64_t)k * p.dcount + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -193,12 +195,18 @@ __device__ __forceinline__ void start_state(const TvPieces& p, uint32_t jj, uint
 // ------------------------------------------------------------------------------------------
 // lane kernel: one lane per piece, full compression per lane.
 // ------------------------------------------------------------------------------------------
+#ifndef TV_LANE_DEPTH
+#define TV_LANE_DEPTH 3   // raw blocks in flight per lane: 3 is 0.8-1.2 % faster than 2, 4 and 6 no better
+                          // (profiles/r02/lane_depth.jsonl; A/B: tools/build_variants.py D_TV_LANE_DEPTH=n)
+#endif
+
+// Wave-group gw of a launch: pieces [64 gw, 64 gw + 64) (clamped to n_main), or, for gw == the first group
+// past n_main, the short last piece alone.  Blocks [blk_begin, blk_end) of p.
 template <bool HASH>
-__global__ __launch_bounds__(256) void tv_lane_kernel(TvPieces p) {
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+__device__ __forceinline__ void lane_group(const TvPieces& p, uint32_t gw) {
     const uint32_t lane = threadIdx.x & 63u;
     // main waves cover [0, n_main); a short last piece (n_main < n) gets the wave after them alone
-    const uint32_t gw = blockIdx.x * 4u + wave, nw_main = (p.n_main + 63u) / 64u;
+    const uint32_t nw_main = (p.n_main + 63u) / 64u;
     const bool last_grp = gw >= nw_main;
     if (last_grp && (gw > nw_main || p.n_main == p.n)) return;  // wave-uniform: no piece here
     const uint32_t j0 = last_grp ? p.last_idx : gw * 64u;
@@ -216,23 +224,24 @@ __global__ __launch_bounds__(256) void tv_lane_kernel(TvPieces p) {
     uint32_t b = g.fast_begin;
     uint32_t w[16];
     if (b < g.fast_end) {
-        // Two register blocks in flight.  Loads are unconditional (the block index is clamped to
-        // the last raw block), so they are never predicated and stay in flight across a block.
+        // TV_LANE_DEPTH register blocks in flight.  Loads are unconditional (the block index is clamped
+        // to the last raw block), so they are never predicated and stay in flight across a block.
+        constexpr int D = TV_LANE_DEPTH;
         const uint32_t last = g.fast_end - 1;
-        uint4 A[4], B[4];
-        load_block(piece, b, A);
-        load_block(piece, b + 1 < last ? b + 1 : last, B);
+        uint4 R[D][4];
+#pragma unroll
+        for (int d = 0; d < D; d++) load_block(piece, b + d < last ? b + d : last, R[d]);
         for (;;) {
-            bswap_block(A, w);
-            load_block(piece, b + 2 < last ? b + 2 : last, A);
-            compress_full(h, w);
-            if (++b >= g.fast_end) break;
-            bswap_block(B, w);
-            load_block(piece, b + 2 < last ? b + 2 : last, B);
-            compress_full(h, w);
-            if (++b >= g.fast_end) break;
+#pragma unroll
+            for (int d = 0; d < D; d++) {
+                bswap_block(R[d], w);
+                load_block(piece, b + D < last ? b + D : last, R[d]);
+                compress_full(h, w);
+                if (++b >= g.fast_end) goto raw_done;
+            }
         }
     }
+raw_done:
     for (; b < g.end; b++) {
         build_tail_block(piece, len, b, w);
         uint32_t r[5];
@@ -243,6 +252,11 @@ __global__ __launch_bounds__(256) void tv_lane_kernel(TvPieces p) {
         }
     }
     finish<HASH>(p, writer, jj, j0, h, last_grp);
+}
+
+template <bool HASH>
+__global__ __launch_bounds__(256) void tv_lane_kernel(TvPieces p) {
+    lane_group<HASH>(p, blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -274,13 +288,15 @@ __device__ __forceinline__ bool avail_bit(const uint64_t* a, uint32_t i) {
 // LIST = incremental verify (tv_verify_list): lane j verifies shard piece idx[j]; one pair per
 // workgroup, geometry from the pair's ballots (the short last piece may sit in any lane; the
 // helper and rounds waves see the same 64 pieces, so their ballots agree).
-template <bool HASH, int PAIRS, bool LIST = false>
-__global__ __launch_bounds__(128 * PAIRS) void tv_split_kernel(TvPieces p) {
+// Workgroup-group wgi of a launch (PAIRS x {rounds, helper} waves, 64*PAIRS pieces), K+W ring in `ring`.
+// The rounds wave calls before_state() (wave-uniform; false = give up) just before it reads its chaining
+// state: the work-queue kernel waits there for the group's previous segment.
+template <bool HASH, int PAIRS, bool LIST, typename BeforeState>
+__device__ __forceinline__ void split_group(const TvPieces& p, uint32_t wgi, uint4* ring, BeforeState before_state) {
     // PAIRS x {rounds, helper} waves; 64*PAIRS pieces.  A workgroup's waves go to distinct SIMDs, so
-    // with <= 1 workgroup per CU no rounds wave shares its SIMD.  Each pair has its own 2 x 20 KiB
+    // with <= 1 workgroup per CU no rounds wave shares its SIMD.  Each pair has its own 3 x 20 KiB
     // K+W ring; the barrier is workgroup-wide, so both pairs run the same (workgroup) block range.
     static_assert(!LIST || PAIRS == 1, "list mode runs one pair per workgroup");
-    __shared__ __attribute__((aligned(16))) uint4 ring[kBufs * PAIRS * kRingWords / 4];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t pair = wave % PAIRS;
@@ -290,8 +306,8 @@ __global__ __launch_bounds__(128 * PAIRS) void tv_split_kernel(TvPieces p) {
     // has no last group (the host puts the last piece's entries in waves of their own).
     const uint32_t span = 64u * PAIRS;
     const uint32_t nlim = LIST ? p.n : p.n_main;
-    const bool last_grp = !LIST && blockIdx.x >= (nlim + span - 1) / span;
-    const uint32_t wg0 = last_grp ? p.last_idx : blockIdx.x * span;
+    const bool last_grp = !LIST && wgi >= (nlim + span - 1) / span;
+    const uint32_t wg0 = last_grp ? p.last_idx : wgi * span;
     const uint32_t j0 = last_grp ? p.last_idx : wg0 + pair * 64u;
     const uint32_t j = last_grp ? p.last_idx : j0 + lane;
     const uint32_t jl = last_grp ? p.last_idx : (j < nlim ? j : nlim - 1);
@@ -333,8 +349,10 @@ __global__ __launch_bounds__(128 * PAIRS) void tv_split_kernel(TvPieces p) {
 
     // ---------------- rounds wave ----------------
     uint32_t h[5];
+    const bool go = before_state();   // (the helper waits at its first barrier meanwhile)
     if (LIST) sha1_iv(h);
-    else start_state(p, jj, h);
+    else if (go) start_state(p, jj, h);
+    else sha1_iv(h);                  // abandoned (watchdog): the bits stay 0
     const uint32_t ring_base = (uint32_t)(uintptr_t)(void*)pring + lane * 16u;
     const uint32_t nb_min = g.nb_min;
     lds_barrier();
@@ -364,7 +382,162 @@ __global__ __launch_bounds__(128 * PAIRS) void tv_split_kernel(TvPieces p) {
         }
         return;
     }
-    finish<HASH>(p, last_grp ? (lane == 0 && pair == 0) : j < p.n_main, jj, j0, h, last_grp);
+    finish<HASH>(p, go && (last_grp ? (lane == 0 && pair == 0) : j < p.n_main), jj, j0, h, last_grp);
+}
+
+template <bool HASH, int PAIRS, bool LIST = false>
+__global__ __launch_bounds__(128 * PAIRS) void tv_split_kernel(TvPieces p) {
+    __shared__ __attribute__((aligned(16))) uint4 ring[kBufs * PAIRS * kRingWords / 4];
+    split_group<HASH, PAIRS, LIST>(p, blockIdx.x, ring, [] { return true; });
+}
+
+// ------------------------------------------------------------------------------------------
+// MIX: persistent split pairs and persistent lane waves serve one FIFO of ready 64-piece groups at once.
+// With 32,768 < P < ~56,000 pieces the lane kernel leaves SIMDs idle (cfg4 on one GPU: 800 waves on 1,024
+// SIMDs) and a piece's SHA-1 is serial: a group advances at its worker's per-piece rate (pair ~1,870
+// cycles per block, lane ~2,650) and a pair costs two SIMDs.  A worker pops a group, runs its next
+// segment (seg_blocks blocks; the 20-byte chaining states go through d_state), and pushes it back at the
+// tail: every group gets the same mix of fast and slow workers and all of them end together.
+// Tickets: pop ticket t < groups is group t's first segment (nothing to wait for); pop ticket t >= groups
+// takes push ticket t - groups, whose slot carries its lap tag; pop tickets >= units mean "drained".
+// Push (release) / pop (acquire) at agent scope: the workers sit on different XCDs.  A pop that waits
+// polls with relaxed loads and s_sleep and has a watchdog, so no wave spins forever: the push it waits
+// for comes from a worker that holds a group and is running (holders never wait), and a worker that gives
+// up sets `error` and every other worker stops at its next pop.
+// ------------------------------------------------------------------------------------------
+namespace {
+
+constexpr uint64_t kWatchdogTicks = 400000000ull;  // s_memrealtime runs at 100 MHz: 4 s
+
+// Handoff ordering.  1: agent-scope release / acquire fences (they write back / invalidate the XCD's whole
+// L2).  0: the only data handed between workers is the chaining state, and it is stored and loaded with
+// device-coherent (sc1) accesses, so the push only waits for those stores to complete and the pop's
+// data loads, issued after the slot load returned, read memory and not a stale L2 line.
+#ifndef TV_QUEUE_FENCES
+#define TV_QUEUE_FENCES 1
+#endif
+constexpr uint32_t kStop = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t q_error(const TvQueue& q) {
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(q.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+__device__ __forceinline__ uint32_t wave_ticket(uint32_t* counter) {
+    uint32_t t = 0;
+    if ((threadIdx.x & 63u) == 0) t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_amdgcn_readfirstlane(t);
+}
+
+// Next unit as (s << 16 | g), or kStop (drained, or a worker gave up).  Wave-uniform.
+__device__ __forceinline__ uint32_t q_pop(const TvQueue& q) {
+    const uint32_t t = wave_ticket(q.head);
+    if (t >= q.units || q_error(q)) return kStop;
+    if (t < q.groups) return t;                 // segment 0 of group t
+    const uint32_t k = t - q.groups;            // the push this pop takes
+    const uint32_t tag = k / q.ring + 1;
+    const uint64_t* slot = q.slots + (k % q.ring);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        // relaxed polls, one acquire fence when the entry is there: the fence invalidates this XCD's L2,
+        // which a poll loop must not do every few hundred cycles under the other waves' payload streams
+        const uint64_t v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+        if (hi == tag) {
+#if TV_QUEUE_FENCES
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+            return __builtin_amdgcn_readfirstlane((uint32_t)v);
+        }
+        if (q_error(q)) return kStop;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kWatchdogTicks) {
+            if ((threadIdx.x & 63u) == 0) __hip_atomic_fetch_or(q.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return kStop;
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+
+// Group g has finished segment s: queue its next segment (the state stores are visible device-wide first).
+__device__ __forceinline__ void q_push(const TvQueue& q, uint32_t g, uint32_t s) {
+    if (s + 1 >= q.segs) return;                // finalised: the group leaves the queue
+#if TV_QUEUE_FENCES
+    __threadfence();
+#else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the state's write-through stores have completed
+#endif
+    const uint32_t k = wave_ticket(q.tail);
+    const uint64_t v = ((uint64_t)(k / q.ring + 1) << 32) | ((s + 1) << 16) | g;
+    if ((threadIdx.x & 63u) == 0)
+        __hip_atomic_store(q.slots + (k % q.ring), v, TV_QUEUE_FENCES ? __ATOMIC_RELEASE : __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void q_trace(const TvQueue& q, uint32_t s, uint32_t g, uint64_t t0, uint64_t t1,
+                                        uint32_t worker) {
+    if ((threadIdx.x & 63u) == 0) {
+        const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
+        uint64_t* r = q.trace + 4ull * ((uint64_t)s * q.groups + g);
+        r[0] = t0;
+        r[1] = t1;
+        r[2] = t2;
+        r[3] = worker;
+    }
+}
+
+__device__ __forceinline__ TvPieces q_unit(const TvPieces& p, const TvQueue& q, uint32_t s) {
+    TvPieces u = p;
+    const bool last = s + 1 == q.segs;
+    u.blk_begin = (uint64_t)s * q.seg_blocks;
+    u.blk_end = last ? UINT64_MAX : (uint64_t)(s + 1) * q.seg_blocks;
+    u.finalize = last ? 1 : 0;
+    return u;
+}
+
+}  // namespace
+
+// Persistent lane workers: every wave of the workgroup serves units on its own.  Dynamic LDS (unused)
+// only limits how many lane workgroups share a CU with a pair workgroup.
+template <bool HASH>
+__global__ __launch_bounds__(256) void tv_qlane_kernel(TvPieces p, TvQueue q) {
+    for (;;) {
+        const uint64_t t0 = q.trace ? __builtin_amdgcn_s_memrealtime() : 0;
+        const uint32_t e = q_pop(q);
+        if (e == kStop) return;
+        const uint32_t s = e >> 16, g = e & 0xFFFFu;
+        const uint64_t t1 = q.trace ? __builtin_amdgcn_s_memrealtime() : 0;
+        lane_group<HASH>(q_unit(p, q, s), g);
+        q_push(q, g, s);
+        if (q.trace) q_trace(q, s, g, t0, t1, 0x10000u + blockIdx.x * 4u + (threadIdx.x >> 6));
+    }
+}
+
+// Persistent split pairs: the rounds wave pops a unit (the acquire included) and hands it to the helper
+// through LDS.  DECL_BUFS >= kBufs ring buffers are declared: 5 (102 KiB) lets at most one pair workgroup
+// onto a CU, 3 (61 KiB) two.
+template <bool HASH, int DECL_BUFS>
+__global__ __launch_bounds__(128) void tv_qsplit_kernel(TvPieces p, TvQueue q) {
+    static_assert(DECL_BUFS >= (int)kBufs, "ring");
+    __shared__ __attribute__((aligned(16))) uint4 ring[DECL_BUFS * kRingWords / 4];
+    __shared__ uint32_t unit_slot;
+    const uint32_t rounds = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
+    for (;;) {
+        const uint64_t t0 = q.trace ? __builtin_amdgcn_s_memrealtime() : 0;
+        if (rounds) {
+            const uint32_t e = q_pop(q);
+            if ((threadIdx.x & 63u) == 0) unit_slot = e;
+        }
+        lds_barrier();
+        const uint32_t e = __builtin_amdgcn_readfirstlane(unit_slot);
+        if (e == kStop) return;   // both waves read the same slot: both stop
+        const uint32_t s = e >> 16, g = e & 0xFFFFu;
+        const uint64_t t1 = q.trace ? __builtin_amdgcn_s_memrealtime() : 0;
+        split_group<HASH, 1, false>(q_unit(p, q, s), g, ring, [] { return true; });
+        if (rounds) {
+            q_push(q, g, s);
+            if (q.trace) q_trace(q, s, g, t0, t1, blockIdx.x);
+        }
+        // the next pop's slot write follows this unit's last barrier, which the helper has passed
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -473,6 +646,29 @@ hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_
         const unsigned grid = (waves + 3) / 4;
         if (hash) hipLaunchKernelGGL(tv_lane_kernel<true>, dim3(grid), dim3(256), 0, s, p);
         else hipLaunchKernelGGL(tv_lane_kernel<false>, dim3(grid), dim3(256), 0, s, p);
+    }
+    return hipGetLastError();
+}
+
+hipError_t tv_launch_mix(const TvPieces& p, const TvQueue& q, bool hash, hipStream_t s_pairs, hipStream_t s_lanes,
+                         const TvMixShape& m) {
+    if (p.n == 0) return hipSuccess;
+    if (q.groups > 0xFFFFu || q.segs > 0xFFFFu || m.lane_waves_per_wg < 1 || m.lane_waves_per_wg > 4 ||
+        (m.pair_lds_bufs != 3 && m.pair_lds_bufs != 5))
+        return hipErrorInvalidValue;
+    const dim3 lb(64 * m.lane_waves_per_wg);
+    if (m.pair_wgs) {
+        if (hash) {
+            if (m.pair_lds_bufs == 5) hipLaunchKernelGGL((tv_qsplit_kernel<true, 5>), dim3(m.pair_wgs), dim3(128), 0, s_pairs, p, q);
+            else hipLaunchKernelGGL((tv_qsplit_kernel<true, 3>), dim3(m.pair_wgs), dim3(128), 0, s_pairs, p, q);
+        } else {
+            if (m.pair_lds_bufs == 5) hipLaunchKernelGGL((tv_qsplit_kernel<false, 5>), dim3(m.pair_wgs), dim3(128), 0, s_pairs, p, q);
+            else hipLaunchKernelGGL((tv_qsplit_kernel<false, 3>), dim3(m.pair_wgs), dim3(128), 0, s_pairs, p, q);
+        }
+    }
+    if (m.lane_wgs) {
+        if (hash) hipLaunchKernelGGL(tv_qlane_kernel<true>, dim3(m.lane_wgs), lb, m.lane_lds, s_lanes, p, q);
+        else hipLaunchKernelGGL(tv_qlane_kernel<false>, dim3(m.lane_wgs), lb, m.lane_lds, s_lanes, p, q);
     }
     return hipGetLastError();
 }
