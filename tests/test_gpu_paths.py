@@ -137,6 +137,33 @@ def test_multi_device_api_on_one_gpu(native, oracle):
     assert bytes(verify_payload(info, payload, devices=[0, 0, 0])) == exp
 
 
+@pytest.mark.parametrize("P,ndev", [(1, 2), (9, 4), (50, 8), (3, 8)])
+def test_small_torrents_on_many_devices(native, oracle, tmp_path, P, ndev):
+    """Fewer pieces than 8 x devices: shard_ranges gives trailing EMPTY shards starting at a piece that need
+    not be a multiple of 8 (P = 1 on 2 devices, 9 on 4, 50 on 8).  Every entry point (verify_payload resident
+    and streamed from host, verify_stream, verify_pieces over a Storage, verify_files from disk, hash_pieces)
+    returns the oracle's bits / digests, like the single-device call."""
+    from torrent_amd import (MemoryStorage, Storage, hash_pieces, make_info, shard_ranges, verify_files,
+                             verify_payload, verify_pieces, verify_stream)
+    assert any(c == 0 and f % 8 for f, c in shard_ranges(P, ndev)) or P == 3
+    L = 4096
+    total = L * (P - 1) + 1000
+    payload = oracle.synth_fill(P * 7 + ndev, 0, total)
+    pieces = bytearray(oracle.hash_pieces(payload, total, L, P))
+    pieces[20 * (P - 1)] ^= 1                      # the last piece fails
+    info = make_info(L, bytes(pieces), "small.bin", length=total)
+    expect = oracle.verify_linear(payload, total, L, bytes(pieces))
+    devs = [0] * ndev
+    assert bytes(verify_payload(info, payload, devices=devs)) == expect
+    assert bytes(verify_payload(info, payload, devices=devs, resident=False)) == expect
+    assert bytes(verify_stream(info, lambda o, n: bytes(payload[o:o + n]), devices=devs)) == expect
+    mem = MemoryStorage({("small.bin",): bytes(payload)})
+    assert bytes(verify_pieces(info, Storage(mem, info, os.getcwd()), devices=devs)) == expect
+    (tmp_path / "small.bin").write_bytes(bytes(payload))
+    assert bytes(verify_files(info, str(tmp_path), devices=devs)) == expect
+    assert hash_pieces(bytes(payload), L, devices=devs) == oracle.hash_pieces(payload, total, L, P)
+
+
 def test_full_size_cfg2_oracle_ground_truth(native, oracle):
     """BASELINE config 2 at full size (16 GiB, 16,384 x 1 MiB, HBM-resident) against the ORACLE on every
     piece: the CPU oracle hashes the whole synthetic torrent on the host's cores (the reference's SHA-1
