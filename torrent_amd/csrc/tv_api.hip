@@ -540,7 +540,7 @@ void copy_into_ring(Pool& pool, uint8_t* dst, const uint8_t* src, uint64_t n, in
     const uint64_t parts = (n + kPart - 1) / kPart;
     pool.run(threads, parts, [&](uint64_t q) {
         const uint64_t o = q * kPart;
-        memcpy(dst + o, src + o, std::min(kPart, n - o));
+        tv_copy_host(dst + o, src + o, std::min(kPart, n - o));
     });
 }
 
@@ -551,7 +551,7 @@ void gather_rows(Pool& pool, uint8_t* dst, const uint8_t* src, uint64_t width, u
     const uint64_t per = std::max<uint64_t>(1, (4ull << 20) / std::max<uint64_t>(1, width));  // rows per task
     const uint64_t tasks = (k + per - 1) / per;
     pool.run(threads, tasks, [&](uint64_t q) {
-        for (uint64_t r = q * per; r < std::min(k, (q + 1) * per); r++) memcpy(dst + r * width, src + r * pitch, width);
+        for (uint64_t r = q * per; r < std::min(k, (q + 1) * per); r++) tv_copy_host(dst + r * width, src + r * pitch, width);
     });
 }
 
