@@ -72,7 +72,7 @@ VALU_DERIVATION = (
 # SHA-1 round mix (tools/ubench_fetch.hip, profiles/r01/ubench_fetch.log); the wave64 cadence is 4.
 LONE_WAVE_CYC = 4.07
 SERIAL_INSTR = {1: 613, 2: 405}  # per-block serial stream: lane kernel / split rounds wave
-KERNEL_NAMES = {1: "lane", 2: "split", 3: "mix", 4: "duo"}
+KERNEL_NAMES = {1: "lane", 2: "split", 3: "mix"}
 MIX_PAIRS, MIX_LANE_WAVES = 256, 512   # MIX workers on a 256-CU MI355X (tv_api.hip launch_resident)
 
 

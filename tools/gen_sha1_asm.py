@@ -227,26 +227,25 @@ def gen_helper(src=None, off_base: int = 0):
     return ins
 
 
-def rounds_loop_text(bufs: int = LDS_BUFS) -> str:
+def rounds_loop_text() -> str:
     """The split kernel's rounds wave over nsteps (>= 1) blocks in which every lane updates, starting
-    at ring buffer 0: one stream over buffers 0, 1, .., bufs-1, 0, ... -- 80 rounds from K+W in LDS,
-    h += r, barrier per block.  One asm statement, so no compiler bookkeeping or asm-boundary s_nop
-    between blocks.  The reads issued ahead for the block after the last one are drained before it
-    returns.  bufs = 2 is the duo kernel's ring (helper one block ahead; four pairs fill 160 KiB)."""
-    pipelined = PIPELINED and bufs == LDS_BUFS
+    at ring buffer 0: one pipelined stream (gen_rounds_block) over buffers 0, 1, 2, 0, ... -- 80 rounds
+    from K+W in LDS, h += r, barrier per block.  One asm statement, so no compiler bookkeeping or
+    asm-boundary s_nop between blocks.  The reads issued ahead for the block after the last one are
+    drained before it returns."""
     L = ["s_waitcnt lgkmcnt(0)", "s_mov_b32 %[cnt], %[nsteps]"]
-    if pipelined:
+    if PIPELINED:
         L.extend(_emit_lines(rounds_prologue(0)))
     L.append("L_rloop_%=:")
-    for k in range(bufs):
-        if pipelined:
-            L.extend(_emit_lines(gen_rounds_block(k * RING_BYTES, ((k + 1) % bufs) * RING_BYTES)))
+    for k in range(LDS_BUFS):
+        if PIPELINED:
+            L.extend(_emit_lines(gen_rounds_block(k * RING_BYTES, ((k + 1) % LDS_BUFS) * RING_BYTES)))
         else:   # per-block stream: its 15 reads issued at the block's start
             L.extend(_emit_lines(gen_lds(k * RING_BYTES, lead_wait=False)))
             L.extend(f"v_add_u32 %[h{i}], %[h{i}], %[r{i}]" for i in range(5))
             L.append("s_barrier")
         L += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_eq_u32 %[cnt], 0",
-              "s_cbranch_scc1 L_rdone_%=" if k < bufs - 1 else "s_cbranch_scc0 L_rloop_%="]
+              "s_cbranch_scc1 L_rdone_%=" if k < LDS_BUFS - 1 else "s_cbranch_scc0 L_rloop_%="]
     L += ["L_rdone_%=:", "s_waitcnt lgkmcnt(0)"]
     return "\n".join(f'    "{l}\\n"' for l in L)
 
@@ -255,7 +254,7 @@ P0_BASE, P1_BASE, VL = 112, 128, 144   # prefetch buffers (2 blocks) and the run
 RING_BYTES = 80 * 64 * 4               # one K+W buffer (also used by rounds_loop_text)
 
 
-def helper_loop_text(bufs: int = LDS_BUFS) -> str:
+def helper_loop_text() -> str:
     """The helper wave's steady state as ONE asm statement (text, not emulated: its body is
     gen_helper, which the emulator checks).  For each raw block: wait for its prefetched words,
     byte-swap them, issue the loads 2 blocks ahead into the freed registers, expand the schedule,
@@ -291,17 +290,17 @@ def helper_loop_text(bufs: int = LDS_BUFS) -> str:
     advance()
     loads(P1_BASE)
     advance()
-    # block 0 into buffer 0; with the helper two blocks ahead (bufs = 3) no barrier follows it:
+    # block 0 into buffer 0; with the helper two blocks ahead (HELPER_AHEAD = 2) no barrier follows it:
     # its first barrier (the rounds wave's starting one) follows the write of block 1
-    step(P0_BASE, 0, barrier=bufs == 2)
+    step(P0_BASE, 0, barrier=HELPER_AHEAD == 1)
     L.append("s_sub_u32 %[cnt], %[nraw], 1")
     L.append("s_cmp_eq_u32 %[cnt], 0")
     L.append("s_cbranch_scc1 L_hdone_%=")
     L.append("L_hloop_%=:")
-    period = 2 * bufs // (2 if bufs % 2 == 0 else 1)   # lcm(prefetch register sets 2, LDS buffers)
+    period = 2 * LDS_BUFS // (2 if LDS_BUFS % 2 == 0 else 1)   # lcm(prefetch register sets 2, LDS buffers)
     for k in range(period):
         blk = k + 1                  # block index (mod period) of this step
-        step((P0_BASE, P1_BASE)[blk % 2], (blk % bufs) * RING_BYTES)
+        step((P0_BASE, P1_BASE)[blk % 2], (blk % LDS_BUFS) * RING_BYTES)
         L.append("s_sub_u32 %[cnt], %[cnt], 1")
         L.append("s_cmp_eq_u32 %[cnt], 0")
         L.append("s_cbranch_scc1 L_hdone_%=" if k < period - 1 else "s_cbranch_scc0 L_hloop_%=")
@@ -615,31 +614,6 @@ __device__ __forceinline__ void tv_sha1_rounds_loop(uint32_t h[5], uint32_t addr
     : {ring_clobbers}, "scc", "memory");
 }}
 
-// The same two loops over a 2-buffer K+W ring (the helper one block ahead): the duo kernel, whose four pairs
-// per workgroup (two waves per SIMD) fill the CU's 160 KiB of LDS with 2 x 20 KiB per pair.
-__device__ __forceinline__ void tv_sha1_helper_loop2(const void* va, uint32_t nraw, uint32_t addr,
-                                                     uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {{
-    uint32_t cnt, adv;
-    uint64_t inc;
-    asm volatile(
-{helper_loop2}
-    : [cnt] "=&s"(cnt), [adv] "=&s"(adv), [inc] "=&s"(inc)
-    : [va] "v"(va), [nraw] "s"(nraw), [addr] "v"(addr), [sel] "s"(0x00010203u),
-      [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
-    : {loop_clobbers}, "scc", "memory");
-}}
-
-__device__ __forceinline__ void tv_sha1_rounds_loop2(uint32_t h[5], uint32_t addr, uint32_t nsteps) {{
-    uint32_t r[5], t0, t1, cnt;
-    asm volatile(
-{rounds_loop2}
-    : [h0] "+v"(h[0]), [h1] "+v"(h[1]), [h2] "+v"(h[2]), [h3] "+v"(h[3]), [h4] "+v"(h[4]),
-      [r0] "=&v"(r[0]), [r1] "=&v"(r[1]), [r2] "=&v"(r[2]), [r3] "=&v"(r[3]), [r4] "=&v"(r[4]),
-      [t0] "=&v"(t0), [t1] "=&v"(t1), [cnt] "=&s"(cnt)
-    : [addr] "v"(addr), [nsteps] "s"(nsteps)
-    : {ring_clobbers}, "scc", "memory");
-}}
-
 // Message schedule of one block for the split kernel's helper wave: raw[16] are the block's words
 // as loaded (little-endian); writes K+W[0..79] to LDS at `addr` (+ q*1024 for quad q).  The LDS
 // writes are left in flight (the caller's barrier waits lgkmcnt(0)).
@@ -667,7 +641,6 @@ def render() -> str:
                          full=emit(gen_full(), True),
                          lds=emit(gen_lds(), False), helper=emit(gen_helper(), False),
                          helper_loop=helper_loop_text(), rounds_loop=rounds_loop_text(),
-                         helper_loop2=helper_loop_text(2), rounds_loop2=rounds_loop_text(2),
                          ring_clobbers=ring, helper_clobbers=helper,
                          loop_clobbers=loop)
 

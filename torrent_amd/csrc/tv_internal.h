@@ -7,7 +7,6 @@
 #define TV_KERNEL_LANE 1
 #define TV_KERNEL_SPLIT 2
 #define TV_KERNEL_MIX 3     // work queue: split pairs + lane waves share 64-piece groups segment by segment
-#define TV_KERNEL_DUO 4     // split pairs two to a SIMD: 4 (rounds, helper) pairs per workgroup, 2-buffer ring
 
 // One launch over a contiguous run of n pieces.  Piece j's byte k (piece-relative) is at
 // data + j*stride + k - data_off.  Blocks [blk_begin, min(blk_end, nb_j)) are processed.

@@ -270,6 +270,7 @@ constexpr int kRingWords = 80 * 64;  // one buffer: [20 quads][64 lanes][4 words
 // wave can keep its 15 LDS reads in flight across block boundaries (tools/gen_sha1_asm.py
 // gen_rounds_block) instead of restarting them, and an LDS latency, at every block.
 constexpr uint32_t kBufs = TV_SHA1_LDS_BUFS;
+constexpr uint32_t kAhead = TV_SHA1_HELPER_AHEAD;
 
 __device__ __forceinline__ void lds_barrier() {
     // LDS writes of this wave complete, then the workgroup barrier.  Deliberately NOT
@@ -290,10 +291,8 @@ __device__ __forceinline__ bool avail_bit(const uint64_t* a, uint32_t i) {
 // Workgroup-group wgi of a launch (PAIRS x {rounds, helper} waves, 64*PAIRS pieces), K+W ring in `ring`.
 // The rounds wave calls before_state() (wave-uniform; false = give up) just before it reads its chaining
 // state: the work-queue kernel waits there for the group's previous segment.
-template <bool HASH, int PAIRS, bool LIST, uint32_t BUFS = kBufs, typename BeforeState>
+template <bool HASH, int PAIRS, bool LIST, typename BeforeState>
 __device__ __forceinline__ void split_group(const TvPieces& p, uint32_t wgi, uint4* ring, BeforeState before_state) {
-    static_assert(BUFS == kBufs || BUFS == 2, "generated loops exist for the default ring and a 2-buffer ring");
-    constexpr uint32_t kAheadT = BUFS - 1;
     // PAIRS x {rounds, helper} waves; 64*PAIRS pieces.  A workgroup's waves go to distinct SIMDs, so
     // with <= 1 workgroup per CU no rounds wave shares its SIMD.  Each pair has its own 3 x 20 KiB
     // K+W ring; the barrier is workgroup-wide, so both pairs run the same (workgroup) block range.
@@ -320,7 +319,7 @@ __device__ __forceinline__ void split_group(const TvPieces& p, uint32_t wgi, uin
     const uint32_t nb = (uint32_t)nblocks(len);
     const uint8_t* piece = p.data + (uint64_t)jj * p.stride - p.data_off;
     const uint32_t b0 = g.fast_begin, end = g.end, fast_end = g.fast_end;
-    uint4* const pring = ring + pair * BUFS * (kRingWords / 4);
+    uint4* const pring = ring + pair * kBufs * (kRingWords / 4);
 
     if (role != 0) {
         // ---------------- helper wave ----------------
@@ -333,10 +332,7 @@ __device__ __forceinline__ void split_group(const TvPieces& p, uint32_t wgi, uin
         const uint32_t lds_lane = (uint32_t)(uintptr_t)(void*)pring + lane * 16u;
         uint32_t b = b0;
         if (fast_end > b0) {
-            if constexpr (BUFS == 2)
-                tv_sha1_helper_loop2(piece + (uint64_t)b0 * 64, fast_end - b0, lds_lane, TV_K0, TV_K1, TV_K2, TV_K3);
-            else
-                tv_sha1_helper_loop(piece + (uint64_t)b0 * 64, fast_end - b0, lds_lane, TV_K0, TV_K1, TV_K2, TV_K3);
+            tv_sha1_helper_loop(piece + (uint64_t)b0 * 64, fast_end - b0, lds_lane, TV_K0, TV_K1, TV_K2, TV_K3);
             b = fast_end;
         }
         for (; b <= end; b++) {
@@ -344,10 +340,10 @@ __device__ __forceinline__ void split_group(const TvPieces& p, uint32_t wgi, uin
             build_tail_block(piece, len, b, w);
 #pragma unroll
             for (int i = 0; i < 16; i++) w[i] = bswap32(w[i]);  // the schedule block byte-swaps
-            tv_sha1_schedule_lds(w, lds_lane + ((b - b0) % BUFS) * (kRingWords * 4u), TV_K0, TV_K1, TV_K2, TV_K3);
-            if (b - b0 + 1 >= kAheadT) lds_barrier();
+            tv_sha1_schedule_lds(w, lds_lane + ((b - b0) % kBufs) * (kRingWords * 4u), TV_K0, TV_K1, TV_K2, TV_K3);
+            if (b - b0 + 1 >= kAhead) lds_barrier();
         }
-        for (uint32_t k = 1; k < kAheadT; k++) lds_barrier();
+        for (uint32_t k = 1; k < kAhead; k++) lds_barrier();
         return;
     }
 
@@ -364,14 +360,13 @@ __device__ __forceinline__ void split_group(const TvPieces& p, uint32_t wgi, uin
     // blocks where every lane of the wave updates: one asm loop (rounds, h += r, barrier)
     const uint32_t full_end = end < nb_min ? end : nb_min;
     if (b < full_end) {
-        if constexpr (BUFS == 2) tv_sha1_rounds_loop2(h, ring_base, full_end - b);
-        else tv_sha1_rounds_loop(h, ring_base, full_end - b);
+        tv_sha1_rounds_loop(h, ring_base, full_end - b);
         b = full_end;
     }
     // the short last piece's wave: lanes past their final block keep their digest
     for (; b < end; b++) {
         uint32_t r[5];
-        tv_sha1_lds(h, r, ring_base + ((b - b0) % BUFS) * (kRingWords * 4u));
+        tv_sha1_lds(h, r, ring_base + ((b - b0) % kBufs) * (kRingWords * 4u));
         if (b < nb) {
 #pragma unroll
             for (int i = 0; i < 5; i++) h[i] += r[i];
@@ -394,27 +389,6 @@ template <bool HASH, int PAIRS, bool LIST = false>
 __global__ __launch_bounds__(128 * PAIRS) void tv_split_kernel(TvPieces p) {
     __shared__ __attribute__((aligned(16))) uint4 ring[kBufs * PAIRS * kRingWords / 4];
     split_group<HASH, PAIRS, LIST>(p, blockIdx.x, ring, [] { return true; });
-}
-
-// ------------------------------------------------------------------------------------------
-// duo kernel: the split kernel with FOUR pairs per 512-thread workgroup over a 2-buffer K+W ring (4 x 2 x
-// 20 KiB = the CU's whole 160 KiB, so one workgroup per CU).  A 512-thread workgroup puts waves w and w + 4
-// on SIMD w % 4 (tools/simd_probe.hip), so every SIMD runs one rounds wave (waves 0-3) and one helper wave
-// (waves 4-7): the helper's schedule VALU fills the issue slots a lone rounds wave leaves empty (a lone
-// wave issues one instruction per ~4 cycles; two waves share the SIMD's 2-cycle issue).  For piece counts
-// where lone split pairs no longer fit (> 512 pairs, > 32,768 pieces per GPU) and the lane kernel leaves
-// SIMDs idle or runs lone waves (< 65,536 pieces).
-// ------------------------------------------------------------------------------------------
-#ifndef TV_DUO_PRIO
-#define TV_DUO_PRIO 0      // 1: s_setprio 1 on the rounds waves (they are already the older half); 2: on the helpers
-#endif
-
-template <bool HASH>
-__global__ __launch_bounds__(512) void tv_duo_kernel(TvPieces p) {
-    __shared__ __attribute__((aligned(16))) uint4 ring[2 * 4 * kRingWords / 4];
-    const bool rounds_wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < 4;
-    if ((TV_DUO_PRIO == 1 && rounds_wave) || (TV_DUO_PRIO == 2 && !rounds_wave)) __builtin_amdgcn_s_setprio(1);
-    split_group<HASH, 4, false, 2>(p, blockIdx.x, ring, [] { return true; });
 }
 
 // ------------------------------------------------------------------------------------------
@@ -667,10 +641,6 @@ hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_
             if (hash) hipLaunchKernelGGL((tv_split_kernel<true, 2>), dim3(grid), dim3(256), 0, s, p);
             else hipLaunchKernelGGL((tv_split_kernel<false, 2>), dim3(grid), dim3(256), 0, s, p);
         }
-    } else if (kernel == TV_KERNEL_DUO) {
-        const unsigned grid = (p.n_main + 255) / 256 + (p.n_main < p.n ? 1 : 0);
-        if (hash) hipLaunchKernelGGL((tv_duo_kernel<true>), dim3(grid), dim3(512), 0, s, p);
-        else hipLaunchKernelGGL((tv_duo_kernel<false>), dim3(grid), dim3(512), 0, s, p);
     } else {
         const unsigned waves = (p.n_main + 63) / 64 + (p.n_main < p.n ? 1 : 0);
         const unsigned grid = (waves + 3) / 4;
