@@ -58,6 +58,8 @@ LDS_BUFS = int(os.environ.get("TV_GEN_BUFS", "3"))      # K+W buffers per pair; 
 # profiles/r02/split_variants.jsonl): LDS data returning under the VALU stream costs more issue cycles
 # than a burst landing while the wave waits.  Kept as a checked option; the shipped build is 0.
 PIPELINED = os.environ.get("TV_GEN_PIPE", "0") == "1"
+PAIR_XOR = os.environ.get("TV_GEN_PAIRXOR", "1") == "1"   # lane compression: schedule words two at a time
+ALIGN_FULL = os.environ.get("TV_GEN_ALIGN", "1") == "1"   # lane compression block starts 8-byte aligned
 HELPER_AHEAD = LDS_BUFS - 1
 assert not PIPELINED or (LDS_BUFS >= 3 and RING_QUADS == 20), "the pipelined stream needs 3 buffers and a 20-quad ring"
 # physical VGPRs of the helper (schedule) block: 16-word W window, xor3 temp, 3 output quads
@@ -102,15 +104,39 @@ def _fop(t, dst, b, c, d):
 
 
 def gen_full():
-    """SHA1_FULL instruction list. Operands: r0-4 (out), w0-15 (in/out), t0-2 (tmp),
-    h0-4 (in), k0-3 (sgpr in)."""
+    """SHA1_FULL instruction list. Operands: r0-4 (out), w0-15 (in/out), t0-3 (tmp),
+    h0-4 (in), k0-3 (sgpr in).
+
+    With PAIR_XOR the schedule words are computed two at a time (W[u], W[u+1] for even u, in round u-1)
+    so that the two 4-byte v_xor_b32 of a pair sit next to each other: every other instruction of the
+    block is an 8-byte VOP3, and an odd number of 4-byte instructions between them would leave every
+    following VOP3 at an address = 4 mod 8.  A lone wave issues long runs of such misaligned 8-byte
+    instructions at ~5.07 instead of 4.07 cycles (tools/ubench_align, profiles/r02/ubench_align.log); the
+    block starts 8-byte aligned (".p2align 3" in the emitted text, ALIGN_FULL)."""
     ins = []
     R = Regs()
     for t in range(80):
         A, B, C, D, E = roles(t)
+        wt = f"w{t & 15}"
+        if PAIR_XOR:
+            us = [t + 1, t + 2] if t % 2 == 1 and 15 <= t <= 77 else []   # pairs (16,17) .. (78,79)
+            tmps = ["t2", "t3"]
+            for i, u in enumerate(us):
+                ins.append(("v_bitop3_b32", tmps[i], f"w{(u - 3) & 15}", f"w{(u - 8) & 15}", f"w{(u - 14) & 15}", 0x96))
+            e_src = R.rd(E)
+            ins.append(("v_add3_u32", R.wr(E), e_src, f"k{t // 20}", wt))
+            ins.append(("v_alignbit_b32", "t0", R.rd(A), R.rd(A), 27))
+            for i, u in enumerate(us):
+                ins.append(("v_xor_b32", f"w{u & 15}", tmps[i], f"w{u & 15}"))
+            ins.append(_fop(t, "t1", R.rd(B), R.rd(C), R.rd(D)))
+            b_src = R.rd(B)
+            ins.append(("v_alignbit_b32", R.wr(B), b_src, b_src, 2))
+            for u in us:
+                ins.append(("v_alignbit_b32", f"w{u & 15}", f"w{u & 15}", f"w{u & 15}", 31))
+            ins.append(("v_add3_u32", R.rd(E), R.rd(E), "t0", "t1"))
+            continue
         u = t + 1
         sched = 16 <= u < 80
-        wt = f"w{t & 15}"
         wu = f"w{u & 15}"
         if sched:
             ins.append(("v_bitop3_b32", "t2", f"w{(u - 3) & 15}", f"w{(u - 8) & 15}", f"w{(u - 14) & 15}", 0x96))
@@ -557,7 +583,7 @@ HEADER = """// GENERATED by tools/gen_sha1_asm.py -- do not edit.  Regenerate wi
 // clobbered.  On return r = working state after round 79; caller does h += r.
 __device__ __forceinline__ void tv_sha1_full(const uint32_t h[5], uint32_t r[5], uint32_t w[16],
                                              uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {{
-    uint32_t t0, t1, t2;
+    uint32_t t0, t1, t2, t3;
     // volatile + "memory": the compiler may not move the caller's prefetch loads across the block
     // (otherwise it sinks them next to their use and the load latency is exposed every block).
     asm volatile(
@@ -567,7 +593,7 @@ __device__ __forceinline__ void tv_sha1_full(const uint32_t h[5], uint32_t r[5],
       [w4] "+v"(w[4]), [w5] "+v"(w[5]), [w6] "+v"(w[6]), [w7] "+v"(w[7]),
       [w8] "+v"(w[8]), [w9] "+v"(w[9]), [w10] "+v"(w[10]), [w11] "+v"(w[11]),
       [w12] "+v"(w[12]), [w13] "+v"(w[13]), [w14] "+v"(w[14]), [w15] "+v"(w[15]),
-      [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2)
+      [t0] "=&v"(t0), [t1] "=&v"(t1), [t2] "=&v"(t2), [t3] "=&v"(t3)
     : [h0] "v"(h[0]), [h1] "v"(h[1]), [h2] "v"(h[2]), [h3] "v"(h[3]), [h4] "v"(h[4]),
       [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
     : "memory");
@@ -638,7 +664,7 @@ def render() -> str:
     helper = ", ".join(f'"v{i}"' for i in hregs)
     loop = ", ".join(f'"v{i}"' for i in hregs + list(range(P0_BASE, VL + 2)))
     return HEADER.format(ring_base=RING_BASE, ring_quads=RING_QUADS, lds_bufs=LDS_BUFS, helper_ahead=HELPER_AHEAD,
-                         full=emit(gen_full(), True),
+                         full=('    ".p2align 3\\n"\n' if ALIGN_FULL else "") + emit(gen_full(), True),
                          lds=emit(gen_lds(), False), helper=emit(gen_helper(), False),
                          helper_loop=helper_loop_text(), rounds_loop=rounds_loop_text(),
                          ring_clobbers=ring, helper_clobbers=helper,
