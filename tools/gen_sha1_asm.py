@@ -60,11 +60,14 @@ LDS_BUFS = int(os.environ.get("TV_GEN_BUFS", "3"))      # K+W buffers per pair; 
 PIPELINED = os.environ.get("TV_GEN_PIPE", "0") == "1"
 PAIR_XOR = os.environ.get("TV_GEN_PAIRXOR", "1") == "1"   # lane compression: schedule words two at a time
 ALIGN_FULL = os.environ.get("TV_GEN_ALIGN", "1") == "1"   # lane compression block starts 8-byte aligned
+HELPER_PAIR = os.environ.get("TV_GEN_HPAIR", "0") == "1"  # split helper: schedule in pairs (4-byte ops paired)
+LOOP_ALIGN = os.environ.get("TV_GEN_LALIGN", "1") == "1"  # split loops: .p2align 3 before every block body
 HELPER_AHEAD = LDS_BUFS - 1
 assert not PIPELINED or (LDS_BUFS >= 3 and RING_QUADS == 20), "the pipelined stream needs 3 buffers and a 20-quad ring"
 # physical VGPRs of the helper (schedule) block: 16-word W window, xor3 temp, 3 output quads
 HW_BASE = 80
 HT = 96
+HT2 = 97   # second schedule temp (HELPER_PAIR)
 HOUT_BASE = 100
 HOUT_QUADS = 3
 
@@ -233,14 +236,27 @@ def gen_helper(src=None, off_base: int = 0):
     """Helper (schedule) block: src = 16 registers holding the block's words as loaded
     (little-endian; default operands raw0-15), sel (sgpr 0x00010203), addr (vgpr, LDS byte address
     of this lane in ring buffer 0), k0-3 (sgpr).  Writes K+W[t] for t = 0..79 to LDS at
-    addr + off_base + (t/4)*1024 as [t/4][lane][4] (one ds_write_b128 per quad)."""
+    addr + off_base + (t/4)*1024 as [t/4][lane][4] (one ds_write_b128 per quad).
+    With HELPER_PAIR the schedule of a quad runs as two pairs (W[t], W[t+1]), each bitop3, bitop3, xor,
+    xor, alignbit, alignbit, so the 4-byte instructions (the xors and the four K adds) come in pairs and
+    the 8-byte ones keep their alignment."""
     if src is None:
         src = [f"raw{i}" for i in range(16)]
     ins = []
     for i in range(16):
         ins.append(("v_perm_b32", hw(i), 0, src[i], "sel"))
     for q in range(20):
-        if q >= 4:
+        if q >= 4 and HELPER_PAIR:
+            for p in range(2):
+                ts = (4 * q + 2 * p, 4 * q + 2 * p + 1)
+                tmp = (f"v{HT}", f"v{HT2}")
+                for i, t in enumerate(ts):
+                    ins.append(("v_bitop3_b32", tmp[i], hw(t - 3), hw(t - 8), hw(t - 14), 0x96))
+                for i, t in enumerate(ts):
+                    ins.append(("v_xor_b32", hw(t), tmp[i], hw(t)))
+                for t in ts:
+                    ins.append(("v_alignbit_b32", hw(t), hw(t), hw(t), 31))
+        elif q >= 4:
             for i in range(4):
                 t = 4 * q + i
                 ins.append(("v_bitop3_b32", f"v{HT}", hw(t - 3), hw(t - 8), hw(t - 14), 0x96))
@@ -267,6 +283,8 @@ def rounds_loop_text() -> str:
         if PIPELINED:
             L.extend(_emit_lines(gen_rounds_block(k * RING_BYTES, ((k + 1) % LDS_BUFS) * RING_BYTES)))
         else:   # per-block stream: its 15 reads issued at the block's start
+            if LOOP_ALIGN:
+                L.append(".p2align 3")
             L.extend(_emit_lines(gen_lds(k * RING_BYTES, lead_wait=False)))
             L.extend(f"v_add_u32 %[h{i}], %[h{i}], %[r{i}]" for i in range(5))
             L.append("s_barrier")
@@ -302,9 +320,13 @@ def helper_loop_text() -> str:
         L.append("s_waitcnt vmcnt(4)")
         body = gen_helper([f"v{pbase + i}" for i in range(16)], off_base)
         perms, rest = body[:16], body[16:]
+        if LOOP_ALIGN:
+            L.append(".p2align 3")
         L.extend(_emit_lines(perms))
         loads(pbase)        # the perms have read pbase: refill it with the block 2 ahead
         advance()
+        if LOOP_ALIGN:
+            L.append(".p2align 3")
         L.extend(_emit_lines(rest))
         if barrier:
             L.append("s_waitcnt lgkmcnt(0)")
@@ -660,7 +682,7 @@ __device__ __forceinline__ void tv_sha1_schedule_lds(const uint32_t raw[16], uin
 
 def render() -> str:
     ring = ", ".join(f'"v{RING_BASE + i}"' for i in range(4 * RING_QUADS))
-    hregs = list(range(HW_BASE, HW_BASE + 16)) + [HT] + list(range(HOUT_BASE, HOUT_BASE + 4 * HOUT_QUADS))
+    hregs = list(range(HW_BASE, HW_BASE + 16)) + [HT, HT2] + list(range(HOUT_BASE, HOUT_BASE + 4 * HOUT_QUADS))
     helper = ", ".join(f'"v{i}"' for i in hregs)
     loop = ", ".join(f'"v{i}"' for i in hregs + list(range(P0_BASE, VL + 2)))
     return HEADER.format(ring_base=RING_BASE, ring_quads=RING_QUADS, lds_bufs=LDS_BUFS, helper_ahead=HELPER_AHEAD,
