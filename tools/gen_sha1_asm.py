@@ -61,6 +61,8 @@ PIPELINED = os.environ.get("TV_GEN_PIPE", "0") == "1"
 PAIR_XOR = os.environ.get("TV_GEN_PAIRXOR", "1") == "1"   # lane compression: schedule words two at a time
 ALIGN_FULL = os.environ.get("TV_GEN_ALIGN", "1") == "1"   # lane compression block starts 8-byte aligned
 HELPER_PAIR = os.environ.get("TV_GEN_HPAIR", "0") == "1"  # split helper: schedule in pairs (4-byte ops paired)
+K_IN_ROUNDS = os.environ.get("TV_GEN_KROUNDS", "0") == "1"  # split: the rounds wave adds K (v_add3 with an SGPR)
+HELPER_X = os.environ.get("TV_GEN_HX", "")   # timing probes only: novalu / nowrite / noload (digests are wrong)
 LOOP_ALIGN = os.environ.get("TV_GEN_LALIGN", "1") == "1"  # split loops: .p2align 3 before every block body
 HELPER_AHEAD = LDS_BUFS - 1
 assert not PIPELINED or (LDS_BUFS >= 3 and RING_QUADS == 20), "the pipelined stream needs 3 buffers and a 20-quad ring"
@@ -178,7 +180,10 @@ def gen_lds(off_base: int = 0, lead_wait: bool = True):
             ins.append(("s_waitcnt_lgkm", min(15, max(0, issued - need))))   # (lgkmcnt is 4 bits)
         A, B, C, D, E = roles(t)
         e_src = R.rd(E)
-        ins.append(("v_add_u32", R.wr(E), ring_reg(g, t % 4), e_src))
+        if K_IN_ROUNDS:
+            ins.append(("v_add3_u32", R.wr(E), e_src, f"k{t // 20}", ring_reg(g, t % 4)))
+        else:
+            ins.append(("v_add_u32", R.wr(E), ring_reg(g, t % 4), e_src))
         if t % 4 == 3 and g + READ_AHEAD < 20:
             ins.append(("ds_read_b128", g + READ_AHEAD, off_base + (g + READ_AHEAD) * 1024))
             issued = g + READ_AHEAD
@@ -207,7 +212,10 @@ def gen_rounds_block(off_cur: int, off_next: int):
             ins.append(("s_waitcnt_lgkm", allowed))
         A, B, C, D, E = roles(t)
         e_src = R.rd(E)
-        ins.append(("v_add_u32", R.wr(E), ring_reg(g, t % 4), e_src))
+        if K_IN_ROUNDS:
+            ins.append(("v_add3_u32", R.wr(E), e_src, f"k{t // 20}", ring_reg(g, t % 4)))
+        else:
+            ins.append(("v_add_u32", R.wr(E), ring_reg(g, t % 4), e_src))
         if t % 4 == 3:
             q = g + READ_AHEAD
             ins.append(("ds_read_b128", q % 20, off_cur + q * 1024 if q < 20 else off_next + (q - 20) * 1024))
@@ -262,6 +270,9 @@ def gen_helper(src=None, off_base: int = 0):
                 ins.append(("v_bitop3_b32", f"v{HT}", hw(t - 3), hw(t - 8), hw(t - 14), 0x96))
                 ins.append(("v_xor_b32", hw(t), f"v{HT}", hw(t)))
                 ins.append(("v_alignbit_b32", hw(t), hw(t), hw(t), 31))
+        if K_IN_ROUNDS:     # the rounds wave adds K: W[4q..4q+3] go to LDS straight from the window
+            ins.append(("ds_write_b128", HW_BASE + ((4 * q) & 15), off_base + q * 1024))
+            continue
         o = HOUT_BASE + 4 * (q % HOUT_QUADS)
         for j in range(4):
             ins.append(("v_add_u32", f"v{o + j}", f"k{q // 5}", hw(4 * q + j)))
@@ -320,10 +331,16 @@ def helper_loop_text() -> str:
         L.append("s_waitcnt vmcnt(4)")
         body = gen_helper([f"v{pbase + i}" for i in range(16)], off_base)
         perms, rest = body[:16], body[16:]
+        # timing-only experiments (wrong digests): drop a class of the helper's work, keep its barriers
+        if HELPER_X == "novalu":
+            rest = [op for op in rest if op[0] == "ds_write_b128"]
+        elif HELPER_X == "nowrite":
+            rest = [op for op in rest if op[0] != "ds_write_b128"]
         if LOOP_ALIGN:
             L.append(".p2align 3")
         L.extend(_emit_lines(perms))
-        loads(pbase)        # the perms have read pbase: refill it with the block 2 ahead
+        if HELPER_X != "noload":
+            loads(pbase)    # the perms have read pbase: refill it with the block 2 ahead
         advance()
         if LOOP_ALIGN:
             L.append(".p2align 3")
@@ -468,7 +485,8 @@ def _check_block(block: bytes, h):
     lds = {}
     emulate(gen_helper(), regs, lds, 0)
     for t in range(80):
-        assert lds[1024 * (t // 4) + 4 * (t % 4)] == (ww[t] + K[t // 20]) & M32, "SHA1_HELPER mismatch"
+        assert lds[1024 * (t // 4) + 4 * (t % 4)] == (ww[t] + (0 if K_IN_ROUNDS else K[t // 20])) & M32, \
+            "SHA1_HELPER mismatch"
     # LDS rounds consume the helper's output
     regs = dict(base)
     emulate(gen_lds(), regs, lds, 0)
@@ -483,7 +501,7 @@ def _kw_words(block: bytes):
     ww = list(struct.unpack(">16I", block)) + [0] * 64
     for t in range(16, 80):
         ww[t] = rotl(ww[t - 3] ^ ww[t - 8] ^ ww[t - 14] ^ ww[t - 16], 1)
-    return [(ww[t] + K[t // 20]) & M32 for t in range(80)]
+    return [(ww[t] + (0 if K_IN_ROUNDS else K[t // 20])) & M32 for t in range(80)]
 
 
 def check_rounds_stream(blocks, h):
@@ -600,6 +618,8 @@ HEADER = """// GENERATED by tools/gen_sha1_asm.py -- do not edit.  Regenerate wi
 // (its first HELPER_AHEAD - 1 writes are not followed by a barrier; it ends with as many extra barriers)
 #define TV_SHA1_LDS_BUFS {lds_bufs}
 #define TV_SHA1_HELPER_AHEAD {helper_ahead}
+// 1: the split helper writes W and the rounds wave adds K (v_add3 with an SGPR); 0: the helper writes K+W
+#define TV_SHA1_K_IN_ROUNDS {k_in_rounds}
 
 // One SHA-1 compression, schedule in-asm.  w[16] holds the big-endian message words and is
 // clobbered.  On return r = working state after round 79; caller does h += r.
@@ -624,13 +644,15 @@ __device__ __forceinline__ void tv_sha1_full(const uint32_t h[5], uint32_t r[5],
 // The 80 rounds of one compression with K+W[0..79] read from LDS at byte address `addr`
 // (+ g*1024 for quad g), as written by tv_sha1_schedule_lds.  Waits for all of its own LDS reads
 // before returning.
-__device__ __forceinline__ void tv_sha1_lds(const uint32_t h[5], uint32_t r[5], uint32_t addr) {{
+__device__ __forceinline__ void tv_sha1_lds(const uint32_t h[5], uint32_t r[5], uint32_t addr,
+                                            uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {{
     uint32_t t0, t1;
     asm volatile(
 {lds}
     : [r0] "=&v"(r[0]), [r1] "=&v"(r[1]), [r2] "=&v"(r[2]), [r3] "=&v"(r[3]), [r4] "=&v"(r[4]),
       [t0] "=&v"(t0), [t1] "=&v"(t1)
-    : [h0] "v"(h[0]), [h1] "v"(h[1]), [h2] "v"(h[2]), [h3] "v"(h[3]), [h4] "v"(h[4]), [addr] "v"(addr)
+    : [h0] "v"(h[0]), [h1] "v"(h[1]), [h2] "v"(h[2]), [h3] "v"(h[3]), [h4] "v"(h[4]), [addr] "v"(addr),
+      [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
     : {ring_clobbers}, "memory");
 }}
 
@@ -651,14 +673,15 @@ __device__ __forceinline__ void tv_sha1_helper_loop(const void* va, uint32_t nra
 
 // The split kernel's rounds wave over nsteps (>= 1) consecutive blocks starting with ring buffer 0,
 // in which every lane updates its chaining value: 80 rounds from LDS, h += r, workgroup barrier.
-__device__ __forceinline__ void tv_sha1_rounds_loop(uint32_t h[5], uint32_t addr, uint32_t nsteps) {{
+__device__ __forceinline__ void tv_sha1_rounds_loop(uint32_t h[5], uint32_t addr, uint32_t nsteps,
+                                                    uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {{
     uint32_t r[5], t0, t1, cnt;
     asm volatile(
 {rounds_loop}
     : [h0] "+v"(h[0]), [h1] "+v"(h[1]), [h2] "+v"(h[2]), [h3] "+v"(h[3]), [h4] "+v"(h[4]),
       [r0] "=&v"(r[0]), [r1] "=&v"(r[1]), [r2] "=&v"(r[2]), [r3] "=&v"(r[3]), [r4] "=&v"(r[4]),
       [t0] "=&v"(t0), [t1] "=&v"(t1), [cnt] "=&s"(cnt)
-    : [addr] "v"(addr), [nsteps] "s"(nsteps)
+    : [addr] "v"(addr), [nsteps] "s"(nsteps), [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
     : {ring_clobbers}, "scc", "memory");
 }}
 
@@ -685,7 +708,7 @@ def render() -> str:
     hregs = list(range(HW_BASE, HW_BASE + 16)) + [HT, HT2] + list(range(HOUT_BASE, HOUT_BASE + 4 * HOUT_QUADS))
     helper = ", ".join(f'"v{i}"' for i in hregs)
     loop = ", ".join(f'"v{i}"' for i in hregs + list(range(P0_BASE, VL + 2)))
-    return HEADER.format(ring_base=RING_BASE, ring_quads=RING_QUADS, lds_bufs=LDS_BUFS, helper_ahead=HELPER_AHEAD,
+    return HEADER.format(k_in_rounds=int(K_IN_ROUNDS), ring_base=RING_BASE, ring_quads=RING_QUADS, lds_bufs=LDS_BUFS, helper_ahead=HELPER_AHEAD,
                          full=('    ".p2align 3\\n"\n' if ALIGN_FULL else "") + emit(gen_full(), True),
                          lds=emit(gen_lds(), False), helper=emit(gen_helper(), False),
                          helper_loop=helper_loop_text(), rounds_loop=rounds_loop_text(),

@@ -360,13 +360,13 @@ __device__ __forceinline__ void split_group(const TvPieces& p, uint32_t wgi, uin
     // blocks where every lane of the wave updates: one asm loop (rounds, h += r, barrier)
     const uint32_t full_end = end < nb_min ? end : nb_min;
     if (b < full_end) {
-        tv_sha1_rounds_loop(h, ring_base, full_end - b);
+        tv_sha1_rounds_loop(h, ring_base, full_end - b, TV_K0, TV_K1, TV_K2, TV_K3);
         b = full_end;
     }
     // the short last piece's wave: lanes past their final block keep their digest
     for (; b < end; b++) {
         uint32_t r[5];
-        tv_sha1_lds(h, r, ring_base + ((b - b0) % kBufs) * (kRingWords * 4u));
+        tv_sha1_lds(h, r, ring_base + ((b - b0) % kBufs) * (kRingWords * 4u), TV_K0, TV_K1, TV_K2, TV_K3);
         if (b < nb) {
 #pragma unroll
             for (int i = 0; i < 5; i++) h[i] += r[i];
