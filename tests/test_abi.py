@@ -55,6 +55,15 @@ def test_asm_generator_emulator():
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr
 
 
+@pytest.mark.parametrize("env", [{"TV_GEN_PAIRXOR": "0"}, {"TV_GEN_KROUNDS": "1"}, {"TV_GEN_HPAIR": "1"},
+                                 {"TV_GEN_PIPE": "1", "TV_GEN_RING": "20"}, {"TV_GEN_BUFS": "2"}])
+def test_asm_generator_emulator_options(env):
+    """The generator's A/B options (tools/build_variants.py) still emit streams that compute SHA-1."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_sha1_asm.py"), "--check"],
+                       capture_output=True, text=True, env=dict(os.environ, **env))
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr
+
+
 def test_generated_header_is_current(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_sha1_asm.py"), "--out",
                         str(tmp_path / "h.h")], capture_output=True, text=True)
