@@ -229,7 +229,7 @@ int tv_host_register(void *ptr, uint64_t bytes);
 int tv_host_unregister(void *ptr);
 
 /* Options (tv_set_option keys). */
-#define TV_OPT_KERNEL 1      /* 0 = auto, 1 = lane, 2 = split (schedule offload), 3 = mix (work queue over split pairs + lane waves; resident calls only) */
+#define TV_OPT_KERNEL 1      /* 0 = auto, 1 = lane, 2 = split (schedule offload), 3 = mix (work queue over split pairs + lane waves; resident calls only), 4 = twin (split with two lanes per piece) */
 #define TV_OPT_STRIDE_PAD 2  /* bytes of padding between resident pieces (default 256) */
 #define TV_OPT_STREAM_CHUNK 3 /* tv_verify_host: bytes of each piece per streamed column chunk */
 #define TV_OPT_SPLIT_PAIRS 4  /* split kernel: (rounds, helper) wave pairs per workgroup, 0 = auto, 1, 2 */

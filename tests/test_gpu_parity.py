@@ -10,7 +10,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = [1, 2, 3]  # lane, split, mix (work queue; streamed calls run it as lane)
+KERNELS = [1, 2, 3, 4]  # lane, split, mix (work queue; streamed calls run it as lane), twin
 
 
 def _ctx(native, kernel=0):

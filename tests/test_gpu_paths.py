@@ -181,7 +181,7 @@ def test_full_size_cfg2_oracle_ground_truth(native, oracle):
         ctx.fill_synthetic(2)
         assert ctx.hash() == truth
         ctx.set_digests(bytes(d2))
-        for k in (1, 2, 3):
+        for k in (1, 2, 3, 4):
             ctx.set_option(native.TV_OPT_KERNEL, k)
             bf = ctx.verify()
             assert ctx.last_kernel()[0] == k
@@ -217,7 +217,7 @@ def test_full_size_cfg4_oracle_ground_truth(native, oracle):
         assert ctx.hash() == truth
         assert ctx.last_kernel()[0] == 1      # auto at 51,200 pieces: lane
         ctx.set_digests(bytes(d2))
-        for k in (1, 2, 3):
+        for k in (1, 2, 3, 4):
             ctx.set_option(native.TV_OPT_KERNEL, k)
             bf = ctx.verify()
             assert ctx.last_kernel()[0] == k

@@ -270,13 +270,59 @@ def gen_helper(src=None, off_base: int = 0):
                 ins.append(("v_bitop3_b32", f"v{HT}", hw(t - 3), hw(t - 8), hw(t - 14), 0x96))
                 ins.append(("v_xor_b32", hw(t), f"v{HT}", hw(t)))
                 ins.append(("v_alignbit_b32", hw(t), hw(t), hw(t), 31))
+        qoff = off_base + q * 1024
         if K_IN_ROUNDS:     # the rounds wave adds K: W[4q..4q+3] go to LDS straight from the window
-            ins.append(("ds_write_b128", HW_BASE + ((4 * q) & 15), off_base + q * 1024))
+            ins.append(("ds_write_b128", HW_BASE + ((4 * q) & 15), qoff))
             continue
         o = HOUT_BASE + 4 * (q % HOUT_QUADS)
         for j in range(4):
             ins.append(("v_add_u32", f"v{o + j}", f"k{q // 5}", hw(4 * q + j)))
-        ins.append(("ds_write_b128", o, off_base + q * 1024))
+        ins.append(("ds_write_b128", o, qoff))
+    return ins
+
+
+# ---- TWIN: two lanes per piece, in the rounds waves AND the helper waves ----
+# A twin workgroup is 2 rounds waves + 2 helper waves over 64 pieces; in every wave lane 2i+b runs piece
+# 32w+i and owns the schedule words of PARITY b.  Rounds: both lanes of a pair run the same 80 rounds on the
+# same state; lane b reads only its own K+W words (10 ds_read_b128 per block instead of 20) and round t's
+# `e + KW` add takes KW from lane t%2 of the pair through DPP (quad_perm [b,b,2+b,2+b]).  Helper: both lanes
+# expand W[16..31] with the standard recurrence, then keep their own parity (v_perm with a per-lane selector)
+# and expand W[32..79] with W[t] = rotl2(W[t-6] ^ W[t-16] ^ W[t-28] ^ W[t-32]), whose terms all have t's
+# parity: 192 VALU + 10 ds_write_b128 per block and lane instead of 308 + 20 (gen_helper2).  Every round is
+# five 8-byte instructions, so each 4-byte s_waitcnt is followed by `s_nop 0` to keep the stream 8-byte
+# aligned (a long misaligned run issues at ~5.07 instead of 4.07 cycles), with two waits per block: before
+# round 0 (reads 0-4) and round 40 (reads 5-9).  Buffer layout [k][wave][lane][4 words]: lane 2i+b of wave w
+# holds W[8k+b], W[8k+b+2], W[8k+b+4], W[8k+b+6] (+K) of piece 32w+i at k*2048 + w*1024 + lane*16, written
+# and read as one contiguous KiB per wave (tools/gen_ubench_dpp.py, profiles/r02/ubench_dpp.log: the rounds
+# stream alone 1,723-1,758 vs 1,818 cycles per block for the shipped 20-read stream).
+TWIN_READ_BYTES = 2048
+TWIN_WAITS = tuple(int(x) for x in os.environ.get("TV_GEN_TWIN_WAITS", "0-5").split("-"))   # reads waited for, in pairs
+TWIN_PRE = os.environ.get("TV_GEN_TWIN_PRE", "1") == "1"   # loop: issue the next block's reads after round 79
+
+
+def gen_twin(off_base: int = 0, reads_next: int | None = None, lead: bool = False):
+    """TWIN rounds block.  lead: issue this block's own 10 reads first (tv_sha1_twin_lds); reads_next:
+    after round 79 issue the 10 reads of the block whose buffer is at that offset (the loop body).
+    Operands as gen_lds: r0-4 (out), t0-1 (tmp), h0-4 (in), addr (this lane's LDS byte address)."""
+    ins = [("ds_read_b128", k, off_base + k * TWIN_READ_BYTES) for k in range(10)] if lead else []
+    R = Regs()
+    for t in range(80):
+        k, b = t // 8, t % 2
+        if t % 8 == 0 and k in TWIN_WAITS:
+            nxt = [x for x in TWIN_WAITS if x > k]
+            ins.append(("s_waitcnt_lgkm", 10 - nxt[0] if nxt else 0))   # reads k .. next wait - 1 retired
+            ins.append(("s_nop",))
+        A, B, C, D, E = roles(t)
+        e_src = R.rd(E)
+        ins.append(("v_add_u32_dpp", R.wr(E), ring_reg(k, (t % 8) // 2), e_src, b))
+        ins.append(("v_alignbit_b32", "t0", R.rd(A), R.rd(A), 27))
+        ins.append(_fop(t, "t1", R.rd(B), R.rd(C), R.rd(D)))
+        b_src = R.rd(B)
+        ins.append(("v_alignbit_b32", R.wr(B), b_src, b_src, 2))
+        ins.append(("v_add3_u32", R.rd(E), R.rd(E), "t0", "t1"))
+    assert R.cur == [f"r{i}" for i in range(5)]
+    if reads_next is not None:
+        ins += [("ds_read_b128", k, reads_next + k * TWIN_READ_BYTES) for k in range(10)]
     return ins
 
 
@@ -305,11 +351,77 @@ def rounds_loop_text() -> str:
     return "\n".join(f'    "{l}\\n"' for l in L)
 
 
+H2_F, H2_P, H2_T, H2_O = 160, 192, 232, 236   # helper2 physical VGPRs: W[0..31], own-parity P[0..39], tmp, 3 out quads
+
+
+def gen_helper2(src=None, off_base: int = 0):
+    """TWIN helper block for a lane pair: src = the 16 registers holding the block's words as loaded
+    (little-endian; default raw0-15, identical in both lanes), sel (sgpr 0x00010203), psel (vgpr: 0x03020100 in
+    lane 0, 0x07060504 in lane 1 of each pair), addr (vgpr, this lane's LDS byte address), k0-3 (sgpr).  Lane b
+    writes K+W[8k+b+2i] (i = 0..3) to addr + off_base + k*2048 for k = 0..9."""
+    if src is None:
+        src = [f"raw{i}" for i in range(16)]
+    F = lambda t: f"v{H2_F + t}"      # noqa: E731  W[t], t < 32 (both parities)
+    P = lambda j: f"v{H2_P + j}"      # noqa: E731  W[2j + b]
+    T = f"v{H2_T}"
+    ins = []
+    nq = [0]
+
+    def quad(k):   # K+W of own-parity words 4k..4k+3 -> LDS
+        o = H2_O + 4 * (nq[0] % 3)
+        nq[0] += 1
+        for i in range(4):
+            ins.append(("v_add_u32", f"v{o + i}", f"k{(4 * k + i) // 10}", P(4 * k + i)))
+        ins.append(("ds_write_b128", o, off_base + k * TWIN_READ_BYTES))
+
+    for i in range(16):
+        ins.append(("v_perm_b32", F(i), 0, src[i], "sel"))
+    for t in range(16, 32):
+        ins.append(("v_bitop3_b32", T, F(t - 3), F(t - 8), F(t - 14), 0x96))
+        ins.append(("v_xor_b32", F(t), T, F(t - 16)))
+        ins.append(("v_alignbit_b32", F(t), F(t), F(t), 31))
+    for j in range(16):
+        ins.append(("v_perm_b32", P(j), F(2 * j + 1), F(2 * j), "psel"))
+        if j % 4 == 3:
+            quad(j // 4)
+    for j in range(16, 40):
+        ins.append(("v_bitop3_b32", T, P(j - 3), P(j - 8), P(j - 14), 0x96))
+        ins.append(("v_xor_b32", P(j), T, P(j - 16)))
+        ins.append(("v_alignbit_b32", P(j), P(j), P(j), 30))
+        if j % 4 == 3:
+            quad(j // 4)
+    return ins
+
+
+def twin_rounds_loop_text() -> str:
+    """The TWIN rounds wave over nsteps (>= 1) blocks starting at ring buffer 0: the first block's reads,
+    then per block gen_twin (its last instructions issue the next block's reads), h += r, barrier.  The
+    reads issued after the final block (of the helper's spare block) are drained before it returns.
+    Safe because the helper runs two blocks ahead: block j + 1 was written before the barrier that
+    started block j, and buffer (j + 1) % 3 is not rewritten until after the barrier that ends block j + 1."""
+    L = ["s_waitcnt lgkmcnt(0)", "s_mov_b32 %[cnt], %[nsteps]"]
+    if TWIN_PRE:
+        L.extend(_emit_lines([("ds_read_b128", k, k * TWIN_READ_BYTES) for k in range(10)]))
+    L.append("L_rloop_%=:")
+    for k in range(LDS_BUFS):
+        L.append(".p2align 3")
+        if TWIN_PRE:
+            L.extend(_emit_lines(gen_twin(k * RING_BYTES, reads_next=((k + 1) % LDS_BUFS) * RING_BYTES)))
+        else:
+            L.extend(_emit_lines(gen_twin(k * RING_BYTES, lead=True)))
+        L.extend(f"v_add_u32 %[h{i}], %[h{i}], %[r{i}]" for i in range(5))
+        L.append("s_barrier")
+        L += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_eq_u32 %[cnt], 0",
+              "s_cbranch_scc1 L_rdone_%=" if k < LDS_BUFS - 1 else "s_cbranch_scc0 L_rloop_%="]
+    L += ["L_rdone_%=:", "s_waitcnt lgkmcnt(0)"]
+    return "\n".join(f'    "{l}\\n"' for l in L)
+
+
 P0_BASE, P1_BASE, VL = 112, 128, 144   # prefetch buffers (2 blocks) and the running load pointer
 RING_BYTES = 80 * 64 * 4               # one K+W buffer (also used by rounds_loop_text)
 
 
-def helper_loop_text() -> str:
+def helper_loop_text(twin: bool = False) -> str:
     """The helper wave's steady state as ONE asm statement (text, not emulated: its body is
     gen_helper, which the emulator checks).  For each raw block: wait for its prefetched words,
     byte-swap them, issue the loads 2 blocks ahead into the freed registers, expand the schedule,
@@ -329,7 +441,7 @@ def helper_loop_text() -> str:
 
     def step(pbase, off_base, barrier=True):
         L.append("s_waitcnt vmcnt(4)")
-        body = gen_helper([f"v{pbase + i}" for i in range(16)], off_base)
+        body = (gen_helper2 if twin else gen_helper)([f"v{pbase + i}" for i in range(16)], off_base)
         perms, rest = body[:16], body[16:]
         # timing-only experiments (wrong digests): drop a class of the helper's work, keep its barriers
         if HELPER_X == "novalu":
@@ -376,11 +488,14 @@ def helper_loop_text() -> str:
 
 # ---------------------------------------------------------------- emulator -------------
 
-def emulate(ins, regs: dict, lds: dict | None = None, addr: int = 0, on_barrier=None, drain: bool = True):
+def emulate(ins, regs: dict, lds: dict | None = None, addr: int = 0, on_barrier=None, drain: bool = True,
+            pending: list | None = None):
     """Execute an instruction list on a dict of 32-bit registers (one lane).  ds_read results
     land only when an s_waitcnt lgkmcnt(N) retires them (in order); reading a register whose
-    load is still in flight, or overwriting one, raises -- so the wait counts are checked too."""
-    pending = []  # [(regs, values, lds addresses)] oldest first
+    load is still in flight, or overwriting one, raises -- so the wait counts are checked too.
+    `pending` (the lane's in-flight reads) may be passed in to carry it across calls."""
+    if pending is None:
+        pending = []  # [(regs, values, lds addresses)] oldest first
 
     def v(x):
         if isinstance(x, str):
@@ -418,10 +533,11 @@ def emulate(ins, regs: dict, lds: dict | None = None, addr: int = 0, on_barrier=
             wr(op[1], v(op[2]) ^ v(op[3]))
         elif o == "v_add_u32":
             wr(op[1], (v(op[2]) + v(op[3])) & M32)
-        elif o == "v_perm_b32":
-            assert op[2] == 0 and regs[op[4]] == 0x00010203
-            x = v(op[3])
-            wr(op[1], int.from_bytes(x.to_bytes(4, "little"), "big"))
+        elif o == "v_perm_b32":   # D.byte[i] = byte sel.byte[i] of {S0:S1} (0-3: S1, 4-7: S0; 12: 0x00)
+            cat = ((v(op[2]) << 32) | v(op[3])).to_bytes(8, "little")
+            sel = v(op[4]).to_bytes(4, "little")
+            assert all(x < 8 or x == 12 for x in sel), "v_perm selector outside the emulated subset"
+            wr(op[1], int.from_bytes(bytes(cat[x] if x < 8 else 0 for x in sel), "little"))
         elif o == "ds_write_b128":
             base, off = op[1], op[2]
             for j in range(4):
@@ -443,11 +559,39 @@ def emulate(ins, regs: dict, lds: dict | None = None, addr: int = 0, on_barrier=
         elif o == "s_barrier":
             if on_barrier is not None:
                 on_barrier({a for _, _, adrs in pending for a in adrs})
+        elif o == "s_nop":
+            pass
         else:
             raise ValueError(o)
     if drain:
         assert not pending, "ds_read still in flight at the end of the block"
     return regs
+
+
+def emulate_twin(ins, regs2, lds, addrs, on_barrier=None, pend=None, drain: bool = True):
+    """Run an instruction list on the two lanes of a TWIN pair in lockstep (regs2 / addrs per lane).
+    v_add_u32_dpp reads its first source from the owning lane (op[4]); every other instruction runs per
+    lane through emulate(), with each lane's in-flight reads carried across instructions."""
+    pend = pend if pend is not None else ([], [])
+    for op in ins:
+        if op[0] == "v_add_u32_dpp":
+            _, dst, src, src1, b = op
+            vals = []
+            for ln in range(2):
+                assert all(src not in rs for rs, _, _ in pend[b]), f"DPP read of {src} in flight"
+                assert all(src1 not in rs and dst not in rs for rs, _, _ in pend[ln]), "in-flight register"
+                vals.append((regs2[b][src] + regs2[ln][src1]) & M32)
+            for ln in range(2):
+                regs2[ln][dst] = vals[ln]
+        elif op[0] == "s_barrier":
+            if on_barrier is not None:
+                on_barrier({a for ln in range(2) for _, _, adrs in pend[ln] for a in adrs})
+        else:
+            for ln in range(2):
+                emulate([op], regs2[ln], lds, addrs[ln], drain=False, pending=pend[ln])
+    if drain:
+        assert not pend[0] and not pend[1], "ds_read still in flight at the end of the block"
+    return regs2
 
 
 def _check_block(block: bytes, h):
@@ -492,6 +636,25 @@ def _check_block(block: bytes, h):
     emulate(gen_lds(), regs, lds, 0)
     got = [(h[i] + regs[f"r{i}"]) & M32 for i in range(5)]
     assert got == exp, "SHA1_LDS mismatch"
+    # TWIN: the helper's twin layout for piece 33 (helper lane 33; rounds wave 1, lanes 2 and 3)
+    if not K_IN_ROUNDS:
+        hregs = []
+        for ln in range(2):
+            regs = {"sel": 0x00010203, "psel": (0x03020100, 0x07060504)[ln]}
+            regs.update({f"k{i}": K[i] for i in range(4)})
+            regs.update({f"raw{i}": int.from_bytes(block[4 * i:4 * i + 4], "little") for i in range(16)})
+            hregs.append(regs)
+        lds = {}
+        # piece 33: lanes 2 and 3 of wave 1 (helper wave 3 writes where rounds wave 1 reads)
+        emulate_twin(gen_helper2(), hregs, lds, [1024 + 2 * 16, 1024 + 3 * 16])
+        for t in range(80):
+            a = 1024 + (t // 8) * TWIN_READ_BYTES + (2 + t % 2) * 16 + 4 * ((t % 8) // 2)
+            assert lds[a] == (ww[t] + K[t // 20]) & M32, "SHA1_HELPER2 mismatch"
+        regs2 = [dict(base), dict(base)]
+        emulate_twin(gen_twin(0, lead=True), regs2, lds, [1024 + 2 * 16, 1024 + 3 * 16])
+        for ln in range(2):
+            got = [(h[i] + regs2[ln][f"r{i}"]) & M32 for i in range(5)]
+            assert got == exp, f"SHA1_TWIN mismatch (lane {ln})"
     return exp
 
 
@@ -541,6 +704,46 @@ def check_rounds_stream(blocks, h):
     return [regs[f"h{i}"] for i in range(5)]
 
 
+def check_twin_stream(blocks, h):
+    """The TWIN rounds loop over consecutive blocks as twin_rounds_loop_text lays it out, for the lane pair
+    of piece 0, against the helper protocol (as check_rounds_stream): at the barrier ending block k, block
+    k+3's buffer is poisoned and block k+2 written; a read in flight there must not be rewritten."""
+    lds = {}
+
+    def put(m, words, in_flight=frozenset()):
+        base = (m % LDS_BUFS) * RING_BYTES
+        for t in range(80):
+            a = base + (t // 8) * TWIN_READ_BYTES + (t % 2) * 16 + 4 * ((t % 8) // 2)
+            assert a not in in_flight, f"LDS {a} rewritten while a ds_read of it is in flight"
+            lds[a] = words[t]
+
+    kws = [_kw_words(b) for b in blocks]
+    put(0, kws[0])
+    if len(blocks) > 1:
+        put(1, kws[1])
+    state = {"k": 0}
+
+    def on_barrier(in_flight):
+        k = state["k"]
+        state["k"] = k + 1
+        put(k + 3, [0xDEADBEEF ^ t for t in range(80)], in_flight)
+        if k + 2 < len(blocks):
+            put(k + 2, kws[k + 2], in_flight)
+
+    regs2 = [{f"h{i}": h[i] for i in range(5)} for _ in range(2)]
+    ins = [("ds_read_b128", k, k * TWIN_READ_BYTES) for k in range(10)] if TWIN_PRE else []
+    for k in range(len(blocks)):
+        if TWIN_PRE:
+            ins += gen_twin((k % LDS_BUFS) * RING_BYTES, reads_next=((k + 1) % LDS_BUFS) * RING_BYTES)
+        else:
+            ins += gen_twin((k % LDS_BUFS) * RING_BYTES, lead=True)
+        ins += [("v_add_u32", f"h{i}", f"h{i}", f"r{i}") for i in range(5)] + [("s_barrier",)]
+    ins.append(("s_waitcnt_lgkm", 0))
+    emulate_twin(ins, regs2, lds, [0, 16], on_barrier=on_barrier)
+    assert all(regs2[0][f"h{i}"] == regs2[1][f"h{i}"] for i in range(5)), "twin lanes disagree"
+    return [regs2[0][f"h{i}"] for i in range(5)]
+
+
 def self_check():
     """Hash several messages through the emulated instruction streams; compare with hashlib."""
     import random
@@ -560,6 +763,13 @@ def self_check():
         h0 = [0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0]
         h = check_rounds_stream([padded[i:i + 64] for i in range(0, len(padded), 64)], h0)
         assert struct.pack(">5I", *h) == hashlib.sha1(msg).digest(), ("stream", n)
+    # the TWIN rounds loop over 1 .. 7 consecutive blocks (every buffer phase)
+    for n in ([0, 55, 64, 119, 200, 310, 400] if LDS_BUFS == 3 and not K_IN_ROUNDS else []):
+        msg = bytes(rng.randrange(256) for _ in range(n))
+        padded = msg + b"\x80" + b"\0" * ((55 - n) % 64) + struct.pack(">Q", 8 * n)
+        h0 = [0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0]
+        h = check_twin_stream([padded[i:i + 64] for i in range(0, len(padded), 64)], h0)
+        assert struct.pack(">5I", *h) == hashlib.sha1(msg).digest(), ("twin stream", n)
     return True
 
 
@@ -591,11 +801,17 @@ def _emit_lines(ins, full: bool = False):
         elif o in ("v_xor_b32", "v_add_u32"):
             lines.append(f"{o} {_opnd(op[1], full)}, {_opnd(op[2], full)}, {_opnd(op[3], full)}")
         elif o == "v_perm_b32":
-            lines.append(f"v_perm_b32 {_opnd(op[1], full)}, 0, {_opnd(op[3], full)}, {_opnd(op[4], full)}")
+            lines.append(f"v_perm_b32 {_opnd(op[1], full)}, {_opnd(op[2], full)}, {_opnd(op[3], full)}, {_opnd(op[4], full)}")
         elif o == "ds_write_b128":
             lines.append(f"ds_write_b128 %[addr], v[{op[1]}:{op[1] + 3}] offset:{op[2]}")
         elif o == "s_barrier":
             lines.append("s_barrier")
+        elif o == "s_nop":
+            lines.append("s_nop 0")
+        elif o == "v_add_u32_dpp":
+            b = op[4]
+            lines.append(f"v_add_u32_dpp {_opnd(op[1], full)}, {_opnd(op[2], full)}, {_opnd(op[3], full)} "
+                         f"quad_perm:[{b},{b},{2 + b},{2 + b}] row_mask:0xf bank_mask:0xf")
         else:
             lines.append(f"{o} " + ", ".join(_opnd(x, full) for x in op[1:]))
     return lines
@@ -703,17 +919,83 @@ __device__ __forceinline__ void tv_sha1_schedule_lds(const uint32_t raw[16], uin
 """
 
 
+TWIN_HEADER = """
+// ---- TWIN kernel: two lanes per piece in the rounds and helper waves (tools/gen_sha1_asm.py gen_twin,
+// gen_helper2).  K+W buffer layout [k][wave][lane][4 words]; a lane's `addr` is ring + (wave & 1)*1024 + lane*16,
+// its `psel` 0x03020100 (even lane) / 0x07060504 (odd lane).
+
+// One block of 80 rounds for a lane pair, with its own 10 LDS reads (waits for them before returning).
+__device__ __forceinline__ void tv_sha1_twin_lds(const uint32_t h[5], uint32_t r[5], uint32_t addr) {{
+    uint32_t t0, t1;
+    asm volatile(
+{twin_lds}
+    : [r0] "=&v"(r[0]), [r1] "=&v"(r[1]), [r2] "=&v"(r[2]), [r3] "=&v"(r[3]), [r4] "=&v"(r[4]),
+      [t0] "=&v"(t0), [t1] "=&v"(t1)
+    : [h0] "v"(h[0]), [h1] "v"(h[1]), [h2] "v"(h[2]), [h3] "v"(h[3]), [h4] "v"(h[4]), [addr] "v"(addr)
+    : {ring_clobbers}, "memory");
+}}
+
+// The TWIN rounds wave over nsteps (>= 1) blocks from ring buffer 0 in which every lane updates.
+__device__ __forceinline__ void tv_sha1_twin_rounds_loop(uint32_t h[5], uint32_t addr, uint32_t nsteps) {{
+    uint32_t r[5], t0, t1, cnt;
+    asm volatile(
+{twin_rounds_loop}
+    : [h0] "+v"(h[0]), [h1] "+v"(h[1]), [h2] "+v"(h[2]), [h3] "+v"(h[3]), [h4] "+v"(h[4]),
+      [r0] "=&v"(r[0]), [r1] "=&v"(r[1]), [r2] "=&v"(r[2]), [r3] "=&v"(r[3]), [r4] "=&v"(r[4]),
+      [t0] "=&v"(t0), [t1] "=&v"(t1), [cnt] "=&s"(cnt)
+    : [addr] "v"(addr), [nsteps] "s"(nsteps)
+    : {ring_clobbers}, "scc", "memory");
+}}
+
+// The TWIN helper wave (64 pieces, one lane each) over its nraw (>= 1) raw blocks: as
+// tv_sha1_helper_loop, writing the twin layout.
+__device__ __forceinline__ void tv_sha1_twin_helper_loop(const void* va, uint32_t nraw, uint32_t addr, uint32_t psel,
+                                                         uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {{
+    uint32_t cnt, adv;
+    uint64_t inc;
+    asm volatile(
+{twin_helper_loop}
+    : [cnt] "=&s"(cnt), [adv] "=&s"(adv), [inc] "=&s"(inc)
+    : [va] "v"(va), [nraw] "s"(nraw), [addr] "v"(addr), [sel] "s"(0x00010203u), [psel] "v"(psel),
+      [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
+    : {twin_loop_clobbers}, "scc", "memory");
+}}
+
+// Message schedule of one block into the twin layout (the helper's padded tail blocks).
+__device__ __forceinline__ void tv_sha1_twin_schedule_lds(const uint32_t raw[16], uint32_t addr, uint32_t psel,
+                                                          uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {{
+    asm volatile(
+{twin_helper}
+    :
+    : [raw0] "v"(raw[0]), [raw1] "v"(raw[1]), [raw2] "v"(raw[2]), [raw3] "v"(raw[3]),
+      [raw4] "v"(raw[4]), [raw5] "v"(raw[5]), [raw6] "v"(raw[6]), [raw7] "v"(raw[7]),
+      [raw8] "v"(raw[8]), [raw9] "v"(raw[9]), [raw10] "v"(raw[10]), [raw11] "v"(raw[11]),
+      [raw12] "v"(raw[12]), [raw13] "v"(raw[13]), [raw14] "v"(raw[14]), [raw15] "v"(raw[15]),
+      [addr] "v"(addr), [sel] "s"(0x00010203u), [psel] "v"(psel), [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
+    : {twin_helper_clobbers}, "memory");
+}}
+"""
+
+
 def render() -> str:
     ring = ", ".join(f'"v{RING_BASE + i}"' for i in range(4 * RING_QUADS))
     hregs = list(range(HW_BASE, HW_BASE + 16)) + [HT, HT2] + list(range(HOUT_BASE, HOUT_BASE + 4 * HOUT_QUADS))
     helper = ", ".join(f'"v{i}"' for i in hregs)
     loop = ", ".join(f'"v{i}"' for i in hregs + list(range(P0_BASE, VL + 2)))
+    h2regs = list(range(H2_F, H2_O + 12))
+    h2 = ", ".join(f'"v{i}"' for i in h2regs)
+    h2loop = ", ".join(f'"v{i}"' for i in h2regs + list(range(P0_BASE, VL + 2)))
     return HEADER.format(k_in_rounds=int(K_IN_ROUNDS), ring_base=RING_BASE, ring_quads=RING_QUADS, lds_bufs=LDS_BUFS, helper_ahead=HELPER_AHEAD,
                          full=('    ".p2align 3\\n"\n' if ALIGN_FULL else "") + emit(gen_full(), True),
                          lds=emit(gen_lds(), False), helper=emit(gen_helper(), False),
                          helper_loop=helper_loop_text(), rounds_loop=rounds_loop_text(),
                          ring_clobbers=ring, helper_clobbers=helper,
-                         loop_clobbers=loop)
+                         loop_clobbers=loop) + ("" if K_IN_ROUNDS else TWIN_HEADER.format(
+                             twin_lds='    ".p2align 3\\n"\n' + emit(gen_twin(0, lead=True), False),
+                             twin_rounds_loop=twin_rounds_loop_text(),
+                             twin_helper_loop=helper_loop_text(twin=True),
+                             twin_helper=emit(gen_helper2(), False),
+                             ring_clobbers=ring, twin_helper_clobbers=h2, twin_loop_clobbers=h2loop))
 
 
 def main():

@@ -35,7 +35,7 @@ TV_OPT_DEBUG_REBOUNCE = 11
 TV_STREAM_RING_SLOTS = 3
 TV_STREAM_SLOT_BYTES = 64 << 20
 
-KERNEL_AUTO, KERNEL_LANE, KERNEL_SPLIT, KERNEL_MIX = 0, 1, 2, 3
+KERNEL_AUTO, KERNEL_LANE, KERNEL_SPLIT, KERNEL_MIX, KERNEL_TWIN = 0, 1, 2, 3, 4
 
 _u64, _i64, _int, _p = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p
 

@@ -400,7 +400,8 @@ int choose_kernel(const tv_ctx* c, bool resident = true) {
     // section 6, profiles/r02/mix_probe.log); its queue entries hold 16-bit group numbers
     const bool mix_ok = resident && (c->count + 63) / 64 + 1 <= 0xFFFF;
     if (c->kernel_opt == TV_KERNEL_MIX) return mix_ok ? TV_KERNEL_MIX : TV_KERNEL_LANE;
-    if (c->kernel_opt == TV_KERNEL_LANE || c->kernel_opt == TV_KERNEL_SPLIT) return c->kernel_opt;
+    if (c->kernel_opt == TV_KERNEL_LANE || c->kernel_opt == TV_KERNEL_SPLIT || c->kernel_opt == TV_KERNEL_TWIN)
+        return c->kernel_opt;
     // Split (schedule offload) while every split pair (64 pieces, 2 waves) has SIMDs to itself:
     // <= 32,768 pieces.  Beyond that rounds waves share SIMDs and the lane kernel wins
     // (measured 40,960 pieces split 1.62 vs lane 2.33 TB/s; 32,768 split 2.50 vs lane 1.87).
@@ -1062,7 +1063,7 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
     std::lock_guard<std::mutex> g(c->mu);
     switch (key) {
         case TV_OPT_KERNEL:
-            if (value < 0 || value > 3) return fail(c, TV_ERR_ARG, "TV_OPT_KERNEL must be 0, 1, 2 or 3");
+            if (value < 0 || value > 4) return fail(c, TV_ERR_ARG, "TV_OPT_KERNEL must be 0, 1, 2, 3 or 4");
             c->kernel_opt = (int)value;
             return TV_OK;
         case TV_OPT_STRIDE_PAD:

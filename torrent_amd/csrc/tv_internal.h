@@ -7,6 +7,7 @@
 #define TV_KERNEL_LANE 1
 #define TV_KERNEL_SPLIT 2
 #define TV_KERNEL_MIX 3     // work queue: split pairs + lane waves share 64-piece groups segment by segment
+#define TV_KERNEL_TWIN 4    // split with two lanes per piece in the rounds waves (half the K+W reads per block)
 
 // One launch over a contiguous run of n pieces.  Piece j's byte k (piece-relative) is at
 // data + j*stride + k - data_off.  Blocks [blk_begin, min(blk_end, nb_j)) are processed.

@@ -392,6 +392,119 @@ __global__ __launch_bounds__(128 * PAIRS) void tv_split_kernel(TvPieces p) {
 }
 
 // ------------------------------------------------------------------------------------------
+// twin kernel: the split kernel with TWO lanes per piece in every wave.  A workgroup is rounds waves 0, 1
+// and helper waves 2, 3 over 64 pieces; in each wave lane 2i + b runs piece 32(wave & 1) + i and owns its
+// schedule words of parity b (tools/gen_sha1_asm.py gen_twin / gen_helper2).  Rounds: both lanes of a pair
+// run the same rounds; lane b reads only its own K+W words and each round's `e + KW` add takes KW from lane
+// t % 2 of the pair through DPP: 10 ds_read_b128 per block instead of 20, serial stream 405 VALU + 10 LDS
+// + 2 waits.  Helper: 192 VALU + 10 ds_write_b128 per block (W[32..79] from the parity-closed recurrence
+// W[t] = rotl2(W[t-6] ^ W[t-16] ^ W[t-28] ^ W[t-32])), half a split helper's stream.  K+W ring: 3 x 20 KiB,
+// the helpers two blocks ahead, one 4-wave barrier per block.  Four waves per 64 pieces fill the SIMDs up
+// to 16,384 pieces (cfg2: 256 workgroups, one per CU).
+// ------------------------------------------------------------------------------------------
+namespace {
+
+// Final step of a twin rounds wave (32 pieces, lane 2i + b = piece j0w + i): as finish(), with the
+// bitfield bits of the even lanes.
+template <bool HASH>
+__device__ __forceinline__ void finish_twin(const TvPieces& p, bool writer, uint32_t jj, uint32_t j0w,
+                                            const uint32_t h[5], bool last_grp) {
+    if (!p.finalize || HASH) {
+        finish<HASH>(p, writer, jj, j0w, h, last_grp);
+        return;
+    }
+    bool ok = writer;
+#pragma unroll
+    for (int k = 0; k < 5; k++) ok &= (h[k] == p.digests[(uint64_t)k * p.dcount + jj]);
+    const uint64_t mask = __ballot(ok);
+    if ((threadIdx.x & 63) == 0) {
+        uint64_t bits;
+        uint32_t w;
+        if (last_grp) {
+            w = jj >> 6;
+            bits = (mask & 1) ? 1ull << (((jj >> 3) & 7) * 8 + 7 - (jj & 7)) : 0;
+        } else {
+            uint64_t x = mask & 0x5555555555555555ull;          // even lanes -> bits 0..31
+            x = (x | (x >> 1)) & 0x3333333333333333ull;
+            x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+            x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+            x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+            x = (x | (x >> 16)) & 0x00000000FFFFFFFFull;
+            w = j0w >> 6;
+            bits = __builtin_bswap64(__builtin_bitreverse64(x << (j0w & 63)));
+        }
+        if (p.avail64) bits &= p.avail64[w];
+        if (bits) atomicOr(reinterpret_cast<unsigned long long*>(p.out64 + w), (unsigned long long)bits);
+    }
+}
+
+}  // namespace
+
+template <bool HASH>
+__global__ __launch_bounds__(256) void tv_twin_kernel(TvPieces p) {
+    __shared__ __attribute__((aligned(16))) uint4 ring[kBufs * kRingWords / 4];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // 0, 1 = rounds; 2, 3 = helpers
+    const uint32_t half = wave & 1u;                                           // pieces 32*half .. +31
+    // main workgroups cover [0, n_main); a short last piece gets one workgroup after them (every lane)
+    const bool last_grp = blockIdx.x >= (p.n_main + 63u) / 64u;
+    const uint32_t wg0 = last_grp ? p.last_idx : blockIdx.x * 64u;
+    const uint32_t j = last_grp ? p.last_idx : wg0 + half * 32u + (lane >> 1);
+    const uint32_t jj = last_grp ? p.last_idx : (j < p.n_main ? j : p.n_main - 1);
+    const WaveGeom g = last_grp ? wave_geom_flags(p, true, true) : wave_geom(p, wg0, 64);
+    const uint64_t len = lane_len(p, jj);
+    const uint32_t nb = (uint32_t)nblocks(len);
+    const uint8_t* piece = p.data + (uint64_t)jj * p.stride - p.data_off;
+    const uint32_t b0 = g.fast_begin, end = g.end, fast_end = g.fast_end;
+    const uint32_t lds_lane = (uint32_t)(uintptr_t)(void*)ring + half * 1024u + lane * 16u;
+
+    if (wave >= 2) {
+        // ---------------- helper waves (as split_group's helper, twin layout) ----------------
+        const uint32_t psel = (lane & 1u) ? 0x07060504u : 0x03020100u;
+        uint32_t b = b0;
+        if (fast_end > b0) {
+            tv_sha1_twin_helper_loop(piece + (uint64_t)b0 * 64, fast_end - b0, lds_lane, psel, TV_K0, TV_K1, TV_K2, TV_K3);
+            b = fast_end;
+        }
+        for (; b <= end; b++) {
+            uint32_t w[16];
+            build_tail_block(piece, len, b, w);
+#pragma unroll
+            for (int i = 0; i < 16; i++) w[i] = bswap32(w[i]);  // the schedule block byte-swaps
+            tv_sha1_twin_schedule_lds(w, lds_lane + ((b - b0) % kBufs) * (kRingWords * 4u), psel, TV_K0, TV_K1, TV_K2, TV_K3);
+            if (b - b0 + 1 >= kAhead) lds_barrier();
+        }
+        for (uint32_t k = 1; k < kAhead; k++) lds_barrier();
+        return;
+    }
+
+    // ---------------- rounds waves ----------------
+    uint32_t h[5];
+    start_state(p, jj, h);
+    const uint32_t ring_base = lds_lane;
+    lds_barrier();
+    uint32_t b = b0;
+    const uint32_t full_end = end < g.nb_min ? end : g.nb_min;
+    if (b < full_end) {
+        tv_sha1_twin_rounds_loop(h, ring_base, full_end - b);
+        b = full_end;
+    }
+    // the short last piece's workgroup: lanes past their final block keep their digest (both lanes of a
+    // pair hold the same piece, so the DPP partner is always in step)
+    for (; b < end; b++) {
+        uint32_t r[5];
+        tv_sha1_twin_lds(h, r, ring_base + ((b - b0) % kBufs) * (kRingWords * 4u));
+        if (b < nb) {
+#pragma unroll
+            for (int i = 0; i < 5; i++) h[i] += r[i];
+        }
+        lds_barrier();
+    }
+    const bool writer = last_grp ? (wave == 0 && lane == 0) : ((lane & 1u) == 0 && j < p.n_main);
+    finish_twin<HASH>(p, writer, jj, wg0 + half * 32u, h, last_grp);
+}
+
+// ------------------------------------------------------------------------------------------
 // MIX: persistent split pairs and persistent lane waves serve one FIFO of ready 64-piece groups at once.
 // With 32,768 < P < ~56,000 pieces the lane kernel leaves SIMDs idle (cfg4 on one GPU: 800 waves on 1,024
 // SIMDs) and a piece's SHA-1 is serial: a group advances at its worker's per-piece rate (pair ~1,870
@@ -641,6 +754,10 @@ hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_
             if (hash) hipLaunchKernelGGL((tv_split_kernel<true, 2>), dim3(grid), dim3(256), 0, s, p);
             else hipLaunchKernelGGL((tv_split_kernel<false, 2>), dim3(grid), dim3(256), 0, s, p);
         }
+    } else if (kernel == TV_KERNEL_TWIN) {
+        const unsigned grid = (p.n_main + 63) / 64 + (p.n_main < p.n ? 1 : 0);
+        if (hash) hipLaunchKernelGGL(tv_twin_kernel<true>, dim3(grid), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL(tv_twin_kernel<false>, dim3(grid), dim3(256), 0, s, p);
     } else {
         const unsigned waves = (p.n_main + 63) / 64 + (p.n_main < p.n ? 1 : 0);
         const unsigned grid = (waves + 3) / 4;
