@@ -71,8 +71,8 @@ VALU_DERIVATION = (
 # Cycles per VALU instruction of a lone wave: 4.07 for 8-byte VOP3 ops in a long loop body, 4.09 for the
 # SHA-1 round mix (tools/ubench_fetch.hip, profiles/r01/ubench_fetch.log); the wave64 cadence is 4.
 LONE_WAVE_CYC = 4.07
-SERIAL_INSTR = {1: 613, 2: 405}  # per-block serial stream: lane kernel / split rounds wave
-KERNEL_NAMES = {1: "lane", 2: "split", 3: "mix"}
+SERIAL_INSTR = {1: 613, 2: 405, 4: 405}  # per-block serial VALU stream: lane kernel / split and twin rounds waves
+KERNEL_NAMES = {1: "lane", 2: "split", 3: "mix", 4: "twin"}
 MIX_PAIRS, MIX_LANE_WAVES = 256, 512   # MIX workers on a 256-CU MI355X (tv_api.hip launch_resident)
 
 
@@ -444,7 +444,7 @@ def main() -> int:
     sc = ap.add_mutually_exclusive_group()
     sc.add_argument("--strong", action="store_true", help="the workload's pieces are the WHOLE torrent, sharded")
     sc.add_argument("--weak", action="store_true", help="the workload's pieces are per GPU")
-    ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 lane, 2 split, 3 mix")
+    ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 lane, 2 split, 3 mix, 4 twin")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-saturating", action="store_true", help="skip the piece_saturated leg (N=1)")
@@ -531,7 +531,7 @@ def main() -> int:
                          "valu_peak_derivation": VALU_DERIVATION,
                          "note": "SHA-1 is serial per piece, so P pieces per GPU cap the rate at P x 64 B / "
                                  "(serial VALU instr x 4.07 cyc) (piece_parallelism_ceiling; 405 instr for the "
-                                 "split rounds wave, 613 for the lane kernel); full R_valu needs >= 65,536 "
+                                 "twin and split rounds waves, 613 for the lane kernel); full R_valu needs >= 65,536 "
                                  "pieces per GPU (piece_saturated)"},
             "ground_truth_s": main_leg["ground_truth_s"],
         }

@@ -232,7 +232,7 @@ int tv_host_unregister(void *ptr);
 #define TV_OPT_KERNEL 1      /* 0 = auto, 1 = lane, 2 = split (schedule offload), 3 = mix (work queue over split pairs + lane waves; resident calls only), 4 = twin (split with two lanes per piece) */
 #define TV_OPT_STRIDE_PAD 2  /* bytes of padding between resident pieces (default 256) */
 #define TV_OPT_STREAM_CHUNK 3 /* tv_verify_host: bytes of each piece per streamed column chunk */
-#define TV_OPT_SPLIT_PAIRS 4  /* split kernel: (rounds, helper) wave pairs per workgroup, 0 = auto, 1, 2 */
+#define TV_OPT_SPLIT_PAIRS 4  /* split and twin kernels: (rounds, helper) wave pairs per workgroup, 0 = auto, 1, 2 */
 #define TV_OPT_FILE_DIRECT 5  /* tv_stage_file: 1 (default) = warm windows DMA'd from registered page-cache pages, 0 = all via the pinned ring */
 #define TV_OPT_FILE_CHUNK 6   /* tv_stage_file: bytes per mapped file window (default 256 MiB, >= 64 KiB) */
 #define TV_OPT_FILE_DIRECT_MIN 7 /* tv_stage_files: segment length that takes the tv_stage_file path (default 32 MiB) */

@@ -5,8 +5,9 @@ A lone wave issues long runs of 8-byte instructions placed at 4 mod 8 at ~5.07 i
 generator paired the schedule's 4-byte xors and aligned the block.  These tests keep that layout:
   * the generated lane compression (tv_sha1_full) starts with .p2align 3 and keeps every 8-byte VOP3 at an
     8-byte offset from its start;
-  * in the built library, the lane kernel's main loop has almost no misaligned 8-byte instructions and the
-    split kernel's rounds loop no misaligned run longer than five (runs up to five are free).
+  * in the built library, the lane kernel's main loop has almost no misaligned 8-byte instructions, the
+    split kernel's rounds loop no misaligned run longer than five (runs up to five are free), and the twin
+    kernel's rounds loop (five 8-byte instructions per round) none at all and no padding s_nop.
 """
 import os
 import re
@@ -61,3 +62,8 @@ def test_built_hot_loops_alignment():
     assert rounds, rep["split"]
     for r in rounds:
         assert max(int(k) for k in r["runs"]) <= 5, r
+    # the twin rounds loop (3 blocks of 80 five-instruction rounds, all 8-byte): fully aligned, and no s_nop
+    twin = [r for r in rep["twin"] if r["instrs"] >= 1000 and r["eight_byte"] > 0.9 * r["instrs"]]
+    assert twin, rep["twin"]
+    for r in twin:
+        assert r["misaligned"] == 0 and r["s_nop"] == 0, r

@@ -5,7 +5,8 @@ DESIGN.md section 4).
     python tools/asm_alignment.py [path/to/libtorrent_verify.so]
 
 Extracts the gfx950 code object with llvm-objdump --offloading (into a temporary directory), disassembles it,
-and for every backward branch of the verify kernels (tv_lane_kernel<false>, tv_split_kernel<false, 1, false>)
+and for every backward branch of the verify kernels (tv_lane_kernel<false>, tv_split_kernel<false, 1, false>,
+tv_twin_kernel<false, 1>)
 reports the loop's instruction count, its 8-byte instructions, how many of them sit at 4 mod 8, and the
 histogram of runs of consecutive misaligned 8-byte instructions.  Prints JSON; used by tests/test_asm_layout.py.
 """
@@ -19,7 +20,8 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
-KERNELS = {"lane": "_Z14tv_lane_kernelILb0EEv8TvPieces", "split": "_Z15tv_split_kernelILb0ELi1ELb0EEv8TvPieces"}
+KERNELS = {"lane": "_Z14tv_lane_kernelILb0EEv8TvPieces", "split": "_Z15tv_split_kernelILb0ELi1ELb0EEv8TvPieces",
+           "twin": "_Z14tv_twin_kernelILb0ELi1EEv8TvPieces"}
 _INS = re.compile(r"\s+(\S.*?)\s+//\s*([0-9A-Fa-f]+):\s*((?:[0-9A-Fa-f]{8}\s*)+)")
 
 

@@ -298,6 +298,7 @@ def gen_helper(src=None, off_base: int = 0):
 TWIN_READ_BYTES = 2048
 TWIN_WAITS = tuple(int(x) for x in os.environ.get("TV_GEN_TWIN_WAITS", "0-5").split("-"))   # reads waited for, in pairs
 TWIN_PRE = os.environ.get("TV_GEN_TWIN_PRE", "1") == "1"   # loop: issue the next block's reads after round 79
+TWIN_NONOP = os.environ.get("TV_GEN_TWIN_NONOP", "1") == "1"  # loop: 4-byte instructions paired without s_nop
 
 
 def gen_twin(off_base: int = 0, reads_next: int | None = None, lead: bool = False):
@@ -402,6 +403,25 @@ def twin_rounds_loop_text() -> str:
     L = ["s_waitcnt lgkmcnt(0)", "s_mov_b32 %[cnt], %[nsteps]"]
     if TWIN_PRE:
         L.extend(_emit_lines([("ds_read_b128", k, k * TWIN_READ_BYTES) for k in range(10)]))
+    if TWIN_PRE and TWIN_WAITS == (0, 5) and TWIN_NONOP:
+        # No s_nop inside the loop: a block's 4-byte instructions come in even groups between its 8-byte runs.
+        # The first wait sits at 4 mod 8 (the previous block's tail -- four 4-byte h adds, barrier, s_cmp,
+        # s_cbranch -- precedes it; h0 += r0 is the 8-byte VOP3 form), and the loop counter's s_sub pairs
+        # with the round-40 wait.
+        L += [".p2align 3", "s_nop 0", "L_rloop_%=:"]
+        for k in range(LDS_BUFS):
+            body = _emit_lines(gen_twin(k * RING_BYTES, reads_next=((k + 1) % LDS_BUFS) * RING_BYTES))
+            nops = [i for i, x in enumerate(body) if x == "s_nop 0"]
+            assert len(nops) == 2 and body[nops[0] - 1].startswith("s_waitcnt") and nops[0] == 1
+            body[nops[1]] = "s_sub_u32 %[cnt], %[cnt], 1"
+            del body[nops[0]]
+            L.extend(body)
+            L.append("v_add_u32_e64 %[h0], %[h0], %[r0]")
+            L.extend(f"v_add_u32 %[h{i}], %[h{i}], %[r{i}]" for i in range(1, 5))
+            L += ["s_barrier", "s_cmp_eq_u32 %[cnt], 0",
+                  "s_cbranch_scc1 L_rdone_%=" if k < LDS_BUFS - 1 else "s_cbranch_scc0 L_rloop_%="]
+        L += ["L_rdone_%=:", "s_waitcnt lgkmcnt(0)"]
+        return "\n".join(f'    "{l}\\n"' for l in L)
     L.append("L_rloop_%=:")
     for k in range(LDS_BUFS):
         L.append(".p2align 3")

@@ -9,7 +9,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from torrent_amd import _native as N  # noqa: E402
 
-VARIANTS = [("lane", 1, 0), ("split1", 2, 1), ("split2", 2, 2), ("mix", 3, 0), ("twin", 4, 0), ("auto", 0, 0)]
+VARIANTS = [("lane", 1, 0), ("split1", 2, 1), ("split2", 2, 2), ("mix", 3, 0), ("twin1", 4, 1), ("twin2", 4, 2), ("auto", 0, 0)]
 if os.environ.get("SWEEP_VARIANTS"):   # e.g. lane,mix (auto is always measured last)
     VARIANTS = [v for v in VARIANTS if v[0] in os.environ["SWEEP_VARIANTS"].split(",")] + [VARIANTS[-1]]
 PS = [1024, 2048, 4096, 8192, 12800, 16384, 20480, 25600, 32768, 40960, 49152, 51200, 65536, 131072, 262144]
@@ -47,7 +47,7 @@ def main():
             assert not any(ctx.verify()), (P, name)    # (no stale bits from the previous variant)
             ctx.set_digests(bytes(d))
             if name == "auto":
-                row["auto_kernel"] = {1: "lane", 2: "split", 3: "mix"}[ctx.last_kernel()[0]]
+                row["auto_kernel"] = {1: "lane", 2: "split", 3: "mix", 4: "twin"}[ctx.last_kernel()[0]]
         ctx.close()
         row["best"] = max((row[n], n) for n, _, _ in VARIANTS[:-1])[1]
         rows.append(row)

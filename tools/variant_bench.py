@@ -3,7 +3,7 @@ piece count, every variant's verify kernel time (HIP events, best and median of 
 synthetic payload; each variant's digests must equal the first variant's and its bitfield be exact.
 
     python tools/variant_bench.py <pieces,...> <name> [<name> ...]      (libs in build/variants/)
-env: KERNEL (default 2 = split), REPS (5), GIB (payload GiB per point, 16)
+env: KERNEL (default 2 = split), PAIRS (TV_OPT_SPLIT_PAIRS, default 0), REPS (5), GIB (payload GiB per point, 16)
 Each variant runs in its own process (one library per process); results as JSON lines."""
 import json
 import os
@@ -20,6 +20,7 @@ P = int(sys.argv[1]); reps = int(sys.argv[2]); kernel = int(sys.argv[3]); gib = 
 L = ((gib << 30) // P) // 64 * 64
 ctx = N.Context(0)
 ctx.set_option(N.TV_OPT_KERNEL, kernel)
+ctx.set_option(N.TV_OPT_SPLIT_PAIRS, int(os.environ.get("PAIRS", "0")))
 ctx.set_layout(L * P, L, P)
 ctx.fill_synthetic(2)
 d = bytearray(ctx.hash())

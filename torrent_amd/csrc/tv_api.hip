@@ -402,9 +402,17 @@ int choose_kernel(const tv_ctx* c, bool resident = true) {
     if (c->kernel_opt == TV_KERNEL_MIX) return mix_ok ? TV_KERNEL_MIX : TV_KERNEL_LANE;
     if (c->kernel_opt == TV_KERNEL_LANE || c->kernel_opt == TV_KERNEL_SPLIT || c->kernel_opt == TV_KERNEL_TWIN)
         return c->kernel_opt;
-    // Split (schedule offload) while every split pair (64 pieces, 2 waves) has SIMDs to itself:
-    // <= 32,768 pieces.  Beyond that rounds waves share SIMDs and the lane kernel wins
-    // (measured 40,960 pieces split 1.62 vs lane 2.33 TB/s; 32,768 split 2.50 vs lane 1.87).
+    // Twin (two lanes per piece, 2-wave workgroups over 32 pieces, 60 KiB of LDS: two per CU) while every
+    // wave has a SIMD to itself: <= 2 workgroups per CU, i.e. 16,384 pieces on 256 CUs (cfg2 1,419 vs split
+    // 1,326 GB/s; +5-6 % at 4,096-12,800 pieces, profiles/r02/sweep_twin.log).  Then split (schedule offload)
+    // while every split pair (64 pieces, 2 waves) has SIMDs to itself: <= 32,768 pieces.  Beyond that rounds
+    // waves share SIMDs and the lane kernel wins (measured 40,960 pieces split 1.62 vs lane 2.33 TB/s; 32,768
+    // split 2.50 vs lane 1.87).
+    const uint64_t last = c->P - 1;
+    const bool short_last = last >= c->first && last < c->first + c->count && piece_len(c, last) != c->L;
+    const uint64_t n_main = c->count - (short_last ? 1 : 0);
+    const uint64_t twin_wgs = (n_main + 31) / 32 + (short_last ? 1 : 0);   // as tv_launch_verify
+    if (c->split_pairs != 2 && twin_wgs <= 2 * (uint64_t)c->cus) return TV_KERNEL_TWIN;
     return c->count <= 32768 ? TV_KERNEL_SPLIT : TV_KERNEL_LANE;
 }
 

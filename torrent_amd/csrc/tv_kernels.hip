@@ -440,25 +440,28 @@ __device__ __forceinline__ void finish_twin(const TvPieces& p, bool writer, uint
 
 }  // namespace
 
-template <bool HASH>
-__global__ __launch_bounds__(256) void tv_twin_kernel(TvPieces p) {
+// HALVES = 2: the 4-wave workgroup above (64 pieces); HALVES = 1: one (rounds, helper) pair over 32 pieces per
+// workgroup (2 waves, half the LDS ring used), two workgroups per CU.
+template <bool HASH, int HALVES>
+__global__ __launch_bounds__(128 * HALVES) void tv_twin_kernel(TvPieces p) {
     __shared__ __attribute__((aligned(16))) uint4 ring[kBufs * kRingWords / 4];
+    constexpr uint32_t span = 32u * HALVES;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // 0, 1 = rounds; 2, 3 = helpers
-    const uint32_t half = wave & 1u;                                           // pieces 32*half .. +31
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // < HALVES: rounds; else helpers
+    const uint32_t half = HALVES == 2 ? (wave & 1u) : 0u;                       // pieces 32*half .. +31
     // main workgroups cover [0, n_main); a short last piece gets one workgroup after them (every lane)
-    const bool last_grp = blockIdx.x >= (p.n_main + 63u) / 64u;
-    const uint32_t wg0 = last_grp ? p.last_idx : blockIdx.x * 64u;
+    const bool last_grp = blockIdx.x >= (p.n_main + span - 1) / span;
+    const uint32_t wg0 = last_grp ? p.last_idx : blockIdx.x * span;
     const uint32_t j = last_grp ? p.last_idx : wg0 + half * 32u + (lane >> 1);
     const uint32_t jj = last_grp ? p.last_idx : (j < p.n_main ? j : p.n_main - 1);
-    const WaveGeom g = last_grp ? wave_geom_flags(p, true, true) : wave_geom(p, wg0, 64);
+    const WaveGeom g = last_grp ? wave_geom_flags(p, true, true) : wave_geom(p, wg0, span);
     const uint64_t len = lane_len(p, jj);
     const uint32_t nb = (uint32_t)nblocks(len);
     const uint8_t* piece = p.data + (uint64_t)jj * p.stride - p.data_off;
     const uint32_t b0 = g.fast_begin, end = g.end, fast_end = g.fast_end;
     const uint32_t lds_lane = (uint32_t)(uintptr_t)(void*)ring + half * 1024u + lane * 16u;
 
-    if (wave >= 2) {
+    if (wave >= HALVES) {
         // ---------------- helper waves (as split_group's helper, twin layout) ----------------
         const uint32_t psel = (lane & 1u) ? 0x07060504u : 0x03020100u;
         uint32_t b = b0;
@@ -755,9 +758,18 @@ hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_
             else hipLaunchKernelGGL((tv_split_kernel<false, 2>), dim3(grid), dim3(256), 0, s, p);
         }
     } else if (kernel == TV_KERNEL_TWIN) {
-        const unsigned grid = (p.n_main + 63) / 64 + (p.n_main < p.n ? 1 : 0);
-        if (hash) hipLaunchKernelGGL(tv_twin_kernel<true>, dim3(grid), dim3(256), 0, s, p);
-        else hipLaunchKernelGGL(tv_twin_kernel<false>, dim3(grid), dim3(256), 0, s, p);
+        // split_pairs: (rounds, helper) pairs per workgroup: 1 (auto) = 2-wave workgroups over 32 pieces, two
+        // per CU; 2 = the 4-wave workgroup over 64 pieces, whose 4-wave barrier couples more jitter (cfg2
+        // 1,419 vs 1,358 GB/s, profiles/r02/sweep_twin.log)
+        if (split_pairs != 2) {
+            const unsigned grid = (p.n_main + 31) / 32 + (p.n_main < p.n ? 1 : 0);
+            if (hash) hipLaunchKernelGGL((tv_twin_kernel<true, 1>), dim3(grid), dim3(128), 0, s, p);
+            else hipLaunchKernelGGL((tv_twin_kernel<false, 1>), dim3(grid), dim3(128), 0, s, p);
+        } else {
+            const unsigned grid = (p.n_main + 63) / 64 + (p.n_main < p.n ? 1 : 0);
+            if (hash) hipLaunchKernelGGL((tv_twin_kernel<true, 2>), dim3(grid), dim3(256), 0, s, p);
+            else hipLaunchKernelGGL((tv_twin_kernel<false, 2>), dim3(grid), dim3(256), 0, s, p);
+        }
     } else {
         const unsigned waves = (p.n_main + 63) / 64 + (p.n_main < p.n ? 1 : 0);
         const unsigned grid = (waves + 3) / 4;
