@@ -14,7 +14,8 @@ for grp in "FETCH_SIZE" \
            "TCC_EA0_RDREQ_DRAM_sum TCC_HIT_sum TCC_MISS_sum" \
            "SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
            "SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_LDS" \
-           "TA_BUSY_avr TA_BUSY_max SQ_INST_CYCLES_VMEM"; do
+           "TA_BUSY_avr TA_BUSY_max SQ_INST_CYCLES_VMEM" \
+           ${PMC_EXTRA:+"$PMC_EXTRA"}; do
   i=$((i+1))
   timeout -k 10 200 rocprofv3 --pmc $grp --output-format csv -d "$OUT/p$i" -o run -- \
       python3 bench.py --workload $W --kernel $K --steps 2 --warmup 1 --no-cpu-baseline --no-saturating --no-cfg4 --e2e-steps 0 > "$OUT/p$i.json" 2> "$OUT/p$i.err" || { echo "PASS $i FAILED: $grp"; tail -5 "$OUT/p$i.err"; exit 1; }
