@@ -299,6 +299,9 @@ TWIN_READ_BYTES = 2048
 TWIN_WAITS = tuple(int(x) for x in os.environ.get("TV_GEN_TWIN_WAITS", "0-5").split("-"))   # reads waited for, in pairs
 TWIN_PRE = os.environ.get("TV_GEN_TWIN_PRE", "1") == "1"   # loop: issue the next block's reads after round 79
 TWIN_NONOP = os.environ.get("TV_GEN_TWIN_NONOP", "1") == "1"  # loop: 4-byte instructions paired without s_nop
+# loop: when the next block's reads are issued -- "end": all 10 after round 79; "mid": 0-4 after the round-40
+# wait, 5-9 after round 79; "spread": read k after round 8k+7 (each as soon as its registers are consumed)
+TWIN_ISSUE = os.environ.get("TV_GEN_TWIN_ISSUE", "mid")   # mid: +1.8 % at cfg2 over end, spread -2 % (profiles/r02/twin_ab.jsonl.log)
 
 
 def gen_twin(off_base: int = 0, reads_next: int | None = None, lead: bool = False):
@@ -306,13 +309,20 @@ def gen_twin(off_base: int = 0, reads_next: int | None = None, lead: bool = Fals
     after round 79 issue the 10 reads of the block whose buffer is at that offset (the loop body).
     Operands as gen_lds: r0-4 (out), t0-1 (tmp), h0-4 (in), addr (this lane's LDS byte address)."""
     ins = [("ds_read_b128", k, off_base + k * TWIN_READ_BYTES) for k in range(10)] if lead else []
+    issue = TWIN_ISSUE if reads_next is not None else "end"
+    assert issue == "end" or TWIN_WAITS == (0, 5)
     R = Regs()
     for t in range(80):
         k, b = t // 8, t % 2
+        if issue == "spread" and t % 8 == 0 and t > 0:
+            ins.append(("ds_read_b128", k - 1, reads_next + (k - 1) * TWIN_READ_BYTES))
         if t % 8 == 0 and k in TWIN_WAITS:
             nxt = [x for x in TWIN_WAITS if x > k]
-            ins.append(("s_waitcnt_lgkm", 10 - nxt[0] if nxt else 0))   # reads k .. next wait - 1 retired
+            # reads k .. (next wait - 1) retired; "spread" has the next block's first 5 behind them at round 40
+            ins.append(("s_waitcnt_lgkm", 5 if issue == "spread" and k == 5 else (10 - nxt[0] if nxt else 0)))
             ins.append(("s_nop",))
+            if issue == "mid" and k == 5:
+                ins += [("ds_read_b128", q, reads_next + q * TWIN_READ_BYTES) for q in range(5)]
         A, B, C, D, E = roles(t)
         e_src = R.rd(E)
         ins.append(("v_add_u32_dpp", R.wr(E), ring_reg(k, (t % 8) // 2), e_src, b))
@@ -323,7 +333,8 @@ def gen_twin(off_base: int = 0, reads_next: int | None = None, lead: bool = Fals
         ins.append(("v_add3_u32", R.rd(E), R.rd(E), "t0", "t1"))
     assert R.cur == [f"r{i}" for i in range(5)]
     if reads_next is not None:
-        ins += [("ds_read_b128", k, reads_next + k * TWIN_READ_BYTES) for k in range(10)]
+        first = {"end": 0, "mid": 5, "spread": 9}[issue]
+        ins += [("ds_read_b128", k, reads_next + k * TWIN_READ_BYTES) for k in range(first, 10)]
     return ins
 
 
