@@ -244,6 +244,9 @@ int tv_host_unregister(void *ptr);
                                     Takes effect at the next tv_set_layout */
 #define TV_OPT_DEBUG_REBOUNCE 11 /* tests: 1 = bounce ring-resident sources through the ring again (the staging
                                     path that once raced); slot leases must keep it exact.  Default 0 */
+#define TV_OPT_TWIN_PACK 12      /* twin kernel with fewer workgroups than 2 per CU: 1 = launch it on a stream
+                                    CU-masked to ceil(workgroups / 2) CUs, two workgroups on each; 0 = spread
+                                    over every CU.  Default 0 */
 int tv_set_option(tv_ctx *ctx, int key, int64_t value);
 int tv_get_option(tv_ctx *ctx, int key, int64_t *value);
 

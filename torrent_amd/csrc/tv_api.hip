@@ -150,6 +150,9 @@ struct tv_ctx {
     int file_threads = 16;                   // tv_stage_files: reader threads
     bool resident = true;                    // TV_OPT_RESIDENT
     bool debug_rebounce = false;             // TV_OPT_DEBUG_REBOUNCE
+    bool twin_pack = false;                  // TV_OPT_TWIN_PACK
+    hipStream_t pack_stream = nullptr;       // twin launches CU-masked to pack_cus CUs (TV_OPT_TWIN_PACK)
+    int pack_cus = 0;
 
     // allocation capacities (tv_set_layout reuses what fits)
     uint64_t cap_payload = 0;   // bytes of d_payload
@@ -443,6 +446,29 @@ TvMixShape mix_shape(const tv_ctx* c) {
 // CU-masked streams, forked after everything queued on c->stream and joined back into it; the queue's error
 // word is copied to h_qerr for check_queue after the call's final sync.
 int launch_resident(tv_ctx* c, const TvPieces& p, int kernel, bool hash) {
+    if (kernel == TV_KERNEL_TWIN && c->twin_pack && (c->split_pairs < 2 || c->split_pairs > 5)) {
+        // 2-wave twin workgroups, 60 KiB of LDS each: at most two per CU.  Fewer than 2 x CUs of them: mask
+        // the launch to ceil(wgs / 2) CUs so that every busy CU holds two (TV_OPT_TWIN_PACK).
+        const uint64_t wgs = (p.n_main + 31) / 32 + (p.n_main < p.n ? 1 : 0);
+        const int k = (int)std::min<uint64_t>((uint64_t)c->cus, (wgs + 1) / 2);
+        if (k < c->cus) {
+            if (c->pack_cus != k) {
+                if (c->pack_stream) TV_HIP(c, hipStreamDestroy(c->pack_stream));
+                c->pack_stream = nullptr;
+                c->pack_cus = 0;
+                std::vector<uint32_t> m((c->cus + 31) / 32, 0);
+                for (int i = 0; i < k; i++) m[i / 32] |= 1u << (i % 32);
+                TV_HIP(c, hipExtStreamCreateWithCUMask(&c->pack_stream, (uint32_t)m.size(), m.data()));
+                c->pack_cus = k;
+            }
+            TV_HIP(c, hipEventRecord(c->ev_mix0, c->stream));
+            TV_HIP(c, hipStreamWaitEvent(c->pack_stream, c->ev_mix0, 0));
+            TV_HIP(c, tv_launch_verify(p, kernel, hash, c->pack_stream, c->split_pairs));
+            TV_HIP(c, hipEventRecord(c->ev_mix1, c->pack_stream));
+            TV_HIP(c, hipStreamWaitEvent(c->stream, c->ev_mix1, 0));
+            return TV_OK;
+        }
+    }
     if (kernel != TV_KERNEL_MIX) {
         TV_HIP(c, tv_launch_verify(p, kernel, hash, c->stream, c->split_pairs));
         return TV_OK;
@@ -1045,6 +1071,7 @@ void tv_destroy(tv_ctx* c) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->copy_stream2) (void)hipStreamDestroy(c->copy_stream2);
+    if (c->pack_stream) (void)hipStreamDestroy(c->pack_stream);
     if (c->mix_pairs) (void)hipStreamDestroy(c->mix_pairs);
     if (c->mix_lanes) (void)hipStreamDestroy(c->mix_lanes);
     delete c;
@@ -1084,7 +1111,7 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
             c->stream_chunk = (uint64_t)value;
             return TV_OK;
         case TV_OPT_SPLIT_PAIRS:
-            if (value < 0 || value > 2) return fail(c, TV_ERR_ARG, "TV_OPT_SPLIT_PAIRS must be 0, 1 or 2");
+            if (value < 0 || value > 5) return fail(c, TV_ERR_ARG, "TV_OPT_SPLIT_PAIRS must be 0 .. 5");
             c->split_pairs = (int)value;
             return TV_OK;
         case TV_OPT_FILE_DIRECT:
@@ -1115,6 +1142,10 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
             if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_DEBUG_REBOUNCE must be 0 or 1");
             c->debug_rebounce = value != 0;
             return TV_OK;
+        case TV_OPT_TWIN_PACK:
+            if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_TWIN_PACK must be 0 or 1");
+            c->twin_pack = value != 0;
+            return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
@@ -1134,6 +1165,7 @@ int tv_get_option(tv_ctx* c, int key, int64_t* value) {
         case TV_OPT_FILE_CONCURRENT: *value = c->file_concurrent ? 1 : 0; return TV_OK;
         case TV_OPT_RESIDENT: *value = c->resident ? 1 : 0; return TV_OK;
         case TV_OPT_DEBUG_REBOUNCE: *value = c->debug_rebounce ? 1 : 0; return TV_OK;
+        case TV_OPT_TWIN_PACK: *value = c->twin_pack ? 1 : 0; return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
