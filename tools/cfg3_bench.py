@@ -38,7 +38,7 @@ with _context(0) as ctx:
     k_ms, _ = ctx.last_timing()
     kern = ctx.last_kernel()[0]
 print(f"verify_payload (host -> HBM stage + verify): best {best * 1e3:.1f} ms = {info.length / best / 1e9:.2f} GB/s; "
-      f"verify kernel {k_ms:.2f} ms = {info.length / k_ms / 1e6:.1f} GB/s ({ {1: 'lane', 2: 'split'}[kern] }); exact", flush=True)
+      f"verify kernel {k_ms:.2f} ms = {info.length / k_ms / 1e6:.1f} GB/s ({ {1: 'lane', 2: 'split', 3: 'mix', 4: 'twin'}[kern] }); exact", flush=True)
 
 t0 = time.perf_counter()
 for path, data in lay["disk_files"]().items():
