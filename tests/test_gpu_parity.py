@@ -76,14 +76,17 @@ def test_kernels_agree_and_avail_mask(native, oracle):
     avail = bytearray(rng.randrange(256) for _ in range((P + 7) // 8))
     expect = oracle.verify_linear(payload, total, L, pieces, bytes(avail))
     outs = []
-    for k, pairs in [(k, 0) for k in KERNELS] + [(2, 2), (4, 2)]:   # + 2 pairs per workgroup: split, twin
+    # + 2 pairs per workgroup (split, twin), the twin SIMD-placement probe shapes, and twin CU-packed
+    for k, pairs, pack in [(k, 0, 0) for k in KERNELS] + [(2, 2, 0), (4, 2, 0), (4, 3, 0), (4, 4, 0), (4, 5, 0),
+                                                          (4, 0, 1)]:
         with _ctx(native, k) as ctx:
             ctx.set_option(native.TV_OPT_SPLIT_PAIRS, pairs)
+            ctx.set_option(native.TV_OPT_TWIN_PACK, pack)
             ctx.set_layout(total, L, P)
             ctx.set_digests(pieces)
             ctx.stage(0, payload)
             outs.append(ctx.verify(bytes(avail)))
-            assert ctx.hash() == pieces, (k, pairs)
+            assert ctx.hash() == pieces, (k, pairs, pack)
     assert all(o == expect for o in outs)
 
 

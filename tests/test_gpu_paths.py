@@ -264,9 +264,9 @@ def test_read_back_and_pinned_stream(native, oracle):
         assert ctx.last_kernel()[1] == 4  # 64 KiB pieces in 16 KiB columns
 
 
-@pytest.mark.parametrize("kernel", [0, 1, 2])
+@pytest.mark.parametrize("kernel", [0, 1, 2, 4])
 def test_verify_list_matches_oracle(native, oracle, kernel):
-    """tv_verify_list (auto / lane list kernel / split kernel in list mode): arbitrary order,
+    """tv_verify_list (auto / lane list kernel / split and twin kernels in list mode): arbitrary order,
     duplicates, the short last piece in any lane position, corrupted pieces, a shard offset;
     > 256 entries (several workgroups)."""
     import random
@@ -286,7 +286,7 @@ def test_verify_list_matches_oracle(native, oracle, kernel):
         lst = [rng.randrange(8, P) for _ in range(600)] + [P - 1, P - 1, 8, 9]
         rng.shuffle(lst)
         got = ctx.verify_list(lst)
-        assert ctx.last_kernel()[0] == (kernel or 2)
+        assert ctx.last_kernel()[0] == (kernel or 4)
         assert list(got) == [0 if i in bad else 1 for i in lst]
         with pytest.raises(native.NativeError):
             ctx.verify_list([0])          # outside the shard

@@ -1694,11 +1694,14 @@ int tv_verify_list(tv_ctx* c, const uint64_t* pieces, uint64_t n, uint8_t* ok_ou
     p.idx = c->d_list;
     p.out_bytes = c->d_list_out;
     TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
-    // split (rounds + helper pair, ~30 % shorter serial stream per block) while one pair per CU
-    // suffices, like choose_kernel; the lane list kernel for longer lists
-    const int kernel = (c->kernel_opt == TV_KERNEL_LANE || c->kernel_opt == TV_KERNEL_SPLIT)
+    // twin (two lanes per piece) while its 2-wave workgroups fit two per CU, then split (rounds + helper pair,
+    // ~30 % shorter serial stream per block than lane) while one pair per CU suffices, like choose_kernel;
+    // the lane list kernel for longer lists
+    const int kernel = (c->kernel_opt == TV_KERNEL_LANE || c->kernel_opt == TV_KERNEL_SPLIT ||
+                        c->kernel_opt == TV_KERNEL_TWIN)
                            ? c->kernel_opt
-                           : (m <= 256 * 64 ? TV_KERNEL_SPLIT : TV_KERNEL_LANE);
+                           : (m <= 64 * (uint64_t)c->cus ? TV_KERNEL_TWIN
+                                                         : (m <= 256 * 64 ? TV_KERNEL_SPLIT : TV_KERNEL_LANE));
     TV_HIP(c, tv_launch_verify_list(p, kernel, c->stream));
     TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
     TV_HIP(c, hipMemcpyAsync(reordered ? ok_launch.data() : ok_out, c->d_list_out, m, hipMemcpyDeviceToHost, c->stream));

@@ -451,7 +451,10 @@ constexpr int kTwinHalf[6][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 1, 0, 1}, {0, 0
 constexpr int kTwinWaves[6] = {0, 2, 4, 4, 4, 4};
 constexpr int kTwinPairs[6] = {0, 1, 2, 2, 1, 1};
 
-template <bool HASH, int SHAPE>
+// LIST = incremental verify (tv_verify_list): pair i of a wave verifies shard piece idx[j]; geometry from the
+// wave's ballots (the rounds and helper waves of a half see the same 32 pieces, so their ballots agree); the
+// host puts the short last piece's entries in 64-entry groups of their own.
+template <bool HASH, int SHAPE, bool LIST = false>
 __global__ __launch_bounds__(64 * kTwinWaves[SHAPE]) void tv_twin_kernel(TvPieces p) {
     __shared__ __attribute__((aligned(16))) uint4 ring[kBufs * kRingWords / 4];
     constexpr uint32_t span = 32u * kTwinPairs[SHAPE];
@@ -460,11 +463,15 @@ __global__ __launch_bounds__(64 * kTwinWaves[SHAPE]) void tv_twin_kernel(TvPiece
     const int role = kTwinRole[SHAPE][wave];                  // 0 rounds, 1 helper, 2 idle
     const uint32_t half = kTwinHalf[SHAPE][wave];             // pieces 32*half .. +31
     // main workgroups cover [0, n_main); a short last piece gets one workgroup after them (every lane)
-    const bool last_grp = blockIdx.x >= (p.n_main + span - 1) / span;
+    const uint32_t nlim = LIST ? p.n : p.n_main;
+    const bool last_grp = !LIST && blockIdx.x >= (nlim + span - 1) / span;
     const uint32_t wg0 = last_grp ? p.last_idx : blockIdx.x * span;
     const uint32_t j = last_grp ? p.last_idx : wg0 + half * 32u + (lane >> 1);
-    const uint32_t jj = last_grp ? p.last_idx : (j < p.n_main ? j : p.n_main - 1);
-    const WaveGeom g = last_grp ? wave_geom_flags(p, true, true) : wave_geom(p, wg0, span);
+    const uint32_t jl = last_grp ? p.last_idx : (j < nlim ? j : nlim - 1);
+    const uint32_t jj = LIST ? p.idx[jl] : jl;
+    const bool is_last = jj == p.last_idx;
+    const WaveGeom g = LIST ? wave_geom_flags(p, __ballot(is_last) != 0, __ballot(!is_last) == 0)
+                            : last_grp ? wave_geom_flags(p, true, true) : wave_geom(p, wg0, span);
     const uint64_t len = lane_len(p, jj);
     const uint32_t nb = (uint32_t)nblocks(len);
     const uint8_t* piece = p.data + (uint64_t)jj * p.stride - p.data_off;
@@ -497,7 +504,8 @@ __global__ __launch_bounds__(64 * kTwinWaves[SHAPE]) void tv_twin_kernel(TvPiece
 
     // ---------------- rounds waves ----------------
     uint32_t h[5];
-    start_state(p, jj, h);
+    if (LIST) sha1_iv(h);
+    else start_state(p, jj, h);
     const uint32_t ring_base = lds_lane;
     lds_barrier();
     uint32_t b = b0;
@@ -516,6 +524,15 @@ __global__ __launch_bounds__(64 * kTwinWaves[SHAPE]) void tv_twin_kernel(TvPiece
             for (int i = 0; i < 5; i++) h[i] += r[i];
         }
         lds_barrier();
+    }
+    if (LIST) {
+        if (j < p.n && (lane & 1u) == 0) {
+            bool ok = p.avail64 ? avail_bit(p.avail64, jj) : true;
+#pragma unroll
+            for (int k = 0; k < 5; k++) ok &= (h[k] == p.digests[(uint64_t)k * p.dcount + jj]);
+            p.out_bytes[j] = ok ? 1 : 0;
+        }
+        return;
     }
     const bool writer = last_grp ? (wave == 0 && lane == 0) : ((lane & 1u) == 0 && j < p.n_main);
     finish_twin<HASH>(p, writer, jj, wg0 + half * 32u, h, last_grp);
@@ -825,7 +842,9 @@ hipError_t tv_launch_mix(const TvPieces& p, const TvQueue& q, bool hash, hipStre
 
 hipError_t tv_launch_verify_list(const TvPieces& p, int kernel, hipStream_t s) {
     if (p.n == 0) return hipSuccess;
-    if (kernel == TV_KERNEL_SPLIT)
+    if (kernel == TV_KERNEL_TWIN)
+        hipLaunchKernelGGL((tv_twin_kernel<false, 1, true>), dim3((p.n + 31) / 32), dim3(128), 0, s, p);
+    else if (kernel == TV_KERNEL_SPLIT)
         hipLaunchKernelGGL((tv_split_kernel<false, 1, true>), dim3((p.n + 63) / 64), dim3(128), 0, s, p);
     else
         hipLaunchKernelGGL(tv_list_kernel, dim3((p.n + 255) / 256), dim3(256), 0, s, p);
