@@ -75,7 +75,7 @@ def main():
                 assert ok == b"\x01" * n
             out[f"verify_list_flush_{n}"] = {"wall_ms_median": med(ws[2:]), "kernel_ms_median": med(ks[2:]),
                                              "call_ms_median": med(ts[2:]),
-                                             "kernel": {1: "lane list", 2: "split list"}[ctx.last_kernel()[0]]}
+                                             "kernel": {1: "lane list", 2: "split list", 4: "twin list"}[ctx.last_kernel()[0]]}
     print(json.dumps(out, indent=1))
 
 
