@@ -250,6 +250,9 @@ def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: b
         pieces[20 * first:20 * (first + count)] = d2
         ctx.set_digests(bytes(pieces))
         expect = _expected_bits(count, bad)
+        # torch's device context is created by the first _device_sync (~1.5 s, GPU idle): do that before the
+        # warmup, so the warmup -- not the first timed steps -- brings the shader clock back up
+        _device_sync(ctx, device)
         for _ in range(warmup):
             ctx.verify()
         _device_sync(ctx, device)
