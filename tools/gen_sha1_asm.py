@@ -231,6 +231,72 @@ def gen_rounds_block(off_cur: int, off_next: int):
     return ins
 
 
+SPLIT_MID = os.environ.get("TV_GEN_SPLIT_MID", "0") == "1"   # split rounds loop: next block's reads mid-block
+
+
+def gen_split_mid_block(off_cur: int, off_next: int):
+    """One block of the split rounds wave with the NEXT block's first 10 K+W quads issued inside this block (the
+    twin kernel's mid-block issue, tools/gen_sha1_asm.py gen_twin): on entry quads 0-9 of this block are in
+    flight; it issues quads 10-14 at its start, quad 15+g after consuming quad g (g < 5), the next block's quads
+    0-4 after round 39 and 5-9 after round 59 (each batch behind a wait that keeps at most 15 reads in flight,
+    lgkmcnt's 4-bit limit), then h += r and the barrier.  Ring of 20 register quads, slot = quad.  The helper's
+    protocol makes it safe: the next block was written before the barrier that started this one."""
+    assert RING_QUADS == 20
+    ins, order = [], [("cur", q) for q in range(10)]   # reads in flight on entry, oldest first
+    retired = 0                                         # reads of `order` known retired
+
+    def wait_for(key):
+        nonlocal retired
+        i = order.index(key)
+        if i >= retired:
+            ins.append(("s_waitcnt_lgkm", min(15, len(order) - 1 - i)))
+            retired = i + 1
+
+    def issue(tag, q):
+        assert len(order) - retired < 15 or True
+        ins.append(("ds_read_b128", q, (off_cur if tag == "cur" else off_next) + q * 1024))
+        order.append((tag, q))
+
+    for q in range(10, 15):
+        issue("cur", q)
+    R = Regs()
+    for t in range(80):
+        g = t // 4
+        if t % 4 == 0:
+            wait_for(("cur", g))
+        A, B, C, D, E = roles(t)
+        e_src = R.rd(E)
+        ins.append(("v_add_u32", R.wr(E), ring_reg(g, t % 4), e_src))
+        ins.append(("v_alignbit_b32", "t0", R.rd(A), R.rd(A), 27))
+        ins.append(_fop(t, "t1", R.rd(B), R.rd(C), R.rd(D)))
+        b_src = R.rd(B)
+        ins.append(("v_alignbit_b32", R.wr(B), b_src, b_src, 2))
+        ins.append(("v_add3_u32", R.rd(E), R.rd(E), "t0", "t1"))
+        if t % 4 == 3 and g < 5:
+            issue("cur", 15 + g)
+        if t == 39:
+            wait_for(("cur", 14))
+            for q in range(5):
+                issue("next", q)
+        if t == 59:
+            wait_for(("cur", 19))
+            for q in range(5, 10):
+                issue("next", q)
+    assert R.cur == [f"r{i}" for i in range(5)]
+    # at most 15 in flight at every issue, counting every read not yet waited for as in flight
+    inflight, waited = 0, 0
+    for op in ins:
+        if op[0] == "ds_read_b128":
+            inflight += 1
+            assert inflight <= 15, "more than 15 LDS reads in flight"
+        elif op[0] == "s_waitcnt_lgkm":
+            inflight = min(inflight, op[1])
+    for i in range(5):
+        ins.append(("v_add_u32", f"h{i}", f"h{i}", f"r{i}"))
+    ins.append(("s_barrier",))
+    return ins
+
+
 def rounds_prologue(off: int = 0):
     """Issue quads 0 .. READ_AHEAD-1 of the first block (buffer at off)."""
     return [("ds_read_b128", g, off + g * 1024) for g in range(READ_AHEAD)]
@@ -347,9 +413,15 @@ def rounds_loop_text() -> str:
     L = ["s_waitcnt lgkmcnt(0)", "s_mov_b32 %[cnt], %[nsteps]"]
     if PIPELINED:
         L.extend(_emit_lines(rounds_prologue(0)))
+    if SPLIT_MID:
+        L.extend(_emit_lines([("ds_read_b128", q, q * 1024) for q in range(10)]))
     L.append("L_rloop_%=:")
     for k in range(LDS_BUFS):
-        if PIPELINED:
+        if SPLIT_MID:
+            if LOOP_ALIGN:
+                L.append(".p2align 3")
+            L.extend(_emit_lines(gen_split_mid_block(k * RING_BYTES, ((k + 1) % LDS_BUFS) * RING_BYTES)))
+        elif PIPELINED:
             L.extend(_emit_lines(gen_rounds_block(k * RING_BYTES, ((k + 1) % LDS_BUFS) * RING_BYTES)))
         else:   # per-block stream: its 15 reads issued at the block's start
             if LOOP_ALIGN:
@@ -735,6 +807,39 @@ def check_rounds_stream(blocks, h):
     return [regs[f"h{i}"] for i in range(5)]
 
 
+def check_split_mid_stream(blocks, h):
+    """The split rounds loop with SPLIT_MID (gen_split_mid_block), checked like check_rounds_stream."""
+    lds = {}
+
+    def put(m, words, in_flight=frozenset()):
+        base = (m % LDS_BUFS) * RING_BYTES
+        for t in range(80):
+            a = base + 1024 * (t // 4) + 4 * (t % 4)
+            assert a not in in_flight, f"LDS {a} rewritten while a ds_read of it is in flight"
+            lds[a] = words[t]
+
+    kws = [_kw_words(b) for b in blocks]
+    put(0, kws[0])
+    if len(blocks) > 1:
+        put(1, kws[1])
+    state = {"k": 0}
+
+    def on_barrier(in_flight):
+        k = state["k"]
+        state["k"] = k + 1
+        put(k + 3, [0xDEADBEEF ^ t for t in range(80)], in_flight)
+        if k + 2 < len(blocks):
+            put(k + 2, kws[k + 2], in_flight)
+
+    regs = {f"h{i}": h[i] for i in range(5)}
+    ins = [("ds_read_b128", q, q * 1024) for q in range(10)]
+    for k in range(len(blocks)):
+        ins += gen_split_mid_block((k % LDS_BUFS) * RING_BYTES, ((k + 1) % LDS_BUFS) * RING_BYTES)
+    ins.append(("s_waitcnt_lgkm", 0))
+    emulate(ins, regs, lds, 0, on_barrier=on_barrier)
+    return [regs[f"h{i}"] for i in range(5)]
+
+
 def check_twin_stream(blocks, h):
     """The TWIN rounds loop over consecutive blocks as twin_rounds_loop_text lays it out, for the lane pair
     of piece 0, against the helper protocol (as check_rounds_stream): at the barrier ending block k, block
@@ -794,6 +899,13 @@ def self_check():
         h0 = [0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0]
         h = check_rounds_stream([padded[i:i + 64] for i in range(0, len(padded), 64)], h0)
         assert struct.pack(">5I", *h) == hashlib.sha1(msg).digest(), ("stream", n)
+    # the split rounds loop with the next block's reads issued mid-block, 1 .. 7 blocks
+    for n in ([0, 55, 64, 119, 200, 310, 400] if SPLIT_MID else []):
+        msg = bytes(rng.randrange(256) for _ in range(n))
+        padded = msg + b"\x80" + b"\0" * ((55 - n) % 64) + struct.pack(">Q", 8 * n)
+        h0 = [0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0]
+        h = check_split_mid_stream([padded[i:i + 64] for i in range(0, len(padded), 64)], h0)
+        assert struct.pack(">5I", *h) == hashlib.sha1(msg).digest(), ("split mid stream", n)
     # the TWIN rounds loop over 1 .. 7 consecutive blocks (every buffer phase)
     for n in ([0, 55, 64, 119, 200, 310, 400] if LDS_BUFS == 3 and not K_IN_ROUNDS else []):
         msg = bytes(rng.randrange(256) for _ in range(n))
