@@ -247,6 +247,10 @@ int tv_host_unregister(void *ptr);
 #define TV_OPT_TWIN_PACK 12      /* twin kernel with fewer workgroups than 2 per CU: 1 = launch it on a stream
                                     CU-masked to ceil(workgroups / 2) CUs, two workgroups on each; 0 = spread
                                     over every CU.  Default 0 */
+#define TV_OPT_TWIN_FILL 13      /* twin kernel with fewer workgroups than 2 per CU (resident calls): 1 (default) =
+                                    add companion workgroups up to 2 per CU that re-hash main workgroups' pieces
+                                    on the otherwise idle SIMDs and discard the result (a CU running one twin
+                                    workgroup is ~4.5 % slower per block than one running two); 0 = real grid only */
 int tv_set_option(tv_ctx *ctx, int key, int64_t value);
 int tv_get_option(tv_ctx *ctx, int key, int64_t *value);
 

@@ -76,12 +76,14 @@ def test_kernels_agree_and_avail_mask(native, oracle):
     avail = bytearray(rng.randrange(256) for _ in range((P + 7) // 8))
     expect = oracle.verify_linear(payload, total, L, pieces, bytes(avail))
     outs = []
-    # + 2 pairs per workgroup (split, twin), the twin SIMD-placement probe shapes, and twin CU-packed
+    # + 2 pairs per workgroup (split, twin), the twin SIMD-placement probe shapes, twin CU-packed (pack 1) and
+    # twin without companion workgroups (pack 2)
     for k, pairs, pack in [(k, 0, 0) for k in KERNELS] + [(2, 2, 0), (4, 2, 0), (4, 3, 0), (4, 4, 0), (4, 5, 0),
-                                                          (4, 0, 1)]:
+                                                          (4, 0, 1), (4, 0, 2)]:
         with _ctx(native, k) as ctx:
             ctx.set_option(native.TV_OPT_SPLIT_PAIRS, pairs)
-            ctx.set_option(native.TV_OPT_TWIN_PACK, pack)
+            ctx.set_option(native.TV_OPT_TWIN_PACK, pack & 1)
+            ctx.set_option(native.TV_OPT_TWIN_FILL, 0 if pack == 2 else 1)
             ctx.set_layout(total, L, P)
             ctx.set_digests(pieces)
             ctx.stage(0, payload)

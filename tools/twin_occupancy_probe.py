@@ -11,17 +11,19 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from torrent_amd import _native as N  # noqa: E402
 
 L = 1 << 20
-for P in (4096, 6400, 8192, 12800, 16384):
+for P in [int(x) for x in os.environ.get("PROBE_PS", "4096,6400,8192,12800,16384").split(",")]:
     ctx = N.Context(0)
     ctx.set_layout(L * P, L, P)
     ctx.fill_synthetic(2)
-    shapes = [("split1", 2, 1, 0), ("twin1", 4, 1, 0), ("twin1_packed", 4, 1, 1)]
+    # pack: bit 0 = TV_OPT_TWIN_PACK, bit 1 = TV_OPT_TWIN_FILL (companion workgroups)
+    shapes = [("split1", 2, 1, 0), ("twin1", 4, 1, 0), ("twin1_packed", 4, 1, 1), ("twin1_companions", 4, 1, 2)]
     if os.environ.get("PROBE_SHAPES"):
         shapes += [("twin2", 4, 2, 0), ("twin_r02_h13", 4, 3, 0), ("twin_r0_h2", 4, 4, 0), ("twin_r0_h1", 4, 5, 0)]
     for name, k, pairs, pack in shapes:
         ctx.set_option(N.TV_OPT_KERNEL, k)
         ctx.set_option(N.TV_OPT_SPLIT_PAIRS, pairs)
-        ctx.set_option(N.TV_OPT_TWIN_PACK, pack)
+        ctx.set_option(N.TV_OPT_TWIN_PACK, pack & 1)
+        ctx.set_option(N.TV_OPT_TWIN_FILL, pack >> 1)
         ms = []
         for _ in range(6):
             ctx.hash()

@@ -32,6 +32,7 @@ TV_OPT_FILE_CONCURRENT = 9
 TV_OPT_RESIDENT = 10
 TV_OPT_DEBUG_REBOUNCE = 11
 TV_OPT_TWIN_PACK = 12
+TV_OPT_TWIN_FILL = 13
 
 TV_STREAM_RING_SLOTS = 3
 TV_STREAM_SLOT_BYTES = 64 << 20

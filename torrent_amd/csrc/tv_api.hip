@@ -151,6 +151,7 @@ struct tv_ctx {
     bool resident = true;                    // TV_OPT_RESIDENT
     bool debug_rebounce = false;             // TV_OPT_DEBUG_REBOUNCE
     bool twin_pack = false;                  // TV_OPT_TWIN_PACK
+    bool twin_fill = true;                   // TV_OPT_TWIN_FILL
     hipStream_t pack_stream = nullptr;       // twin launches CU-masked to pack_cus CUs (TV_OPT_TWIN_PACK)
     int pack_cus = 0;
 
@@ -445,7 +446,14 @@ TvMixShape mix_shape(const tv_ctx* c) {
 // One launch over the resident shard with the chosen kernel.  MIX: the pair and lane workers run on the two
 // CU-masked streams, forked after everything queued on c->stream and joined back into it; the queue's error
 // word is copied to h_qerr for check_queue after the call's final sync.
-int launch_resident(tv_ctx* c, const TvPieces& p, int kernel, bool hash) {
+int launch_resident(tv_ctx* c, const TvPieces& p_in, int kernel, bool hash) {
+    TvPieces p = p_in;
+    // A CU running ONE 2-wave twin workgroup spends ~80 more shader cycles per block than one running two
+    // (PMC GRBM_GUI_ACTIVE: 1,806 vs 1,727; sleeping fillers do not help, working ones do: DESIGN.md section 5).
+    // With fewer real workgroups than 2 per CU, companions fill the grid to 2 x CUs: they re-hash main
+    // workgroups' pieces on otherwise idle SIMDs and discard the result (TV_OPT_TWIN_FILL, default on).
+    if (kernel == TV_KERNEL_TWIN && c->twin_fill && !c->twin_pack && (c->split_pairs < 2 || c->split_pairs > 5))
+        p.fill_to = 2u * (uint32_t)c->cus;
     if (kernel == TV_KERNEL_TWIN && c->twin_pack && (c->split_pairs < 2 || c->split_pairs > 5)) {
         // 2-wave twin workgroups, 60 KiB of LDS each: at most two per CU.  Fewer than 2 x CUs of them: mask
         // the launch to ceil(wgs / 2) CUs so that every busy CU holds two (TV_OPT_TWIN_PACK).
@@ -1146,6 +1154,10 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
             if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_TWIN_PACK must be 0 or 1");
             c->twin_pack = value != 0;
             return TV_OK;
+        case TV_OPT_TWIN_FILL:
+            if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_TWIN_FILL must be 0 or 1");
+            c->twin_fill = value != 0;
+            return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
@@ -1166,6 +1178,7 @@ int tv_get_option(tv_ctx* c, int key, int64_t* value) {
         case TV_OPT_RESIDENT: *value = c->resident ? 1 : 0; return TV_OK;
         case TV_OPT_DEBUG_REBOUNCE: *value = c->debug_rebounce ? 1 : 0; return TV_OK;
         case TV_OPT_TWIN_PACK: *value = c->twin_pack ? 1 : 0; return TV_OK;
+        case TV_OPT_TWIN_FILL: *value = c->twin_fill ? 1 : 0; return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }

@@ -32,6 +32,9 @@ struct TvPieces {
     uint32_t* out_digests;   // hash mode: [5][dcount]
     const uint32_t* idx;     // list mode: lane j verifies shard piece idx[j] (data = base + idx*stride)
     uint8_t* out_bytes;      // list mode: out_bytes[j] = 1 iff piece idx[j] matches
+    uint32_t fill_to;        // twin: launch this many workgroups in all (0 = the real grid only); the ones past
+                             // the real grid are COMPANIONS that re-hash a main workgroup's pieces and discard
+                             // the result (TV_OPT_TWIN_FILL)
 };
 
 // Work queue of the MIX launch (tv_launch_mix): a FIFO of ready 64-piece groups.  A unit is segment s

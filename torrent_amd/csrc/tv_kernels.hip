@@ -464,8 +464,13 @@ __global__ __launch_bounds__(64 * kTwinWaves[SHAPE]) void tv_twin_kernel(TvPiece
     const uint32_t half = kTwinHalf[SHAPE][wave];             // pieces 32*half .. +31
     // main workgroups cover [0, n_main); a short last piece gets one workgroup after them (every lane)
     const uint32_t nlim = LIST ? p.n : p.n_main;
-    const bool last_grp = !LIST && blockIdx.x >= (nlim + span - 1) / span;
-    const uint32_t wg0 = last_grp ? p.last_idx : blockIdx.x * span;
+    // companions (blockIdx past the real grid, TV_OPT_TWIN_FILL): re-hash main workgroup (blockIdx - real) % main
+    const uint32_t nmain_wgs = (nlim + span - 1) / span;
+    const uint32_t real_wgs = nmain_wgs + (!LIST && p.n_main < p.n ? 1u : 0u);
+    const bool companion = blockIdx.x >= real_wgs;
+    const uint32_t wgi = companion ? (blockIdx.x - real_wgs) % nmain_wgs : blockIdx.x;
+    const bool last_grp = !LIST && wgi >= nmain_wgs;
+    const uint32_t wg0 = last_grp ? p.last_idx : wgi * span;
     const uint32_t j = last_grp ? p.last_idx : wg0 + half * 32u + (lane >> 1);
     const uint32_t jl = last_grp ? p.last_idx : (j < nlim ? j : nlim - 1);
     const uint32_t jj = LIST ? p.idx[jl] : jl;
@@ -525,6 +530,7 @@ __global__ __launch_bounds__(64 * kTwinWaves[SHAPE]) void tv_twin_kernel(TvPiece
         }
         lds_barrier();
     }
+    if (companion) return;   // its digests duplicate a main workgroup's: nothing to write
     if (LIST) {
         if (j < p.n && (lane & 1u) == 0) {
             bool ok = p.avail64 ? avail_bit(p.avail64, jj) : true;
@@ -795,7 +801,8 @@ hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_
         // (3-5: SIMD-placement probe shapes, see tv_twin_kernel)
         const int shape = split_pairs >= 2 && split_pairs <= 5 ? split_pairs : 1;
         const unsigned span = 32u * kTwinPairs[shape];
-        const unsigned grid = (p.n_main + span - 1) / span + (p.n_main < p.n ? 1 : 0);
+        const unsigned real = (p.n_main + span - 1) / span + (p.n_main < p.n ? 1 : 0);
+        const unsigned grid = (p.fill_to > real && p.n_main > 0) ? p.fill_to : real;
         const dim3 blk(64 * kTwinWaves[shape]);
 #define TV_TWIN_LAUNCH(S)                                                              \
     if (hash) hipLaunchKernelGGL((tv_twin_kernel<true, S>), dim3(grid), blk, 0, s, p); \
