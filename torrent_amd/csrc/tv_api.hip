@@ -1715,6 +1715,7 @@ int tv_verify_list(tv_ctx* c, const uint64_t* pieces, uint64_t n, uint8_t* ok_ou
                            ? c->kernel_opt
                            : (m <= 64 * (uint64_t)c->cus ? TV_KERNEL_TWIN
                                                          : (m <= 256 * 64 ? TV_KERNEL_SPLIT : TV_KERNEL_LANE));
+    if (kernel == TV_KERNEL_TWIN && c->twin_fill) p.fill_to = 2u * (uint32_t)c->cus;   // companions, as resident
     TV_HIP(c, tv_launch_verify_list(p, kernel, c->stream));
     TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
     TV_HIP(c, hipMemcpyAsync(reordered ? ok_launch.data() : ok_out, c->d_list_out, m, hipMemcpyDeviceToHost, c->stream));

@@ -849,8 +849,10 @@ hipError_t tv_launch_mix(const TvPieces& p, const TvQueue& q, bool hash, hipStre
 
 hipError_t tv_launch_verify_list(const TvPieces& p, int kernel, hipStream_t s) {
     if (p.n == 0) return hipSuccess;
-    if (kernel == TV_KERNEL_TWIN)
-        hipLaunchKernelGGL((tv_twin_kernel<false, 1, true>), dim3((p.n + 31) / 32), dim3(128), 0, s, p);
+    if (kernel == TV_KERNEL_TWIN) {
+        const unsigned real = (p.n + 31) / 32;
+        hipLaunchKernelGGL((tv_twin_kernel<false, 1, true>), dim3(p.fill_to > real ? p.fill_to : real), dim3(128), 0, s, p);
+    }
     else if (kernel == TV_KERNEL_SPLIT)
         hipLaunchKernelGGL((tv_split_kernel<false, 1, true>), dim3((p.n + 63) / 64), dim3(128), 0, s, p);
     else
