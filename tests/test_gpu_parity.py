@@ -254,3 +254,33 @@ def test_geometry_that_overflows_offsets_is_rejected(native):
         ctx.set_digests(hashlib.sha1(bytes(64)).digest() + hashlib.sha1(bytes(36)).digest())
         ctx.stage(0, bytes(100))
         assert ctx.verify() == b"\xc0"
+
+
+@pytest.mark.parametrize("L,P,last", [(4096, 1, 4096), (4096, 1, 1000), (8192, 40, 8192), (8192, 40, 77),
+                                      (65536, 33, 65536), (1 << 20, 20, 5)])
+def test_twin_companions_exact(native, oracle, L, P, last):
+    """Twin companion workgroups (TV_OPT_TWIN_FILL, default on) re-hash main pieces and must write nothing:
+    with a handful of pieces nearly the whole 2 x CUs grid is companions.  Verify (corrupted digests, an
+    availability mask), creation mode and the list path equal the oracle with companions on and off."""
+    total = L * (P - 1) + last
+    payload = oracle.synth_fill(P * 7 + 1, 0, total)
+    good = oracle.hash_pieces(payload, total, L, P)
+    pieces = bytearray(good)
+    bad = {0, P // 2, P - 1}
+    for i in bad:
+        pieces[20 * i + 3] ^= 0x20
+    avail = bytearray(b"\xff" * ((P + 7) // 8))
+    if P > 2:
+        avail[0] &= 0xBF                       # piece 1 unavailable
+    expect = oracle.verify_linear(payload, total, L, bytes(pieces), bytes(avail))
+    lst = [P - 1, 0, P // 2, P - 1] + list(range(P))
+    for fill in (1, 0):
+        with _ctx(native, 4) as ctx:
+            ctx.set_option(native.TV_OPT_TWIN_FILL, fill)
+            ctx.set_layout(total, L, P)
+            ctx.stage(0, payload)
+            assert ctx.hash() == good, fill
+            ctx.set_digests(bytes(pieces))
+            assert ctx.verify(bytes(avail)) == expect, fill
+            assert ctx.last_kernel()[0] == 4
+            assert list(ctx.verify_list(lst)) == [0 if i in bad else 1 for i in lst], fill
