@@ -59,7 +59,7 @@ def test_asm_generator_emulator():
                                  {"TV_GEN_PIPE": "1", "TV_GEN_RING": "20"}, {"TV_GEN_BUFS": "2"},
                                  {"TV_GEN_TWIN_ISSUE": "end"}, {"TV_GEN_TWIN_ISSUE": "spread"},
                                  {"TV_GEN_TWIN_PRE": "0"}, {"TV_GEN_TWIN_WAITS": "0-2-4-6-8", "TV_GEN_TWIN_ISSUE": "end"},
-                                 {"TV_GEN_SPLIT_MID": "1", "TV_GEN_RING": "20"}])
+                                 {"TV_GEN_SPLIT_MID": "1", "TV_GEN_RING": "20"}, {"TV_GEN_SPLIT_PRE": "1"}])
 def test_asm_generator_emulator_options(env):
     """The generator's A/B options (tools/build_variants.py) still emit streams that compute SHA-1."""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_sha1_asm.py"), "--check"],

@@ -232,6 +232,24 @@ def gen_rounds_block(off_cur: int, off_next: int):
 
 
 SPLIT_MID = os.environ.get("TV_GEN_SPLIT_MID", "0") == "1"   # split rounds loop: next block's reads mid-block
+SPLIT_PRE = os.environ.get("TV_GEN_SPLIT_PRE", "0") == "1"   # split rounds loop: next block's 15 reads after round 79
+
+
+def gen_split_pre_block(off_cur: int, off_next: int):
+    """One block of the split rounds wave whose first READ_AHEAD reads were issued by the previous block: the
+    shipped per-block stream (gen_lds) without its leading reads, followed after round 79 by the next block's
+    leading reads (so they land during h += r and the barrier instead of after it), then h += r and the
+    barrier.  Safe for the same reason as the twin kernel's: the next block was written before the barrier
+    that started this one, and its buffer is not rewritten before the barrier that ends it."""
+    body = gen_lds(off_cur, lead_wait=False)
+    lead = [op for op in body[:READ_AHEAD] if op[0] == "ds_read_b128"]
+    assert len(lead) == READ_AHEAD
+    ins = body[READ_AHEAD:]
+    ins += [("ds_read_b128", q, off_next + q * 1024) for q in range(READ_AHEAD)]
+    for i in range(5):
+        ins.append(("v_add_u32", f"h{i}", f"h{i}", f"r{i}"))
+    ins.append(("s_barrier",))
+    return ins
 
 
 def gen_split_mid_block(off_cur: int, off_next: int):
@@ -415,9 +433,15 @@ def rounds_loop_text() -> str:
         L.extend(_emit_lines(rounds_prologue(0)))
     if SPLIT_MID:
         L.extend(_emit_lines([("ds_read_b128", q, q * 1024) for q in range(10)]))
+    if SPLIT_PRE:
+        L.extend(_emit_lines([("ds_read_b128", q, q * 1024) for q in range(READ_AHEAD)]))
     L.append("L_rloop_%=:")
     for k in range(LDS_BUFS):
-        if SPLIT_MID:
+        if SPLIT_PRE:
+            if LOOP_ALIGN:
+                L.append(".p2align 3")
+            L.extend(_emit_lines(gen_split_pre_block(k * RING_BYTES, ((k + 1) % LDS_BUFS) * RING_BYTES)))
+        elif SPLIT_MID:
             if LOOP_ALIGN:
                 L.append(".p2align 3")
             L.extend(_emit_lines(gen_split_mid_block(k * RING_BYTES, ((k + 1) % LDS_BUFS) * RING_BYTES)))
@@ -807,8 +831,9 @@ def check_rounds_stream(blocks, h):
     return [regs[f"h{i}"] for i in range(5)]
 
 
-def check_split_mid_stream(blocks, h):
-    """The split rounds loop with SPLIT_MID (gen_split_mid_block), checked like check_rounds_stream."""
+def check_split_mid_stream(blocks, h, pre: bool = False):
+    """The split rounds loop with SPLIT_MID (gen_split_mid_block) or SPLIT_PRE (gen_split_pre_block, pre=True),
+    checked like check_rounds_stream."""
     lds = {}
 
     def put(m, words, in_flight=frozenset()):
@@ -832,9 +857,10 @@ def check_split_mid_stream(blocks, h):
             put(k + 2, kws[k + 2], in_flight)
 
     regs = {f"h{i}": h[i] for i in range(5)}
-    ins = [("ds_read_b128", q, q * 1024) for q in range(10)]
+    ins = [("ds_read_b128", q, q * 1024) for q in range(READ_AHEAD if pre else 10)]
     for k in range(len(blocks)):
-        ins += gen_split_mid_block((k % LDS_BUFS) * RING_BYTES, ((k + 1) % LDS_BUFS) * RING_BYTES)
+        ins += (gen_split_pre_block if pre else gen_split_mid_block)((k % LDS_BUFS) * RING_BYTES,
+                                                                     ((k + 1) % LDS_BUFS) * RING_BYTES)
     ins.append(("s_waitcnt_lgkm", 0))
     emulate(ins, regs, lds, 0, on_barrier=on_barrier)
     return [regs[f"h{i}"] for i in range(5)]
@@ -906,6 +932,12 @@ def self_check():
         h0 = [0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0]
         h = check_split_mid_stream([padded[i:i + 64] for i in range(0, len(padded), 64)], h0)
         assert struct.pack(">5I", *h) == hashlib.sha1(msg).digest(), ("split mid stream", n)
+    for n in ([0, 55, 64, 119, 200, 310, 400] if SPLIT_PRE else []):
+        msg = bytes(rng.randrange(256) for _ in range(n))
+        padded = msg + b"\x80" + b"\0" * ((55 - n) % 64) + struct.pack(">Q", 8 * n)
+        h0 = [0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0]
+        h = check_split_mid_stream([padded[i:i + 64] for i in range(0, len(padded), 64)], h0, pre=True)
+        assert struct.pack(">5I", *h) == hashlib.sha1(msg).digest(), ("split pre stream", n)
     # the TWIN rounds loop over 1 .. 7 consecutive blocks (every buffer phase)
     for n in ([0, 55, 64, 119, 200, 310, 400] if LDS_BUFS == 3 and not K_IN_ROUNDS else []):
         msg = bytes(rng.randrange(256) for _ in range(n))
