@@ -45,6 +45,7 @@ import os
 import sys
 import time
 
+T_START = time.perf_counter()
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -72,23 +73,17 @@ VALU_DERIVATION = (
 # SHA-1 round mix (tools/ubench_fetch.hip, profiles/r01/ubench_fetch.log); the wave64 cadence is 4.
 LONE_WAVE_CYC = 4.07
 SERIAL_INSTR = {1: 613, 2: 405, 4: 405}  # per-block serial VALU stream: lane kernel / split and twin rounds waves
-KERNEL_NAMES = {1: "lane", 2: "split", 3: "mix", 4: "twin"}
-MIX_PAIRS, MIX_LANE_WAVES = 256, 512   # MIX workers on a 256-CU MI355X (tv_api.hip launch_resident)
+KERNEL_NAMES = {1: "lane", 2: "split", 4: "twin"}
 
 
 def piece_ceiling(kernel: int, count: int) -> float:
-    """GB/s if every piece (64-piece group for MIX) advanced at its serial SHA-1 stream's lone-wave rate:
-    lane / split = count pieces at that kernel's rate; MIX = its fastest ceil(count/64) workers busy
-    (split pairs first, then lane waves), 64 pieces each.  Capped at R_valu."""
-    rate = {k: 64 * CLOCK_HZ / (v * LONE_WAVE_CYC) for k, v in SERIAL_INSTR.items()}   # B/s per piece
-    if kernel == 3:
-        groups = (count + 63) // 64
-        pg = min(groups, MIX_PAIRS)
-        lg = min(groups - pg, MIX_LANE_WAVES)
-        bps = 64 * (pg * rate[2] + lg * rate[1])
-    else:
-        bps = count * rate.get(kernel, rate[1])
-    return min(VALU_PEAK_GBPS, bps / 1e9)
+    """GB/s if every piece advanced at its kernel's serial SHA-1 stream's lone-wave rate (count pieces x
+    64 B per block / (serial instructions per block x 4.07 cycles)), capped at R_valu."""
+    rate = 64 * CLOCK_HZ / (SERIAL_INSTR.get(kernel, SERIAL_INSTR[1]) * LONE_WAVE_CYC)   # B/s per piece
+    return min(VALU_PEAK_GBPS, count * rate / 1e9)
+
+# one page-locked 1 GiB host -> HBM copy on a gpurun box (tools/pcie_probe.py, profiles/r02/pcie_ceiling.json)
+PCIE_H2D_GBPS = 57.6
 
 MiB = 1 << 20
 WORKLOADS = {
@@ -146,6 +141,39 @@ def _sum(dist, x: float) -> float:
     t = torch.tensor([x], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
+
+
+def pick_device(local_rank: int, visible: int) -> int:
+    """HIP device of a rank: LOCAL_RANK when the rank sees every GPU of the node, 0 when the launcher made
+    one GPU visible per rank (HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES), and ranks wrap round when there
+    are more ranks than GPUs (rehearsals on one GPU)."""
+    return local_rank % max(1, visible)
+
+
+def _pci_bus_id(device: int) -> str:
+    """PCI bus id of HIP device `device` (hipDeviceGetPCIBusId), to tell physical GPUs apart across ranks."""
+    import ctypes
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        buf = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, device) == 0:
+            return buf.value.decode()
+    except OSError:
+        pass
+    return f"unknown-{device}"
+
+
+def rank_placement(dist, ws: int, rank: int, local: int, device: int, ndev: int) -> list:
+    """Every rank's (rank, LOCAL_RANK, device, PCI bus id, visibility variables), gathered on all ranks."""
+    me = {"rank": rank, "local_rank": local, "device": device, "visible_devices": ndev,
+          "pci_bus_id": _pci_bus_id(device), "host": os.uname().nodename,
+          **{k: os.environ.get(k) for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+             if os.environ.get(k) is not None}}
+    if dist is None:
+        return [me]
+    out = [None] * ws
+    dist.all_gather_object(out, me)
+    return out
 
 
 def _device_sync(ctx, device: int) -> None:
@@ -237,7 +265,9 @@ def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: b
         P = n * ws
         first, count = rank * n, n
     total = L * P
+    t_leg = time.perf_counter()
     dig, gt_s = ground_truth(seed, total, L, P, first, count, threads)
+    t_setup = time.perf_counter()
     ctx = _native.Context(device)
     try:
         ctx.set_option(_native.TV_OPT_KERNEL, kernel_opt)
@@ -253,9 +283,11 @@ def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: b
         # torch's device context is created by the first _device_sync (~1.5 s, GPU idle): do that before the
         # warmup, so the warmup -- not the first timed steps -- brings the shader clock back up
         _device_sync(ctx, device)
+        t_warm = time.perf_counter()
         for _ in range(warmup):
             ctx.verify()
         _device_sync(ctx, device)
+        t_warm_end = time.perf_counter()
         _barrier(dist)
         kernel_ms = []
         t0 = time.perf_counter()
@@ -268,6 +300,7 @@ def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: b
         kernel, _ = ctx.last_kernel()
     finally:
         ctx.close()
+    t_end = time.perf_counter()
     elapsed = _max(dist, t1 - t0)
     exact = _sum(dist, 1.0 if (bf == expect and creation_exact) else 0.0) == ws
     avg = sum(kernel_ms) / len(kernel_ms)
@@ -284,14 +317,39 @@ def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: b
            "piece_parallelism_ceiling": round(ceiling, 1), "frac_of_piece_ceiling": round(achieved / ceiling, 4),
            "frac_of_valu_peak": round(achieved / VALU_PEAK_GBPS, 4),
            "bitfield_exact": exact, "expected": "oracle digests of every piece, 1 % corrupted",
-           "ground_truth_s": round(gt_s, 2), "ground_truth_threads": threads}
+           "ground_truth_s": round(gt_s, 2), "ground_truth_threads": threads,
+           "phase_s": {"ground_truth": round(gt_s, 2), "setup": round(t_warm - t_setup, 2),
+                       "warmup": round(t_warm_end - t_warm, 3), "timed": round(t1 - t0, 3),
+                       "leg": round(t_end - t_leg, 2), "leg_max_over_ranks": round(_max(dist, t_end - t_leg), 2),
+                       "note": "this rank's wall seconds; setup = context, layout, device fill, creation-mode "
+                               "hash check and digests"}}
     if want_digests:
         out["_digests"] = dig
         out["_first"] = first
     return out
 
 
-def e2e_cfg5(dist, ws: int, rank: int, device: int, steps: int, threads: int, shard_digests=None) -> dict:
+def producer_rate(ctx, seed: int, seconds: float = 1.0) -> float:
+    """GB/s of the host generator alone (tv_stream_fill_synthetic into one lent ring slot, no DMA), on the
+    ctx's TV_OPT_FILE_THREADS threads.  Every rank runs it at the same time, so the sum over ranks is what
+    the node's CPU share generates with this per-rank budget."""
+    ctx.stream_begin()
+    try:
+        req = ctx.stream_next()
+        nbytes = req.rows * req.width
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            ctx.stream_fill_synthetic(req, seed)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                return nbytes * reps / el / 1e9
+    finally:
+        ctx.stream_abort()
+
+
+def e2e_cfg5(dist, ws: int, rank: int, device: int, steps: int, threads: int, shard_digests=None,
+             share: dict = None, physical_gpus: int = 1) -> dict:
     """BASELINE configs[4]: the cfg4 torrent (200 GiB, 51,200 x 4 MiB) streamed host -> PCIe -> HBM through the
     library's bounded pinned ring (tv_stream_*), each rank its shard_ranges shard, no resident payload."""
     from oracle import oracle as O
@@ -315,12 +373,19 @@ def e2e_cfg5(dist, ws: int, rank: int, device: int, steps: int, threads: int, sh
     try:
         ctx.set_option(_native.TV_OPT_RESIDENT, 0)
         ctx.set_option(_native.TV_OPT_STREAM_CHUNK, E2E_CHUNK)
-        # generator threads: half the allowed cores generate at ~100 GB/s (tools/pcie_probe.py), and more
-        # do not raise the streamed rate (tools/e2e_gen_probe.py: 8, 12, 16 threads all 40.5 GB/s)
-        gen_threads = max(1, threads // 2)
+        # generator threads: 8 of a 16-core share generate at ~100 GB/s (tools/pcie_probe.py) and more do not
+        # raise the streamed rate (tools/e2e_gen_probe.py); a rank with a smaller share (several ranks on one
+        # node's quota) generates on all of its cores -- the calling thread is one of them and otherwise only
+        # waits for slots
+        gen_threads = max(1, min(8, threads))
         ctx.set_option(_native.TV_OPT_FILE_THREADS, gen_threads)
         ctx.set_layout(total, L, P, first, count)
         ctx.set_digests(bytes(pieces))
+        t_gen = time.perf_counter()
+        _barrier(dist)
+        gen_alone = producer_rate(ctx, seed)
+        gen_alone_all = _sum(dist, gen_alone)
+        t_gen_end = time.perf_counter()
 
         phase = {"next_s": 0.0, "fill_commit_s": 0.0}
 
@@ -359,7 +424,9 @@ def e2e_cfg5(dist, ws: int, rank: int, device: int, steps: int, threads: int, sh
             return bf, reqs, _max(dist, t1 - t0)
 
         phase.update(next_s=0.0, fill_commit_s=0.0)
+        t_g0 = time.perf_counter()
         bf, reqs, el = timed(gen)
+        t_g1 = time.perf_counter()
         gen_phase = {k: round(v, 3) for k, v in phase.items()}
         ok = _sum(dist, 1.0 if bf == expect else 0.0) == ws
         out["generated"] = {"value": round(total * steps / el / 1e9, 2), "ms_per_step": round(el * 1e3 / steps, 1),
@@ -367,6 +434,7 @@ def e2e_cfg5(dist, ws: int, rank: int, device: int, steps: int, threads: int, sh
                             "producer": f"host generator (tv_stream_fill_synthetic, {gen_threads} threads) writing "
                                         "the bytes into the ring slots inside the timed region"}
         # pinned_pool: the torrent is a 1 GiB page-locked pool of 256 pieces repeated; rows DMA'd from it
+        t_p0 = time.perf_counter()
         pool = _native.PinnedBuffer(POOL_PIECES * L)
         pool.mv[:] = O.synth_fill(seed + 100, 0, POOL_PIECES * L)
         pool_dig = O.hash_pieces(pool.mv, POOL_PIECES * L, L, POOL_PIECES, threads=threads)
@@ -381,16 +449,34 @@ def e2e_cfg5(dist, ws: int, rank: int, device: int, steps: int, threads: int, sh
             ctx.stream_commit_from(req, pool.mv, L, ((req.piece - first) % POOL_PIECES) * L + req.offset)
 
         phase.update(next_s=0.0, fill_commit_s=0.0)
+        t_p1 = time.perf_counter()
         bf, reqs, el = timed(from_pool)
+        t_p2 = time.perf_counter()
         pool_phase = {k: round(v, 3) for k, v in phase.items()}
         ok = _sum(dist, 1.0 if bf == _expected_bits(count, bad2) else 0.0) == ws
         out["pinned_pool"] = {"value": round(total * steps / el / 1e9, 2), "ms_per_step": round(el * 1e3 / steps, 1),
                               "bitfield_exact": ok, "requests_per_step": reqs, "rank0_phase_s": pool_phase,
                               "producer": f"rows DMA'd straight from a {POOL_PIECES * L >> 20} MiB page-locked pool "
                                           f"(piece first+j = pool piece j % {POOL_PIECES})"}
-        out["value"] = out["generated"]["value"]
         out["bitfield_exact"] = out["generated"]["bitfield_exact"] and ok
         out["kernel"] = KERNEL_NAMES.get(ctx.last_kernel()[0], "?")
+        # what bounds the generated figure: the producer (the node's generator rate at this per-rank thread
+        # budget, measured alone on every rank at once) or the PCIe links (PCIE_H2D_GBPS per physical GPU)
+        pcie_all = PCIE_H2D_GBPS * physical_gpus
+        out["producer"] = {
+            "producer_threads": gen_threads, "threads_per_rank": threads,
+            "cpu_quota_per_rank": (share or {}).get("cores_per_rank"),
+            "cpu_share_node": (share or {}).get("cores"), "cpu_share_source": (share or {}).get("source"),
+            "generator_alone_gbps_rank0": round(gen_alone, 1), "generator_alone_gbps_all_ranks": round(gen_alone_all, 1),
+            "pcie_h2d_gbps_all_gpus": round(pcie_all, 1), "physical_gpus": physical_gpus,
+            "bound": "producer" if gen_alone_all < pcie_all else "pcie",
+            "note": "generated is bounded by min(generator_alone_gbps_all_ranks, pcie_h2d_gbps_all_gpus); "
+                    "pinned_pool takes the producer out (the PCIe path alone)"}
+        # the leg's value is the PCIe path (pinned_pool); the generated figure stays beside it with its bound
+        out["value"] = out["pinned_pool"]["value"]
+        out["value_is"] = "pinned_pool (PCIe path); generated beside it, bounded as producer.bound says"
+        out["phase_s"] = {"producer_probe": round(t_gen_end - t_gen, 2), "generated": round(t_g1 - t_g0, 2),
+                          "pool_setup": round(t_p1 - t_p0, 2), "pinned_pool": round(t_p2 - t_p1, 2)}
     finally:
         if pool is not None:
             pool.close()
@@ -447,7 +533,7 @@ def main() -> int:
     sc = ap.add_mutually_exclusive_group()
     sc.add_argument("--strong", action="store_true", help="the workload's pieces are the WHOLE torrent, sharded")
     sc.add_argument("--weak", action="store_true", help="the workload's pieces are per GPU")
-    ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 lane, 2 split, 3 mix, 4 twin")
+    ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 lane, 2 split, 4 twin")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-saturating", action="store_true", help="skip the piece_saturated leg (N=1)")
@@ -457,10 +543,14 @@ def main() -> int:
     a = ap.parse_args()
 
     dist, rank, ws, local = _dist()
-    device = local % max(1, _native.device_count())
+    ndev = _native.device_count()
+    device = pick_device(local, ndev)
     share = cpu_share()
     # the node's allowed cores are shared by the ranks on it (ground truth, generators)
     threads = max(1, share["cores"] // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1"))))
+    share["cores_per_rank"] = threads
+    placement = rank_placement(dist, ws, rank, local, device, ndev)
+    physical = len({p["pci_bus_id"] for p in placement}) if placement else 1
     workload = a.workload or ("cfg2" if ws == 1 else "cfg4")
     strong = a.strong or (not a.weak and a.workload is None and ws > 1)
 
@@ -480,7 +570,8 @@ def main() -> int:
         legs["cfg2_weak"] = resident_leg(dist, ws, rank, device, "cfg2", False, a.leg_steps, 1, a.kernel, threads)
     if a.e2e_steps > 0:
         try:
-            legs["e2e_cfg5"] = e2e_cfg5(dist, ws, rank, device, a.e2e_steps, threads, cfg4_digests)
+            legs["e2e_cfg5"] = e2e_cfg5(dist, ws, rank, device, a.e2e_steps, threads, cfg4_digests, share,
+                                        physical)
         except Exception as exc:  # reported, never fatal to the bench line
             legs["e2e_cfg5"] = {"skipped": f"{type(exc).__name__}: {exc}"}
     cfg4_digests = None
@@ -541,6 +632,14 @@ def main() -> int:
         out.update(legs)
         if ws == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(share, a.cpu_seconds)
+        out["placement"] = {"ranks": placement, "physical_gpus": physical, "visible_devices": ndev,
+                            "rule": "device = LOCAL_RANK % (devices visible to the rank): LOCAL_RANK on a node "
+                                    "where every rank sees all GPUs, 0 where the launcher gives each rank one "
+                                    "(HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES)"}
+        if physical < ws:
+            out["placement"]["note"] = (f"{ws} ranks share {physical} physical GPU(s): a rehearsal of the N = {ws} "
+                                        "path, not a scaling point")
+        out["wall_s"] = round(time.perf_counter() - T_START, 1)
         print(json.dumps(out), flush=True)
     ok = main_leg["bitfield_exact"] and all(v.get("bitfield_exact", True) for v in legs.values())
     if dist is not None:
