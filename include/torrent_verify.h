@@ -107,7 +107,11 @@ int tv_stage(tv_ctx *ctx, uint64_t linear_offset, const uint8_t *src, uint64_t l
  * anything is staged (a read error part-way also returns TV_ERR_IO): the host marks the pieces the
  * segment touches unreadable, as Storage.get returning null makes them.  Unlike
  * fsStorage.get (which opens with create: true, storage.ts:28-32,158) a missing file is never created.
- * len == 0 succeeds without opening the file.
+ * The file is opened as fsStorage.get opens it (read + write, storage.ts:28-32,158): a file this process
+ * may not write returns TV_ERR_IO, as Deno.open fails there.  len == 0 reads nothing but still checks the
+ * open: TV_ERR_IO when fsStorage.get's open would fail (a directory, a missing parent directory, no
+ * permission); a missing file in a writable directory succeeds (fsStorage.get would create it; this call
+ * creates nothing).
  */
 int tv_stage_file(tv_ctx *ctx, const char *path, uint64_t file_offset, uint64_t linear_offset, uint64_t len);
 
@@ -122,10 +126,15 @@ int tv_stage_file(tv_ctx *ctx, const char *path, uint64_t file_offset, uint64_t 
  *     them (open, pread, close; default 16), and each run of linear-contiguous segments is one DMA.
  *     A slot's DMA overlaps the reads of the next slot. This is the many-small-files case: a
  *     10,000-file torrent is one call, not 10,000.
- * status_out[k] = TV_OK, or TV_ERR_IO when the file is missing, unreadable or shorter than the
- * segment; the host marks the pieces that segment touches unreadable (Storage.get -> null).  The call
- * itself returns TV_OK unless an argument or HIP error occurs; the first I/O failure's message is
- * kept for tv_last_error.  Bytes outside the shard are skipped; zero-length segments succeed.
+ * status_out[k] = TV_OK, or TV_ERR_IO when the file is missing, unreadable, not writable or shorter than
+ * the segment; the host marks the pieces that segment touches unreadable (Storage.get -> null).
+ *   - Zero-length segments belong in the list: Storage.get's walk emits them for a file that ends where a
+ *     piece starts and for a zero-length file inside a piece (storage.ts:109-110), and fsStorage.get still
+ *     opens them (storage.ts:158).  Such a segment reads nothing; its status is TV_ERR_IO exactly when that
+ *     open would fail (tv_stage_file, len == 0), and nothing is created.  Its piece is linear_offsets[k] /
+ *     piece_length.
+ * The call itself returns TV_OK unless an argument or HIP error occurs; the first I/O failure's message is
+ * kept for tv_last_error.  Bytes outside the shard are skipped.
  */
 int tv_stage_files(tv_ctx *ctx, uint64_t n, const char *const *paths, const uint64_t *file_offsets,
                    const uint64_t *linear_offsets, const uint64_t *lens, int32_t *status_out);
@@ -229,7 +238,8 @@ int tv_host_register(void *ptr, uint64_t bytes);
 int tv_host_unregister(void *ptr);
 
 /* Options (tv_set_option keys). */
-#define TV_OPT_KERNEL 1      /* 0 = auto, 1 = lane, 2 = split (schedule offload), 3 = mix (work queue over split pairs + lane waves; resident calls only), 4 = twin (split with two lanes per piece) */
+#define TV_OPT_KERNEL 1      /* 0 = auto, 1 = lane, 2 = split (schedule offload), 4 = twin (split with two lanes per
+                                piece); 3 is unused (it was MIX, a work queue measured slower than lane, removed) */
 #define TV_OPT_STRIDE_PAD 2  /* bytes of padding between resident pieces (default 256) */
 #define TV_OPT_STREAM_CHUNK 3 /* tv_verify_host: bytes of each piece per streamed column chunk */
 #define TV_OPT_SPLIT_PAIRS 4  /* split and twin kernels: (rounds, helper) wave pairs per workgroup, 0 = auto, 1, 2 */
@@ -250,7 +260,10 @@ int tv_host_unregister(void *ptr);
 #define TV_OPT_TWIN_FILL 13      /* twin kernel with fewer workgroups than 2 per CU (resident calls): 1 (default) =
                                     add companion workgroups up to 2 per CU that re-hash main workgroups' pieces
                                     on the otherwise idle SIMDs and discard the result (a CU running one twin
-                                    workgroup is ~4.5 % slower per block than one running two); 0 = real grid only */
+                                    workgroup is ~4.5 % slower per block than one running two); 0 = real grid only.
+                                    tv_verify_list adds them only to a list of >= 32 x CUs pieces (one workgroup
+                                    per CU): a shorter flush would fill the GPU with copies of a few pieces;
+                                    2 = add them to every list too (measurement only) */
 int tv_set_option(tv_ctx *ctx, int key, int64_t value);
 int tv_get_option(tv_ctx *ctx, int key, int64_t *value);
 
@@ -258,8 +271,20 @@ int tv_get_option(tv_ctx *ctx, int key, int64_t *value);
  * library's compute stream: kernel_ms = the verify kernel(s) only; total_ms = whole call. */
 int tv_last_timing(tv_ctx *ctx, double *kernel_ms, double *total_ms);
 
-/* Kernel chosen for the last call (1 lane, 2 split, 3 mix) and launches it used. */
+/* Kernel chosen for the last call (1 lane, 2 split, 4 twin) and launches it used. */
 int tv_last_kernel(tv_ctx *ctx, int *kernel, int *launches);
+
+/* Resource counters of a ctx (tv_get_counter keys): how often tv_set_layout and the calls after it had to
+ * allocate device memory, and what the ctx holds now.  A run of small layouts on a ctx (verify_piece, list
+ * flushes) must not reallocate, and a small call must not evict a bulk call's payload; these make both
+ * observable.  No reference counterpart (the reference holds no device memory). */
+#define TV_COUNTER_PAYLOAD_ALLOCS 1 /* resident payload allocations since tv_create */
+#define TV_COUNTER_DEVICE_ALLOCS 2  /* device allocations of every kind since tv_create */
+#define TV_COUNTER_PAYLOAD_BYTES 3  /* bytes of the resident payload allocation held now (0: none) */
+#define TV_COUNTER_DEVICE_BYTES 4   /* bytes of device memory held now */
+#define TV_COUNTER_LAST_WORKGROUPS 5 /* workgroups of the last verify / hash / list launch (companion
+                                        workgroups of TV_OPT_TWIN_FILL included) */
+int tv_get_counter(tv_ctx *ctx, int key, uint64_t *value);
 
 /* Block until all work queued by the ctx is complete. */
 int tv_synchronize(tv_ctx *ctx);

@@ -157,7 +157,30 @@ static int run_gpu(void) {
         CHECK(tv_stage_file(c, path, 5, 0, 7) == TV_ERR_IO, "short file must be TV_ERR_IO");
         CHECK(tv_last_error(c, msg0, sizeof msg0) > 0 && strstr(msg0, "bytes"), "message: %s", msg0);
         CHECK(tv_stage_file(c, "/nonexistent/tv_file", 0, 0, 7) == TV_ERR_IO, "missing file must be TV_ERR_IO");
-        OK(tv_stage_file(c, "/nonexistent/tv_file", 0, 0, 0), c); /* zero-length read: no file needed */
+        /* zero-length segments still open the path as fsStorage.get does (storage.ts:109-110,158) */
+        CHECK(tv_stage_file(c, "/nonexistent/tv_file", 0, 0, 0) == TV_ERR_IO, "zero-length, missing parent dir");
+        CHECK(tv_stage_file(c, "/tmp", 0, 0, 0) == TV_ERR_IO, "zero-length on a directory must be TV_ERR_IO");
+        char absent[] = "/tmp/tv_abi_consumer_absent_XXXXXX";
+        int afd = mkstemp(absent);
+        if (afd >= 0) { close(afd); unlink(absent); }
+        OK(tv_stage_file(c, absent, 0, 0, 0), c); /* a missing file in a writable directory opens */
+        CHECK(access(absent, F_OK) != 0, "tv_stage_file must not create %s", absent);
+        /* one tv_stage_files call: the data segment, then zero-length segments on piece 2 (a directory),
+           piece 1 (a missing directory) and piece 0 (a missing file in /tmp: fine, not created) */
+        {
+            const char *paths[4] = {path, "/tmp", "/nonexistent/tv_file", absent};
+            const uint64_t fo[4] = {2, 0, 0, 0}, lin[4] = {0, 6, 3, 0}, lens[4] = {7, 0, 0, 0};
+            int32_t st[4] = {9, 9, 9, 9};
+            OK(tv_stage_files(c, 4, paths, fo, lin, lens, st), c);
+            CHECK(st[0] == TV_OK && st[1] == TV_ERR_IO && st[2] == TV_ERR_IO && st[3] == TV_OK,
+                  "stage_files statuses %d %d %d %d", st[0], st[1], st[2], st[3]);
+            CHECK(access(absent, F_OK) != 0, "tv_stage_files must not create %s", absent);
+            uint8_t avail = 0xE0;  /* the host clears piece lin / L of each failed zero-length segment */
+            for (int k = 0; k < 4; k++)
+                if (st[k] == TV_ERR_IO && lens[k] == 0) avail &= (uint8_t)~(0x80u >> (lin[k] / 3));
+            OK(tv_verify(c, &avail, &bf), c);
+            CHECK(bf == 0x80, "stage_files zero-length bitfield %02x, want 80", bf);
+        }
         unlink(path);
     }
 

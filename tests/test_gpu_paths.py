@@ -181,7 +181,7 @@ def test_full_size_cfg2_oracle_ground_truth(native, oracle):
         ctx.fill_synthetic(2)
         assert ctx.hash() == truth
         ctx.set_digests(bytes(d2))
-        for k in (1, 2, 3, 4):
+        for k in (1, 2, 4):
             ctx.set_option(native.TV_OPT_KERNEL, k)
             bf = ctx.verify()
             assert ctx.last_kernel()[0] == k
@@ -199,7 +199,7 @@ def _threads():
 def test_full_size_cfg4_oracle_ground_truth(native, oracle):
     """BASELINE config 4 at its largest single-GPU size: 200 GiB, 51,200 x 4 MiB pieces resident in HBM
     (linear offsets to 214,748,364,800), against the ORACLE's digests of all 51,200 pieces: creation mode
-    equals them; verify with them (1 % corrupted) is exact with the lane, split and MIX kernels; and the 8-GPU
+    equals them; verify with them (1 % corrupted) is exact with the lane, split and twin kernels; and the 8-GPU
     shard geometry of the same torrent (the last shard, pieces [44800, 51200), at linear offsets > 187 GB)
     hashes and verifies to the oracle's slice."""
     from torrent_amd import release_contexts, shard_ranges
@@ -217,7 +217,7 @@ def test_full_size_cfg4_oracle_ground_truth(native, oracle):
         assert ctx.hash() == truth
         assert ctx.last_kernel()[0] == 1      # auto at 51,200 pieces: lane
         ctx.set_digests(bytes(d2))
-        for k in (1, 2, 3, 4):
+        for k in (1, 2, 4):
             ctx.set_option(native.TV_OPT_KERNEL, k)
             bf = ctx.verify()
             assert ctx.last_kernel()[0] == k

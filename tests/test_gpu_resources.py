@@ -1,0 +1,202 @@
+"""GPU tests of the round-3 boundary rules: zero-length segments checked behind the ABI (tv_stage_files),
+allocation reuse and release (tv_set_layout, tv_get_counter), verify_piece's own context, the f1 flush
+policy on the HIP path, and list flushes without companion workgroups."""
+import hashlib
+import os
+import shutil
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+MiB = 1 << 20
+
+
+def _bits(bf, n):
+    return [(bf[i >> 3] >> (7 - (i & 7))) & 1 for i in range(n)]
+
+
+def test_verify_files_zero_length_segments_match_fs_storage(native, tmp_path, monkeypatch):
+    """Storage.get's zero-length segments (storage.ts:109-110: a file ending where a piece starts, a
+    zero-length file inside a piece) go to tv_stage_files, which reports TV_ERR_IO where fsStorage.get's open
+    (storage.ts:158) would fail: a directory in a zero-length file's place, or a zero-length file in a
+    missing directory.  verify_files gives, piece for piece, the bits of Storage(fs_storage).get + SHA-1
+    (run on a copy of the tree: that get creates files), and creates nothing itself."""
+    from torrent_amd import make_info, verify_files
+    from torrent_amd.metainfo import FileInfo
+    from torrent_amd.piece import piece_length
+    from torrent_amd.storage import Storage, fs_storage
+
+    L = 4096
+    names = [("a",), ("z_dir",), ("b",), ("nodir", "z"), ("c",), ("z_missing",), ("d",), ("z_ok",), ("e",)]
+    sizes = [3 * L, 0, 2 * L + 100, 0, L - 100, 0, 2 * L, 0, L + 7]   # a, b end exactly on piece starts
+    payload = bytes((k * 13 + 1) & 0xFF for k in range(sum(sizes)))
+    P = -(-len(payload) // L)
+    digests = bytearray(b"".join(hashlib.sha1(payload[i * L:(i + 1) * L]).digest() for i in range(P)))
+    digests[20 * 5] ^= 1                                          # one corrupted digest too
+    info = make_info(L, bytes(digests), "t", files=[FileInfo(n, list(p)) for n, p in zip(sizes, names)])
+    root = tmp_path / "t0"
+    off = 0
+    for n, p in zip(sizes, names):
+        q = root.joinpath(*p)
+        if p == ("z_dir",):
+            q.mkdir(parents=True)
+        elif p not in (("nodir", "z"), ("z_missing",)):
+            q.parent.mkdir(parents=True, exist_ok=True)
+            q.write_bytes(payload[off:off + n])
+        off += n
+    ref_root = tmp_path / "t1"
+    shutil.copytree(root, ref_root)
+    monkeypatch.chdir(tmp_path)
+    ref = Storage(fs_storage, info, str(ref_root))
+    expect = []
+    for i in range(P):
+        got = ref.get(i * L, piece_length(i, info))
+        expect.append(int(got is not None and hashlib.sha1(got).digest() == bytes(digests[20 * i:20 * i + 20])))
+    assert 0 < sum(expect) < P - 1
+    before = sorted(str(x) for x in root.rglob("*"))
+    for devices in ([0], [0, 0]):
+        assert _bits(verify_files(info, str(root), devices=devices, threads=2), P) == expect, devices
+    assert sorted(str(x) for x in root.rglob("*")) == before     # nothing created
+
+
+def test_streamed_layout_after_a_resident_one_has_no_payload(native):
+    """A layout set with TV_OPT_RESIDENT = 0 after a smaller resident one: the resident calls fail with
+    TV_ERR_STATE (never run on the old, too-small buffer), and the payload is released."""
+    with native.Context(0) as ctx:
+        ctx.set_layout(64 * 1024, 4096, 16)                     # small resident layout
+        ctx.set_digests(bytes(20 * 16))
+        assert ctx.counter(native.TV_COUNTER_PAYLOAD_BYTES) > 0
+        ctx.set_option(native.TV_OPT_RESIDENT, 0)
+        ctx.set_layout(64 * MiB, MiB, 64)                       # larger, streamed-only
+        ctx.set_digests(bytes(20 * 64))
+        assert ctx.counter(native.TV_COUNTER_PAYLOAD_BYTES) == 0
+        for call in (ctx.verify, ctx.hash, lambda: ctx.stage(0, b"x" * 100), lambda: ctx.fill_synthetic(1),
+                     lambda: ctx.read(0, bytearray(100)), lambda: ctx.verify_list([3])):
+            with pytest.raises(native.NativeError) as e:
+                call()
+            assert e.value.code == native.TV_ERR_STATE
+
+
+def test_chunk_buffers_are_released_for_a_resident_layout(native, oracle):
+    """The streamed path's two device chunk buffers are not kept beside a resident payload, and a streamed
+    layout that fits them reuses them."""
+    from torrent_amd import make_info, verify_payload, verify_stream
+    L, P = MiB, 96
+    payload = bytes(oracle.synth_fill(3, 0, L * P))
+    info = make_info(L, oracle.hash_pieces(payload, L * P, L, P), "t", length=L * P)
+    read = lambda off, n: payload[off:off + n]                      # noqa: E731
+    from torrent_amd import verify as V
+    V.release_contexts()
+    assert verify_stream(info, read) == b"\xff" * (P // 8)
+    c0 = V.context_counters()[(0, 0)]
+    assert c0["payload_bytes"] == 0 and c0["device_bytes"] >= 2 * P * MiB
+    assert verify_stream(info, read) == b"\xff" * (P // 8)        # same geometry: chunks reused
+    c1 = V.context_counters()[(0, 0)]
+    assert c1["device_allocs"] == c0["device_allocs"]
+    assert verify_payload(info, payload) == b"\xff" * (P // 8)    # resident: chunks released first
+    c2 = V.context_counters()[(0, 0)]
+    assert c2["payload_bytes"] >= L * P
+    assert c2["device_bytes"] < c2["payload_bytes"] + 64 * MiB
+    V.release_contexts()
+
+
+def test_piece_calls_do_not_evict_the_bulk_payload(native, oracle):
+    """verify_piece runs on its own cached context: a 1 GiB verify_payload interleaved with 100 verify_piece
+    calls allocates its resident payload once (library counter), and so does verify_piece."""
+    from torrent_amd import make_info, verify_payload, verify_piece
+    from torrent_amd import verify as V
+    L, P = 4 * MiB, 256
+    payload = bytes(oracle.synth_fill(21, 0, L * P))
+    pieces = bytearray(oracle.hash_pieces(payload, L * P, L, P))
+    pieces[20 * 7] ^= 1
+    info = make_info(L, bytes(pieces), "t", length=L * P)
+    want = bytearray(b"\xff" * (P // 8))
+    want[0] &= ~0x01 & 0xFF
+    V.release_contexts()
+    for rnd in range(4):
+        assert verify_payload(info, payload) == want
+        for k in range(25):
+            i = (rnd * 25 + k) * 2 % P
+            assert verify_piece(info, i, payload[i * L:(i + 1) * L]) is (i != 7)
+    cnt = V.context_counters()
+    assert cnt[(0, 0)]["payload_allocs"] == 1, cnt
+    assert cnt[(0, V._PIECE_SLOT)]["payload_allocs"] == 1, cnt
+    assert cnt[(0, 0)]["payload_bytes"] >= L * P
+    V.release_contexts()
+
+
+def test_flush_policy_on_the_gpu(native, oracle):
+    """IncrementalVerifier flushes by itself at K pending pieces (tv_verify_list launches counted through
+    the callback), and the results match the oracle, a corrupted block included."""
+    import random
+    from torrent_amd import make_info
+    from torrent_amd.incremental import IncrementalVerifier
+    from torrent_amd.piece import BLOCK_SIZE, PieceMsg
+    L, P = 2 * BLOCK_SIZE, 61
+    total = L * (P - 1) + 777
+    payload = bytes(oracle.synth_fill(5, 0, total))
+    info = make_info(L, oracle.hash_pieces(payload, total, L, P), "t.bin", length=total)
+    got = {}
+    v = IncrementalVerifier(info, flush_pieces=8, flush_age_ms=None, on_verified=got.__setitem__)
+    msgs = []
+    for i in range(P):
+        n = L if i < P - 1 else total - (P - 1) * L
+        msgs += [PieceMsg(i, o, payload[i * L + o:i * L + min(n, o + BLOCK_SIZE)]) for o in range(0, n, BLOCK_SIZE)]
+    random.Random(3).shuffle(msgs)
+    bad = msgs[4]
+    msgs[4] = PieceMsg(bad.index, bad.offset, bytes(b ^ 0x20 for b in bad.block))
+    for m in msgs:
+        v.on_block(m)
+    assert v.auto_flushes == P // 8 and len(got) == 8 * (P // 8)
+    for i, ok in v.flush():
+        got[i] = ok
+    assert got == {i: i != bad.index for i in range(P)}
+    v.close()
+
+
+@pytest.mark.parametrize("n", [1, 5, 64, 300])
+def test_short_lists_run_without_companions(native, oracle, n):
+    """tv_verify_list with fewer pieces than one twin workgroup holds launches no companion workgroups
+    (they would all re-hash the same few pieces); results are exact either way."""
+    L, P = 256 << 10, 512
+    total = L * P
+    payload = bytes(oracle.synth_fill(9, 0, total))
+    pieces = bytearray(oracle.hash_pieces(payload, total, L, P))
+    pieces[20 * 3 + 2] ^= 1
+    with native.Context(0) as ctx:
+        ctx.set_layout(total, L, P)
+        ctx.set_digests(bytes(pieces))
+        ctx.stage(0, payload)
+        lst = [(3 + 7 * k) % P for k in range(n)]
+        assert list(ctx.verify_list(lst)) == [int(i != 3) for i in lst]
+        assert ctx.last_kernel()[0] == native.KERNEL_TWIN
+        assert ctx.counter(native.TV_COUNTER_LAST_WORKGROUPS) == -(-n // 32)      # the real grid only
+        ctx.set_option(native.TV_OPT_TWIN_FILL, 2)                                  # companions forced
+        assert list(ctx.verify_list(lst)) == [int(i != 3) for i in lst]
+        assert ctx.counter(native.TV_COUNTER_LAST_WORKGROUPS) == 2 * _cus()
+
+
+def _cus():
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    n = ctypes.c_int(0)
+    assert hip.hipDeviceGetAttribute(ctypes.byref(n), 63, 0) == 0     # hipDeviceAttributeMultiprocessorCount
+    return n.value
+
+
+def test_long_lists_keep_companions(native, oracle):
+    """A list that gives every CU a twin workgroup (>= 32 x CUs pieces) keeps its companions (2 x CUs
+    workgroups), as resident launches do."""
+    cus = _cus()
+    L, P = 16 << 10, 32 * cus
+    total = L * P
+    with native.Context(0) as ctx:
+        ctx.set_layout(total, L, P)
+        ctx.fill_synthetic(4)
+        d = bytearray(ctx.hash())
+        d[20 * 9] ^= 1
+        ctx.set_digests(bytes(d))
+        lst = list(range(P))
+        assert list(ctx.verify_list(lst)) == [int(i != 9) for i in lst]
+        assert ctx.counter(native.TV_COUNTER_LAST_WORKGROUPS) == 2 * cus

@@ -4,6 +4,7 @@ Ports of the reference's own test cases (metainfo_test.ts, storage_test.ts) plus
 file-to-piece mapping quirks the device offset table relies on.
 """
 import os
+import random
 
 import pytest
 
@@ -169,6 +170,33 @@ def test_segments_quirks():
     assert Storage(MemoryStorage(), single, os.path.join(os.getcwd(), "dl")).segments(3, 4) == [(["dl", "s.bin"], 3, 4, 0)]
 
 
+def test_zero_length_segments_equal_the_walk():
+    """Storage.zero_length_segments lists exactly the zero-length entries of segments(i*L, len_i) over every
+    piece of a range (storage.ts:109-110: `fileEnd >= offset` at a piece start, and zero-length files), with
+    the file offset the walk gives them, on random layouts full of zero-length files and exact boundaries."""
+    rng = random.Random(5)
+    for trial in range(60):
+        L = rng.choice([16, 64, 100])
+        sizes = [rng.choice([0, 0, 1, L, 2 * L, rng.randint(0, 3 * L)]) for _ in range(rng.randint(1, 25))]
+        if sum(sizes) == 0:
+            sizes.append(L + 3)
+        total = sum(sizes)
+        P = -(-total // L)
+        info = make_info(L, bytes(20 * P), "t", files=[FileInfo(n, [f"f{k}"]) for k, n in enumerate(sizes)])
+        st = Storage(MemoryStorage(), info, "/tmp/seg")
+        first = rng.randrange(P)
+        count = rng.randint(1, P - first)
+        want = []
+        for i in range(first, first + count):
+            for path, foff, n, s0 in st.segments(i * L, piece_length(i, info)) or ():
+                if n == 0:
+                    want.append((int(path[-1][1:]), foff, i * L + s0))
+        hi = (first + count - 1) * L + piece_length(first + count - 1, info)
+        k, fo, lin = st.zero_length_segments(first * L, hi - first * L, L)
+        assert sorted(zip(k.tolist(), fo.tolist(), lin.tolist())) == sorted(want), (trial, sizes, first, count)
+        assert all(first <= x // L < first + count for x in lin.tolist())
+
+
 @pytest.mark.parametrize("dir_path", ["/tmp/seg", "/", "", "/tmp/seg/"])
 def test_segment_arrays_equal_the_walk(dir_path):
     """Storage.segment_arrays (the vectorised walk verify_files stages from) equals segments() minus
@@ -296,6 +324,21 @@ def test_info_hash_is_sha1_of_the_original_info_bytes(name):
     assert m.info_hash == hashlib.sha1(raw_info).digest()
 
 
+def _fs_openable(path: str) -> bool:
+    """Would fsStorage.get's Deno.open(path, {read, write, create}) succeed (storage.ts:28-32,158)?  Without
+    creating anything: an existing non-directory with read + write access, or a missing file in an existing,
+    writable directory.  (The CPU stand-in's copy of tv_api.hip fs_openable.)"""
+    import stat
+    try:
+        st = os.stat(path)
+    except FileNotFoundError:
+        parent = os.path.dirname(path) or "."
+        return os.path.isdir(parent) and os.access(parent, os.W_OK | os.X_OK)
+    except OSError:
+        return False
+    return not stat.S_ISDIR(st.st_mode) and os.access(path, os.R_OK | os.W_OK)
+
+
 class _ImageCtx:
     """Stand-in for a tv_ctx on CPU: tv_stage_files writes into a linear image of the shard, so
     verify_files' staging plan (the storage.ts segment mapping, one batched call, status -> unreadable
@@ -323,6 +366,9 @@ class _ImageCtx:
         self.calls += 1
         out = []
         for path, foff, off, n in zip(paths, file_offsets, linear_offsets, lens):
+            if n == 0:   # the library's zero-length rule (tv_api.hip fs_openable), restated
+                out.append(0 if _fs_openable(path) else -5)
+                continue
             try:
                 with open(path, "rb") as f:
                     f.seek(foff)

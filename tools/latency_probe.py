@@ -5,6 +5,8 @@ and 4,096 resident 256 KiB pieces (incremental verify, SURVEY 8f row f1: torrent
 Wall time per call (median of `reps` after warmup) with the library's own HIP-event split: kernel_ms (the
 verify kernel) and total_ms (the whole call on the compute stream).  SHA-1 is serial within a piece, so a
 256 KiB piece is 4,097 dependent compressions on ONE lane: the kernel time is the floor of every call.
+Round 3: each list length with companion workgroups on short lists (TV_OPT_TWIN_FILL 2, the round-2
+behaviour) and without (1, auto), twice each, interleaved.
 usage: python tools/latency_probe.py [reps]"""
 import json
 import os
@@ -62,20 +64,27 @@ def main():
         ctx.set_layout(P * L, L, P)
         ctx.fill_synthetic(3)
         ctx.set_digests(ctx.hash())
-        for n in (1, 64, 4096):
+        # TV_OPT_TWIN_FILL 1 (auto: companions only for lists of >= 32 x CUs pieces) against 2 (companions on
+        # every list, the round-2 behaviour), interleaved per list length
+        for n in (1, 64, 4096, 8192):
             lst = list(range(0, P, P // n))[:n]
-            ws, ks, ts = [], [], []
-            for _ in range(reps + 2):
-                t0 = time.perf_counter()
-                ok = ctx.verify_list(lst)
-                ws.append((time.perf_counter() - t0) * 1e3)
-                k, t = ctx.last_timing()
-                ks.append(k)
-                ts.append(t)
-                assert ok == b"\x01" * n
-            out[f"verify_list_flush_{n}"] = {"wall_ms_median": med(ws[2:]), "kernel_ms_median": med(ks[2:]),
-                                             "call_ms_median": med(ts[2:]),
-                                             "kernel": {1: "lane list", 2: "split list", 4: "twin list"}[ctx.last_kernel()[0]]}
+            for fill in (1, 2, 1, 2):
+                ctx.set_option(N.TV_OPT_TWIN_FILL, fill)
+                ws, ks, ts = [], [], []
+                for _ in range(reps + 2):
+                    t0 = time.perf_counter()
+                    ok = ctx.verify_list(lst)
+                    ws.append((time.perf_counter() - t0) * 1e3)
+                    k, t = ctx.last_timing()
+                    ks.append(k)
+                    ts.append(t)
+                    assert ok == b"\x01" * n
+                key = f"verify_list_flush_{n}" + ("" if fill == 1 else "_companions_forced")
+                rec = {"wall_ms_median": med(ws[2:]), "kernel_ms_median": med(ks[2:]), "call_ms_median": med(ts[2:]),
+                       "workgroups": ctx.counter(N.TV_COUNTER_LAST_WORKGROUPS),
+                       "kernel": {1: "lane list", 2: "split list", 4: "twin list"}[ctx.last_kernel()[0]]}
+                out.setdefault(key, []).append(rec)
+        ctx.set_option(N.TV_OPT_TWIN_FILL, 1)
     print(json.dumps(out, indent=1))
 
 

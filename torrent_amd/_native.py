@@ -34,10 +34,16 @@ TV_OPT_DEBUG_REBOUNCE = 11
 TV_OPT_TWIN_PACK = 12
 TV_OPT_TWIN_FILL = 13
 
+TV_COUNTER_PAYLOAD_ALLOCS = 1
+TV_COUNTER_DEVICE_ALLOCS = 2
+TV_COUNTER_PAYLOAD_BYTES = 3
+TV_COUNTER_DEVICE_BYTES = 4
+TV_COUNTER_LAST_WORKGROUPS = 5
+
 TV_STREAM_RING_SLOTS = 3
 TV_STREAM_SLOT_BYTES = 64 << 20
 
-KERNEL_AUTO, KERNEL_LANE, KERNEL_SPLIT, KERNEL_MIX, KERNEL_TWIN = 0, 1, 2, 3, 4
+KERNEL_AUTO, KERNEL_LANE, KERNEL_SPLIT, KERNEL_TWIN = 0, 1, 2, 4   # (3 was MIX, removed)
 
 _u64, _i64, _int, _p = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p
 
@@ -79,6 +85,7 @@ SYMBOLS = [
     ("tv_get_option", _int, [_p, _int, ctypes.POINTER(_i64)]),
     ("tv_last_timing", _int, [_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     ("tv_last_kernel", _int, [_p, ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    ("tv_get_counter", _int, [_p, _int, ctypes.POINTER(_u64)]),
     ("tv_synchronize", _int, [_p]),
     ("tv_host_alloc", _int, [_u64, ctypes.POINTER(_p)]),
     ("tv_host_free", _int, [_p]),
@@ -390,6 +397,12 @@ class Context:
         k, n = _int(0), _int(0)
         self._check(self._L.tv_last_kernel(self._h, ctypes.byref(k), ctypes.byref(n)))
         return k.value, n.value
+
+    def counter(self, key: int) -> int:
+        """tv_get_counter: device allocations since creation / bytes held now (TV_COUNTER_*)."""
+        v = _u64(0)
+        self._check(self._L.tv_get_counter(self._h, key, ctypes.byref(v)))
+        return v.value
 
     def synchronize(self) -> None:
         self._check(self._L.tv_synchronize(self._h))

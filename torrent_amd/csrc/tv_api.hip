@@ -34,10 +34,6 @@ thread_local std::string g_thread_error;
 constexpr uint64_t kSlack = 256;                          // bytes past the last resident piece (tail over-read)
 constexpr int kRingSlots = TV_STREAM_RING_SLOTS;          // pinned staging buffers per lane
 constexpr size_t kRingSlotBytes = TV_STREAM_SLOT_BYTES;
-constexpr uint32_t kMixSegBlocks = 1024;    // MIX unit: 64 KiB of each of a group's 64 pieces
-
-// SHA-1 blocks of an n-byte message (data + 0x80 + 8-byte length, padded to 64)
-constexpr uint64_t nblocks_of(uint64_t n) { return (n + 8) / 64 + 1; }
 
 // Persistent host workers (one pool per staging lane): run(threads, tasks, fn) calls fn(0..tasks-1) on up
 // to `threads` threads, the caller included, and returns when every task is done.  Spawning threads for
@@ -127,10 +123,7 @@ struct tv_ctx {
     hipStream_t stream = nullptr;       // kernels
     hipStream_t copy_stream = nullptr;  // H2D staging
     hipStream_t copy_stream2 = nullptr; // H2D staging of the second lane (tv_stage_files' long segments)
-    // MIX launch (opt-in): pair workers on mix_pairs (CU mask: the low half of the CUs), lane workers on
-    // mix_lanes (the high half), created at the first MIX call; fork / join events
-    hipStream_t mix_pairs = nullptr, mix_lanes = nullptr;
-    hipEvent_t ev_mix0 = nullptr, ev_mix1 = nullptr, ev_mix2 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;  // TV_OPT_TWIN_PACK launches on pack_stream
     int cus = 256;                      // compute units of the device
     hipEvent_t ev_call0 = nullptr, ev_k0 = nullptr, ev_k1 = nullptr, ev_call1 = nullptr;
 
@@ -151,7 +144,7 @@ struct tv_ctx {
     bool resident = true;                    // TV_OPT_RESIDENT
     bool debug_rebounce = false;             // TV_OPT_DEBUG_REBOUNCE
     bool twin_pack = false;                  // TV_OPT_TWIN_PACK
-    bool twin_fill = true;                   // TV_OPT_TWIN_FILL
+    int twin_fill = 1;                       // TV_OPT_TWIN_FILL: 0 off, 1 auto, 2 also on short lists
     hipStream_t pack_stream = nullptr;       // twin launches CU-masked to pack_cus CUs (TV_OPT_TWIN_PACK)
     int pack_cus = 0;
 
@@ -196,9 +189,6 @@ struct tv_ctx {
     Pool pool[2];                     // host workers of lane 0 / lane 1
     std::mutex err_mu;                // fail() may run on a tv_stage_files helper thread
     uint8_t* h_bits = nullptr;        // pinned bitfield bounce buffer
-    uint32_t* d_queue = nullptr;      // MIX work queue: head, tail, error, pad, then 64-bit slots
-    uint64_t queue_cap = 0;           // bytes of d_queue
-    uint32_t* h_qerr = nullptr;       // pinned copy of the queue's error word
     size_t h_bits_cap = 0;
 
     // streamed verify (tv_stream_*)
@@ -206,9 +196,13 @@ struct tv_ctx {
     hipEvent_t col_ev[2] = {nullptr, nullptr};   // copies of the column into chunk buffer k queued before it
     hipEvent_t done_ev[2] = {nullptr, nullptr};  // the kernel that last read chunk buffer k
 
+    // counters (tv_get_counter): device allocations since tv_create
+    uint64_t n_payload_allocs = 0, n_device_allocs = 0;
+
     // last call
     float kernel_ms = 0.f, total_ms = 0.f;
     int last_kernel = 0, last_launches = 0;
+    uint32_t last_workgroups = 0;      // grid of the last verify / hash / list launch, companions included
 };
 
 namespace {
@@ -243,6 +237,30 @@ uint64_t piece_len(const tv_ctx* c, uint64_t i) {  // piece.ts:16-19
 inline void set_bit(uint8_t* bf, uint64_t i) { bf[i >> 3] |= (uint8_t)(0x80u >> (i & 7)); }
 inline bool get_bit(const uint8_t* bf, uint64_t i) { return (bf[i >> 3] >> (7 - (i & 7))) & 1; }
 
+// May this process read and write the existing file `path` (fsStorage.get opens every segment with
+// {read: true, write: true, create: true}, storage.ts:28-32,158)?  0, or the errno that open would fail with.
+int rw_access(const char* path) {
+    return faccessat(AT_FDCWD, path, R_OK | W_OK, AT_EACCESS) == 0 ? 0 : errno;
+}
+
+// Would fsStorage.get's Deno.open(path, {read, write, create}) succeed (storage.ts:28-32,158)?  Checked
+// without creating anything: an existing non-directory this process may read and write, or a missing file
+// whose parent directory exists and may be written.  A zero-length segment of Storage.get's walk
+// (storage.ts:109-110: a file ending where the piece starts, or a zero-length file inside the piece) reads
+// nothing, but its open still decides whether the piece is null.  0, or the errno.
+int fs_openable(const char* path) {
+    if (!path[0]) return ENOENT;
+    struct stat st;
+    if (stat(path, &st) == 0) return S_ISDIR(st.st_mode) ? EISDIR : rw_access(path);
+    if (errno != ENOENT) return errno;
+    std::string parent(path);
+    const size_t cut = parent.find_last_of('/');
+    parent = cut == std::string::npos ? std::string(".") : (cut == 0 ? std::string("/") : parent.substr(0, cut));
+    if (stat(parent.c_str(), &st) != 0) return errno;          // a missing parent directory: open fails
+    if (!S_ISDIR(st.st_mode)) return ENOTDIR;
+    return faccessat(AT_FDCWD, parent.c_str(), W_OK | X_OK, AT_EACCESS) == 0 ? 0 : errno;
+}
+
 void free_payload(tv_ctx* c) {
     (void)hipFree(c->d_payload); c->d_payload = nullptr;
     c->cap_payload = 0;
@@ -264,15 +282,23 @@ void free_words(tv_ctx* c) {
     c->cap_words = 0;
 }
 
+void free_chunks(tv_ctx* c) {
+    for (auto& p : c->d_chunk) { (void)hipFree(p); p = nullptr; }
+    c->chunk_bytes = 0;
+}
+
+void free_list(tv_ctx* c) {
+    (void)hipFree(c->d_list); c->d_list = nullptr;
+    (void)hipFree(c->d_list_out); c->d_list_out = nullptr;
+    c->list_cap = 0;
+}
+
 void free_device(tv_ctx* c) {
     free_payload(c);
     free_per_piece(c);
     free_words(c);
-    for (auto& p : c->d_chunk) { (void)hipFree(p); p = nullptr; }
-    c->chunk_bytes = 0;
-    (void)hipFree(c->d_list); c->d_list = nullptr;
-    (void)hipFree(c->d_list_out); c->d_list_out = nullptr;
-    c->list_cap = 0;
+    free_chunks(c);
+    free_list(c);
 }
 
 // An allocation of `cap` units is reused for `need` units when it holds them and is not more than twice
@@ -396,14 +422,8 @@ int launch_avail(tv_ctx* c, const uint8_t* avail_bits, const uint64_t** out) {
     return TV_OK;
 }
 
-// Kernel of a launch over the whole shard.  resident: a one-launch call on the resident payload (MIX
-// needs it: its queue runs every segment of every piece in one launch); streamed columns fall back to
-// lane where MIX would be chosen.
-int choose_kernel(const tv_ctx* c, bool resident = true) {
-    // MIX (TV_OPT_KERNEL 3) is opt-in only: measured slower than lane wherever lane is chosen (DESIGN.md
-    // section 6, profiles/r02/mix_probe.log); its queue entries hold 16-bit group numbers
-    const bool mix_ok = resident && (c->count + 63) / 64 + 1 <= 0xFFFF;
-    if (c->kernel_opt == TV_KERNEL_MIX) return mix_ok ? TV_KERNEL_MIX : TV_KERNEL_LANE;
+// Kernel of a launch over the whole shard (resident calls and streamed columns alike).
+int choose_kernel(const tv_ctx* c) {
     if (c->kernel_opt == TV_KERNEL_LANE || c->kernel_opt == TV_KERNEL_SPLIT || c->kernel_opt == TV_KERNEL_TWIN)
         return c->kernel_opt;
     // Twin (two lanes per piece, 2-wave workgroups over 32 pieces, 60 KiB of LDS: two per CU) while every
@@ -420,32 +440,8 @@ int choose_kernel(const tv_ctx* c, bool resident = true) {
     return c->count <= 32768 ? TV_KERNEL_SPLIT : TV_KERNEL_LANE;
 }
 
-// MIX workers, the shape measured best (profiles/r02/mix_probe.log): split pairs on the low half of the CUs,
-// two pair workgroups per CU (3 K+W buffers of LDS each); 4-wave lane workgroups, one per CU, on the high
-// half.  Without the CU masks the dispatcher puts lane waves on SIMDs that already hold a wave (up to 6x
-// slower units).  Streams created at the first MIX call.
-int mix_streams(tv_ctx* c) {
-    if (c->mix_pairs) return TV_OK;
-    std::vector<uint32_t> lo((c->cus + 31) / 32, 0), hi((c->cus + 31) / 32, 0);
-    for (int i = 0; i < c->cus; i++) (i < c->cus / 2 ? lo : hi)[i / 32] |= 1u << (i % 32);
-    TV_HIP(c, hipExtStreamCreateWithCUMask(&c->mix_pairs, (uint32_t)lo.size(), lo.data()));
-    TV_HIP(c, hipExtStreamCreateWithCUMask(&c->mix_lanes, (uint32_t)hi.size(), hi.data()));
-    return TV_OK;
-}
-
-TvMixShape mix_shape(const tv_ctx* c) {
-    TvMixShape m{};
-    m.pair_wgs = (unsigned)c->cus;          // 2 per CU on cus / 2 CUs
-    m.pair_lds_bufs = 3;
-    m.lane_wgs = (unsigned)(c->cus / 2);    // 1 per CU on cus / 2 CUs, 4 waves each
-    m.lane_waves_per_wg = 4;
-    m.lane_lds = 0;
-    return m;
-}
-
-// One launch over the resident shard with the chosen kernel.  MIX: the pair and lane workers run on the two
-// CU-masked streams, forked after everything queued on c->stream and joined back into it; the queue's error
-// word is copied to h_qerr for check_queue after the call's final sync.
+// One launch over the resident shard with the chosen kernel (TV_OPT_TWIN_PACK: on the CU-masked pack_stream,
+// forked after everything queued on c->stream and joined back into it).
 int launch_resident(tv_ctx* c, const TvPieces& p_in, int kernel, bool hash) {
     TvPieces p = p_in;
     // A CU running ONE 2-wave twin workgroup spends ~80 more shader cycles per block than one running two
@@ -469,56 +465,15 @@ int launch_resident(tv_ctx* c, const TvPieces& p_in, int kernel, bool hash) {
                 TV_HIP(c, hipExtStreamCreateWithCUMask(&c->pack_stream, (uint32_t)m.size(), m.data()));
                 c->pack_cus = k;
             }
-            TV_HIP(c, hipEventRecord(c->ev_mix0, c->stream));
-            TV_HIP(c, hipStreamWaitEvent(c->pack_stream, c->ev_mix0, 0));
-            TV_HIP(c, tv_launch_verify(p, kernel, hash, c->pack_stream, c->split_pairs));
-            TV_HIP(c, hipEventRecord(c->ev_mix1, c->pack_stream));
-            TV_HIP(c, hipStreamWaitEvent(c->stream, c->ev_mix1, 0));
+            TV_HIP(c, hipEventRecord(c->ev_fork, c->stream));
+            TV_HIP(c, hipStreamWaitEvent(c->pack_stream, c->ev_fork, 0));
+            TV_HIP(c, tv_launch_verify(p, kernel, hash, c->pack_stream, c->split_pairs, &c->last_workgroups));
+            TV_HIP(c, hipEventRecord(c->ev_join, c->pack_stream));
+            TV_HIP(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
             return TV_OK;
         }
     }
-    if (kernel != TV_KERNEL_MIX) {
-        TV_HIP(c, tv_launch_verify(p, kernel, hash, c->stream, c->split_pairs));
-        return TV_OK;
-    }
-    TvQueue q{};
-    q.groups = (p.n_main + 63) / 64 + (p.n_main < p.n ? 1 : 0);
-    const uint64_t nb = nblocks_of(p.L);
-    q.seg_blocks = (uint32_t)std::max<uint64_t>(kMixSegBlocks, (nb + 0xFFFE) / 0xFFFF);   // segs < 65,536
-    q.segs = (uint32_t)((nb + q.seg_blocks - 1) / q.seg_blocks);
-    q.units = q.groups * q.segs;
-    q.ring = q.groups;
-    const uint64_t bytes = 16 + 8ull * q.ring;   // head, tail, error, pad, slots[ring]
-    if (c->queue_cap < bytes) {
-        (void)hipFree(c->d_queue); c->d_queue = nullptr; c->queue_cap = 0;
-        TV_HIP(c, hipMalloc((void**)&c->d_queue, bytes));
-        c->queue_cap = bytes;
-    }
-    if (!c->h_qerr) TV_HIP(c, hipHostMalloc((void**)&c->h_qerr, 64, hipHostMallocDefault));
-    q.head = c->d_queue;
-    q.tail = c->d_queue + 1;
-    q.error = c->d_queue + 2;
-    q.slots = reinterpret_cast<uint64_t*>(c->d_queue + 4);
-    q.trace = nullptr;
-    TV_HIP(c, hipMemsetAsync(c->d_queue, 0, bytes, c->stream));
-    int rc = mix_streams(c);
-    if (rc) return rc;
-    TV_HIP(c, hipEventRecord(c->ev_mix0, c->stream));
-    TV_HIP(c, hipStreamWaitEvent(c->mix_pairs, c->ev_mix0, 0));
-    TV_HIP(c, hipStreamWaitEvent(c->mix_lanes, c->ev_mix0, 0));
-    TV_HIP(c, tv_launch_mix(p, q, hash, c->mix_pairs, c->mix_lanes, mix_shape(c)));
-    TV_HIP(c, hipEventRecord(c->ev_mix1, c->mix_pairs));
-    TV_HIP(c, hipEventRecord(c->ev_mix2, c->mix_lanes));
-    TV_HIP(c, hipStreamWaitEvent(c->stream, c->ev_mix1, 0));
-    TV_HIP(c, hipStreamWaitEvent(c->stream, c->ev_mix2, 0));
-    TV_HIP(c, hipMemcpyAsync(c->h_qerr, q.error, 4, hipMemcpyDeviceToHost, c->stream));
-    return TV_OK;
-}
-
-// After the call's final sync: a MIX launch whose watchdog fired has no valid output.
-int check_queue(tv_ctx* c, int kernel) {
-    if (kernel == TV_KERNEL_MIX && *c->h_qerr)
-        return fail(c, TV_ERR_HIP, "work queue watchdog expired (a MIX worker waited > 4 s for a ready group)");
+    TV_HIP(c, tv_launch_verify(p, kernel, hash, c->stream, c->split_pairs, &c->last_workgroups));
     return TV_OK;
 }
 
@@ -855,6 +810,11 @@ uint64_t stream_column(const tv_ctx* c) {
     return std::max<uint64_t>(64, std::min<uint64_t>(C, kRingSlotBytes));
 }
 
+// Bytes of each of the two device chunk buffers a stream over the current geometry needs.
+uint64_t stream_chunk_need(const tv_ctx* c) {
+    return c->count ? (stream_column(c) + 256) * c->count + kSlack : 0;
+}
+
 int stream_begin_locked(tv_ctx* c, const uint8_t* avail_bits) {
     StreamState& st = c->st;
     st = StreamState{};
@@ -867,15 +827,17 @@ int stream_begin_locked(tv_ctx* c, const uint8_t* avail_bits) {
     st.C = stream_column(c);
     st.row_pitch = st.C + 256;  // (tail over-read slack per row)
     const uint64_t need = st.row_pitch * c->count + kSlack;
-    if (c->chunk_bytes < need) {
-        for (auto& p : c->d_chunk) { (void)hipFree(p); p = nullptr; }
-        c->chunk_bytes = 0;
-        for (auto& p : c->d_chunk) TV_HIP(c, hipMalloc((void**)&p, need));
+    if (!reuse_fits(need, c->chunk_bytes)) {
+        free_chunks(c);
+        for (auto& p : c->d_chunk) {
+            TV_HIP(c, hipMalloc((void**)&p, need));
+            c->n_device_allocs++;
+        }
         c->chunk_bytes = need;
     }
     st.ncol = (c->L + st.C - 1) / st.C;
     st.rows_per_req = std::max<uint64_t>(1, kRingSlotBytes / st.C);
-    st.kernel = choose_kernel(c, false);
+    st.kernel = choose_kernel(c);
     st.p = resident_launch(c);
     st.p.stride = st.row_pitch;
     TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
@@ -965,7 +927,7 @@ int stream_commit_locked(tv_ctx* c, const tv_stream_req* req, const uint8_t* src
     p.blk_begin = r.offset / 64;
     p.blk_end = last ? UINT64_MAX : (r.offset + st.C) / 64;
     p.finalize = last ? 1 : 0;
-    TV_HIP(c, tv_launch_verify(p, st.kernel, false, c->stream, c->split_pairs));
+    TV_HIP(c, tv_launch_verify(p, st.kernel, false, c->stream, c->split_pairs, &c->last_workgroups));
     TV_HIP(c, hipEventRecord(c->done_ev[buf], c->stream));
     st.col++;
     st.row = 0;
@@ -1032,9 +994,8 @@ int tv_create(tv_ctx** out, int device) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy_stream2, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_mix0, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_mix1, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_mix2, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device);
     if (e == hipSuccess) e = hipEventCreate(&c->ev_call0);
     if (e == hipSuccess) e = hipEventCreate(&c->ev_k0);
@@ -1060,11 +1021,8 @@ void tv_destroy(tv_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     if (c->copy_stream2) (void)hipStreamSynchronize(c->copy_stream2);
-    if (c->mix_pairs) (void)hipStreamSynchronize(c->mix_pairs);
-    if (c->mix_lanes) (void)hipStreamSynchronize(c->mix_lanes);
+    if (c->pack_stream) (void)hipStreamSynchronize(c->pack_stream);
     free_device(c);
-    if (c->d_queue) (void)hipFree(c->d_queue);
-    if (c->h_qerr) (void)hipHostFree(c->h_qerr);
     for (int s = 0; s < kRingSlots; s++) {
         if (c->ring[s]) (void)hipHostFree(c->ring[s]);
         if (c->ring_ev[s]) (void)hipEventDestroy(c->ring_ev[s]);
@@ -1073,15 +1031,12 @@ void tv_destroy(tv_ctx* c) {
     }
     if (c->h_bits) (void)hipHostFree(c->h_bits);
     for (hipEvent_t ev : {c->ev_call0, c->ev_k0, c->ev_k1, c->ev_call1, c->ev_avail, c->col_ev[0], c->col_ev[1],
-                          c->done_ev[0], c->done_ev[1], c->ev_mix0, c->ev_mix1,
-                          c->ev_mix2})
+                          c->done_ev[0], c->done_ev[1], c->ev_fork, c->ev_join})
         if (ev) (void)hipEventDestroy(ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->copy_stream2) (void)hipStreamDestroy(c->copy_stream2);
     if (c->pack_stream) (void)hipStreamDestroy(c->pack_stream);
-    if (c->mix_pairs) (void)hipStreamDestroy(c->mix_pairs);
-    if (c->mix_lanes) (void)hipStreamDestroy(c->mix_lanes);
     delete c;
 }
 
@@ -1106,7 +1061,8 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
     std::lock_guard<std::mutex> g(c->mu);
     switch (key) {
         case TV_OPT_KERNEL:
-            if (value < 0 || value > 4) return fail(c, TV_ERR_ARG, "TV_OPT_KERNEL must be 0, 1, 2, 3 or 4");
+            if (value < 0 || value > 4 || value == 3)   // (3 was MIX, removed)
+                return fail(c, TV_ERR_ARG, "TV_OPT_KERNEL must be 0 (auto), 1 (lane), 2 (split) or 4 (twin)");
             c->kernel_opt = (int)value;
             return TV_OK;
         case TV_OPT_STRIDE_PAD:
@@ -1155,8 +1111,8 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
             c->twin_pack = value != 0;
             return TV_OK;
         case TV_OPT_TWIN_FILL:
-            if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_TWIN_FILL must be 0 or 1");
-            c->twin_fill = value != 0;
+            if (value < 0 || value > 2) return fail(c, TV_ERR_ARG, "TV_OPT_TWIN_FILL must be 0, 1 or 2");
+            c->twin_fill = (int)value;
             return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
@@ -1178,7 +1134,7 @@ int tv_get_option(tv_ctx* c, int key, int64_t* value) {
         case TV_OPT_RESIDENT: *value = c->resident ? 1 : 0; return TV_OK;
         case TV_OPT_DEBUG_REBOUNCE: *value = c->debug_rebounce ? 1 : 0; return TV_OK;
         case TV_OPT_TWIN_PACK: *value = c->twin_pack ? 1 : 0; return TV_OK;
-        case TV_OPT_TWIN_FILL: *value = c->twin_fill ? 1 : 0; return TV_OK;
+        case TV_OPT_TWIN_FILL: *value = c->twin_fill; return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
@@ -1222,19 +1178,28 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
     // Keep every allocation the new geometry fits (reuse_fits): a run of small layouts (verify_piece,
     // a flush of tv_verify_list) allocates once.  Everything else is released first, so a big payload
     // is never held beside its replacement.
+    // A layout without a resident payload (TV_OPT_RESIDENT = 0) releases the old one: the resident calls must
+    // see no payload (TV_ERR_STATE), never a smaller buffer left by an earlier layout.  The streamed path's
+    // chunk buffers are kept only for a streamed layout they fit (a resident payload must not be allocated
+    // beside them), and the list buffers only while they are not far larger than the shard.
     const uint64_t need_payload = (shard_count && c->resident) ? shard_count * c->stride + kSlack : 0;
-    if (!reuse_fits(need_payload, c->cap_payload)) free_payload(c);
+    if (!need_payload || !reuse_fits(need_payload, c->cap_payload)) free_payload(c);
     if (!reuse_fits(shard_count, c->cap_count)) free_per_piece(c);
     if (!reuse_fits(c->bit_words, c->cap_words)) free_words(c);
+    if (c->chunk_bytes && (need_payload || !reuse_fits(stream_chunk_need(c), c->chunk_bytes))) free_chunks(c);
+    if (c->list_cap > std::max<uint64_t>(1024, 2 * shard_count)) free_list(c);
     if (need_payload && !c->d_payload) {
         TV_HIP(c, hipMalloc((void**)&c->d_payload, need_payload));
         c->cap_payload = need_payload;
+        c->n_payload_allocs++;
+        c->n_device_allocs++;
     }
     if (shard_count && !c->d_digests) {
         TV_HIP(c, hipMalloc((void**)&c->d_digests, 5 * shard_count * sizeof(uint32_t)));
         TV_HIP(c, hipMalloc((void**)&c->d_state, 5 * shard_count * sizeof(uint32_t)));
         TV_HIP(c, hipMalloc((void**)&c->d_hash, 5 * shard_count * sizeof(uint32_t)));
         c->cap_count = shard_count;
+        c->n_device_allocs += 3;
     }
     if (shard_count && !c->d_out) {
         TV_HIP(c, hipMalloc((void**)&c->d_avail, c->bit_words * 8));
@@ -1242,6 +1207,7 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
         TV_HIP(c, hipHostMalloc((void**)&c->h_avail, c->bit_words * 8, hipHostMallocDefault));
         TV_HIP(c, hipMalloc((void**)&c->d_out, c->bit_words * 8));
         c->cap_words = c->bit_words;
+        c->n_device_allocs += 3;
     }
     if (need_payload) {  // the tail over-read slack past the last piece reads zeros
         TV_HIP(c, hipMemsetAsync(c->d_payload + shard_count * c->stride, 0, kSlack, c->stream));
@@ -1313,7 +1279,11 @@ int stage_file_locked(tv_ctx* c, const char* path, uint64_t file_offset, uint64_
                       int lane = 0) {
     hipStream_t cs = lane_stream(c, lane);
     int rc = TV_OK;
-    if (len == 0) return TV_OK;  // a zero-length read succeeds without touching the file
+    if (len == 0) {  // reads nothing, but fsStorage.get still opens the path (storage.ts:158)
+        const int e = fs_openable(path);
+        return e ? fail(c, TV_ERR_IO, "open %s: %s", path, strerror(e)) : TV_OK;
+    }
+    if (const int e = rw_access(path)) return fail(c, TV_ERR_IO, "open %s for read and write: %s", path, strerror(e));
     FileWindows win;  // before `drain`: destroyed after the streams are drained
     win.fd = open(path, O_RDONLY | O_CLOEXEC);
     if (win.fd < 0) return fail(c, TV_ERR_IO, "open %s: %s", path, strerror(errno));
@@ -1400,10 +1370,10 @@ void read_segments(const std::vector<SmallSeg>& segs, size_t lo, size_t hi, cons
             const SmallSeg& sg = segs[items[it].first];
             const uint64_t part0 = items[it].second, part1 = std::min(sg.len, part0 + kPart);
             const char* path = paths[sg.k];
-            int e = 0;
-            const int fd = open(path, O_RDONLY | O_CLOEXEC);
+            int e = rw_access(path);  // opened as fsStorage.get opens it: read + write (storage.ts:28-32)
+            const int fd = e ? -1 : open(path, O_RDONLY | O_CLOEXEC);
             if (fd < 0) {
-                e = errno;
+                if (!e) e = errno;
             } else {
                 uint64_t o = part0;
                 while (o < part1) {
@@ -1473,10 +1443,18 @@ int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64
     std::vector<LongSeg> longs;
     std::vector<SmallSeg> small;
     uint64_t small_bytes = 0;
+    std::string zero_err;
     for (uint64_t k = 0; k < n; k++) {
+        if (lens[k] == 0) {  // Storage.get's zero-length segments: only the open decides (storage.ts:109-110,158)
+            if (const int e = fs_openable(paths[k])) {
+                status_out[k] = TV_ERR_IO;
+                if (zero_err.empty()) zero_err = std::string(paths[k]) + ": " + strerror(e);
+            }
+            continue;
+        }
         uint64_t a, b;
         clip_to_shard(c, linear_offsets[k], lens[k], &a, &b);
-        if (a >= b) continue;  // nothing of this segment is resident here (zero-length reads succeed)
+        if (a >= b) continue;  // nothing of this segment is resident here
         const uint64_t fo = file_offsets[k] + (a - linear_offsets[k]);
         if (b - a >= direct_min) {
             longs.push_back({k, fo, a, b - a});
@@ -1531,7 +1509,7 @@ int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64
         if (rc == TV_ERR_IO) status_out[sg.k] = TV_ERR_IO;
         else if (rc) return rc;
     }
-    std::string first_err;
+    std::string first_err = zero_err;
     std::mutex err_mu;
     DrainGuard drain(c);
     size_t i = 0;
@@ -1643,8 +1621,6 @@ int tv_verify(tv_ctx* c, const uint8_t* avail_bits, uint8_t* bitfield_out) {
     TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
     rc = read_bits(c, bitfield_out);
     if (rc) return rc;
-    rc = check_queue(c, kernel);
-    if (rc) return rc;
     c->last_kernel = kernel;
     c->last_launches = 1;
     return finish_timing(c);
@@ -1691,13 +1667,12 @@ int tv_verify_list(tv_ctx* c, const uint64_t* pieces, uint64_t n, uint8_t* ok_ou
     TV_HIP(c, hipSetDevice(c->device));
     DrainGuard drain(c);  // after the host vectors: their H2D / D2H copies end before return
     if (c->list_cap < m) {
-        (void)hipFree(c->d_list); c->d_list = nullptr;
-        (void)hipFree(c->d_list_out); c->d_list_out = nullptr;
-        c->list_cap = 0;
+        free_list(c);
         const uint64_t cap = std::max<uint64_t>(m, 1024);
         TV_HIP(c, hipMalloc((void**)&c->d_list, cap * 4));
         TV_HIP(c, hipMalloc((void**)&c->d_list_out, cap));
         c->list_cap = cap;
+        c->n_device_allocs += 2;
     }
     TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
     TV_HIP(c, hipMemcpyAsync(c->d_list, launch.data(), m * 4, hipMemcpyHostToDevice, c->stream));
@@ -1715,8 +1690,13 @@ int tv_verify_list(tv_ctx* c, const uint64_t* pieces, uint64_t n, uint8_t* ok_ou
                            ? c->kernel_opt
                            : (m <= 64 * (uint64_t)c->cus ? TV_KERNEL_TWIN
                                                          : (m <= 256 * 64 ? TV_KERNEL_SPLIT : TV_KERNEL_LANE));
-    if (kernel == TV_KERNEL_TWIN && c->twin_fill) p.fill_to = 2u * (uint32_t)c->cus;   // companions, as resident
-    TV_HIP(c, tv_launch_verify_list(p, kernel, c->stream));
+    // Companions (as resident launches) only for a list that gives every CU a workgroup: a shorter one would
+    // fill 2 x CUs workgroups with copies re-hashing the same few pieces (a 1-piece flush: 512 copies) for a
+    // ~4 % shorter flush (r03 latency: tools/latency_probe.py)
+    const uint64_t list_wgs = (m + 31) / 32;
+    if (kernel == TV_KERNEL_TWIN && (c->twin_fill == 2 || (c->twin_fill == 1 && list_wgs >= (uint64_t)c->cus)))
+        p.fill_to = 2u * (uint32_t)c->cus;
+    TV_HIP(c, tv_launch_verify_list(p, kernel, c->stream, &c->last_workgroups));
     TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
     TV_HIP(c, hipMemcpyAsync(reordered ? ok_launch.data() : ok_out, c->d_list_out, m, hipMemcpyDeviceToHost, c->stream));
     TV_HIP(c, hipEventRecord(c->ev_call1, c->stream));
@@ -1750,8 +1730,6 @@ int tv_hash(tv_ctx* c, uint8_t* digests_out) {
     TV_HIP(c, hipMemcpyAsync(soa.data(), c->d_hash, soa.size() * 4, hipMemcpyDeviceToHost, c->stream));
     TV_HIP(c, hipEventRecord(c->ev_call1, c->stream));
     TV_HIP(c, hipEventSynchronize(c->ev_call1));
-    rc = check_queue(c, kernel);
-    if (rc) return rc;
     for (uint64_t j = 0; j < c->count; j++)
         for (int k = 0; k < 5; k++) {
             const uint32_t v = soa[(uint64_t)k * c->count + j];
@@ -1932,6 +1910,22 @@ int tv_last_timing(tv_ctx* c, double* kernel_ms, double* total_ms) {
     if (kernel_ms) *kernel_ms = c->kernel_ms;
     if (total_ms) *total_ms = c->total_ms;
     return TV_OK;
+}
+
+int tv_get_counter(tv_ctx* c, int key, uint64_t* value) {
+    if (!c || !value) return fail(c, TV_ERR_ARG, "NULL argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    switch (key) {
+        case TV_COUNTER_PAYLOAD_ALLOCS: *value = c->n_payload_allocs; return TV_OK;
+        case TV_COUNTER_DEVICE_ALLOCS: *value = c->n_device_allocs; return TV_OK;
+        case TV_COUNTER_PAYLOAD_BYTES: *value = c->cap_payload; return TV_OK;
+        case TV_COUNTER_DEVICE_BYTES:
+            *value = c->cap_payload + c->cap_count * 3 * 5 * sizeof(uint32_t) + c->cap_words * 8 * 3 +
+                     2 * c->chunk_bytes + c->list_cap * 5;
+            return TV_OK;
+        case TV_COUNTER_LAST_WORKGROUPS: *value = c->last_workgroups; return TV_OK;
+    }
+    return fail(c, TV_ERR_ARG, "unknown counter %d", key);
 }
 
 int tv_last_kernel(tv_ctx* c, int* kernel, int* launches) {

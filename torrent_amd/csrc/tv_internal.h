@@ -6,7 +6,8 @@
 #define TV_KERNEL_AUTO 0
 #define TV_KERNEL_LANE 1
 #define TV_KERNEL_SPLIT 2
-#define TV_KERNEL_MIX 3     // work queue: split pairs + lane waves share 64-piece groups segment by segment
+// (3 was MIX, a work queue over split pairs and lane waves: measured 8.6 % slower than lane where lane is
+//  chosen, removed in round 3; the value stays unused)
 #define TV_KERNEL_TWIN 4    // split with two lanes per piece in the rounds waves (half the K+W reads per block)
 
 // One launch over a contiguous run of n pieces.  Piece j's byte k (piece-relative) is at
@@ -37,32 +38,9 @@ struct TvPieces {
                              // the result (TV_OPT_TWIN_FILL)
 };
 
-// Work queue of the MIX launch (tv_launch_mix): a FIFO of ready 64-piece groups.  A unit is segment s
-// (blocks [s * seg_blocks, (s + 1) * seg_blocks); the last one runs to the end and finalises) of group g;
-// entries are (lap tag << 32 | s << 16 | g), so groups and segs are < 65,536.
-struct TvQueue {
-    uint32_t* head;      // pop tickets   (head, tail, error: zeroed before the launch)
-    uint32_t* tail;      // push tickets
-    uint32_t* error;     // nonzero: a worker's wait exceeded the watchdog; the launch's output is invalid
-    uint64_t* slots;     // [ring] entries (zeroed before the launch)
-    uint32_t ring;       // >= groups
-    uint32_t groups, segs, seg_blocks, units;  // units = groups * segs
-    uint64_t* trace;     // diagnostics (tools/mix_probe.cpp), null in the library: per unit (s * groups + g)
-                         // {pop, start, end} s_memrealtime ticks and the worker id
-};
-
-// Worker shape of a MIX launch: pair_wgs split-pair workgroups declaring pair_lds_bufs (3 or 5) K+W
-// buffers of LDS, lane_wgs lane workgroups of lane_waves_per_wg (1..4) waves each, lane_lds bytes of
-// (unused) dynamic LDS per lane workgroup.
-struct TvMixShape {
-    unsigned pair_wgs, pair_lds_bufs, lane_wgs, lane_waves_per_wg, lane_lds;
-};
-
-hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_t s, int split_pairs = 0);
-// The MIX launch: the pair workers on s_pairs and the lane workers on s_lanes, concurrently, over the
-// queue q (the short last piece, if any, is a group of its own like in tv_launch_verify).
-hipError_t tv_launch_mix(const TvPieces& p, const TvQueue& q, bool hash, hipStream_t s_pairs, hipStream_t s_lanes,
-                         const TvMixShape& m);
-hipError_t tv_launch_verify_list(const TvPieces& p, int kernel, hipStream_t s);
+// workgroups (optional): set to the launch's grid size, companions included.
+hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_t s, int split_pairs = 0,
+                            uint32_t* workgroups = nullptr);
+hipError_t tv_launch_verify_list(const TvPieces& p, int kernel, hipStream_t s, uint32_t* workgroups = nullptr);
 hipError_t tv_launch_fill(uint8_t* payload, uint64_t stride, uint64_t first, uint32_t n, uint64_t L,
                           uint64_t seed, hipStream_t s);

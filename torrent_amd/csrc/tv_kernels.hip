@@ -6,15 +6,21 @@
 // the digest equals info.pieces[i] (metainfo.ts:111) and the bytes were readable
 // (Storage.get non-null, storage.ts:50-65), MSB-first (torrent.ts:147-149).
 //
-// Parallelism is one LANE per piece (SHA-1 is serial inside a piece).  Two kernels:
-//   lane  : each lane loads its own 64-byte blocks (register prefetch, 2 blocks ahead) and runs
-//           the full compression (schedule + rounds) as one generated asm block (613 VALU/block).
+// SHA-1 is serial inside a piece, so parallelism comes from pieces only.  Three kernels (plus list modes):
+//   lane  : one lane per piece; each lane loads its own 64-byte blocks (register prefetch, TV_LANE_DEPTH = 3
+//           blocks ahead) and runs the full compression (schedule + rounds) as one generated asm block
+//           (613 VALU per block).  For > 32,768 pieces per GPU, where every SIMD has a wave.
 //   split : schedule offload.  A workgroup is PAIRS x (rounds, helper) waves, 64 pieces per pair: a helper
-//           loads the blocks and writes K+W[0..79] into an LDS double buffer (generated asm: v_perm
-//           bswap, v_bitop3 xor3, K adds, ds_write_b128); the rounds wave runs only the 80 rounds from
-//           LDS (405 VALU + 20 ds_read_b128 + 5 waits per block).  A lone wave issues one VALU per
+//           loads the blocks and writes K+W[0..79] into a 3-buffer LDS ring two blocks ahead (generated asm:
+//           v_perm bswap, v_bitop3 xor3, K adds, ds_write_b128); the rounds wave runs only the 80 rounds
+//           from LDS (405 VALU + 20 ds_read_b128 + 5 waits per block).  A lone wave issues one VALU per
 //           ~4.07 cycles (tools/ubench_fetch.hip), so with fewer pieces than SIMDs the per-lane
 //           instruction count IS the bound; this cuts the serial stream from 613 to 405 VALU per block.
+//           For 16,384 < pieces <= 32,768 per GPU.
+//   twin  : split with TWO lanes per piece: a lane pair runs the same rounds, each lane reads only the K+W
+//           quads of its parity (10 ds_read_b128 per block) and takes the other parity's word from its
+//           partner by DPP; a two-lane helper expands the schedule by parity.  For <= 16,384 pieces per GPU
+//           (every wave still has a SIMD to itself).
 //
 // HBM layout: resident piece j (shard-local) starts at payload + j*stride, stride = L + pad
 // (pad breaks the power-of-two stride that would put all 64 lanes of a wave on one channel).
@@ -154,8 +160,7 @@ __device__ __forceinline__ void finish(const TvPieces& p, bool writer, uint32_t 
     if (!p.finalize) {
         if (writer) {
 #pragma unroll
-            for (int k = 0; k < 5; k++)   // device-coherent (write-through) store: a MIX successor may read it
-                __hip_atomic_store(p.state + (uint64_t)k * p.dcount + jj, h[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int k = 0; k < 5; k++) p.state[(uint64_t)k * p.dcount + jj] = h[k];   // the next column's launch reads it
         }
         return;
     }
@@ -185,8 +190,7 @@ __device__ __forceinline__ void start_state(const TvPieces& p, uint32_t jj, uint
         sha1_iv(h);
     } else {
 #pragma unroll
-        for (int k = 0; k < 5; k++)       // device-coherent load (a MIX predecessor on another XCD wrote it)
-            h[k] = __hip_atomic_load(p.state + (uint64_t)k * p.dcount + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int k = 0; k < 5; k++) h[k] = p.state[(uint64_t)k * p.dcount + jj];  // the previous column's chaining value
     }
 }
 
@@ -545,155 +549,6 @@ __global__ __launch_bounds__(64 * kTwinWaves[SHAPE]) void tv_twin_kernel(TvPiece
 }
 
 // ------------------------------------------------------------------------------------------
-// MIX: persistent split pairs and persistent lane waves serve one FIFO of ready 64-piece groups at once.
-// With 32,768 < P < ~56,000 pieces the lane kernel leaves SIMDs idle (cfg4 on one GPU: 800 waves on 1,024
-// SIMDs) and a piece's SHA-1 is serial: a group advances at its worker's per-piece rate (pair ~1,870
-// cycles per block, lane ~2,650) and a pair costs two SIMDs.  A worker pops a group, runs its next
-// segment (seg_blocks blocks; the 20-byte chaining states go through d_state), and pushes it back at the
-// tail: every group gets the same mix of fast and slow workers and all of them end together.
-// Tickets: pop ticket t < groups is group t's first segment (nothing to wait for); pop ticket t >= groups
-// takes push ticket t - groups, whose slot carries its lap tag; pop tickets >= units mean "drained".
-// Push (release) / pop (acquire) at agent scope: the workers sit on different XCDs.  A pop that waits
-// polls with relaxed loads and s_sleep and has a watchdog, so no wave spins forever: the push it waits
-// for comes from a worker that holds a group and is running (holders never wait), and a worker that gives
-// up sets `error` and every other worker stops at its next pop.
-// ------------------------------------------------------------------------------------------
-namespace {
-
-constexpr uint64_t kWatchdogTicks = 400000000ull;  // s_memrealtime runs at 100 MHz: 4 s
-
-// Handoff ordering.  1: agent-scope release / acquire fences (they write back / invalidate the XCD's whole
-// L2).  0: the only data handed between workers is the chaining state, and it is stored and loaded with
-// device-coherent (sc1) accesses, so the push only waits for those stores to complete and the pop's
-// data loads, issued after the slot load returned, read memory and not a stale L2 line.
-#ifndef TV_QUEUE_FENCES
-#define TV_QUEUE_FENCES 1
-#endif
-constexpr uint32_t kStop = 0xFFFFFFFFu;
-
-__device__ __forceinline__ uint32_t q_error(const TvQueue& q) {
-    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(q.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-
-__device__ __forceinline__ uint32_t wave_ticket(uint32_t* counter) {
-    uint32_t t = 0;
-    if ((threadIdx.x & 63u) == 0) t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return __builtin_amdgcn_readfirstlane(t);
-}
-
-// Next unit as (s << 16 | g), or kStop (drained, or a worker gave up).  Wave-uniform.
-__device__ __forceinline__ uint32_t q_pop(const TvQueue& q) {
-    const uint32_t t = wave_ticket(q.head);
-    if (t >= q.units || q_error(q)) return kStop;
-    if (t < q.groups) return t;                 // segment 0 of group t
-    const uint32_t k = t - q.groups;            // the push this pop takes
-    const uint32_t tag = k / q.ring + 1;
-    const uint64_t* slot = q.slots + (k % q.ring);
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-        // relaxed polls, one acquire fence when the entry is there: the fence invalidates this XCD's L2,
-        // which a poll loop must not do every few hundred cycles under the other waves' payload streams
-        const uint64_t v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-        if (hi == tag) {
-#if TV_QUEUE_FENCES
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
-            return __builtin_amdgcn_readfirstlane((uint32_t)v);
-        }
-        if (q_error(q)) return kStop;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kWatchdogTicks) {
-            if ((threadIdx.x & 63u) == 0) __hip_atomic_fetch_or(q.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return kStop;
-        }
-        __builtin_amdgcn_s_sleep(8);
-    }
-}
-
-// Group g has finished segment s: queue its next segment (the state stores are visible device-wide first).
-__device__ __forceinline__ void q_push(const TvQueue& q, uint32_t g, uint32_t s) {
-    if (s + 1 >= q.segs) return;                // finalised: the group leaves the queue
-#if TV_QUEUE_FENCES
-    __threadfence();
-#else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the state's write-through stores have completed
-#endif
-    const uint32_t k = wave_ticket(q.tail);
-    const uint64_t v = ((uint64_t)(k / q.ring + 1) << 32) | ((s + 1) << 16) | g;
-    if ((threadIdx.x & 63u) == 0)
-        __hip_atomic_store(q.slots + (k % q.ring), v, TV_QUEUE_FENCES ? __ATOMIC_RELEASE : __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ void q_trace(const TvQueue& q, uint32_t s, uint32_t g, uint64_t t0, uint64_t t1,
-                                        uint32_t worker) {
-    if ((threadIdx.x & 63u) == 0) {
-        const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
-        uint64_t* r = q.trace + 4ull * ((uint64_t)s * q.groups + g);
-        r[0] = t0;
-        r[1] = t1;
-        r[2] = t2;
-        r[3] = worker;
-    }
-}
-
-__device__ __forceinline__ TvPieces q_unit(const TvPieces& p, const TvQueue& q, uint32_t s) {
-    TvPieces u = p;
-    const bool last = s + 1 == q.segs;
-    u.blk_begin = (uint64_t)s * q.seg_blocks;
-    u.blk_end = last ? UINT64_MAX : (uint64_t)(s + 1) * q.seg_blocks;
-    u.finalize = last ? 1 : 0;
-    return u;
-}
-
-}  // namespace
-
-// Persistent lane workers: every wave of the workgroup serves units on its own.  Dynamic LDS (unused)
-// only limits how many lane workgroups share a CU with a pair workgroup.
-template <bool HASH>
-__global__ __launch_bounds__(256) void tv_qlane_kernel(TvPieces p, TvQueue q) {
-    for (;;) {
-        const uint64_t t0 = q.trace ? __builtin_amdgcn_s_memrealtime() : 0;
-        const uint32_t e = q_pop(q);
-        if (e == kStop) return;
-        const uint32_t s = e >> 16, g = e & 0xFFFFu;
-        const uint64_t t1 = q.trace ? __builtin_amdgcn_s_memrealtime() : 0;
-        lane_group<HASH>(q_unit(p, q, s), g);
-        q_push(q, g, s);
-        if (q.trace) q_trace(q, s, g, t0, t1, 0x10000u + blockIdx.x * 4u + (threadIdx.x >> 6));
-    }
-}
-
-// Persistent split pairs: the rounds wave pops a unit (the acquire included) and hands it to the helper
-// through LDS.  DECL_BUFS >= kBufs ring buffers are declared: 5 (102 KiB) lets at most one pair workgroup
-// onto a CU, 3 (61 KiB) two.
-template <bool HASH, int DECL_BUFS>
-__global__ __launch_bounds__(128) void tv_qsplit_kernel(TvPieces p, TvQueue q) {
-    static_assert(DECL_BUFS >= (int)kBufs, "ring");
-    __shared__ __attribute__((aligned(16))) uint4 ring[DECL_BUFS * kRingWords / 4];
-    __shared__ uint32_t unit_slot;
-    const uint32_t rounds = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
-    for (;;) {
-        const uint64_t t0 = q.trace ? __builtin_amdgcn_s_memrealtime() : 0;
-        if (rounds) {
-            const uint32_t e = q_pop(q);
-            if ((threadIdx.x & 63u) == 0) unit_slot = e;
-        }
-        lds_barrier();
-        const uint32_t e = __builtin_amdgcn_readfirstlane(unit_slot);
-        if (e == kStop) return;   // both waves read the same slot: both stop
-        const uint32_t s = e >> 16, g = e & 0xFFFFu;
-        const uint64_t t1 = q.trace ? __builtin_amdgcn_s_memrealtime() : 0;
-        split_group<HASH, 1, false>(q_unit(p, q, s), g, ring, [] { return true; });
-        if (rounds) {
-            q_push(q, g, s);
-            if (q.trace) q_trace(q, s, g, t0, t1, blockIdx.x);
-        }
-        // the next pop's slot write follows this unit's last barrier, which the helper has passed
-    }
-}
-
-// ------------------------------------------------------------------------------------------
 // list kernel (incremental verify): lane j verifies shard piece idx[j]; same compression path as
 // the lane kernel, geometry from wave ballots (the short last piece may sit in any lane).
 // ------------------------------------------------------------------------------------------
@@ -779,7 +634,9 @@ __global__ __launch_bounds__(256) void tv_fill_bytes_kernel(uint8_t* payload, ui
 // ------------------------------------------------------------------------------------------
 // host-side launchers (called by tv_api.hip)
 // ------------------------------------------------------------------------------------------
-hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_t s, int split_pairs) {
+hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_t s, int split_pairs,
+                            uint32_t* workgroups) {
+    if (workgroups) *workgroups = 0;
     if (p.n == 0) return hipSuccess;
     if (kernel == TV_KERNEL_SPLIT) {
         // one pair per workgroup: with its 60 KiB LDS ring at most two workgroups share a CU, and up to
@@ -787,6 +644,7 @@ hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_
         // barrier couples more jitter) at every piece count up to there, by 1.7-3 % (profiles/r02/sweep_3buf.log)
         const int pairs = (split_pairs == 1 || split_pairs == 2) ? split_pairs : 1;
         const unsigned grid = (p.n_main + 64 * pairs - 1) / (64 * pairs) + (p.n_main < p.n ? 1 : 0);
+        if (workgroups) *workgroups = grid;
         if (pairs == 1) {
             if (hash) hipLaunchKernelGGL((tv_split_kernel<true, 1>), dim3(grid), dim3(128), 0, s, p);
             else hipLaunchKernelGGL((tv_split_kernel<false, 1>), dim3(grid), dim3(128), 0, s, p);
@@ -803,6 +661,7 @@ hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_
         const unsigned span = 32u * kTwinPairs[shape];
         const unsigned real = (p.n_main + span - 1) / span + (p.n_main < p.n ? 1 : 0);
         const unsigned grid = (p.fill_to > real && p.n_main > 0) ? p.fill_to : real;
+        if (workgroups) *workgroups = grid;
         const dim3 blk(64 * kTwinWaves[shape]);
 #define TV_TWIN_LAUNCH(S)                                                              \
     if (hash) hipLaunchKernelGGL((tv_twin_kernel<true, S>), dim3(grid), blk, 0, s, p); \
@@ -818,45 +677,29 @@ hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_
     } else {
         const unsigned waves = (p.n_main + 63) / 64 + (p.n_main < p.n ? 1 : 0);
         const unsigned grid = (waves + 3) / 4;
+        if (workgroups) *workgroups = grid;
         if (hash) hipLaunchKernelGGL(tv_lane_kernel<true>, dim3(grid), dim3(256), 0, s, p);
         else hipLaunchKernelGGL(tv_lane_kernel<false>, dim3(grid), dim3(256), 0, s, p);
     }
     return hipGetLastError();
 }
 
-hipError_t tv_launch_mix(const TvPieces& p, const TvQueue& q, bool hash, hipStream_t s_pairs, hipStream_t s_lanes,
-                         const TvMixShape& m) {
+hipError_t tv_launch_verify_list(const TvPieces& p, int kernel, hipStream_t s, uint32_t* workgroups) {
+    if (workgroups) *workgroups = 0;
     if (p.n == 0) return hipSuccess;
-    if (q.groups > 0xFFFFu || q.segs > 0xFFFFu || m.lane_waves_per_wg < 1 || m.lane_waves_per_wg > 4 ||
-        (m.pair_lds_bufs != 3 && m.pair_lds_bufs != 5))
-        return hipErrorInvalidValue;
-    const dim3 lb(64 * m.lane_waves_per_wg);
-    if (m.pair_wgs) {
-        if (hash) {
-            if (m.pair_lds_bufs == 5) hipLaunchKernelGGL((tv_qsplit_kernel<true, 5>), dim3(m.pair_wgs), dim3(128), 0, s_pairs, p, q);
-            else hipLaunchKernelGGL((tv_qsplit_kernel<true, 3>), dim3(m.pair_wgs), dim3(128), 0, s_pairs, p, q);
-        } else {
-            if (m.pair_lds_bufs == 5) hipLaunchKernelGGL((tv_qsplit_kernel<false, 5>), dim3(m.pair_wgs), dim3(128), 0, s_pairs, p, q);
-            else hipLaunchKernelGGL((tv_qsplit_kernel<false, 3>), dim3(m.pair_wgs), dim3(128), 0, s_pairs, p, q);
-        }
-    }
-    if (m.lane_wgs) {
-        if (hash) hipLaunchKernelGGL(tv_qlane_kernel<true>, dim3(m.lane_wgs), lb, m.lane_lds, s_lanes, p, q);
-        else hipLaunchKernelGGL(tv_qlane_kernel<false>, dim3(m.lane_wgs), lb, m.lane_lds, s_lanes, p, q);
-    }
-    return hipGetLastError();
-}
-
-hipError_t tv_launch_verify_list(const TvPieces& p, int kernel, hipStream_t s) {
-    if (p.n == 0) return hipSuccess;
+    unsigned grid;
     if (kernel == TV_KERNEL_TWIN) {
         const unsigned real = (p.n + 31) / 32;
-        hipLaunchKernelGGL((tv_twin_kernel<false, 1, true>), dim3(p.fill_to > real ? p.fill_to : real), dim3(128), 0, s, p);
+        grid = p.fill_to > real ? p.fill_to : real;
+        hipLaunchKernelGGL((tv_twin_kernel<false, 1, true>), dim3(grid), dim3(128), 0, s, p);
+    } else if (kernel == TV_KERNEL_SPLIT) {
+        grid = (p.n + 63) / 64;
+        hipLaunchKernelGGL((tv_split_kernel<false, 1, true>), dim3(grid), dim3(128), 0, s, p);
+    } else {
+        grid = (p.n + 255) / 256;
+        hipLaunchKernelGGL(tv_list_kernel, dim3(grid), dim3(256), 0, s, p);
     }
-    else if (kernel == TV_KERNEL_SPLIT)
-        hipLaunchKernelGGL((tv_split_kernel<false, 1, true>), dim3((p.n + 63) / 64), dim3(128), 0, s, p);
-    else
-        hipLaunchKernelGGL(tv_list_kernel, dim3((p.n + 255) / 256), dim3(256), 0, s, p);
+    if (workgroups) *workgroups = grid;
     return hipGetLastError();
 }
 

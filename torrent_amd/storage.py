@@ -122,6 +122,32 @@ class Storage:
         k, lo, n = k[keep], lo[keep], n[keep]
         return k, lo - starts[k], n, lo - offset
 
+    def zero_length_segments(self, offset: int, length: int, piece_length: int):
+        """The zero-length segments of the walks Storage.get makes for the pieces tiling [offset, offset +
+        length) (offset a multiple of piece_length), as arrays (file_index, file_offset, linear_offset).
+        findAndDo (storage.ts:105-128) emits one for every file whose end e lies inside the piece's range
+        [o, o + n) and that contributes nothing there: a file ending exactly where the piece starts (e == o,
+        `fileEnd >= offset`, :109-110) or a zero-length file inside the piece.  Their piece is
+        linear_offset // piece_length.  fsStorage.get still opens such a path (storage.ts:158), so its
+        open decides whether the piece is null (tv_stage_files checks it)."""
+        import numpy as np
+
+        if self.info.files is None or length <= 0:
+            return tuple(np.zeros(0, np.int64) for _ in range(3))
+        if self._table is None:
+            lens = np.fromiter((f.length for f in self.info.files), dtype=np.int64, count=len(self.info.files))
+            ends = np.cumsum(lens)
+            self._table = (ends - lens, ends)
+        starts, ends = self._table
+        lens = ends - starts
+        a = int(np.searchsorted(ends, offset, side="left"))
+        b = int(np.searchsorted(ends, offset + length, side="left"))
+        k = np.arange(a, b, dtype=np.int64)
+        e = ends[a:b]
+        keep = (lens[a:b] == 0) | (e % piece_length == 0)
+        k, e = k[keep], e[keep]
+        return k, lens[k], e
+
     def file_paths(self) -> List[str]:
         """os.path.join(*segment path) for every file index of segment_arrays (fs_storage's paths)."""
         if self._joined is None:

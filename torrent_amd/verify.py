@@ -25,8 +25,6 @@ and asyncio wrappers verify_pieces_async / verify_piece_async (the reference API
 from __future__ import annotations
 
 import asyncio
-import os
-import stat
 import threading
 from concurrent.futures import ThreadPoolExecutor
 from contextlib import contextmanager
@@ -70,6 +68,10 @@ def _concat(slices: Sequence[bytes], ranges: Sequence[tuple], n_pieces: int) -> 
 
 
 _ctx_cache: dict = {}          # (device, slot) -> (Context, Lock)
+# verify_piece's context slot: a one-piece layout on a bulk call's context (slot 0) would free its payload
+# (tv_set_layout keeps an allocation only while the new geometry is at least half of it) and the next bulk
+# call would allocate it again
+_PIECE_SLOT = -1
 _ctx_lock = threading.Lock()
 
 
@@ -88,6 +90,20 @@ def _context(device: int, slot: int = 0):
     ctx, lock = e
     with lock:
         yield ctx
+
+
+def context_counters() -> dict:
+    """{(device, slot): {payload_allocs, device_allocs, payload_bytes, device_bytes}} of the cached contexts
+    (tv_get_counter): how often each had to allocate device memory, and what it holds now."""
+    with _ctx_lock:
+        entries = list(_ctx_cache.items())
+    out = {}
+    for key, (ctx, lock) in entries:
+        with lock:
+            out[key] = {name: ctx.counter(k) for name, k in (
+                ("payload_allocs", _native.TV_COUNTER_PAYLOAD_ALLOCS), ("device_allocs", _native.TV_COUNTER_DEVICE_ALLOCS),
+                ("payload_bytes", _native.TV_COUNTER_PAYLOAD_BYTES), ("device_bytes", _native.TV_COUNTER_DEVICE_BYTES))}
+    return out
 
 
 def release_contexts() -> None:
@@ -174,7 +190,12 @@ def verify_payload(info: InfoDict, payload, devices=None, resident: bool = True,
     mv = memoryview(payload).cast("B")
 
     def shard(ctx, first: int, count: int) -> bytes:
-        ctx.set_layout(info.length, L, P, first, count)
+        if not resident:        # the streamed path needs no resident payload (tv_verify_host)
+            ctx.set_option(_native.TV_OPT_RESIDENT, 0)
+        try:
+            ctx.set_layout(info.length, L, P, first, count)
+        finally:
+            ctx.set_option(_native.TV_OPT_RESIDENT, 1)
         ctx.set_digests(info.pieces_raw)
         av = _shard_avail(avail, first, count)
         lo = min(first * L, len(mv))
@@ -261,53 +282,6 @@ def verify_stream(info: InfoDict, read, devices=None, avail: Optional[bytes] = N
     return _concat(slices, ranges, P)
 
 
-def _openable(path: str) -> bool:
-    """Would fsStorage.get's Deno.open(path, {read, write, create}) succeed (storage.ts:149-160)?  Checked
-    without creating the file: an existing non-directory, or a missing file in an existing directory."""
-    try:
-        st = os.stat(path)
-    except FileNotFoundError:
-        parent = os.path.dirname(path) or "."
-        return os.path.isdir(parent) and os.access(parent, os.W_OK | os.X_OK)
-    except OSError:
-        return False
-    return not stat.S_ISDIR(st.st_mode) and os.access(path, os.R_OK | os.W_OK)
-
-
-def _zero_length_faults(info: InfoDict, storage, first: int, count: int, clear) -> None:
-    """The zero-length segments of Storage.get's walk (storage.ts:105-128): a file ending exactly where a
-    piece starts (`fileEnd >= offset`), and zero-length files inside a piece.  fsStorage.get still opens
-    them (storage.ts:158), so a path that cannot be opened -- a directory, a missing parent directory --
-    makes the piece null.  segment_arrays drops these segments, so they are checked here, only for the
-    pieces whose range holds such a boundary."""
-    import numpy as np
-
-    if info.files is None or count == 0:
-        return
-    L = info.piece_length
-    lens = np.fromiter((f.length for f in info.files), dtype=np.int64, count=len(info.files))
-    ends = np.cumsum(lens)
-    starts = ends - lens
-    lo, hi = first * L, (first + count) * L
-    cand = set()
-    on_start = ends[(ends >= lo) & (ends < hi) & (ends % L == 0)]              # a file ends where a piece starts
-    cand.update(((on_start // L) - first).tolist())
-    zs = starts[(lens == 0) & (starts >= lo) & (starts < hi)]                  # zero-length files
-    cand.update(((zs // L) - first).tolist())
-    cache = {}
-    for j in sorted(cand):
-        i = first + j
-        segs = storage.segments(i * L, piece_length(i, info))
-        for path, _, n, _ in segs or ():
-            if n == 0:
-                p = os.path.join(*path)
-                if p not in cache:
-                    cache[p] = _openable(p)
-                if not cache[p]:
-                    clear(j, j)
-                    break
-
-
 def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: int = 16,
                  direct_min: Optional[int] = None) -> bytearray:
     """Stage the shard's pieces from files into HBM and return the shard's readability bits.
@@ -317,7 +291,8 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
     >= direct_min bytes (default 32 MiB) are DMA'd from the page cache (tv_stage_file's path), shorter
     ones are read by `threads` library threads into pinned slots, one DMA per run of adjacent bytes.
     A piece touching a missing or short file is unreadable (fsStorage.get -> null,
-    storage.ts:150-172); zero-length segments succeed; missing files are never created."""
+    storage.ts:150-172); so is a piece whose zero-length segment (storage.ts:109-110) names a path
+    fsStorage.get could not open (the library checks it, tv_stage_files); missing files are never created."""
     L = info.piece_length
     avail = bytearray(b"\xff" * ((count + 7) // 8))
     if count % 8:
@@ -340,18 +315,27 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
     segs = storage.segment_arrays(lo, span) if span else None
     if span and segs is None:         # unmappable (Storage.get -> null for every piece)
         clear(0, count - 1)
-    _zero_length_faults(info, storage, first, count, clear)
-    if segs is None or len(segs[0]) == 0:
+    if segs is None:
         return avail
+    import numpy as np
+
     k, foff, nbytes, start = segs
+    lin = start + lo
+    # the walk's zero-length segments too: the library checks their open as fsStorage.get would make it
+    zk, zfoff, zlin = storage.zero_length_segments(lo, span, L)
+    if len(zk):
+        k, foff, lin = np.concatenate([k, zk]), np.concatenate([foff, zfoff]), np.concatenate([lin, zlin])
+        nbytes = np.concatenate([nbytes, np.zeros(len(zk), np.int64)])
+    if len(k) == 0:
+        return avail
     paths = storage.file_paths()
     ctx.set_option(_native.TV_OPT_FILE_THREADS, max(1, threads))
     ctx.set_option(_native.TV_OPT_FILE_DIRECT_MIN, _DIRECT_MIN_BYTES if direct_min is None else direct_min)
-    status = ctx.stage_files([paths[i] for i in k.tolist()], foff, start + lo, nbytes)
+    status = ctx.stage_files([paths[i] for i in k.tolist()], foff, lin, nbytes)
     for q, st in enumerate(status):
         if st != _native.TV_OK:
-            s0, n = int(start[q]), int(nbytes[q])
-            clear(s0 // L, (s0 + n - 1) // L)
+            s0, n = int(lin[q]) - lo, int(nbytes[q])
+            clear(s0 // L, (s0 + max(n, 1) - 1) // L)     # a zero-length segment: piece s0 // L
     return avail
 
 
@@ -418,7 +402,7 @@ def verify_piece(info: InfoDict, index: int, data) -> bool:
     n = memoryview(data).nbytes
     if n != piece_length(index, info) or len(info.pieces[index]) != 20 or n == 0:
         return False
-    with _context(0) as ctx:
+    with _context(0, _PIECE_SLOT) as ctx:      # its own context: never evicts a bulk call's payload
         ctx.set_layout(n, n, 1, 0, 1)
         ctx.set_digests(bytes(info.pieces[index]))
         ctx.stage(0, data)

@@ -50,6 +50,7 @@ const SYMBOLS = {
   tv_get_option: { parameters: ["pointer", "i32", "pointer"], result: "i32" },
   tv_last_timing: { parameters: ["pointer", "pointer", "pointer"], result: "i32" },
   tv_last_kernel: { parameters: ["pointer", "pointer", "pointer"], result: "i32" },
+  tv_get_counter: { parameters: ["pointer", "i32", "pointer"], result: "i32" },
   tv_synchronize: { parameters: ["pointer"], result: "i32" },
   tv_host_alloc: { parameters: ["u64", "pointer"], result: "i32" },
   tv_host_free: { parameters: ["pointer"], result: "i32" },
@@ -202,6 +203,8 @@ export async function verifyPieces(
 }
 
 const TV_ERR_IO = -5;
+/** storage.get calls a streamed verify keeps outstanding (file descriptors, not bandwidth, bound it) */
+const READS_IN_FLIGHT = 32;
 const TV_OPT_STREAM_CHUNK = 3;
 const TV_OPT_RESIDENT = 10;
 
@@ -243,15 +246,20 @@ export async function verifyStream(info: InfoDict, storage: Storage, opts: Verif
           if (rows === 0) break;
           const piece = Number(req[0]), offset = Number(req[2]), width = Number(req[3]);
           const slot = new Uint8Array(Deno.UnsafePointerView.getArrayBuffer(Deno.UnsafePointer.create(req[4])!, rows * width));
-          // every read of the request outstanding at once (make_torrent.ts:96,111 keeps its digests in flight)
-          const got = await Promise.all(Array.from({ length: rows }, (_, q) => {
-            const n = Math.max(0, Math.min(width, pieceLength(piece + q, info) - offset));
-            return n ? storage.get((piece + q) * L + offset, n) : Promise.resolve(new Uint8Array(0));
-          }));
-          got.forEach((bytes, q) => {
-            if (bytes) slot.set(bytes, q * width);
-            else check(l, ctx, l.symbols.tv_stream_unreadable(ctx, BigInt(piece + q)));
-          });
+          // READS_IN_FLIGHT reads of the request outstanding at a time: each fsStorage.get is a Deno.open, and
+          // an EMFILE from a thousand opens at once would come back as null -- a valid piece reported 0
+          let next = 0;
+          const worker = async () => {
+            for (let q = next++; q < rows; q = next++) {
+              const n = Math.max(0, Math.min(width, pieceLength(piece + q, info) - offset));
+              if (n === 0) continue;
+              const bytes = await storage.get((piece + q) * L + offset, n);
+              // a row must be exactly n bytes: more would spill into the next row (Python: unreadable too)
+              if (bytes && bytes.length === n) slot.set(bytes, q * width);
+              else check(l, ctx, l.symbols.tv_stream_unreadable(ctx, BigInt(piece + q)));
+            }
+          };
+          await Promise.all(Array.from({ length: Math.min(READS_IN_FLIGHT, rows) }, worker));
           check(l, ctx, await l.symbols.tv_stream_commit(ctx, reqp));
         }
         const out = new Uint8Array(Math.ceil(count / 8));
@@ -274,8 +282,9 @@ export async function verifyStream(info: InfoDict, storage: Storage, opts: Verif
  * [dir, name], multi-file [dir, ...path]).  All file segments of a shard go to tv_stage_files in one
  * call: long segments are DMA'd to HBM from the page cache when the file is warm (parallel preads when
  * cold); short ones (many small files) are read by the library's thread pool into pinned slots.
- * A missing or short file (TV_ERR_IO) makes the pieces it touches 0, like fsStorage.get returning
- * null (storage.ts:163-171); unlike fsStorage.get, no missing file is created.  Same behaviour as
+ * A missing, short or unwritable file (TV_ERR_IO) makes the pieces it touches 0, like fsStorage.get
+ * returning null (storage.ts:163-171), and so does a zero-length segment whose open would fail (a directory,
+ * a missing parent directory); unlike fsStorage.get, no missing file is created.  Same behaviour as
  * torrent_amd.verify_files.
  */
 export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptions = {}): Promise<Uint8Array> {
@@ -305,6 +314,9 @@ export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptio
       const hi = Math.min(info.length, (first + count - 1) * L + pieceLength(first + count - 1, info));
       // findAndDo's walk over the files in order (storage.ts:105-128), restricted to [lo, hi): every
       // segment of the shard goes to the library in ONE tv_stage_files call
+      // The walk's zero-length segments go too (storage.ts:109-110: a file ending exactly where a piece starts,
+      // a zero-length file inside a piece): fsStorage.get still opens them (storage.ts:158), and the library
+      // reports TV_ERR_IO where that open would fail.  Such a segment's piece is linear / L.
       const segs: { path: Uint8Array; fileOffset: number; linear: number; len: number }[] = [];
       let fileStart = 0;
       for (const f of files) {
@@ -312,6 +324,10 @@ export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptio
         const a = Math.max(lo, fileStart);
         const b = Math.min(hi, fileEnd);
         if (b > a) segs.push({ path: new TextEncoder().encode(f.path + "\0"), fileOffset: a - fileStart, linear: a, len: b - a });
+        // (a file with bytes in the range also gives one when it ends on a later piece's start)
+        if (fileEnd >= lo && fileEnd < hi && (f.length === 0 || fileEnd % L === 0)) {
+          segs.push({ path: new TextEncoder().encode(f.path + "\0"), fileOffset: f.length, linear: fileEnd, len: 0 });
+        }
         fileStart = fileEnd;
         if (fileStart >= hi) break;
       }
@@ -331,7 +347,9 @@ export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptio
                                                      ptr(u8(len)), ptr(u8(status))));
         // `segs` (the path strings) stays referenced until here, after the nonblocking call settled
         segs.forEach((sg, k) => {
-          if (status[k] === TV_ERR_IO) clear(Math.floor((sg.linear - lo) / L), Math.floor((sg.linear + sg.len - 1 - lo) / L));
+          if (status[k] === TV_ERR_IO) {
+            clear(Math.floor((sg.linear - lo) / L), Math.floor((sg.linear + Math.max(sg.len, 1) - 1 - lo) / L));
+          }
         });
       }
       const out = new Uint8Array(Math.ceil(count / 8));
@@ -347,7 +365,9 @@ export async function verifyPiece(info: InfoDict, index: number, bytes: Uint8Arr
   if (index >= info.pieces.length) throw new Error(`verifyPiece: invalid piece index ${index}`);
   if (bytes.length !== pieceLength(index, info) || info.pieces[index].length !== 20) return false;
   const l = load(opts.libPath);
-  return await withContext(l, (opts.devices ?? [0])[0], 0, async (ctx) => {
+  // its own cached context (slot -1): a one-piece layout on a bulk call's context would free that context's
+  // payload (tv_set_layout keeps an allocation only while the new geometry is at least half of it)
+  return await withContext(l, (opts.devices ?? [0])[0], -1, async (ctx) => {
     const n = BigInt(bytes.length);
     check(l, ctx, l.symbols.tv_set_layout(ctx, n, n, 1n, 0n, 1n)); // reuses the context's allocations
     check(l, ctx, l.symbols.tv_set_digests(ctx, ptr(info.pieces[index]), 20n));
