@@ -264,6 +264,9 @@ int tv_host_unregister(void *ptr);
                                     tv_verify_list adds them only to a list of >= 32 x CUs pieces (one workgroup
                                     per CU): a shorter flush would fill the GPU with copies of a few pieces;
                                     2 = add them to every list too (measurement only) */
+#define TV_OPT_TWIN_FILL_READS 14 /* companion workgroups' loads: 0 (default) = every lane of a companion reads its
+                                    main workgroup's first piece (the same instruction stream, 1/32 of the bytes);
+                                    1 = the main workgroup's 32 pieces (round 2; 1.14-1.42 x payload of HBM reads) */
 int tv_set_option(tv_ctx *ctx, int key, int64_t value);
 int tv_get_option(tv_ctx *ctx, int key, int64_t *value);
 

@@ -35,7 +35,7 @@ def _worker(rank, ws, port, q):
     for i in range(0, P, 17):
         pieces[20 * i + 3] ^= 1
     first, count = shard_ranges(P, w)[r]
-    assert first % 8 == 0
+    assert first % 8 == 0 or count == 0       # an empty trailing shard may start anywhere
     full = O.verify_linear(payload, total, L, bytes(pieces))
     # shard-local verify: bits of pieces [first, first+count) (oracle as the stand-in worker)
     sl = bytearray((count + 7) // 8)
@@ -51,11 +51,12 @@ def _worker(rank, ws, port, q):
     out = bytearray((P + 7) // 8)
     for f, b in gathered:
         out[f // 8:f // 8 + len(b)] = b
-    q.put((r, t, ok, bytes(out) == full))
+    placement = bench.rank_placement(dist, w, r, r, bench.pick_device(r, 1), 1)
+    q.put((r, t, ok, bytes(out) == full, placement))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws", [2])
+@pytest.mark.parametrize("ws", [2, 4, 8])
 def test_gloo_two_ranks_shard_and_reduce(ws):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
@@ -68,10 +69,23 @@ def test_gloo_two_ranks_shard_and_reduce(ws):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for r, t, ok, match in res:
+    for r, t, ok, match, placement in res:
         assert t == float(ws)      # max over ranks
         assert ok == float(ws)     # sum over ranks
         assert match               # concatenated slices == single-shard bitfield
+        # every rank sees every rank's placement (gathered over gloo), in rank order
+        assert [p["rank"] for p in placement] == list(range(ws))
+        assert all(p["device"] == 0 and p["local_rank"] == p["rank"] for p in placement)
+
+
+def test_device_placement_rule():
+    """bench.pick_device: LOCAL_RANK on a node where each rank sees all GPUs; 0 when the launcher gives each
+    rank one GPU (HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES); ranks wrap round on fewer GPUs (rehearsals)."""
+    import bench
+    assert [bench.pick_device(r, 8) for r in range(8)] == list(range(8))
+    assert [bench.pick_device(r, 1) for r in range(8)] == [0] * 8
+    assert [bench.pick_device(r, 4) for r in range(8)] == [0, 1, 2, 3, 0, 1, 2, 3]
+    assert bench.pick_device(3, 0) == 0
 
 
 @pytest.mark.gpu

@@ -76,14 +76,15 @@ def test_kernels_agree_and_avail_mask(native, oracle):
     avail = bytearray(rng.randrange(256) for _ in range((P + 7) // 8))
     expect = oracle.verify_linear(payload, total, L, pieces, bytes(avail))
     outs = []
-    # + 2 pairs per workgroup (split, twin), the twin SIMD-placement probe shapes, twin CU-packed (pack 1) and
-    # twin without companion workgroups (pack 2)
+    # + 2 pairs per workgroup (split, twin), the twin SIMD-placement probe shapes, twin CU-packed (pack 1),
+    # twin without companion workgroups (pack 2) and with companions reading all 32 pieces (pack 3)
     for k, pairs, pack in [(k, 0, 0) for k in KERNELS] + [(2, 2, 0), (4, 2, 0), (4, 3, 0), (4, 4, 0), (4, 5, 0),
-                                                          (4, 0, 1), (4, 0, 2)]:
+                                                          (4, 0, 1), (4, 0, 2), (4, 0, 3)]:
         with _ctx(native, k) as ctx:
             ctx.set_option(native.TV_OPT_SPLIT_PAIRS, pairs)
-            ctx.set_option(native.TV_OPT_TWIN_PACK, pack & 1)
+            ctx.set_option(native.TV_OPT_TWIN_PACK, pack & 1 if pack != 3 else 0)
             ctx.set_option(native.TV_OPT_TWIN_FILL, 0 if pack == 2 else 1)
+            ctx.set_option(native.TV_OPT_TWIN_FILL_READS, 1 if pack == 3 else 0)
             ctx.set_layout(total, L, P)
             ctx.set_digests(pieces)
             ctx.stage(0, payload)
@@ -261,7 +262,8 @@ def test_geometry_that_overflows_offsets_is_rejected(native):
 def test_twin_companions_exact(native, oracle, L, P, last):
     """Twin companion workgroups (TV_OPT_TWIN_FILL, default on) re-hash main pieces and must write nothing:
     with a handful of pieces nearly the whole 2 x CUs grid is companions.  Verify (corrupted digests, an
-    availability mask), creation mode and the list path equal the oracle with companions on and off."""
+    availability mask), creation mode and the list path equal the oracle with companions on and off, reading
+    one piece or all 32 of the workgroup they copy."""
     total = L * (P - 1) + last
     payload = oracle.synth_fill(P * 7 + 1, 0, total)
     good = oracle.hash_pieces(payload, total, L, P)
@@ -274,9 +276,11 @@ def test_twin_companions_exact(native, oracle, L, P, last):
         avail[0] &= 0xBF                       # piece 1 unavailable
     expect = oracle.verify_linear(payload, total, L, bytes(pieces), bytes(avail))
     lst = [P - 1, 0, P // 2, P - 1] + list(range(P))
-    for fill in (1, 0):
+    # companions on (1; 2 also on short lists), with either read mode, and off
+    for fill, reads in [(1, 0), (1, 1), (2, 0), (2, 1), (0, 0)]:
         with _ctx(native, 4) as ctx:
             ctx.set_option(native.TV_OPT_TWIN_FILL, fill)
+            ctx.set_option(native.TV_OPT_TWIN_FILL_READS, reads)
             ctx.set_layout(total, L, P)
             ctx.stage(0, payload)
             assert ctx.hash() == good, fill

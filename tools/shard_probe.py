@@ -2,7 +2,7 @@
 exact per-GPU geometry the driver's multi-GPU bench gives each rank, for rocprofv3 kernel traces and PMC passes.
 
     python tools/shard_probe.py [--pieces 51200] [--piece-mib 4] [--shards 2] [--rank 0]
-                                [--kernel 0] [--twin-fill 1] [--reps 5] [--warmup 2]
+                                [--kernel 0] [--twin-fill 1] [--fill-reads 0] [--reps 5] [--warmup 2]
 
 Fills the shard with the synthetic payload on the device, hashes it (creation mode) to get the digests,
 corrupts 1 %, then times `reps` verify calls (HIP events on the library's stream) and checks every bit.
@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--kernel", type=int, default=0)
     ap.add_argument("--twin-fill", type=int, default=1)
+    ap.add_argument("--fill-reads", type=int, default=0)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     a = ap.parse_args()
@@ -37,6 +38,7 @@ def main():
     with N.Context(0) as ctx:
         ctx.set_option(N.TV_OPT_KERNEL, a.kernel)
         ctx.set_option(N.TV_OPT_TWIN_FILL, a.twin_fill)
+        ctx.set_option(N.TV_OPT_TWIN_FILL_READS, a.fill_reads)
         ctx.set_layout(L * P, L, P, first, count)
         ctx.fill_synthetic(4)
         dig = bytearray(ctx.hash())
@@ -58,7 +60,7 @@ def main():
     gbps = L * count / (avg / 1e3) / 1e9
     ceil = bench.piece_ceiling(kernel, count)
     print(json.dumps({"pieces_per_gpu": count, "piece_length": L, "shard": [first, count], "shards": a.shards,
-                      "kernel": bench.KERNEL_NAMES.get(kernel, kernel), "twin_fill": a.twin_fill, "workgroups": wgs,
+                      "kernel": bench.KERNEL_NAMES.get(kernel, kernel), "twin_fill": a.twin_fill, "fill_reads": a.fill_reads, "workgroups": wgs,
                       "kernel_ms": [round(x, 3) for x in ms], "kernel_ms_avg": round(avg, 3),
                       "kernel_ms_median": round(statistics.median(ms), 3), "gbps": round(gbps, 1),
                       "piece_ceiling_gbps": round(ceil, 1), "frac_of_piece_ceiling": round(gbps / ceil, 4),

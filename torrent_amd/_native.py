@@ -33,6 +33,7 @@ TV_OPT_RESIDENT = 10
 TV_OPT_DEBUG_REBOUNCE = 11
 TV_OPT_TWIN_PACK = 12
 TV_OPT_TWIN_FILL = 13
+TV_OPT_TWIN_FILL_READS = 14
 
 TV_COUNTER_PAYLOAD_ALLOCS = 1
 TV_COUNTER_DEVICE_ALLOCS = 2

@@ -145,6 +145,7 @@ struct tv_ctx {
     bool debug_rebounce = false;             // TV_OPT_DEBUG_REBOUNCE
     bool twin_pack = false;                  // TV_OPT_TWIN_PACK
     int twin_fill = 1;                       // TV_OPT_TWIN_FILL: 0 off, 1 auto, 2 also on short lists
+    bool fill_all = false;                   // TV_OPT_TWIN_FILL_READS
     hipStream_t pack_stream = nullptr;       // twin launches CU-masked to pack_cus CUs (TV_OPT_TWIN_PACK)
     int pack_cus = 0;
 
@@ -448,8 +449,10 @@ int launch_resident(tv_ctx* c, const TvPieces& p_in, int kernel, bool hash) {
     // (PMC GRBM_GUI_ACTIVE: 1,806 vs 1,727; sleeping fillers do not help, working ones do: DESIGN.md section 5).
     // With fewer real workgroups than 2 per CU, companions fill the grid to 2 x CUs: they re-hash main
     // workgroups' pieces on otherwise idle SIMDs and discard the result (TV_OPT_TWIN_FILL, default on).
-    if (kernel == TV_KERNEL_TWIN && c->twin_fill && !c->twin_pack && (c->split_pairs < 2 || c->split_pairs > 5))
+    if (kernel == TV_KERNEL_TWIN && c->twin_fill && !c->twin_pack && (c->split_pairs < 2 || c->split_pairs > 5)) {
         p.fill_to = 2u * (uint32_t)c->cus;
+        p.fill_all = c->fill_all ? 1u : 0u;
+    }
     if (kernel == TV_KERNEL_TWIN && c->twin_pack && (c->split_pairs < 2 || c->split_pairs > 5)) {
         // 2-wave twin workgroups, 60 KiB of LDS each: at most two per CU.  Fewer than 2 x CUs of them: mask
         // the launch to ceil(wgs / 2) CUs so that every busy CU holds two (TV_OPT_TWIN_PACK).
@@ -1114,6 +1117,10 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
             if (value < 0 || value > 2) return fail(c, TV_ERR_ARG, "TV_OPT_TWIN_FILL must be 0, 1 or 2");
             c->twin_fill = (int)value;
             return TV_OK;
+        case TV_OPT_TWIN_FILL_READS:
+            if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_TWIN_FILL_READS must be 0 or 1");
+            c->fill_all = value != 0;
+            return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
@@ -1135,6 +1142,7 @@ int tv_get_option(tv_ctx* c, int key, int64_t* value) {
         case TV_OPT_DEBUG_REBOUNCE: *value = c->debug_rebounce ? 1 : 0; return TV_OK;
         case TV_OPT_TWIN_PACK: *value = c->twin_pack ? 1 : 0; return TV_OK;
         case TV_OPT_TWIN_FILL: *value = c->twin_fill; return TV_OK;
+        case TV_OPT_TWIN_FILL_READS: *value = c->fill_all ? 1 : 0; return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
@@ -1694,8 +1702,10 @@ int tv_verify_list(tv_ctx* c, const uint64_t* pieces, uint64_t n, uint8_t* ok_ou
     // fill 2 x CUs workgroups with copies re-hashing the same few pieces (a 1-piece flush: 512 copies) for a
     // ~4 % shorter flush (r03 latency: tools/latency_probe.py)
     const uint64_t list_wgs = (m + 31) / 32;
-    if (kernel == TV_KERNEL_TWIN && (c->twin_fill == 2 || (c->twin_fill == 1 && list_wgs >= (uint64_t)c->cus)))
+    if (kernel == TV_KERNEL_TWIN && (c->twin_fill == 2 || (c->twin_fill == 1 && list_wgs >= (uint64_t)c->cus))) {
         p.fill_to = 2u * (uint32_t)c->cus;
+        p.fill_all = c->fill_all ? 1u : 0u;
+    }
     TV_HIP(c, tv_launch_verify_list(p, kernel, c->stream, &c->last_workgroups));
     TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
     TV_HIP(c, hipMemcpyAsync(reordered ? ok_launch.data() : ok_out, c->d_list_out, m, hipMemcpyDeviceToHost, c->stream));

@@ -36,6 +36,8 @@ struct TvPieces {
     uint32_t fill_to;        // twin: launch this many workgroups in all (0 = the real grid only); the ones past
                              // the real grid are COMPANIONS that re-hash a main workgroup's pieces and discard
                              // the result (TV_OPT_TWIN_FILL)
+    uint32_t fill_all;       // companions: 0 = every lane hashes the main workgroup's FIRST piece (the same
+                             // instruction stream, 1/32 of the reads), 1 = its 32 pieces (TV_OPT_TWIN_FILL_READS)
 };
 
 // workgroups (optional): set to the launch's grid size, companions included.

@@ -475,7 +475,9 @@ __global__ __launch_bounds__(64 * kTwinWaves[SHAPE]) void tv_twin_kernel(TvPiece
     const uint32_t wgi = companion ? (blockIdx.x - real_wgs) % nmain_wgs : blockIdx.x;
     const bool last_grp = !LIST && wgi >= nmain_wgs;
     const uint32_t wg0 = last_grp ? p.last_idx : wgi * span;
-    const uint32_t j = last_grp ? p.last_idx : wg0 + half * 32u + (lane >> 1);
+    // a companion keeps the instruction stream of the workgroup it copies but, unless fill_all, points every
+    // lane at that workgroup's first piece: the same loads, one piece's bytes instead of 32 pieces'
+    const uint32_t j = last_grp ? p.last_idx : (companion && !p.fill_all ? wg0 : wg0 + half * 32u + (lane >> 1));
     const uint32_t jl = last_grp ? p.last_idx : (j < nlim ? j : nlim - 1);
     const uint32_t jj = LIST ? p.idx[jl] : jl;
     const bool is_last = jj == p.last_idx;

@@ -397,20 +397,47 @@ export async function hashPieces(payload: Uint8Array, pieceLength: number, opts:
   });
 }
 
+/** Options of PieceVerifier's flush policy (same defaults as torrent_amd/incremental.py). */
+export interface FlushPolicy {
+  /** flush once this many completed pieces are pending (default 4,096: a flush's time is flat up to there) */
+  flushPieces?: number | null;
+  /** flush once the oldest pending piece is this old (default 10 x the flush cost, >= 5 ms: ~30 ms at 256 KiB) */
+  flushAgeMs?: number | null;
+  /** results of automatic flushes (else they are returned by the next flush()) */
+  onVerified?: (index: number, ok: boolean) => void;
+}
+
+/** GPU time of one list flush of pieces of `pieceLength` bytes: one piece's serial SHA-1, ~0.73 us per 64-B
+ * block (3.0 ms for 256 KiB, whether 1 or 4,096 pieces: profiles/r02/latency_twin.json, profiles/r03). */
+export function flushCostMs(pieceLength: number): number {
+  return (Math.floor((pieceLength + 8) / 64) + 1) * 0.73e-3 + 0.06;
+}
+
 /**
  * Incremental verification on piece completion (SURVEY 8f row f1), for the MsgId.piece handler
  * (torrent.ts:183-193): onBlock() per received 16 KiB block (after validateReceivedBlock and
- * storage.set), flush() verifies every completed piece in ONE list launch (tv_verify_list) and
- * sets its have-bit (torrent.ts:147-149).  Same behaviour as torrent_amd/incremental.py.
+ * storage.set); completed pieces are verified in ONE list launch (tv_verify_list) per flush, and their
+ * have-bits set (torrent.ts:147-149).  The verifier flushes by itself when flushPieces are pending or the
+ * oldest pending piece is flushAgeMs old (a timer is armed when the first piece becomes pending), so a
+ * handler never pays a ~3 ms flush per piece.  Same behaviour as torrent_amd/incremental.py.
  */
 export class PieceVerifier {
   readonly bitfield: Uint8Array;
+  autoFlushes = 0;
   #l: Lib;
   #ctx: Deno.PointerValue;
   #bufs = new Map<number, { bytes: Uint8Array; blocks: Set<number> }>();
   #pending: number[] = [];
+  #pendingSet = new Set<number>();
+  #oldest = 0;
+  #timer: number | undefined;
+  #results: [number, boolean][] = [];
+  #flushPieces: number | null;
+  #flushAgeMs: number | null;
+  #onVerified?: (index: number, ok: boolean) => void;
+  #busy: Promise<unknown> = Promise.resolve();
 
-  constructor(readonly info: InfoDict, opts: VerifyOptions = {}) {
+  constructor(readonly info: InfoDict, opts: VerifyOptions & FlushPolicy = {}) {
     this.#l = load(opts.libPath);
     const P = info.pieces.length;
     const h = new BigUint64Array(1);
@@ -420,12 +447,16 @@ export class PieceVerifier {
     check(this.#l, this.#ctx, this.#l.symbols.tv_set_layout(this.#ctx, BigInt(info.length), BigInt(info.pieceLength), BigInt(P), 0n, BigInt(P)));
     check(this.#l, this.#ctx, this.#l.symbols.tv_set_digests(this.#ctx, ptr(raw), BigInt(raw.length)));
     this.bitfield = new Uint8Array(Math.ceil(P / 8));
+    this.#flushPieces = opts.flushPieces === undefined ? 4096 : opts.flushPieces;
+    this.#flushAgeMs = opts.flushAgeMs === undefined ? Math.max(5, 10 * flushCostMs(info.pieceLength)) : opts.flushAgeMs;
+    this.#onVerified = opts.onVerified;
   }
 
   /** One received block (already validated); true when it completed its piece. */
   async onBlock(index: number, offset: number, block: Uint8Array): Promise<boolean> {
+    await this.#autoFlush();                                  // the age bound, checked on every block
     if (this.bitfield[index >> 3] & (128 >> (index % 8))) return false;
-    if (this.#pending.includes(index)) return false; // complete, waiting for flush(): ignore re-sends
+    if (this.#pendingSet.has(index)) return false; // complete, waiting for a flush: ignore re-sends
     const len = pieceLength(index, this.info);
     if (offset >= len) return false;
     if (offset + block.length > len) block = block.subarray(0, len - offset); // never into the next piece
@@ -436,23 +467,61 @@ export class PieceVerifier {
     if (e.blocks.size < Math.ceil(len / 16384)) return false;
     check(this.#l, this.#ctx, await this.#l.symbols.tv_stage(this.#ctx, BigInt(index * this.info.pieceLength), ptr(e.bytes), BigInt(len)));
     this.#bufs.delete(index);
+    if (this.#pending.length === 0) {
+      this.#oldest = performance.now();
+      // the age bound also holds when no further block arrives
+      if (this.#flushAgeMs !== null) this.#timer = setTimeout(() => void this.#autoFlush(), this.#flushAgeMs);
+    }
     this.#pending.push(index);
+    this.#pendingSet.add(index);
+    await this.#autoFlush();                                  // the count bound
     return true;
   }
 
-  /** Verify all completed pieces in one launch; returns [index, ok] and sets the have-bits. */
+  /** Would the policy flush now? */
+  due(): boolean {
+    if (this.#pending.length === 0) return false;
+    if (this.#flushPieces !== null && this.#pending.length >= this.#flushPieces) return true;
+    return this.#flushAgeMs !== null && performance.now() - this.#oldest >= this.#flushAgeMs;
+  }
+
+  async #autoFlush(): Promise<void> {
+    if (!this.due()) return;
+    this.autoFlushes++;
+    const res = await this.#flushPending();
+    if (this.#onVerified) for (const [i, ok] of res) this.#onVerified(i, ok);
+    else this.#results.push(...res);
+  }
+
+  async #flushPending(): Promise<[number, boolean][]> {
+    // one list launch at a time on the verifier's context (the timer and onBlock may both flush)
+    const run = this.#busy.then(async () => {
+      if (this.#pending.length === 0) return [] as [number, boolean][];
+      clearTimeout(this.#timer);
+      const pending = this.#pending;
+      this.#pending = [];
+      this.#pendingSet.clear();
+      const idx = BigUint64Array.from(pending.map(BigInt));
+      const ok = new Uint8Array(idx.length);
+      check(this.#l, this.#ctx, await this.#l.symbols.tv_verify_list(this.#ctx, ptr(new Uint8Array(idx.buffer)), BigInt(idx.length), ptr(ok)));
+      const out: [number, boolean][] = pending.map((i, k) => [i, ok[k] === 1]);
+      for (const [i, good] of out) if (good) this.bitfield[i >> 3] |= 128 >> (i % 8);
+      return out;
+    });
+    this.#busy = run.catch(() => {});
+    return await run;
+  }
+
+  /** Verify all completed pieces in one launch; returns [index, ok] (after the results of automatic
+   * flushes not yet handed out) and sets the have-bits. */
   async flush(): Promise<[number, boolean][]> {
-    if (this.#pending.length === 0) return [];
-    const idx = BigUint64Array.from(this.#pending.map(BigInt));
-    const ok = new Uint8Array(idx.length);
-    check(this.#l, this.#ctx, await this.#l.symbols.tv_verify_list(this.#ctx, ptr(new Uint8Array(idx.buffer)), BigInt(idx.length), ptr(ok)));
-    const out: [number, boolean][] = this.#pending.map((i, k) => [i, ok[k] === 1]);
-    for (const [i, good] of out) if (good) this.bitfield[i >> 3] |= 128 >> (i % 8);
-    this.#pending = [];
-    return out;
+    const earlier = this.#results;
+    this.#results = [];
+    return [...earlier, ...await this.#flushPending()];
   }
 
   close(): void {
+    clearTimeout(this.#timer);
     this.#l.symbols.tv_destroy(this.#ctx);
   }
 }
