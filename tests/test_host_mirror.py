@@ -472,3 +472,14 @@ def test_files_shard_zero_length_segments_match_fs_storage(tmp_path, monkeypatch
         got += [bool((avail[j >> 3] >> (7 - (j & 7))) & 1) for j in range(count)]
     assert got == expect
     assert sorted(str(x) for x in root.rglob("*")) == before      # nothing created
+
+
+def test_file_paths_equal_os_path_join():
+    """Storage.file_paths' fast join equals os.path.join(*dir, *path) (fsStorage.get's join, storage.ts:153)
+    for every kind of part: empty, absolute, containing separators."""
+    cases = [["a"], ["a", "b"], ["", "a"], ["a", ""], ["/abs"], ["a", "/b"], ["a", "", "b"], ["a/b"], ["a//b"],
+             ["a/"], ["x", "y", "z"]]
+    for d in ["/tmp/x", "/", "rel/dir", ".", "/tmp/x/"]:
+        info = make_info(4096, bytes(20), "t", files=[FileInfo(1, c) for c in cases])
+        st = Storage(FsStorage(), info, d)
+        assert st.file_paths() == [os.path.join(*st.dir_path, *c) for c in cases], d

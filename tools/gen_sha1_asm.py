@@ -383,6 +383,22 @@ TWIN_READ_BYTES = 2048
 TWIN_WAITS = tuple(int(x) for x in os.environ.get("TV_GEN_TWIN_WAITS", "0-5").split("-"))   # reads waited for, in pairs
 TWIN_PRE = os.environ.get("TV_GEN_TWIN_PRE", "1") == "1"   # loop: issue the next block's reads after round 79
 TWIN_NONOP = os.environ.get("TV_GEN_TWIN_NONOP", "1") == "1"  # loop: 4-byte instructions paired without s_nop
+# 64-byte placement of the twin loops: rounds loop head at (4 + 8 k) mod 64 for TV_GEN_TWIN_RALIGN = k, helper
+# loop head at 4 m mod 64 for TV_GEN_TWIN_HALIGN = m ("none": wherever the code before them puts them).  The
+# rounds loop at 4 mod 64 (and the helper's at 60) is 0.7-1.6 % faster at cfg2 than at 28, 52 or 60
+# (profiles/r03/twin_ralign.jsonl: 11.89-11.91 vs 11.98-12.08 ms), so both are pinned there: a code change
+# before the loops no longer moves them.
+TWIN_RALIGN = os.environ.get("TV_GEN_TWIN_RALIGN", "0")
+TWIN_HALIGN = os.environ.get("TV_GEN_TWIN_HALIGN", "15")
+TWIN_RALIGN = None if TWIN_RALIGN == "none" else TWIN_RALIGN
+TWIN_HALIGN = None if TWIN_HALIGN == "none" else TWIN_HALIGN
+# the same for the split kernel's loops: rounds loop head at 8 k mod 64 (TV_GEN_SPLIT_RALIGN = k; its block
+# bodies start with .p2align 3), helper loop head at 4 m mod 64 (TV_GEN_SPLIT_HALIGN = m).  At 25,600 pieces
+# the rounds loop's eight placements are within 0.5 % of each other (profiles/r03/split_ralign.jsonl); k = 6
+# (48 mod 64) was the fastest of the two rounds by 0.2 % and is pinned so that code changes cannot move it.
+SPLIT_RALIGN = os.environ.get("TV_GEN_SPLIT_RALIGN", "6")
+SPLIT_HALIGN = os.environ.get("TV_GEN_SPLIT_HALIGN")
+SPLIT_RALIGN = None if SPLIT_RALIGN == "none" else SPLIT_RALIGN
 # loop: when the next block's reads are issued -- "end": all 10 after round 79; "mid": 0-4 after the round-40
 # wait, 5-9 after round 79; "spread": read k after round 8k+7 (each as soon as its registers are consumed)
 TWIN_ISSUE = os.environ.get("TV_GEN_TWIN_ISSUE", "mid")   # mid: +1.8 % at cfg2 over end, spread -2 % (profiles/r02/twin_ab.jsonl.log)
@@ -435,6 +451,9 @@ def rounds_loop_text() -> str:
         L.extend(_emit_lines([("ds_read_b128", q, q * 1024) for q in range(10)]))
     if SPLIT_PRE:
         L.extend(_emit_lines([("ds_read_b128", q, q * 1024) for q in range(READ_AHEAD)]))
+    if SPLIT_RALIGN is not None:
+        L.append(".p2align 6")
+        L.extend(["s_nop 0"] * (2 * int(SPLIT_RALIGN)))
     L.append("L_rloop_%=:")
     for k in range(LDS_BUFS):
         if SPLIT_PRE:
@@ -515,7 +534,10 @@ def twin_rounds_loop_text() -> str:
         # The first wait sits at 4 mod 8 (the previous block's tail -- four 4-byte h adds, barrier, s_cmp,
         # s_cbranch -- precedes it; h0 += r0 is the 8-byte VOP3 form), and the loop counter's s_sub pairs
         # with the round-40 wait.
-        L += [".p2align 3", "s_nop 0", "L_rloop_%=:"]
+        if TWIN_RALIGN is not None:
+            L += [".p2align 6"] + ["s_nop 0"] * (1 + 2 * int(TWIN_RALIGN)) + ["L_rloop_%=:"]
+        else:
+            L += [".p2align 3", "s_nop 0", "L_rloop_%=:"]
         for k in range(LDS_BUFS):
             body = _emit_lines(gen_twin(k * RING_BYTES, reads_next=((k + 1) % LDS_BUFS) * RING_BYTES))
             nops = [i for i, x in enumerate(body) if x == "s_nop 0"]
@@ -600,6 +622,12 @@ def helper_loop_text(twin: bool = False) -> str:
     L.append("s_sub_u32 %[cnt], %[nraw], 1")
     L.append("s_cmp_eq_u32 %[cnt], 0")
     L.append("s_cbranch_scc1 L_hdone_%=")
+    if twin and TWIN_HALIGN is not None:
+        L.append(".p2align 6")
+        L.extend(["s_nop 0"] * int(TWIN_HALIGN))
+    if not twin and SPLIT_HALIGN is not None:
+        L.append(".p2align 6")
+        L.extend(["s_nop 0"] * int(SPLIT_HALIGN))
     L.append("L_hloop_%=:")
     period = 2 * LDS_BUFS // (2 if LDS_BUFS % 2 == 0 else 1)   # lcm(prefetch register sets 2, LDS buffers)
     for k in range(period):

@@ -50,7 +50,9 @@ def main():
         ref = None
         for rnd in range(2):                     # two interleaved passes over the variants
             for name in names:
-                env = dict(os.environ, TV_ROOT=ROOT,
+                # a variant may bring its own host package (an older build's ABI): build/variants/root_<name>
+                vroot = os.path.join(ROOT, "build", "variants", f"root_{name}")
+                env = dict(os.environ, TV_ROOT=vroot if os.path.isdir(vroot) else ROOT,
                            TORRENT_VERIFY_LIB=os.path.join(ROOT, "build", "variants", f"libtv_{name}.so"))
                 r = subprocess.run([sys.executable, "-c", CHILD, str(P), str(reps), str(kernel), str(gib)], env=env,
                                    capture_output=True, text=True, timeout=300)

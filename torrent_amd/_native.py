@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 from typing import Optional
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
@@ -272,8 +273,12 @@ class Context:
             return []
         if any(len(v) != n for v in (file_offsets, linear_offsets, lens)):
             raise ValueError("stage_files: paths, file_offsets, linear_offsets and lens differ in length")
-        # all paths in one NUL-separated buffer (paths hold no NUL), and the char* array pointing into it
-        blob = b"\0".join(os.fsencode(x) for x in paths) + b"\0"
+        # all paths in one NUL-separated buffer (paths hold no NUL), and the char* array pointing into it;
+        # str paths are encoded in one call (os.fsencode per path cost ~5 ms for 10,000 files)
+        if all(type(x) is str for x in paths):
+            blob = ("\0".join(paths) + "\0").encode(sys.getfilesystemencoding(), "surrogateescape")
+        else:
+            blob = b"\0".join(os.fsencode(x) for x in paths) + b"\0"
         if blob.count(b"\0") != n:
             raise ValueError("stage_files: a path contains a NUL byte")
         cblob = ctypes.create_string_buffer(blob, len(blob))

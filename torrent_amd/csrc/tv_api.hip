@@ -1365,48 +1365,41 @@ struct SmallSeg {
     uint64_t k, file_offset, linear, len, packed;
 };
 
-void read_segments(const std::vector<SmallSeg>& segs, size_t lo, size_t hi, const char* const* paths,
+void read_segments(Pool& pool, const std::vector<SmallSeg>& segs, size_t lo, size_t hi, const char* const* paths,
                    uint8_t* slot, int32_t* status, int threads, std::string* first_err, std::mutex* err_mu) {
-    // work items: (segment, part) with parts of at most 4 MiB, so one long segment is read by many threads
+    // work items: (segment, part) with parts of at most 4 MiB, so one long segment is read by many threads;
+    // run on the lane's persistent workers (a thread spawn per 64 MiB slot cost ~15 x 20-50 us per slot)
     constexpr uint64_t kPart = 4ull << 20;
     std::vector<std::pair<size_t, uint64_t>> items;
     for (size_t q = lo; q < hi; q++)
         for (uint64_t o = 0; o < segs[q].len; o += kPart) items.emplace_back(q, o);
-    std::atomic<size_t> next{0};
-    auto work = [&]() {
-        for (size_t it = next++; it < items.size(); it = next++) {
-            const SmallSeg& sg = segs[items[it].first];
-            const uint64_t part0 = items[it].second, part1 = std::min(sg.len, part0 + kPart);
-            const char* path = paths[sg.k];
-            int e = rw_access(path);  // opened as fsStorage.get opens it: read + write (storage.ts:28-32)
-            const int fd = e ? -1 : open(path, O_RDONLY | O_CLOEXEC);
-            if (fd < 0) {
-                if (!e) e = errno;
-            } else {
-                uint64_t o = part0;
-                while (o < part1) {
-                    const ssize_t got = pread(fd, slot + sg.packed + o, part1 - o, (off_t)(sg.file_offset + o));
-                    if (got < 0 && errno == EINTR) continue;
-                    if (got <= 0) {
-                        e = got < 0 ? errno : EIO;  // 0 bytes: the file is shorter than the segment
-                        break;
-                    }
-                    o += (uint64_t)got;
+    pool.run(threads, items.size(), [&](uint64_t it) {
+        const SmallSeg& sg = segs[items[it].first];
+        const uint64_t part0 = items[it].second, part1 = std::min(sg.len, part0 + kPart);
+        const char* path = paths[sg.k];
+        int e = rw_access(path);  // opened as fsStorage.get opens it: read + write (storage.ts:28-32)
+        const int fd = e ? -1 : open(path, O_RDONLY | O_CLOEXEC);
+        if (fd < 0) {
+            if (!e) e = errno;
+        } else {
+            uint64_t o = part0;
+            while (o < part1) {
+                const ssize_t got = pread(fd, slot + sg.packed + o, part1 - o, (off_t)(sg.file_offset + o));
+                if (got < 0 && errno == EINTR) continue;
+                if (got <= 0) {
+                    e = got < 0 ? errno : EIO;  // 0 bytes: the file is shorter than the segment
+                    break;
                 }
-                close(fd);
+                o += (uint64_t)got;
             }
-            if (e) {
-                status[sg.k] = TV_ERR_IO;
-                std::lock_guard<std::mutex> g(*err_mu);
-                if (first_err->empty()) *first_err = std::string(path) + ": " + strerror(e);
-            }
+            close(fd);
         }
-    };
-    const int t = (int)std::min<size_t>((size_t)std::max(1, threads), items.size());
-    std::vector<std::thread> th;
-    for (int i = 1; i < t; i++) th.emplace_back(work);
-    work();
-    for (auto& x : th) x.join();
+        if (e) {
+            status[sg.k] = TV_ERR_IO;
+            std::lock_guard<std::mutex> g(*err_mu);
+            if (first_err->empty()) *first_err = std::string(path) + ": " + strerror(e);
+        }
+    });
 }
 
 }  // namespace
@@ -1535,7 +1528,7 @@ int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64
         SlotLease slot(c, 0);  // lent until every copy out of it is queued
         rc = slot.take();
         if (rc) return rc;
-        read_segments(small, i, j, paths, slot.ptr(), status_out, c->file_threads, &first_err, &err_mu);
+        read_segments(c->pool[0], small, i, j, paths, slot.ptr(), status_out, c->file_threads, &first_err, &err_mu);
         for (size_t q = i; q < j;) {  // one copy per run of readable, linear-contiguous segments
             if (status_out[small[q].k] != TV_OK) { q++; continue; }
             size_t r = q + 1;

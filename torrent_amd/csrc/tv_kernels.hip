@@ -258,8 +258,15 @@ raw_done:
     finish<HASH>(p, writer, jj, j0, h, last_grp);
 }
 
+// TV_LANE_PAD (A/B knob): 64-byte-align the kernel's first instructions, then TV_LANE_PAD 4-byte s_nops, which
+// moves the raw-block loop through the 16 word positions of a 64-byte line (tools/build_variants.py D_TV_LANE_PAD)
+#define TV_STR2(x) #x
+#define TV_STR(x) TV_STR2(x)
 template <bool HASH>
 __global__ __launch_bounds__(256) void tv_lane_kernel(TvPieces p) {
+#ifdef TV_LANE_PAD
+    asm volatile(".p2align 6\n.rept " TV_STR(TV_LANE_PAD) "\ns_nop 0\n.endr\n" ::: "memory");
+#endif
     lane_group<HASH>(p, blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
 }
 

@@ -156,14 +156,17 @@ class Storage:
             else:
                 base = os.path.join(*self.dir_path) if self.dir_path else ""
                 head = base if (not base or base.endswith(os.sep)) else base + os.sep
+                sep, dsep = os.sep, os.sep + os.sep
                 out = []
                 for f in self.info.files:
-                    parts = f.path
-                    # os.path.join(*dir, *parts) without its per-call cost when no part is empty or absolute
-                    if parts and all(q and not q.startswith(os.sep) for q in parts):
-                        out.append(head + os.sep.join(parts))
+                    # os.path.join(*dir, *parts) without its per-call cost: the plain join equals it exactly
+                    # when no part is empty or absolute, i.e. when the joined string neither starts nor ends
+                    # with the separator and holds no doubled separator
+                    j = sep.join(f.path)
+                    if j and j[0] != sep and j[-1] != sep and dsep not in j:
+                        out.append(head + j)
                     else:
-                        out.append(os.path.join(*self.dir_path, *parts))
+                        out.append(os.path.join(*self.dir_path, *f.path))
                 self._joined = out
         return self._joined
 
