@@ -1,0 +1,154 @@
+"""Seeded random layouts through every host path on the HIP library, against the reference's semantics.
+
+For each seed a torrent is drawn with a random piece length (powers of two and odd lengths, some not a
+multiple of 64), 1-40 files with zero-length, tiny and piece-boundary-aligned files, missing and truncated
+files on disk, corrupted pieces, and sometimes a ragged digest string or more digests than data.  The
+expected bit of piece i follows the reference exactly: Storage.get(i * L, pieceLength(i)) over the on-disk
+files (storage.ts:50-65, 89-137; the Python mirror, pinned by tests/test_host_mirror.py) is non-null and its
+SHA-1 (hashlib, the checker) equals slice i of info.pieces (metainfo.ts:111, _bytes.ts:92-99).  The GPU
+bitfields of verify_pieces (Storage.get reads), verify_payload (resident and streamed), verify_stream
+(bounded ring) and verify_files (files on disk, tv_stage_files) must all equal it, on one and on three
+shards."""
+import hashlib
+import random
+
+import pytest
+
+SEEDS = list(range(24))
+
+
+def _draw(seed):
+    from torrent_amd.metainfo import FileInfo, make_info
+    rng = random.Random(1000 + seed)
+    L = rng.choice([64, 100, 1000, 4096, 16384 + 7, 65536, 262144])
+    n_files = rng.choice([1, 1, 2, 5, 17, 40])
+    target = rng.randrange(L // 2 + 1, min(60 * L, 3 << 20))
+    sizes = []
+    while sum(sizes) < target and len(sizes) < n_files:
+        kind = rng.random()
+        if kind < 0.15:
+            sizes.append(0)
+        elif kind < 0.3:
+            sizes.append(rng.randrange(1, 64))
+        elif kind < 0.45:                          # end the file exactly on a piece boundary
+            pos = sum(sizes)
+            sizes.append((-pos) % L or L)
+        else:
+            sizes.append(rng.randrange(1, 4 * L))
+    if sum(sizes) == 0:
+        sizes.append(L + 3)
+    total = sum(sizes)
+    P = -(-total // L)
+    payload = bytearray(rng.getrandbits(8) for _ in range(total))
+    digests = bytearray(b"".join(hashlib.sha1(bytes(payload[i * L:(i + 1) * L])).digest() for i in range(P)))
+    for i in rng.sample(range(P), max(1, P // 10)):            # corrupted data
+        payload[i * L + rng.randrange(min(L, total - i * L))] ^= 1 << rng.randrange(8)
+    extra = rng.random() < 0.2
+    if extra:                                                   # more digests than data: those pieces null
+        digests += bytes(rng.getrandbits(8) for _ in range(20 * rng.randrange(1, 9)))
+    if rng.random() < 0.2:                                      # ragged digest string: last slice short
+        digests = digests[:-rng.randrange(1, 20)]
+    single = len(sizes) == 1 and rng.random() < 0.5
+    files = None if single else [FileInfo(s, [f"s{k % 3}", f"f{k}.bin"]) for k, s in enumerate(sizes)]
+    info = make_info(L, bytes(digests), "t.bin", files=files, length=total)
+    # on disk: some files missing, some truncated
+    missing, short = set(), {}
+    for k, s in enumerate(sizes):
+        r = rng.random()
+        if r < 0.08:
+            missing.add(k)
+        elif r < 0.14 and s > 0:
+            short[k] = rng.randrange(s)
+    return info, bytes(payload), sizes, missing, short, single
+
+
+def _disk(info, payload, sizes, missing, short, single):
+    """{path tuple: bytes} as on disk (missing files absent, short ones truncated)."""
+    out, o = {}, 0
+    for k, s in enumerate(sizes):
+        if k not in missing:
+            key = (info.name,) if single else tuple(info.files[k].path)
+            out[key] = payload[o:o + short.get(k, s)]
+        o += s
+    return out
+
+
+def _expected(info, storage):
+    from torrent_amd.piece import piece_length
+    P, L = info.n_pieces, info.piece_length
+    bits = []
+    for i in range(P):
+        got = storage.get(i * L, piece_length(i, info))
+        d = info.pieces_raw[20 * i:20 * i + 20]
+        bits.append(int(got is not None and len(d) == 20 and hashlib.sha1(bytes(got)).digest() == d))
+    return bits
+
+
+def _bits(bf, n):
+    return [(bf[i >> 3] >> (7 - (i & 7))) & 1 for i in range(n)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", SEEDS)
+def test_random_layouts_every_host_path(native, tmp_path, monkeypatch, seed):
+    import shutil
+    from torrent_amd import MemoryStorage, Storage, verify_files, verify_payload, verify_pieces, verify_stream
+    from torrent_amd.piece import piece_length
+    from torrent_amd.storage import fs_storage
+    info, payload, sizes, missing, short, single = _draw(seed)
+    P, L = info.n_pieces, info.piece_length
+    monkeypatch.chdir(tmp_path)
+    disk = _disk(info, payload, sizes, missing, short, single)
+    # in memory: Storage paths are [*dir, name] / [*dir, *file.path] (storage.ts:99-114)
+    mem = MemoryStorage()
+    st = Storage(mem, info, str(tmp_path / "dl"))
+    mem.files = {tuple(st.dir_path) + k: bytearray(v) for k, v in disk.items()}
+    want = _expected(info, st)
+    # on disk, for verify_files; its expectation is fsStorage.get's (a zero-length file in a missing
+    # directory does not open), taken on a copy because that get creates files
+    for root in ("dl", "ref"):
+        for k, data in disk.items():
+            p = tmp_path.joinpath(root, *k)
+            p.parent.mkdir(parents=True, exist_ok=True)
+            p.write_bytes(data)
+    want_fs = _expected(info, Storage(fs_storage, info, str(tmp_path / "ref")))
+    shutil.rmtree(tmp_path / "ref")
+    # the linear payload's availability as Storage.get sees it (verify_payload takes one buffer)
+    avail = bytearray((P + 7) // 8)
+    for i in range(P):
+        if st.get(i * L, piece_length(i, info)) is not None:
+            avail[i >> 3] |= 0x80 >> (i & 7)
+    lin = payload[:info.length]
+    before = sorted(str(x) for x in (tmp_path / "dl").rglob("*"))
+    for devices in ([0], [0, 0, 0]):
+        assert _bits(verify_pieces(info, st, devices=devices), P) == want, ("pieces", seed, devices)
+        assert _bits(verify_payload(info, lin, devices=devices, avail=bytes(avail)), P) == want, ("payload", seed)
+        assert _bits(verify_payload(info, lin, devices=devices, resident=False, avail=bytes(avail)), P) == want, \
+            ("payload streamed", seed)
+        assert _bits(verify_stream(info, st.get, devices=devices), P) == want, ("stream", seed, devices)
+        assert _bits(verify_files(info, str(tmp_path / "dl"), devices=devices, threads=3), P) == want_fs, \
+            ("files", seed, devices)
+    assert sorted(str(x) for x in (tmp_path / "dl").rglob("*")) == before      # verify_files created nothing
+
+
+def test_fuzz_layouts_cover_the_edge_cases():
+    """The seeds above draw every edge case at least once (CPU-only check of the generator)."""
+    seen = set()
+    for seed in SEEDS:
+        info, payload, sizes, missing, short, single = _draw(seed)
+        L = info.piece_length
+        seen.add("odd_L" if L % 64 else "L64")
+        seen |= {"zero_file"} if 0 in sizes else set()
+        seen |= {"missing"} if missing else set()
+        seen |= {"short"} if short else set()
+        seen |= {"single"} if single else {"multi"}
+        seen |= {"ragged"} if len(info.pieces_raw) % 20 else set()
+        seen |= {"extra_digests"} if len(info.pieces_raw) // 20 > -(-info.length // L) else set()
+        seen |= {"short_last"} if info.length % L else set()
+        ends, o = [], 0
+        for s in sizes:
+            o += s
+            ends.append(o)
+        seen |= {"boundary_file"} if any(e % L == 0 and 0 < e < info.length for e in ends) else set()
+    assert {"odd_L", "L64", "zero_file", "missing", "short", "single", "multi", "ragged", "extra_digests",
+            "short_last", "boundary_file"} <= seen, seen

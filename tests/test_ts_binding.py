@@ -1,0 +1,248 @@
+"""ts/verify.ts, executed: the Deno binding run under Node 12 with a Deno FFI shim (tests/ts_harness).
+
+Deno is absent from the image, so the binding a maintainer would add to the reference is type-erased
+(tests/ts_harness/erase_ts.py: annotations, interfaces, casts, generics, modifiers only) and run by Node 12
+with `Deno.dlopen` / `Deno.UnsafePointer` / `Deno.UnsafePointerView` provided by a small N-API addon
+(tests/ts_harness/deno_ffi.cc) that calls the real libtorrent_verify.so.  On CPU: the erased module parses,
+its pure helpers equal the Python host's, and the whole symbol table binds through the shim.  On the GPU
+(`-m gpu`): verifyPieces, verifyStream, verifyFiles (zero-length segments in a directory's place and in a
+missing directory), verifyPiece, hashPieces and the PieceVerifier flush policy return the reference's bits,
+computed here with the Python mirror and hashlib as the checker -- the same inputs the Python host is
+tested on, so the two hosts cannot drift apart unseen.
+"""
+import base64
+import hashlib
+import json
+import os
+import random
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HARNESS = os.path.join(ROOT, "tests", "ts_harness")
+ADDON = os.path.join(HARNESS, "deno_ffi.node")
+LIB = os.path.join(ROOT, "torrent_amd", "libtorrent_verify.so")
+NODE = shutil.which("node")
+
+pytestmark = pytest.mark.skipif(NODE is None, reason="needs node")
+
+
+def build_addon() -> str:
+    """Compile the N-API Deno FFI shim (test infrastructure; __graft_entry__.build() also builds it)."""
+    src = os.path.join(HARNESS, "deno_ffi.cc")
+    if not os.path.exists(ADDON) or os.path.getmtime(ADDON) < os.path.getmtime(src):
+        subprocess.check_call(["g++", "-O2", "-shared", "-fPIC", "-std=c++17", "-DNODE_GYP_MODULE_NAME=deno_ffi",
+                               "-I/usr/include/node", src, "-o", ADDON])
+    return ADDON
+
+
+def erased_module(tmp_path) -> str:
+    import sys
+    sys.path.insert(0, HARNESS)
+    from erase_ts import erase
+    out = os.path.join(str(tmp_path), "verify.mjs")
+    with open(out, "w") as f:
+        f.write(erase(open(os.path.join(ROOT, "ts", "verify.ts")).read()))
+    return out
+
+
+def run_node(tmp_path, script: str) -> str:
+    path = os.path.join(str(tmp_path), "probe.mjs")
+    with open(path, "w") as f:
+        f.write(script)
+    r = subprocess.run([NODE, path], capture_output=True, text=True, timeout=120, cwd=HARNESS)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+def test_erased_binding_parses_and_helpers_match(tmp_path):
+    """The erased module is valid Node 12 JavaScript; shardRanges and flushCostMs equal the Python host's."""
+    from torrent_amd.incremental import flush_cost_ms
+    from torrent_amd.verify import shard_ranges
+    mod = erased_module(tmp_path)
+    r = subprocess.run([NODE, "--check", mod], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    build_addon()
+    cases = [(0, 1), (1, 1), (7, 3), (203, 8), (51200, 8), (16384, 3), (100, 16)]
+    out = run_node(tmp_path, f"""
+import {{ createRequire }} from "module";
+const require = createRequire("{HARNESS}/");
+require("./deno_shim.js");
+import("{mod}").then((m) => {{
+  const cases = {json.dumps(cases)};
+  console.log(JSON.stringify({{ shards: cases.map(([p, n]) => m.shardRanges(p, n)),
+                               costs: [16384, 262144, 1048576, 4194304].map((L) => m.flushCostMs(L)) }}));
+}}).catch((e) => {{ console.error(e); process.exit(1); }});
+""")
+    got = json.loads(out)
+    assert got["shards"] == [[list(x) for x in shard_ranges(p, n)] for p, n in cases]
+    for L, c in zip([16384, 262144, 1048576, 4194304], got["costs"]):
+        assert abs(c - flush_cost_ms(L)) < 1e-9
+
+
+def test_symbol_table_binds_through_the_shim(tmp_path):
+    """Deno.dlopen of the binding's whole SYMBOLS table on the real library (every symbol resolves, the ABI
+    version check passes): a zero-piece verifyPieces loads the library and returns an empty bitfield without
+    touching a device."""
+    mod = erased_module(tmp_path)
+    build_addon()
+    out = run_node(tmp_path, f"""
+import {{ createRequire }} from "module";
+const require = createRequire("{HARNESS}/");
+require("./deno_shim.js");
+import("{mod}").then(async (m) => {{
+  const info = {{ pieceLength: 16384, length: 0, pieces: [], name: "t", private: 0 }};
+  const bf = await m.verifyPieces(info, {{ async get() {{ return null; }} }}, {{ libPath: "{LIB}" }});
+  console.log(JSON.stringify({{ n: bf.length }}));
+}}).catch((e) => {{ console.error(e); process.exit(1); }});
+""")
+    assert json.loads(out) == {"n": 0}
+
+
+# ------------------------------------------------------------------------------------------------ GPU
+
+def _b64(b) -> str:
+    return base64.b64encode(bytes(b)).decode()
+
+
+def _info_json(L, total, digests, files=None, name="t.bin"):
+    d = {"pieceLength": L, "length": total, "pieces": _b64(digests), "name": name}
+    if files is not None:
+        d["files"] = [{"length": n, "path": list(p)} for n, p in files]
+    return d
+
+
+def _expect_linear(payload, L, digests, unreadable=()):
+    total = len(payload)
+    P = len(digests) // 20 + (1 if len(digests) % 20 else 0)
+    bits = bytearray((P + 7) // 8)
+    for i in range(P):
+        n = (total % L) if (i == P - 1 and total % L) else L
+        d = digests[20 * i:20 * i + 20]
+        if i in unreadable or i * L + n > total or len(d) != 20:
+            continue
+        if hashlib.sha1(payload[i * L:i * L + n]).digest() == d:
+            bits[i >> 3] |= 0x80 >> (i & 7)
+    return bits.hex()
+
+
+@pytest.mark.gpu
+def test_ts_binding_on_the_gpu(native, tmp_path, monkeypatch):
+    from torrent_amd.metainfo import FileInfo, make_info
+    from torrent_amd.piece import BLOCK_SIZE, piece_length
+    from torrent_amd.storage import Storage, fs_storage
+    mod = erased_module(tmp_path)
+    build_addon()
+    rng = random.Random(7)
+    cases, expect = [], {}
+
+    # verifyPieces / verifyStream over in-memory storage: short last piece, corrupted data, unreadable pieces,
+    # a ragged digest string; one and three shards; streamed with a narrow column (several per piece)
+    for k, (L, P, last) in enumerate([(16384, 61, 999), (65536 + 64, 40, 65536 + 64), (262144, 9, 5)]):
+        total = L * (P - 1) + last
+        payload = bytearray(rng.getrandbits(8) for _ in range(total))
+        digests = bytearray(b"".join(hashlib.sha1(bytes(payload[i * L:(i + 1) * L])).digest() for i in range(P)))
+        for i in rng.sample(range(P), 3):
+            payload[i * L] ^= 0x40
+        if k == 2:
+            digests = digests[:-7]
+        unreadable = sorted(rng.sample(range(P), 2))
+        for devices in ([0], [0, 0, 0]):
+            for kind in ("pieces", "stream"):
+                name = f"{kind}{k}_{len(devices)}"
+                cases.append({"name": name, "kind": kind, "info": _info_json(L, total, digests), "devices": devices,
+                              "payload": _b64(payload), "unreadable": unreadable, "chunk": 4096 if k == 1 else 0})
+                expect[name] = _expect_linear(bytes(payload), L, bytes(digests), set(unreadable))
+        # a row of the wrong length makes its piece unreadable (verifyStream)
+        name = f"stream_wrong{k}"
+        cases.append({"name": name, "kind": "stream", "info": _info_json(L, total, digests), "devices": [0],
+                      "payload": _b64(payload), "unreadable": [], "wrongLength": [1]})
+        expect[name] = _expect_linear(bytes(payload), L, bytes(digests), {1})
+
+    # verifyFiles on disk: a directory and a missing directory in zero-length files' places, a missing file,
+    # a short file; expected bits from Storage(fs_storage).get on a copy (that get creates files)
+    L = 4096
+    names = [("a",), ("z_dir",), ("b",), ("nodir", "z"), ("c",), ("z_missing",), ("d",), ("gone",), ("e",), ("short",)]
+    sizes = [3 * L, 0, 2 * L + 100, 0, L - 100, 0, 2 * L, 700, L + 7, 3000]
+    payload = bytes(rng.getrandbits(8) for _ in range(sum(sizes)))
+    P = -(-len(payload) // L)
+    digests = b"".join(hashlib.sha1(payload[i * L:(i + 1) * L]).digest() for i in range(P))
+    files = list(zip(sizes, names))
+    for root in ("dl", "ref"):
+        off = 0
+        for n, p in files:
+            q = tmp_path.joinpath(root, *p)
+            if p == ("z_dir",):
+                q.mkdir(parents=True, exist_ok=True)
+            elif p not in (("nodir", "z"), ("z_missing",), ("gone",)):
+                q.parent.mkdir(parents=True, exist_ok=True)
+                q.write_bytes(payload[off:off + (n - 1 if p == ("short",) else n)])
+            off += n
+    monkeypatch.chdir(tmp_path)
+    info = make_info(L, digests, "t", files=[FileInfo(n, list(p)) for n, p in files])
+    ref = Storage(fs_storage, info, str(tmp_path / "ref"))
+    bits = bytearray((P + 7) // 8)
+    for i in range(P):
+        got = ref.get(i * L, piece_length(i, info))
+        if got is not None and hashlib.sha1(bytes(got)).digest() == digests[20 * i:20 * i + 20]:
+            bits[i >> 3] |= 0x80 >> (i & 7)
+    assert 0 < sum(bin(x).count("1") for x in bits) < P
+    before = sorted(str(x) for x in (tmp_path / "dl").rglob("*"))
+    for devices in ([0], [0, 0]):
+        name = f"files_{len(devices)}"
+        cases.append({"name": name, "kind": "files", "info": _info_json(L, len(payload), digests, files, "t"),
+                      "dir": str(tmp_path / "dl"), "devices": devices})
+        expect[name] = bits.hex()
+
+    # verifyPiece and hashPieces
+    L = 262144
+    blob = bytes(rng.getrandbits(8) for _ in range(3 * L + 12345))
+    digests = b"".join(hashlib.sha1(blob[i * L:(i + 1) * L]).digest() for i in range(4))
+    for i, data, want in [(0, blob[:L], True), (3, blob[3 * L:], True), (1, blob[L:2 * L - 1] + b"x", False),
+                          (2, blob[2 * L:3 * L - 1], False)]:
+        cases.append({"name": f"piece{i}", "kind": "piece", "info": _info_json(L, len(blob), digests),
+                      "index": i, "bytes": _b64(data)})
+        expect[f"piece{i}"] = want
+    cases.append({"name": "hash", "kind": "hash", "payload": _b64(blob), "pieceLength": L})
+    expect["hash"] = digests.hex()
+
+    # PieceVerifier: blocks in random order, one corrupted, automatic flushes at 8 pending pieces
+    L, P = 2 * BLOCK_SIZE, 37
+    total = L * (P - 1) + BLOCK_SIZE + 100
+    payload = bytes(rng.getrandbits(8) for _ in range(total))
+    digests = b"".join(hashlib.sha1(payload[i * L:(i + 1) * L]).digest() for i in range(P))
+    blocks = []
+    for i in range(P):
+        n = L if i < P - 1 else total - (P - 1) * L
+        blocks += [[i, o, payload[i * L + o:i * L + min(n, o + BLOCK_SIZE)]] for o in range(0, n, BLOCK_SIZE)]
+    rng.shuffle(blocks)
+    bad = blocks[5][0]
+    blocks[5][2] = bytes(b ^ 1 for b in blocks[5][2])
+    cases.append({"name": "verifier", "kind": "verifier", "info": _info_json(L, total, digests),
+                  "flushPieces": 8, "flushAgeMs": None, "blocks": [[i, o, _b64(d)] for i, o, d in blocks]})
+
+    spec = tmp_path / "spec.json"
+    spec.write_text(json.dumps({"lib": LIB, "cases": cases}))
+    out = tmp_path / "out.json"
+    r = subprocess.run([NODE, os.path.join(HARNESS, "run_verify_ts.mjs"), mod, str(spec), str(out)],
+                       capture_output=True, text=True, timeout=600, cwd=HARNESS)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = {x["name"]: x for x in json.loads(out.read_text())}
+    for name, want in expect.items():
+        got = res[name]
+        assert "error" not in got, (name, got.get("error"))
+        key = {"piece": "ok", "hash": "pieces"}.get(got["kind"], "bitfield")
+        assert got[key] == want, (name, got[key], want)
+    assert sorted(str(x) for x in (tmp_path / "dl").rglob("*")) == before        # verifyFiles created nothing
+    v = res["verifier"]
+    assert "error" not in v, v.get("error")
+    results = {i: ok for i, ok in v["auto"] + v["final"]}
+    assert results == {i: i != bad for i in range(P)}
+    assert v["autoFlushes"] == len(v["auto"]) // 8 and len(v["auto"]) == 8 * (P // 8)
+    want_bits = bytearray((P + 7) // 8)
+    for i in range(P):
+        if i != bad:
+            want_bits[i >> 3] |= 0x80 >> (i & 7)
+    assert v["bitfield"] == want_bits.hex()

@@ -72,7 +72,7 @@ let lib: Lib | null = null;
 
 function load(path?: string): Lib {
   if (!lib) {
-    lib = Deno.dlopen(path ?? "./torrent_amd/libtorrent_verify.so", SYMBOLS);
+    lib = Deno.dlopen(path === undefined ? "./torrent_amd/libtorrent_verify.so" : path, SYMBOLS);
     if (lib.symbols.tv_abi_version() !== 1) throw new Error("libtorrent_verify ABI mismatch");
   }
   return lib;
@@ -120,7 +120,7 @@ export async function releaseContexts(): Promise<void> {
   contexts.clear();
   for (const e of all) {
     await e.tail;
-    lib?.symbols.tv_destroy(e.ctx);
+    if (lib) lib.symbols.tv_destroy(e.ctx);
   }
 }
 
@@ -167,10 +167,10 @@ export async function verifyPieces(
   const l = load(opts.libPath);
   const P = info.pieces.length;
   const L = info.pieceLength;
-  const devices = opts.devices ?? [0];
+  const devices = opts.devices || [0];
   const raw = piecesRaw(info);
   const bitfield = new Uint8Array(Math.ceil(P / 8));
-  const batch = Math.max(1, Math.floor((opts.batchBytes ?? 256 * 2 ** 20) / L));
+  const batch = Math.max(1, Math.floor((opts.batchBytes || 256 * 2 ** 20) / L));
 
   await Promise.all(shardRanges(P, devices.length).map(async ([first, count], s) => {
     if (count === 0) return;
@@ -222,14 +222,14 @@ export async function verifyStream(info: InfoDict, storage: Storage, opts: Verif
   const l = load(opts.libPath);
   const P = info.pieces.length;
   const L = info.pieceLength;
-  const devices = opts.devices ?? [0];
+  const devices = opts.devices || [0];
   const raw = piecesRaw(info);
   const bitfield = new Uint8Array(Math.ceil(P / 8));
   await Promise.all(shardRanges(P, devices.length).map(async ([first, count], s) => {
     if (count === 0) return;
     await withContext(l, devices[s], s, async (ctx) => {
       check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_RESIDENT, 0n));
-      check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_STREAM_CHUNK, BigInt(opts.chunk ?? 0)));
+      check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_STREAM_CHUNK, BigInt(opts.chunk || 0)));
       try {
         check(l, ctx, l.symbols.tv_set_layout(ctx, BigInt(info.length), BigInt(L), BigInt(P), BigInt(first), BigInt(count)));
       } finally {
@@ -291,7 +291,7 @@ export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptio
   const l = load(opts.libPath);
   const P = info.pieces.length;
   const L = info.pieceLength;
-  const devices = opts.devices ?? [0];
+  const devices = opts.devices || [0];
   const raw = piecesRaw(info);
   const files = "files" in info
     ? info.files.map((f) => ({ length: f.length, path: [dir, ...f.path].join("/") }))
@@ -367,7 +367,7 @@ export async function verifyPiece(info: InfoDict, index: number, bytes: Uint8Arr
   const l = load(opts.libPath);
   // its own cached context (slot -1): a one-piece layout on a bulk call's context would free that context's
   // payload (tv_set_layout keeps an allocation only while the new geometry is at least half of it)
-  return await withContext(l, (opts.devices ?? [0])[0], -1, async (ctx) => {
+  return await withContext(l, (opts.devices || [0])[0], -1, async (ctx) => {
     const n = BigInt(bytes.length);
     check(l, ctx, l.symbols.tv_set_layout(ctx, n, n, 1n, 0n, 1n)); // reuses the context's allocations
     check(l, ctx, l.symbols.tv_set_digests(ctx, ptr(info.pieces[index]), 20n));
@@ -387,7 +387,7 @@ export async function hashPieces(payload: Uint8Array, pieceLength: number, opts:
   const P = Math.ceil(payload.length / pieceLength);
   if (P === 0) return new Uint8Array(0);
   const l = load(opts.libPath);
-  return await withContext(l, (opts.devices ?? [0])[0], 0, async (ctx) => {
+  return await withContext(l, (opts.devices || [0])[0], 0, async (ctx) => {
     check(l, ctx, l.symbols.tv_set_layout(ctx, BigInt(payload.length), BigInt(pieceLength), BigInt(P), 0n, BigInt(P)));
     check(l, ctx, l.symbols.tv_set_digests(ctx, null, 0n));
     check(l, ctx, await l.symbols.tv_stage(ctx, 0n, ptr(payload), BigInt(payload.length)));
@@ -436,12 +436,16 @@ export class PieceVerifier {
   #flushAgeMs: number | null;
   #onVerified?: (index: number, ok: boolean) => void;
   #busy: Promise<unknown> = Promise.resolve();
+  #timerError: unknown = null;   // a timer-driven flush that failed: rethrown by the next call
 
-  constructor(readonly info: InfoDict, opts: VerifyOptions & FlushPolicy = {}) {
+  readonly info: InfoDict;
+
+  constructor(info: InfoDict, opts: VerifyOptions & FlushPolicy = {}) {
+    this.info = info;
     this.#l = load(opts.libPath);
     const P = info.pieces.length;
     const h = new BigUint64Array(1);
-    check(this.#l, null, this.#l.symbols.tv_create(ptr(new Uint8Array(h.buffer)), (opts.devices ?? [0])[0]));
+    check(this.#l, null, this.#l.symbols.tv_create(ptr(new Uint8Array(h.buffer)), (opts.devices || [0])[0]));
     this.#ctx = Deno.UnsafePointer.create(h[0]);
     const raw = piecesRaw(info);
     check(this.#l, this.#ctx, this.#l.symbols.tv_set_layout(this.#ctx, BigInt(info.length), BigInt(info.pieceLength), BigInt(P), 0n, BigInt(P)));
@@ -454,7 +458,8 @@ export class PieceVerifier {
 
   /** One received block (already validated); true when it completed its piece. */
   async onBlock(index: number, offset: number, block: Uint8Array): Promise<boolean> {
-    await this.#autoFlush();                                  // the age bound, checked on every block
+    this._rethrow();
+    await this._autoFlush();                                  // the age bound, checked on every block
     if (this.bitfield[index >> 3] & (128 >> (index % 8))) return false;
     if (this.#pendingSet.has(index)) return false; // complete, waiting for a flush: ignore re-sends
     const len = pieceLength(index, this.info);
@@ -470,12 +475,26 @@ export class PieceVerifier {
     if (this.#pending.length === 0) {
       this.#oldest = performance.now();
       // the age bound also holds when no further block arrives
-      if (this.#flushAgeMs !== null) this.#timer = setTimeout(() => void this.#autoFlush(), this.#flushAgeMs);
+      if (this.#flushAgeMs !== null) {
+        this.#timer = setTimeout(() => {
+          this._autoFlush().catch((e) => {
+            this.#timerError = e;
+          });
+        }, this.#flushAgeMs);
+      }
     }
     this.#pending.push(index);
     this.#pendingSet.add(index);
-    await this.#autoFlush();                                  // the count bound
+    await this._autoFlush();                                  // the count bound
     return true;
+  }
+
+  private _rethrow(): void {
+    if (this.#timerError !== null) {
+      const e = this.#timerError;
+      this.#timerError = null;
+      throw e;
+    }
   }
 
   /** Would the policy flush now? */
@@ -485,15 +504,15 @@ export class PieceVerifier {
     return this.#flushAgeMs !== null && performance.now() - this.#oldest >= this.#flushAgeMs;
   }
 
-  async #autoFlush(): Promise<void> {
+  private async _autoFlush(): Promise<void> {
     if (!this.due()) return;
     this.autoFlushes++;
-    const res = await this.#flushPending();
+    const res = await this._flushPending();
     if (this.#onVerified) for (const [i, ok] of res) this.#onVerified(i, ok);
     else this.#results.push(...res);
   }
 
-  async #flushPending(): Promise<[number, boolean][]> {
+  private async _flushPending(): Promise<[number, boolean][]> {
     // one list launch at a time on the verifier's context (the timer and onBlock may both flush)
     const run = this.#busy.then(async () => {
       if (this.#pending.length === 0) return [] as [number, boolean][];
@@ -515,9 +534,10 @@ export class PieceVerifier {
   /** Verify all completed pieces in one launch; returns [index, ok] (after the results of automatic
    * flushes not yet handed out) and sets the have-bits. */
   async flush(): Promise<[number, boolean][]> {
+    this._rethrow();
     const earlier = this.#results;
     this.#results = [];
-    return [...earlier, ...await this.#flushPending()];
+    return [...earlier, ...await this._flushPending()];
   }
 
   close(): void {
