@@ -103,9 +103,11 @@ int tv_stage(tv_ctx *ctx, uint64_t linear_offset, const uint8_t *src, uint64_t l
  * read by parallel preads (4 MiB requests, TV_OPT_FILE_THREADS in flight) into the pinned ring and
  * DMA'd from there.
  * TV_OPT_FILE_DIRECT = 0 forces the second form.  Either way, window k+1 is read while window k
- * copies.  Bytes outside the shard are skipped.  A missing or short file returns TV_ERR_IO before
- * anything is staged (a read error part-way also returns TV_ERR_IO): the host marks the pieces the
- * segment touches unreadable, as Storage.get returning null makes them.  Unlike
+ * copies.  Bytes outside the shard are skipped.  A missing, unopenable or short file (or a read error
+ * part-way) returns TV_ERR_IO, and the library marks the pieces Storage.get would return null for
+ * (storage.ts:50-65 reads piece by piece): from the piece holding the first byte the file cannot supply
+ * to the segment's end.  The whole pieces before that byte are staged and stay readable.  Marked pieces
+ * are reported 0 by tv_verify until the next tv_set_layout; the host marks nothing.  Unlike
  * fsStorage.get (which opens with create: true, storage.ts:28-32,158) a missing file is never created.
  * The file is opened as fsStorage.get opens it (read + write, storage.ts:28-32,158): a file this process
  * may not write returns TV_ERR_IO, as Deno.open fails there.  len == 0 reads nothing but still checks the
@@ -127,12 +129,15 @@ int tv_stage_file(tv_ctx *ctx, const char *path, uint64_t file_offset, uint64_t 
  *     A slot's DMA overlaps the reads of the next slot. This is the many-small-files case: a
  *     10,000-file torrent is one call, not 10,000.
  * status_out[k] = TV_OK, or TV_ERR_IO when the file is missing, unreadable, not writable or shorter than
- * the segment; the host marks the pieces that segment touches unreadable (Storage.get -> null).
+ * the segment.  As for tv_stage_file, the library itself marks the pieces Storage.get would return null
+ * for (from the piece holding the first unreadable byte to the segment's end; the whole pieces before it
+ * are staged), tv_verify reports them 0 until the next tv_set_layout, and the status is informational: a
+ * host that cleared every piece a failed segment touches would lose a short file's readable pieces.
  *   - Zero-length segments belong in the list: Storage.get's walk emits them for a file that ends where a
  *     piece starts and for a zero-length file inside a piece (storage.ts:109-110), and fsStorage.get still
  *     opens them (storage.ts:158).  Such a segment reads nothing; its status is TV_ERR_IO exactly when that
- *     open would fail (tv_stage_file, len == 0), and nothing is created.  Its piece is linear_offsets[k] /
- *     piece_length.
+ *     open would fail (tv_stage_file, len == 0), and nothing is created.  Its piece, linear_offsets[k] /
+ *     piece_length, is then marked unreadable.
  * The call itself returns TV_OK unless an argument or HIP error occurs; the first I/O failure's message is
  * kept for tv_last_error.  Bytes outside the shard are skipped.
  */

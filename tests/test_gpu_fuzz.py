@@ -112,7 +112,7 @@ def test_random_layouts_every_host_path(native, tmp_path, monkeypatch, seed):
             p.parent.mkdir(parents=True, exist_ok=True)
             p.write_bytes(data)
     want_fs = _expected(info, Storage(fs_storage, info, str(tmp_path / "ref")))
-    shutil.rmtree(tmp_path / "ref")
+    shutil.rmtree(tmp_path / "ref", ignore_errors=True)          # absent when no file was written or created
     # the linear payload's availability as Storage.get sees it (verify_payload takes one buffer)
     avail = bytearray((P + 7) // 8)
     for i in range(P):
@@ -152,3 +152,42 @@ def test_fuzz_layouts_cover_the_edge_cases():
         seen |= {"boundary_file"} if any(e % L == 0 and 0 < e < info.length for e in ends) else set()
     assert {"odd_L", "L64", "zero_file", "missing", "short", "single", "multi", "ragged", "extra_digests",
             "short_last", "boundary_file"} <= seen, seen
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_random_layouts_files_plan_on_cpu(tmp_path, monkeypatch, seed):
+    """verify_files' staging plan for every seed on CPU (the library's read and recovery rules restated in
+    tests/test_host_mirror._ImageCtx): readable bits equal Storage(fs_storage).get's per piece (on a copy,
+    since that get creates files) over 1 and 3 shards, and every readable piece's bytes are staged."""
+    import shutil
+    from tests.test_host_mirror import _ImageCtx
+    from torrent_amd import Storage, verify
+    from torrent_amd.piece import piece_length
+    from torrent_amd.storage import fs_storage
+    info, payload, sizes, missing, short, single = _draw(seed)
+    P, L, total = info.n_pieces, info.piece_length, info.length
+    monkeypatch.chdir(tmp_path)
+    for root in ("dl", "ref"):
+        for k, data in _disk(info, payload, sizes, missing, short, single).items():
+            p = tmp_path.joinpath(root, *k)
+            p.parent.mkdir(parents=True, exist_ok=True)
+            p.write_bytes(data)
+    ref = Storage(fs_storage, info, str(tmp_path / "ref"))
+    want = [ref.get(i * L, piece_length(i, info)) is not None for i in range(P)]
+    shutil.rmtree(tmp_path / "ref", ignore_errors=True)
+    st = Storage(fs_storage, info, str(tmp_path / "dl"))
+    for n in (1, 3):
+        got = []
+        for first, count in verify.shard_ranges(P, n):
+            if not count:
+                continue
+            last = first + count - 1
+            hi = min(total, last * L + piece_length(last, info))
+            ctx = _ImageCtx(total, first * L, hi, L)
+            bits = ctx.avail(verify._files_shard(ctx, info, st, first, count, threads=2), first, count)
+            got += bits
+            for j, ok in enumerate(bits):
+                a = (first + j) * L
+                if ok:
+                    assert ctx.img[a:a + piece_length(first + j, info)] == payload[a:a + piece_length(first + j, info)]
+        assert got == want, (seed, n)

@@ -376,7 +376,9 @@ def test_stage_file_windows_offsets_and_failures(native, oracle, tmp_path, direc
     """tv_stage_file: the torrent bytes sit at an unaligned offset inside the file; windows of
     200,000 bytes (not a page multiple) over a shard window [8, 128) of 130 pieces with a short last
     piece; registered page-cache DMA (direct=1) and the pinned-ring copy (direct=0) stage the same
-    bytes.  A short or missing file stages nothing and returns False; len 0 needs no file."""
+    bytes.  A short or missing file returns False and stages no byte of a piece it cannot complete (the
+    library marks those pieces unreadable: tv_verify reports them 0 though their bytes are right); len 0
+    needs no file."""
     L, P = 65536, 130
     total = L * (P - 1) + 12345
     payload = oracle.synth_fill(77, 0, total)
@@ -412,6 +414,8 @@ def test_stage_file_windows_offsets_and_failures(native, oracle, tmp_path, direc
         assert ctx.stage_file(str(tmp_path / "missing.bin"), 0, 9 * L, 0)
         ctx.read(0, out)
         assert out[8 * L:] == payload[8 * L:]
+        bf = ctx.verify()
+        assert not (bf[0] >> 6) & 1 and bf[0] >> 7 == want[0] >> 7     # piece 9 marked, piece 8 as before
         # a range partly outside the shard: only the shard's bytes are staged
         ctx.stage_file(str(short), 0, 8 * L - 500, 1000)
         ctx.read(0, out)
@@ -664,9 +668,11 @@ def test_concurrent_calls_do_not_interleave(native, oracle):
 
 def test_verify_files_read_faults_are_unreadable_pieces(native, tmp_path):
     """Read faults (the storage_test.ts:96-108 idea, applied to verify_files' own reads): a path that
-    opens but cannot be read (a directory where a file should be: EISDIR), a short file and a missing
-    file make exactly the pieces they touch unreadable (bit 0), never an exception, through both the
-    reader pool and the tv_stage_file path; tv_stage_files reports each as TV_ERR_IO."""
+    opens but cannot be read (a directory where a file should be: EISDIR) and a missing file make the
+    pieces they touch unreadable (bit 0); a file one byte short makes only the piece holding its last byte
+    unreadable, since Storage.get reads piece by piece (storage.ts:50-65,150-172) -- never an exception,
+    through both the reader pool and the tv_stage_file path, with the same bits as Storage(fs_storage).get.
+    tv_stage_files reports each as TV_ERR_IO, and the library itself marks the pieces (no host clearing)."""
     import hashlib as _h
     from torrent_amd import FileInfo, make_info, verify_files
     L = 4096
@@ -681,9 +687,10 @@ def test_verify_files_read_faults_are_unreadable_pieces(native, tmp_path):
     (tmp_path / "f1").mkdir()                                      # a directory: open ok, read fails
     (tmp_path / "f2").write_bytes(payload[starts[2]:starts[3] - 1])  # one byte short
     (tmp_path / "f4").write_bytes(payload[starts[4]:starts[5]])       # f3 missing
-    bad = set()
-    for k in (1, 2, 3):
+    bad = {(starts[3] - 1) // L}                                      # f2's last byte
+    for k in (1, 3):
         bad |= set(range(starts[k] // L, (starts[k + 1] - 1) // L + 1))
+    assert not bad & set(range(9, 12))                               # f2's whole pieces stay readable
     cwd = os.getcwd()
     os.chdir(tmp_path)
     try:
@@ -695,8 +702,11 @@ def test_verify_files_read_faults_are_unreadable_pieces(native, tmp_path):
         os.chdir(cwd)
     with native.Context(0) as ctx:
         ctx.set_layout(total, L, P)
+        ctx.set_digests(pieces)
         st = ctx.stage_files([str(tmp_path / f"f{k}") for k in range(5)], [0] * 5, starts[:5], sizes)
         assert st == [0, native.TV_ERR_IO, native.TV_ERR_IO, native.TV_ERR_IO, 0]
+        bf = ctx.verify()                                            # no availability from the host
+        assert [(bf[i >> 3] >> (7 - (i & 7))) & 1 for i in range(P)] == [0 if i in bad else 1 for i in range(P)]
 
 
 @pytest.mark.parametrize("concurrent", [1, 0])

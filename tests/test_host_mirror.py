@@ -341,15 +341,30 @@ def _fs_openable(path: str) -> bool:
 
 class _ImageCtx:
     """Stand-in for a tv_ctx on CPU: tv_stage_files writes into a linear image of the shard, so
-    verify_files' staging plan (the storage.ts segment mapping, one batched call, status -> unreadable
-    pieces) is checked without a GPU.  Files are read the way the library reads them (missing / short /
-    unreadable -> TV_ERR_IO, nothing staged for that segment)."""
+    verify_files' staging plan (the storage.ts segment mapping, one batched call) is checked without a GPU.
+    Files are read the way the library reads them, and a failed segment is handled as tv_api.hip
+    recover_segment does (restated): the whole pieces of the file's readable prefix are staged, the pieces
+    from the first unreadable byte to the segment's end are marked (`bad`, linear piece indices), and a
+    failed zero-length segment marks its piece."""
 
-    def __init__(self, total, lo, hi):
+    def __init__(self, total, lo, hi, L):
         self.img = bytearray(total)
         self.written = bytearray(total)
-        self.lo, self.hi = lo, hi
+        self.lo, self.hi, self.L = lo, hi, L
         self.calls = 0
+        self.bad = set()
+
+    def _mark(self, a, b):
+        if a == b:
+            if self.lo <= a < self.hi:
+                self.bad.add(a // self.L)
+            return
+        a, b = max(a, self.lo), min(b, self.hi)
+        self.bad |= set(range(a // self.L, (b - 1) // self.L + 1)) if b > a else set()
+
+    def avail(self, host_bits, first, count):
+        """The bits tv_verify applies: the host's availability and not the marked pieces."""
+        return [bool((host_bits[j >> 3] >> (7 - (j & 7))) & 1) and first + j not in self.bad for j in range(count)]
 
     def set_option(self, key, value):
         pass
@@ -366,21 +381,26 @@ class _ImageCtx:
         self.calls += 1
         out = []
         for path, foff, off, n in zip(paths, file_offsets, linear_offsets, lens):
+            foff, off, n = int(foff), int(off), int(n)
             if n == 0:   # the library's zero-length rule (tv_api.hip fs_openable), restated
-                out.append(0 if _fs_openable(path) else -5)
+                ok = _fs_openable(path)
+                out.append(0 if ok else -5)
+                if not ok:
+                    self._mark(off, off)
                 continue
-            try:
+            data = b""
+            if _fs_openable(path) and os.path.isfile(path):
                 with open(path, "rb") as f:
                     f.seek(foff)
                     data = f.read(n)
-            except OSError:
-                out.append(-5)
+            if len(data) == n:
+                self._put(off, data)
+                out.append(0)
                 continue
-            if len(data) < n:
-                out.append(-5)
-                continue
-            self._put(off, data)
-            out.append(0)
+            r = max(0, (off + len(data)) // self.L * self.L - off)    # the prefix's whole pieces
+            self._put(off, data[:r])
+            self._mark(off + r, off + n)
+            out.append(-5)
         return out
 
 
@@ -406,13 +426,13 @@ def test_files_shard_staging_plan(tmp_path, monkeypatch, layout):
         if not count:
             continue
         hi = (first + count - 1) * L + (total % L if first + count == P and total % L else L)
-        ctx = _ImageCtx(total, first * L, hi)
-        avail = verify._files_shard(ctx, info, st, first, count, threads=4)
+        ctx = _ImageCtx(total, first * L, hi, L)
+        avail = ctx.avail(verify._files_shard(ctx, info, st, first, count, threads=4), first, count)
         assert ctx.calls == 1
         for j in range(count):
             i = first + j
             want = (lay["avail"][i >> 3] >> (7 - (i & 7))) & 1
-            assert (avail[j >> 3] >> (7 - (j & 7))) & 1 == want, (layout, i)
+            assert avail[j] == want, (layout, i)
             if want:
                 a, b = i * L, min(total, (i + 1) * L)
                 assert ctx.img[a:b] == lay["payload"][a:b], (layout, i)
@@ -468,8 +488,8 @@ def test_files_shard_zero_length_segments_match_fs_storage(tmp_path, monkeypatch
         if not count:
             continue
         hi = (first + count - 1) * L + piece_length(first + count - 1, info)
-        avail = verify._files_shard(_ImageCtx(info.length, first * L, hi), info, st, first, count, threads=2)
-        got += [bool((avail[j >> 3] >> (7 - (j & 7))) & 1) for j in range(count)]
+        ctx = _ImageCtx(info.length, first * L, hi, L)
+        got += ctx.avail(verify._files_shard(ctx, info, st, first, count, threads=2), first, count)
     assert got == expect
     assert sorted(str(x) for x in root.rglob("*")) == before      # nothing created
 

@@ -255,8 +255,9 @@ class Context:
 
     def stage_file(self, path, file_offset: int, linear_offset: int, length: int) -> bool:
         """tv_stage_file: stage `length` bytes of file `path` from `file_offset` as linear bytes
-        [linear_offset, +length).  False when the file is missing or short (TV_ERR_IO: the
-        reference's fsStorage.get -> null, so the pieces it touches are unreadable)."""
+        [linear_offset, +length).  False when the file is missing, unopenable or short (TV_ERR_IO): the
+        library then marks the pieces the reference's fsStorage.get would return null for (from the one
+        holding the first missing byte on; tv_verify reports them 0 until the next set_layout)."""
         rc = self._L.tv_stage_file(self._h, os.fsencode(path), file_offset, linear_offset, length)
         if rc == TV_ERR_IO:
             return False
@@ -265,7 +266,8 @@ class Context:
 
     def stage_files(self, paths, file_offsets, linear_offsets, lens) -> list:
         """tv_stage_files: stage many file segments in one call.  Returns one status per segment:
-        TV_OK, or TV_ERR_IO for a missing / unreadable / short file (its pieces are unreadable)."""
+        TV_OK, or TV_ERR_IO for a missing / unreadable / short file.  The library marks the pieces
+        fsStorage.get would return null for itself (tv_verify reports them 0); the status is informational."""
         import numpy as np
 
         n = len(paths)

@@ -174,6 +174,10 @@ struct tv_ctx {
     bool digests_set = false;
     std::vector<uint8_t> digest_ok;   // shard-relative MSB-first bits: digest slice is 20 bytes
     std::vector<uint8_t> base_avail;  // host copy of d_base_avail (bit_words * 8 bytes)
+    // shard-relative MSB-first bits of the pieces a tv_stage_file(s) call could not read as fsStorage.get
+    // reads them (until the next tv_set_layout); tv_verify reports them 0
+    std::vector<uint8_t> file_bad;
+    bool any_file_bad = false;
 
     // pinned staging ring.  A slot is LENT from take_slot until release_slot records its event after the
     // last copy queued from it; take_slot never hands out a lent slot (it takes the next free one), so a
@@ -408,15 +412,20 @@ int upload_base_avail(tv_ctx* c) {
 }
 
 // Availability for one launch: the base bits, or base & the caller's bits (Storage.get -> null for
-// a missing / short file) queued on the compute stream from the pinned bounce buffer (no host sync).
+// a missing / short file) & not the pieces file staging could not read, queued on the compute stream from
+// the pinned bounce buffer (no host sync).
 int launch_avail(tv_ctx* c, const uint8_t* avail_bits, const uint64_t** out) {
-    if (!avail_bits) {
+    if (!avail_bits && !c->any_file_bad) {
         *out = c->d_base_avail;
         return TV_OK;
     }
     TV_HIP(c, hipEventSynchronize(c->ev_avail));  // the previous copy out of h_avail is done
     const size_t nbytes = c->bit_words * 8, used = (c->count + 7) / 8;
-    for (size_t k = 0; k < nbytes; k++) c->h_avail[k] = c->base_avail[k] & (k < used ? avail_bits[k] : 0);
+    for (size_t k = 0; k < nbytes; k++) {
+        const uint8_t caller = k < used ? (avail_bits ? avail_bits[k] : 0xFF) : 0;
+        const uint8_t bad = k < used ? c->file_bad[k] : 0;
+        c->h_avail[k] = c->base_avail[k] & caller & (uint8_t)~bad;
+    }
     TV_HIP(c, hipMemcpyAsync(c->d_avail, c->h_avail, nbytes, hipMemcpyHostToDevice, c->stream));
     TV_HIP(c, hipEventRecord(c->ev_avail, c->stream));
     *out = c->d_avail;
@@ -1183,6 +1192,8 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
     c->stride = stride;
     c->bit_words = ((shard_count + 255) / 256) * 4;
     c->digest_ok.assign((shard_count + 7) / 8 + 8, 0);
+    c->file_bad.assign((shard_count + 7) / 8 + 8, 0);
+    c->any_file_bad = false;
     // Keep every allocation the new geometry fits (reuse_fits): a run of small layouts (verify_piece,
     // a flush of tv_verify_list) allocates once.  Everything else is released first, so a big payload
     // is never held beside its replacement.
@@ -1402,6 +1413,54 @@ void read_segments(Pool& pool, const std::vector<SmallSeg>& segs, size_t lo, siz
     });
 }
 
+// Mark the shard pieces holding linear bytes [a, b) unreadable (tv_verify reports them 0).
+void mark_bad(tv_ctx* c, uint64_t a, uint64_t b) {
+    const uint64_t lo = c->first * c->L;
+    const uint64_t last = c->first + c->count - 1;
+    const uint64_t hi = last * c->L + piece_len(c, last);
+    if (a == b) {  // a zero-length segment: the piece it sits in
+        if (a < lo || a >= hi) return;
+        b = a + 1;
+    }
+    a = std::max(a, lo);
+    b = std::min(b, hi);
+    if (a >= b) return;
+    for (uint64_t j = a / c->L - c->first; j <= (b - 1) / c->L - c->first; j++) set_bit(c->file_bad.data(), j);
+    c->any_file_bad = true;
+}
+
+// Bytes of [file_offset, file_offset + len) that fsStorage.get's read of `path` would return: 0 when the
+// open (read + write, storage.ts:28-32,158) fails or the path is not a regular file, else what the file holds.
+uint64_t readable_prefix(const char* path, uint64_t file_offset, uint64_t len) {
+    if (rw_access(path)) return 0;
+    struct stat st;
+    if (stat(path, &st) != 0 || !S_ISREG(st.st_mode)) return 0;
+    const uint64_t size = (uint64_t)st.st_size;
+    return size <= file_offset ? 0 : std::min(len, size - file_offset);
+}
+
+// A file segment staging could not read whole: Storage.get reads per piece (storage.ts:50-65), so the
+// pieces inside the file's readable prefix are still readable.  Stage that prefix again and mark the pieces
+// from the first missing byte to the segment's end unreadable (a zero-length segment: its piece).
+int recover_segment(tv_ctx* c, const char* path, uint64_t file_offset, uint64_t linear_offset, uint64_t len) {
+    if (len == 0) {
+        mark_bad(c, linear_offset, linear_offset);
+        return TV_OK;
+    }
+    uint64_t r = readable_prefix(path, file_offset, len);
+    if (r == len) r = 0;  // readable by size yet the read failed (an I/O error): nothing of it counts
+    // only the prefix's whole pieces are staged: the piece holding its first missing byte is marked below
+    const uint64_t whole = (linear_offset + r) / c->L * c->L;
+    r = whole > linear_offset ? whole - linear_offset : 0;
+    if (r) {
+        const int rc = stage_file_locked(c, path, file_offset, linear_offset, r);
+        if (rc == TV_ERR_IO) r = 0;
+        else if (rc) return rc;
+    }
+    mark_bad(c, linear_offset + r, linear_offset + len);
+    return TV_OK;
+}
+
 }  // namespace
 
 int tv_stage_file(tv_ctx* c, const char* path, uint64_t file_offset, uint64_t linear_offset, uint64_t len) {
@@ -1412,7 +1471,13 @@ int tv_stage_file(tv_ctx* c, const char* path, uint64_t file_offset, uint64_t li
     if (!path) return fail(c, TV_ERR_ARG, "path is NULL");
     if (linear_offset + len < linear_offset || file_offset + len < file_offset)
         return fail(c, TV_ERR_ARG, "offset + len overflows");
-    return stage_file_locked(c, path, file_offset, linear_offset, len);
+    rc = stage_file_locked(c, path, file_offset, linear_offset, len);
+    if (rc != TV_ERR_IO || c->count == 0) return rc;
+    const std::string err = c->err;
+    const int r = recover_segment(c, path, file_offset, linear_offset, len);
+    if (r) return r;
+    fail(c, TV_ERR_IO, "%s", err.c_str());  // the first failure stays the call's message
+    return TV_ERR_IO;
 }
 
 int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64_t* file_offsets,
@@ -1546,6 +1611,12 @@ int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64
     TV_HIP(c, hipStreamSynchronize(c->copy_stream));
     if (helper.joinable()) helper.join();
     if (helper_rc) return helper_rc;
+    // the failed segments: their readable prefixes staged again, the rest of their pieces marked unreadable
+    for (uint64_t k = 0; k < n; k++) {
+        if (status_out[k] != TV_ERR_IO) continue;
+        rc = recover_segment(c, paths[k], file_offsets[k], linear_offsets[k], lens[k]);
+        if (rc) return rc;
+    }
     if (!first_err.empty()) fail(c, TV_OK, "tv_stage_files: %s (and possibly more; see status_out)", first_err.c_str());
     return TV_OK;
 }

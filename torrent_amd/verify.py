@@ -303,9 +303,10 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
     (storage.ts:89-137), and ALL segments go to the library in one tv_stage_files call: segments of
     >= direct_min bytes (default 32 MiB) are DMA'd from the page cache (tv_stage_file's path), shorter
     ones are read by `threads` library threads into pinned slots, one DMA per run of adjacent bytes.
-    A piece touching a missing or short file is unreadable (fsStorage.get -> null,
-    storage.ts:150-172); so is a piece whose zero-length segment (storage.ts:109-110) names a path
-    fsStorage.get could not open (the library checks it, tv_stage_files); missing files are never created."""
+    The library marks the unreadable pieces itself, exactly as Storage.get(i * L, len_i) would return null
+    (storage.ts:50-65,150-172): a piece with a byte in a missing, unopenable or too-short part of a file,
+    and a piece whose zero-length segment (storage.ts:109-110) names a path fsStorage.get could not open;
+    a short file's pieces before its end stay readable.  Missing files are never created."""
     L = info.piece_length
     avail = bytearray(b"\xff" * ((count + 7) // 8))
     if count % 8:
@@ -344,11 +345,9 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
     paths = storage.file_paths()
     ctx.set_option(_native.TV_OPT_FILE_THREADS, max(1, threads))
     ctx.set_option(_native.TV_OPT_FILE_DIRECT_MIN, _DIRECT_MIN_BYTES if direct_min is None else direct_min)
-    status = ctx.stage_files([paths[i] for i in k.tolist()], foff, lin, nbytes)
-    for q, st in enumerate(status):
-        if st != _native.TV_OK:
-            s0, n = int(lin[q]) - lo, int(nbytes[q])
-            clear(s0 // L, (s0 + max(n, 1) - 1) // L)     # a zero-length segment: piece s0 // L
+    # a failed segment's pieces are marked inside the library (tv_verify reports them 0): from the piece
+    # holding its first unreadable byte on, as Storage.get reads piece by piece; the statuses are informational
+    ctx.stage_files([paths[i] for i in k.tolist()], foff, lin, nbytes)
     return avail
 
 

@@ -282,9 +282,9 @@ export async function verifyStream(info: InfoDict, storage: Storage, opts: Verif
  * [dir, name], multi-file [dir, ...path]).  All file segments of a shard go to tv_stage_files in one
  * call: long segments are DMA'd to HBM from the page cache when the file is warm (parallel preads when
  * cold); short ones (many small files) are read by the library's thread pool into pinned slots.
- * A missing, short or unwritable file (TV_ERR_IO) makes the pieces it touches 0, like fsStorage.get
- * returning null (storage.ts:163-171), and so does a zero-length segment whose open would fail (a directory,
- * a missing parent directory); unlike fsStorage.get, no missing file is created.  Same behaviour as
+ * The library marks the pieces fsStorage.get would return null for (storage.ts:163-171): a byte in a
+ * missing, unopenable or unwritable file or past a short file's end, or a zero-length segment whose open
+ * would fail (a directory, a missing parent directory); unlike fsStorage.get, no missing file is created.  Same behaviour as
  * torrent_amd.verify_files.
  */
 export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptions = {}): Promise<Uint8Array> {
@@ -343,14 +343,12 @@ export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptio
         });
         const status = new Int32Array(n);
         const u8 = (a: ArrayBufferView) => new Uint8Array(a.buffer, a.byteOffset, a.byteLength);
+        // a failed segment's pieces are marked inside the library (tv_verify reports them 0), from the piece
+        // holding its first unreadable byte on, as Storage.get reads piece by piece: `status` is informational
         check(l, ctx, await l.symbols.tv_stage_files(ctx, BigInt(n), ptr(u8(paths)), ptr(u8(fo)), ptr(u8(lin)),
                                                      ptr(u8(len)), ptr(u8(status))));
         // `segs` (the path strings) stays referenced until here, after the nonblocking call settled
-        segs.forEach((sg, k) => {
-          if (status[k] === TV_ERR_IO) {
-            clear(Math.floor((sg.linear - lo) / L), Math.floor((sg.linear + Math.max(sg.len, 1) - 1 - lo) / L));
-          }
-        });
+        if (segs.length !== n) throw new Error("verifyFiles: segment list changed");
       }
       const out = new Uint8Array(Math.ceil(count / 8));
       check(l, ctx, await l.symbols.tv_verify(ctx, ptr(avail), ptr(out)));
