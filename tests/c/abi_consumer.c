@@ -168,6 +168,9 @@ static int run_gpu(void) {
         /* one tv_stage_files call: the data segment, then zero-length segments on piece 2 (a directory),
            piece 1 (a missing directory) and piece 0 (a missing file in /tmp: fine, not created) */
         {
+            /* a fresh layout: the failed calls above marked pieces 0-2 unreadable until the next one */
+            OK(tv_set_layout(c, 7, 3, 3, 0, 3), c);
+            OK(tv_set_digests(c, digests, 60), c);
             const char *paths[4] = {path, "/tmp", "/nonexistent/tv_file", absent};
             const uint64_t fo[4] = {2, 0, 0, 0}, lin[4] = {0, 6, 3, 0}, lens[4] = {7, 0, 0, 0};
             int32_t st[4] = {9, 9, 9, 9};
