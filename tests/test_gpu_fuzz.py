@@ -191,3 +191,65 @@ def test_random_layouts_files_plan_on_cpu(tmp_path, monkeypatch, seed):
                 if ok:
                     assert ctx.img[a:a + piece_length(first + j, info)] == payload[a:a + piece_length(first + j, info)]
         assert got == want, (seed, n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", SEEDS[:12])
+def test_random_layouts_incremental_hash_and_piece(native, seed):
+    """The same seeded torrents through the per-piece paths: IncrementalVerifier fed every data piece's
+    blocks in random order with duplicates, a corrupted block later re-sent intact, and a random flush
+    policy (f1, torrent.ts:183-193); verify_piece on random pieces; hash_pieces (creation, f3) of the
+    linear payload.  Expected: hashlib over the same bytes (the reference's crypto.subtle.digest)."""
+    from torrent_amd import hash_pieces, verify_piece
+    from torrent_amd.incremental import IncrementalVerifier
+    from torrent_amd.piece import BLOCK_SIZE, PieceMsg, piece_length
+    info, payload, sizes, missing, short, single = _draw(seed)
+    P, L, total = info.n_pieces, info.piece_length, info.length
+    rng = random.Random(seed)
+    data_pieces = [i for i in range(P) if i * L + piece_length(i, info) <= total]
+    truth = {i: hashlib.sha1(payload[i * L:i * L + piece_length(i, info)]).digest()
+             == info.pieces_raw[20 * i:20 * i + 20] for i in data_pieces}
+    # creation: the linear payload's pieces string
+    n_data = -(-total // L)
+    assert hash_pieces(payload, L) == b"".join(hashlib.sha1(payload[i * L:(i + 1) * L]).digest()
+                                               for i in range(n_data))
+    # one piece at a time
+    for i in rng.sample(data_pieces, min(4, len(data_pieces))):
+        assert verify_piece(info, i, payload[i * L:i * L + piece_length(i, info)]) is truth[i], (seed, i)
+    # incremental
+    msgs = []
+    for i in data_pieces:
+        n = piece_length(i, info)
+        msgs += [PieceMsg(i, o, payload[i * L + o:i * L + min(n, o + BLOCK_SIZE)]) for o in range(0, n, BLOCK_SIZE)]
+    rng.shuffle(msgs)
+    msgs += rng.sample(msgs, len(msgs) // 5)                        # duplicates, some after completion
+    bad = None
+    if msgs:
+        k = rng.randrange(len(msgs))
+        m = msgs[k]
+        bad = m.index
+        msgs[k] = PieceMsg(m.index, m.offset, bytes(b ^ 0x10 for b in m.block))
+        msgs.append(m)                                              # the intact block, re-sent at the end
+    seen = {}
+    v = IncrementalVerifier(info, flush_pieces=rng.choice([1, 7, None]), flush_age_ms=None,
+                            on_verified=lambda i, ok: seen.setdefault(i, []).append(ok))
+    try:
+        for m in msgs:
+            v.on_block(m)
+        for i, ok in v.flush():
+            seen.setdefault(i, []).append(ok)
+        # the corrupted piece: verified False once it completed with the bad block; the final intact
+        # re-send then completes it again only if its earlier copy had already failed and been flushed
+        got = [bool(v.bitfield[i >> 3] & (0x80 >> (i & 7))) for i in range(P)]
+        for i in data_pieces:
+            results = seen.get(i, [])
+            assert results, (seed, i)
+            assert results[-1] == got[i], (seed, i, results)
+            if i != bad:
+                assert results == [truth[i]] or (not truth[i] and all(r is False for r in results)), (seed, i, results)
+                assert got[i] == truth[i], (seed, i)
+            else:
+                assert all(r is False for r in results[:-1]), (seed, i, results)
+        assert not any(got[i] for i in range(P) if i not in truth)
+    finally:
+        v.close()
