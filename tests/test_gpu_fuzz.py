@@ -220,7 +220,13 @@ def test_random_layouts_incremental_hash_and_piece(native, seed):
     msgs = []
     for i in data_pieces:
         n = piece_length(i, info)
-        msgs += [PieceMsg(i, o, payload[i * L + o:i * L + min(n, o + BLOCK_SIZE)]) for o in range(0, n, BLOCK_SIZE)]
+        for o in range(0, n, BLOCK_SIZE):
+            if i == P - 1 and o + BLOCK_SIZE >= n:                  # the torrent's last block: exact length
+                blk = payload[i * L + o:i * L + n]
+            else:                                                   # every other block is BLOCK_SIZE long
+                blk = payload[i * L + o:i * L + o + BLOCK_SIZE]     # (piece.ts:39-65), past the piece if L
+                blk += bytes(BLOCK_SIZE - len(blk))                 # % BLOCK_SIZE != 0: the verifier cuts it
+            msgs.append(PieceMsg(i, o, blk))
     rng.shuffle(msgs)
     msgs += rng.sample(msgs, len(msgs) // 5)                        # duplicates, some after completion
     bad = None
