@@ -3,10 +3,12 @@
 Deno is absent from the image, so the binding a maintainer would add to the reference is type-erased
 (tests/ts_harness/erase_ts.py: annotations, interfaces, casts, generics, modifiers only) and run by Node 12
 with `Deno.dlopen` / `Deno.UnsafePointer` / `Deno.UnsafePointerView` provided by a small N-API addon
-(tests/ts_harness/deno_ffi.cc) that calls the real libtorrent_verify.so.  On CPU: the erased module parses,
+(tests/ts_harness/deno_ffi.cc) that calls the real libtorrent_verify.so (`nonblocking` symbols on libuv worker
+threads, as Deno runs them on its blocking pool, so shards' calls overlap).  On CPU: the erased module parses,
 its pure helpers equal the Python host's, and the whole symbol table binds through the shim.  On the GPU
 (`-m gpu`): verifyPieces, verifyStream, verifyFiles (zero-length segments in a directory's place and in a
-missing directory), verifyPiece, hashPieces and the PieceVerifier flush policy return the reference's bits,
+missing directory), verifyPiece, hashPieces and the PieceVerifier flush policy (the count bound, and the
+age timer alone) return the reference's bits,
 computed here with the Python mirror and hashlib as the checker -- the same inputs the Python host is
 tested on, so the two hosts cannot drift apart unseen.
 """
@@ -222,6 +224,10 @@ def test_ts_binding_on_the_gpu(native, tmp_path, monkeypatch):
     blocks[5][2] = bytes(b ^ 1 for b in blocks[5][2])
     cases.append({"name": "verifier", "kind": "verifier", "info": _info_json(L, total, digests),
                   "flushPieces": 8, "flushAgeMs": None, "blocks": [[i, o, _b64(d)] for i, o, d in blocks]})
+    # the age bound only: the timer flushes what is pending while no block arrives
+    cases.append({"name": "verifier_age", "kind": "verifier", "info": _info_json(L, total, digests),
+                  "flushPieces": None, "flushAgeMs": 2, "settleMs": 200,
+                  "blocks": [[i, o, _b64(d)] for i, o, d in blocks]})
 
     spec = tmp_path / "spec.json"
     spec.write_text(json.dumps({"lib": LIB, "cases": cases}))
@@ -246,3 +252,7 @@ def test_ts_binding_on_the_gpu(native, tmp_path, monkeypatch):
         if i != bad:
             want_bits[i >> 3] |= 0x80 >> (i & 7)
     assert v["bitfield"] == want_bits.hex()
+    va = res["verifier_age"]
+    assert "error" not in va, va.get("error")
+    assert {i: ok for i, ok in va["auto"] + va["final"]} == {i: i != bad for i in range(P)}
+    assert va["autoFlushes"] >= 1 and va["final"] == [] and va["bitfield"] == want_bits.hex()

@@ -6,6 +6,7 @@
 //   open(path) -> handle (BigInt)          sym(handle, name) -> function address (BigInt)
 //   call(fn, args: BigInt[] (<= 7, each the 64-bit register image of an integer / pointer argument),
 //        result: 0 void | 1 i32) -> number | undefined
+//   callAsync(fn, args, result) -> Promise of the same, the call run on a libuv worker thread
 //   addressOf(typedArray) -> BigInt        arrayBuffer(address: BigInt, length) -> ArrayBuffer over it
 //
 // Every argument of the ABI is an integer or a pointer (include/torrent_verify.h), so on x86-64 System V
@@ -93,6 +94,61 @@ napi_value Call(napi_env env, napi_callback_info info) {
     return out;
 }
 
+// callAsync: the same call on a libuv worker thread, returning a Promise -- Deno runs a `nonblocking` symbol
+// on its blocking-task pool and resolves the promise on the event loop, so calls on different contexts
+// really overlap, as they do under Deno.
+struct AsyncCall {
+    uint64_t fn;
+    uint64_t a[7];
+    int32_t kind;
+    int64_t r;
+    napi_deferred deferred;
+    napi_async_work work;
+};
+
+void AsyncExecute(napi_env, void* data) {
+    AsyncCall* c = (AsyncCall*)data;
+    c->r = ((Fn7)(uintptr_t)c->fn)(c->a[0], c->a[1], c->a[2], c->a[3], c->a[4], c->a[5], c->a[6]);
+}
+
+void AsyncComplete(napi_env env, napi_status, void* data) {
+    AsyncCall* c = (AsyncCall*)data;
+    napi_value v;
+    if (c->kind == 0) napi_get_undefined(env, &v);
+    else napi_create_int32(env, (int32_t)c->r, &v);
+    napi_resolve_deferred(env, c->deferred, v);
+    napi_delete_async_work(env, c->work);
+    delete c;
+}
+
+napi_value CallAsync(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3];
+    napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr);
+    AsyncCall* c = new AsyncCall();
+    uint32_t nargs = 0;
+    if (argc < 3 || !get_u64(env, argv[0], &c->fn) || napi_get_array_length(env, argv[1], &nargs) != napi_ok ||
+        nargs > 7) {
+        delete c;
+        return throw_error(env, "callAsync(fn, args: at most 7 BigInts, result)");
+    }
+    for (uint32_t i = 0; i < nargs; i++) {
+        napi_value e;
+        napi_get_element(env, argv[1], i, &e);
+        if (!get_u64(env, e, &c->a[i])) {
+            delete c;
+            return throw_error(env, "callAsync: every argument must be a BigInt");
+        }
+    }
+    napi_get_value_int32(env, argv[2], &c->kind);
+    napi_value promise, name;
+    napi_create_promise(env, &c->deferred, &promise);
+    napi_create_string_utf8(env, "deno_ffi_call", NAPI_AUTO_LENGTH, &name);
+    napi_create_async_work(env, nullptr, name, AsyncExecute, AsyncComplete, c, &c->work);
+    napi_queue_async_work(env, c->work);
+    return promise;
+}
+
 napi_value AddressOf(napi_env env, napi_callback_info info) {
     size_t argc = 1;
     napi_value argv[1];
@@ -127,6 +183,7 @@ napi_value Init(napi_env env, napi_value exports) {
         {"open", nullptr, Open, nullptr, nullptr, nullptr, napi_default, nullptr},
         {"sym", nullptr, Sym, nullptr, nullptr, nullptr, napi_default, nullptr},
         {"call", nullptr, Call, nullptr, nullptr, nullptr, napi_default, nullptr},
+        {"callAsync", nullptr, CallAsync, nullptr, nullptr, nullptr, napi_default, nullptr},
         {"addressOf", nullptr, AddressOf, nullptr, nullptr, nullptr, napi_default, nullptr},
         {"arrayBuffer", nullptr, ArrayBufferAt, nullptr, nullptr, nullptr, napi_default, nullptr},
     };

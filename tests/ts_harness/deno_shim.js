@@ -3,7 +3,8 @@
 //   Deno.dlopen(path, symbols)            symbol table as ts/verify.ts declares it ({parameters, result,
 //                                         nonblocking}); "pointer" arguments are BigInt addresses or null,
 //                                         "u64" / "usize" / "i64" BigInt, "i32" number.  A nonblocking symbol
-//                                         returns a Promise (the call itself runs synchronously here).
+//                                         returns a Promise and runs on a libuv worker thread (Deno: its
+//                                         blocking-task pool), so calls on different contexts overlap.
 //   Deno.UnsafePointer.of / create / value, Deno.UnsafePointerView.getArrayBuffer
 //   performance (Node 12 keeps it in perf_hooks)
 "use strict";
@@ -35,19 +36,20 @@ const Deno = {
       const kinds = def.parameters;
       const ret = def.result === "void" ? 0 : def.result === "i32" ? 1 : -1;
       if (ret < 0) throw new Error(`deno_shim: result kind ${def.result} is not supported`);
-      const call = (...args) => {
+      const regs = (args) => {
         if (args.length !== kinds.length) throw new Error(`${name}: ${args.length} arguments, ${kinds.length} declared`);
-        return native.call(fn, kinds.map((k, i) => arg(k, args[i])), ret);
+        return kinds.map((k, i) => arg(k, args[i]));
       };
+      // a nonblocking symbol runs on a worker thread and resolves later, as Deno's blocking pool does
       out[name] = def.nonblocking
-        ? (...args) => new Promise((resolve, reject) => {
+        ? (...args) => {
           try {
-            resolve(call(...args));
+            return native.callAsync(fn, regs(args), ret);
           } catch (e) {
-            reject(e);
+            return Promise.reject(e);
           }
-        })
-        : call;
+        }
+        : (...args) => native.call(fn, regs(args), ret);
     }
     return { symbols: out, close() {} };
   },

@@ -9,7 +9,8 @@
 //   "files"    verifyFiles(info, dir)
 //   "piece"    verifyPiece(info, index, bytes)
 //   "hash"     hashPieces(payload, pieceLength)
-//   "verifier" PieceVerifier: onBlock per block, automatic flushes (onVerified), then flush()
+//   "verifier" PieceVerifier: onBlock per block, automatic flushes (onVerified), optionally `settleMs` of
+//              idle time for the age timer, then flush()
 // Bytes travel as base64.  Every result goes to out.json; the Python side compares.
 import { createRequire } from "module";
 import { pathToFileURL } from "url";
@@ -70,6 +71,8 @@ async function main() {
         });
         let completed = 0;
         for (const [index, offset, data] of c.blocks) if (await pv.onBlock(index, offset, b64(data))) completed++;
+        // the age bound also fires without further blocks (its timer): let it
+        if (c.settleMs) await new Promise((res) => setTimeout(res, c.settleMs));
         r.auto = got.slice();
         r.autoFlushes = pv.autoFlushes;
         r.final = await pv.flush();
