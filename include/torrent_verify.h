@@ -107,7 +107,7 @@ int tv_stage(tv_ctx *ctx, uint64_t linear_offset, const uint8_t *src, uint64_t l
  * part-way) returns TV_ERR_IO, and the library marks the pieces Storage.get would return null for
  * (storage.ts:50-65 reads piece by piece): from the piece holding the first byte the file cannot supply
  * to the segment's end.  The whole pieces before that byte are staged and stay readable.  Marked pieces
- * are reported 0 by tv_verify until the next tv_set_layout; the host marks nothing.  Unlike
+ * are reported 0 by tv_verify and tv_verify_list until the next tv_set_layout; the host marks nothing.  Unlike
  * fsStorage.get (which opens with create: true, storage.ts:28-32,158) a missing file is never created.
  * The file is opened as fsStorage.get opens it (read + write, storage.ts:28-32,158): a file this process
  * may not write returns TV_ERR_IO, as Deno.open fails there.  len == 0 reads nothing but still checks the

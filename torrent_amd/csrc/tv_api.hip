@@ -1778,6 +1778,9 @@ int tv_verify_list(tv_ctx* c, const uint64_t* pieces, uint64_t n, uint8_t* ok_ou
     if (reordered)
         for (uint64_t i = 0; i < m; i++)
             if (origin[i] >= 0) ok_out[origin[i]] = ok_launch[i];
+    if (c->any_file_bad)  // pieces file staging could not read (recover_segment) are 0 here too
+        for (uint64_t k = 0; k < n; k++)
+            if (get_bit(c->file_bad.data(), pieces[k] - c->first)) ok_out[k] = 0;
     c->last_kernel = kernel;
     c->last_launches = 1;
     return finish_timing(c);
