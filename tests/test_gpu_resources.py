@@ -228,3 +228,29 @@ def test_failed_segment_marks_last_until_the_next_layout(native, tmp_path):
         ctx.set_digests(digests)
         ctx.stage(0, payload)
         assert _bits(ctx.verify(), P) == [1] * P
+
+
+def test_hash_files_refuses_a_short_or_missing_file(native, tmp_path):
+    """Creation from disk (f3, make_torrent.ts:62-113) hashes the files concatenated in order, and raises
+    instead of hashing a file that is short or missing -- the library's recovery keeps a short file's whole
+    pieces readable for verification, so hash_files checks the statuses, not the availability bits."""
+    from torrent_amd.metainfo import FileInfo, make_info
+    from torrent_amd.verify import hash_files
+    L = 4096
+    sizes = [5 * L + 11, 0, 3 * L, 2 * L + 9]
+    payload = bytes((k * 31 + 5) & 0xFF for k in range(sum(sizes)))
+    P = -(-len(payload) // L)
+    want = b"".join(hashlib.sha1(payload[i * L:(i + 1) * L]).digest() for i in range(P))
+    info = make_info(L, bytes(20 * P), "t", files=[FileInfo(n, [f"f{k}"]) for k, n in enumerate(sizes)])
+    off = 0
+    for k, n in enumerate(sizes):
+        (tmp_path / f"f{k}").write_bytes(payload[off:off + n])
+        off += n
+    for devices in ([0], [0, 0]):
+        assert hash_files(info, str(tmp_path), devices=devices) == want
+    (tmp_path / "f2").write_bytes(payload[sizes[0]:sizes[0] + 3 * L - 1])     # one byte short
+    with pytest.raises(FileNotFoundError):
+        hash_files(info, str(tmp_path))
+    (tmp_path / "f2").unlink()
+    with pytest.raises(FileNotFoundError):
+        hash_files(info, str(tmp_path), devices=[0, 0])

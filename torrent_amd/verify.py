@@ -296,7 +296,7 @@ def verify_stream(info: InfoDict, read, devices=None, avail: Optional[bytes] = N
 
 
 def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: int = 16,
-                 direct_min: Optional[int] = None) -> bytearray:
+                 direct_min: Optional[int] = None, status_out: Optional[list] = None) -> bytearray:
     """Stage the shard's pieces from files into HBM and return the shard's readability bits.
 
     The shard's linear range is mapped to file segments exactly as Storage.get maps it
@@ -306,7 +306,8 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
     The library marks the unreadable pieces itself, exactly as Storage.get(i * L, len_i) would return null
     (storage.ts:50-65,150-172): a piece with a byte in a missing, unopenable or too-short part of a file,
     and a piece whose zero-length segment (storage.ts:109-110) names a path fsStorage.get could not open;
-    a short file's pieces before its end stay readable.  Missing files are never created."""
+    a short file's pieces before its end stay readable.  Missing files are never created.  `status_out`, if
+    given, receives the per-segment statuses (hash_files raises on any failure)."""
     L = info.piece_length
     avail = bytearray(b"\xff" * ((count + 7) // 8))
     if count % 8:
@@ -347,7 +348,9 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
     ctx.set_option(_native.TV_OPT_FILE_DIRECT_MIN, _DIRECT_MIN_BYTES if direct_min is None else direct_min)
     # a failed segment's pieces are marked inside the library (tv_verify reports them 0): from the piece
     # holding its first unreadable byte on, as Storage.get reads piece by piece; the statuses are informational
-    ctx.stage_files([paths[i] for i in k.tolist()], foff, lin, nbytes)
+    status = ctx.stage_files([paths[i] for i in k.tolist()], foff, lin, nbytes)
+    if status_out is not None:
+        status_out.extend(status)
     return avail
 
 
@@ -392,11 +395,12 @@ def hash_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
         ctx.set_layout(info.length, L, P, first, count)
         if count == 0:
             return b""
-        avail = _files_shard(ctx, info, storage, first, count, threads, direct_min)
+        status: list = []
+        avail = _files_shard(ctx, info, storage, first, count, threads, direct_min, status)
         full = bytearray(b"\xff" * ((count + 7) // 8))
         if count % 8:
             full[-1] = (0xFF00 >> (count % 8)) & 0xFF
-        if avail != full:
+        if avail != full or any(st != _native.TV_OK for st in status):
             raise FileNotFoundError("hash_files: a file is missing or shorter than its declared length")
         return ctx.hash()
 
