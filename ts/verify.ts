@@ -202,7 +202,6 @@ export async function verifyPieces(
   return bitfield;
 }
 
-const TV_ERR_IO = -5;
 /** storage.get calls a streamed verify keeps outstanding (file descriptors, not bandwidth, bound it) */
 const READS_IN_FLIGHT = 32;
 const TV_OPT_STREAM_CHUNK = 3;
@@ -316,7 +315,7 @@ export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptio
       // segment of the shard goes to the library in ONE tv_stage_files call
       // The walk's zero-length segments go too (storage.ts:109-110: a file ending exactly where a piece starts,
       // a zero-length file inside a piece): fsStorage.get still opens them (storage.ts:158), and the library
-      // reports TV_ERR_IO where that open would fail.  Such a segment's piece is linear / L.
+      // marks the segment's piece (linear / L) where that open would fail.
       const segs: { path: Uint8Array; fileOffset: number; linear: number; len: number }[] = [];
       let fileStart = 0;
       for (const f of files) {
