@@ -256,3 +256,70 @@ def test_ts_binding_on_the_gpu(native, tmp_path, monkeypatch):
     assert "error" not in va, va.get("error")
     assert {i: ok for i, ok in va["auto"] + va["final"]} == {i: i != bad for i in range(P)}
     assert va["autoFlushes"] >= 1 and va["final"] == [] and va["bitfield"] == want_bits.hex()
+
+
+def test_piece_verifier_policy_on_cpu(tmp_path):
+    """PieceVerifier's flush policy on CPU against a JavaScript model of the library (tests/ts_harness/
+    fake_deno.js: node's SHA-1 as the checker, nonblocking calls resolving on a later turn of the event loop):
+    the count bound flushes every K completed pieces; the age bound alone, through its timer, delivers every
+    result within the settle time even when the timer fires before the oldest piece is T ms old (timers are
+    millisecond-granular), over 40 trials with bursts and idle gaps; a corrupted block re-sent intact
+    verifies."""
+    mod = erased_module(tmp_path)
+    out = run_node(tmp_path, f"""
+import {{ createRequire }} from "module";
+const require = createRequire("{HARNESS}/");
+const Deno = require("./fake_deno.js");
+const crypto = require("crypto");
+const sleep = (ms) => new Promise((r) => setTimeout(r, ms));
+import("{mod}").then(async (m) => {{
+  const L = 32768, P = 29, total = L * (P - 1) + 1000;
+  const payload = crypto.randomBytes(total);
+  const pieces = [];
+  for (let i = 0; i < P; i++) pieces.push(crypto.createHash("sha1").update(payload.slice(i * L, (i + 1) * L)).digest());
+  const info = {{ pieceLength: L, length: total, pieces, name: "t", private: 0 }};
+  const blocks = [];
+  for (let i = 0; i < P; i++) {{
+    const n = i === P - 1 ? 1000 : L;
+    for (let o = 0; o < n; o += 16384) blocks.push([i, o, payload.slice(i * L + o, i * L + Math.min(n, o + 16384))]);
+  }}
+  const res = {{ count: null, age: [] }};
+  // count bound
+  {{
+    const got = [];
+    const pv = new m.PieceVerifier(info, {{ flushPieces: 4, flushAgeMs: null, onVerified: (i, ok) => got.push([i, ok]) }});
+    for (const [i, o, b] of blocks) await pv.onBlock(i, o, b);
+    const fin = await pv.flush();
+    res.count = {{ auto: got.length, autoFlushes: pv.autoFlushes, final: fin.length,
+                   all: [...got, ...fin].filter(([, ok]) => ok).length }};
+    pv.close();
+  }}
+  // age bound only, bursts and gaps
+  for (let trial = 0; trial < 40; trial++) {{
+    const got = [];
+    const pv = new m.PieceVerifier(info, {{ flushPieces: null, flushAgeMs: 2, onVerified: (i, ok) => got.push([i, ok]) }});
+    const order = blocks.slice().sort(() => Math.random() - 0.5);
+    let k = 0;
+    for (const [i, o, b] of order) {{
+      await pv.onBlock(i, o, i === 3 && o === 0 && trial % 2 ? Buffer.alloc(b.length) : b);
+      if (++k % (3 + trial % 5) === 0) await sleep(trial % 3);
+    }}
+    if (trial % 2) {{                                 // once the corrupted piece failed: both blocks re-sent
+      await sleep(10);                                 // (re-sends of a piece still pending are ignored)
+      for (const o of [0, 16384]) await pv.onBlock(3, o, payload.slice(3 * L + o, 3 * L + o + 16384));
+    }}
+    await sleep(60);
+    const fin = await pv.flush();
+    const have = Array.from({{ length: P }}, (_, i) => (pv.bitfield[i >> 3] >> (7 - (i % 8))) & 1);
+    res.age.push({{ auto: got.length, final: fin.length, autoFlushes: pv.autoFlushes, have: have.join("") }});
+    pv.close();
+  }}
+  console.log(JSON.stringify(res));
+}}).catch((e) => {{ console.error(e); process.exit(1); }});
+""")
+    res = json.loads(out)
+    P = 29
+    assert res["count"] == {"auto": 28, "autoFlushes": 7, "final": 1, "all": P}
+    for t, r in enumerate(res["age"]):
+        assert r["final"] == 0, (t, r)                     # the timer delivered everything
+        assert r["autoFlushes"] >= 1 and r["have"] == "1" * P, (t, r)

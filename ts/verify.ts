@@ -472,18 +472,28 @@ export class PieceVerifier {
     if (this.#pending.length === 0) {
       this.#oldest = performance.now();
       // the age bound also holds when no further block arrives
-      if (this.#flushAgeMs !== null) {
-        this.#timer = setTimeout(() => {
-          this._autoFlush().catch((e) => {
-            this.#timerError = e;
-          });
-        }, this.#flushAgeMs);
-      }
+      if (this.#flushAgeMs !== null) this._armTimer(this.#flushAgeMs);
     }
     this.#pending.push(index);
     this.#pendingSet.add(index);
     await this._autoFlush();                                  // the count bound
     return true;
+  }
+
+  private _armTimer(delayMs: number): void {
+    this.#timer = setTimeout(() => {
+      if (this.#pending.length === 0) return;
+      // timers are millisecond-granular and may fire a little before the oldest piece is flushAgeMs old:
+      // then wait out the rest instead of leaving the pending pieces to the next block
+      const wait = (this.#flushAgeMs || 0) - (performance.now() - this.#oldest);
+      if (wait > 0) {
+        this._armTimer(Math.max(1, Math.ceil(wait)));
+        return;
+      }
+      this._autoFlush().catch((e) => {
+        this.#timerError = e;
+      });
+    }, delayMs);
   }
 
   private _rethrow(): void {
