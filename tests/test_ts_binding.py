@@ -323,3 +323,90 @@ import("{mod}").then(async (m) => {{
     for t, r in enumerate(res["age"]):
         assert r["final"] == 0, (t, r)                     # the timer delivered everything
         assert r["autoFlushes"] >= 1 and r["have"] == "1" * P, (t, r)
+
+
+class _PlanCtx:
+    """Records what verify._files_shard hands the library (the Python host's plan)."""
+
+    def __init__(self):
+        self.segments = []
+
+    def set_option(self, key, value):
+        pass
+
+    def stage_files(self, paths, fo, lin, lens):
+        # (Storage keeps the directory relative to the working directory, storage.ts; compare absolute paths)
+        self.segments += [[os.path.abspath(p), int(a), int(b), int(c)] for p, a, b, c in zip(paths, fo, lin, lens)]
+        return [0] * len(paths)
+
+
+def test_verify_files_plan_equals_the_python_host(tmp_path):
+    """verifyFiles (ts/verify.ts) and verify_files (torrent_amd/verify.py) walk the file table on their own;
+    for the 24 seeded random layouts of tests/test_gpu_fuzz.py, on 1 and 3 shards, both hand the library the
+    same segments (path, file offset, linear offset, length; zero-length ones included) and the same
+    availability bits -- checked on CPU with the JS model of the library recording the TS plan."""
+    from tests.test_gpu_fuzz import SEEDS, _draw
+    from torrent_amd import verify
+    from torrent_amd.storage import Storage, fs_storage
+    mod = erased_module(tmp_path)
+    d = "/nonexistent/plan/dl"
+    spec, want = [], []
+    for seed in SEEDS:
+        info = _draw(seed)[0]
+        spec.append(_info_json(info.piece_length, info.length, info.pieces_raw,
+                               None if info.files is None else [(f.length, f.path) for f in info.files],
+                               info.name))
+        st = Storage(fs_storage, info, d)
+        per_n = {}
+        for n in (1, 3):
+            shards, bits = {}, []
+            for first, count in verify.shard_ranges(info.n_pieces, n):
+                if not count:
+                    continue
+                ctx = _PlanCtx()
+                avail = verify._files_shard(ctx, info, st, first, count, threads=1)
+                shards[str(first)] = sorted(ctx.segments)
+                bits += [(avail[j >> 3] >> (7 - (j & 7))) & 1 for j in range(count)]
+            per_n[str(n)] = {"shards": shards, "bits": "".join(map(str, bits))}
+        want.append(per_n)
+    (tmp_path / "spec.json").write_text(json.dumps(spec))
+    out = run_node(tmp_path, f"""
+import {{ createRequire }} from "module";
+const require = createRequire("{HARNESS}/");
+const Deno = require("./fake_deno.js");
+const fs = require("fs");
+import("{mod}").then(async (m) => {{
+  const spec = JSON.parse(fs.readFileSync("{tmp_path}/spec.json", "utf8"));
+  const res = [];
+  for (const d of spec) {{
+    const raw = Buffer.from(d.pieces, "base64");
+    const pieces = [];
+    for (let i = 0; i < raw.length; i += 20) pieces.push(new Uint8Array(raw.subarray(i, Math.min(raw.length, i + 20))));
+    const info = {{ pieceLength: d.pieceLength, length: d.length, pieces, name: d.name, private: 0 }};
+    if (d.files) info.files = d.files;
+    const per = {{}};
+    for (const n of [1, 3]) {{
+      await m.releaseContexts();
+      Deno.fakeReset();
+      const bf = await m.verifyFiles(info, "{d}", {{ devices: Array(n).fill(0) }});
+      const shards = {{}};
+      for (const c of Deno.fakeContexts.values()) {{
+        if (c.segments) shards[String(c.first)] = c.segments.slice().sort((x, y) =>
+          x[0] < y[0] ? -1 : x[0] > y[0] ? 1 : x[1] - y[1] || x[2] - y[2] || x[3] - y[3]);
+      }}
+      let bits = "";
+      for (let i = 0; i < pieces.length; i++) bits += (bf[i >> 3] >> (7 - (i % 8))) & 1;
+      per[String(n)] = {{ shards, bits }};
+    }}
+    res.push(per);
+  }}
+  console.log(JSON.stringify(res));
+}}).catch((e) => {{ console.error(e); process.exit(1); }});
+""")
+    got = json.loads(out)
+    for seed, g, w in zip(SEEDS, got, want):
+        for n in ("1", "3"):
+            g[n]["shards"] = {k: sorted([os.path.abspath(x[0])] + x[1:] for x in v) for k, v in g[n]["shards"].items()}
+            assert g[n]["bits"] == w[n]["bits"], (seed, n)
+            ws = {k: v for k, v in w[n]["shards"].items() if v}
+            assert g[n]["shards"] == ws, (seed, n)

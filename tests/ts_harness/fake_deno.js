@@ -1,17 +1,35 @@
 // fake_deno.js -- a CPU model of the library behind the Deno FFI, for the TS host logic on CPU (test
 // infrastructure only; tests/test_ts_binding.py).  Deno.dlopen returns JavaScript implementations of the
 // calls PieceVerifier makes (tv_create / tv_set_layout / tv_set_digests / tv_stage / tv_verify_list /
-// tv_destroy / tv_last_error / tv_abi_version), with SHA-1 from node's crypto as the checker; every other
-// symbol throws if called.  Pointers are the typed arrays themselves.  `nonblocking` symbols resolve on a
+// tv_destroy / tv_last_error / tv_abi_version), with SHA-1 from node's crypto as the checker, and the
+// calls verifyFiles makes (tv_set_option, tv_stage_files recording the host's segment plan, tv_verify
+// returning the host's availability bits); every other symbol throws if called.  Pointers are BigInt
+// addresses of registered typed arrays.  `nonblocking` symbols resolve on a
 // later turn of the event loop, as Deno's do, so the verifier's timer and its block handler interleave.
 "use strict";
 const crypto = require("crypto");
 
 const contexts = new Map();
 let nextHandle = 1n;
+// pointers: UnsafePointer.of registers a typed array under a BigInt address, as the real one returns one
+const memory = new Map();
+let nextAddress = 0x1000n;
 
 function bytesOf(p) {
-  return p instanceof Uint8Array ? p : new Uint8Array(p.buffer, p.byteOffset, p.byteLength);
+  const ta = typeof p === "bigint" ? memory.get(p) : p;
+  if (!ta) throw new Error("fake_deno: unknown pointer " + p);
+  return ta instanceof Uint8Array ? ta : new Uint8Array(ta.buffer, ta.byteOffset, ta.byteLength);
+}
+
+function u64s(p, n) {
+  const b = bytesOf(p);
+  return new BigUint64Array(b.buffer.slice(b.byteOffset, b.byteOffset + 8 * n));
+}
+
+function cString(p) {
+  const b = bytesOf(p);
+  const end = b.indexOf(0);
+  return Buffer.from(b.subarray(0, end < 0 ? b.length : end)).toString("utf8");
 }
 
 const impl = {
@@ -51,6 +69,26 @@ const impl = {
     });
     return 0;
   },
+  tv_set_option: () => 0,
+  // tv_stage_files records the segments it is given (the host's plan) and reports them all readable
+  tv_stage_files(ctx, n, pathsp, fop, linp, lenp, statusp) {
+    const k = Number(n);
+    const paths = u64s(pathsp, k), fo = u64s(fop, k), lin = u64s(linp, k), len = u64s(lenp, k);
+    const c = contexts.get(ctx);
+    c.segments = c.segments || [];
+    for (let q = 0; q < k; q++) c.segments.push([cString(paths[q]), Number(fo[q]), Number(lin[q]), Number(len[q])]);
+    new Int32Array(bytesOf(statusp).buffer, bytesOf(statusp).byteOffset, k).fill(0);
+    return 0;
+  },
+  // tv_verify hands back the host's availability bits (shard-relative), so the host's own clearing shows
+  tv_verify(ctx, availp, outp) {
+    const c = contexts.get(ctx);
+    const out = bytesOf(outp);
+    const n = Math.ceil(c.count / 8);
+    if (availp === null) out.fill(0xff, 0, n);
+    else out.set(bytesOf(availp).subarray(0, n));
+    return 0;
+  },
   tv_destroy(ctx) {
     contexts.delete(ctx);
   },
@@ -76,9 +114,22 @@ const Deno = {
     }
     return { symbols: out, close() {} };
   },
-  UnsafePointer: { of: (ta) => ta, create: (v) => (v === 0n ? null : v), value: (p) => p },
+  UnsafePointer: {
+    of(ta) {
+      const a = nextAddress;
+      nextAddress += 0x1000n;
+      memory.set(a, ta);
+      return a;
+    },
+    create: (v) => (v === 0n ? null : v),
+    value: (p) => (p === null ? 0n : p),
+  },
   UnsafePointerView: {},
   fakeContexts: contexts,
+  fakeReset() {
+    contexts.clear();
+    memory.clear();
+  },
 };
 
 globalThis.Deno = Deno;
