@@ -410,3 +410,76 @@ import("{mod}").then(async (m) => {{
             assert g[n]["bits"] == w[n]["bits"], (seed, n)
             ws = {k: v for k, v in w[n]["shards"].items() if v}
             assert g[n]["shards"] == ws, (seed, n)
+
+
+def test_verify_stream_host_logic_on_cpu(tmp_path):
+    """verifyStream's host side (ts/verify.ts: request loop, row lengths, unreadable rows, the worker pool of
+    reads, shard concatenation) on CPU against the JS model of the tv_stream_* protocol (several requests per
+    column; column widths L, 64 B and 4 KiB) for the 24 seeded fuzz layouts on 1 and 3 shards, with
+    unreadable pieces and rows one byte too long: the bits equal hashlib over Storage.get's bytes."""
+    from tests.test_gpu_fuzz import SEEDS, _draw
+    from torrent_amd.piece import piece_length
+    import random as _random
+    mod = erased_module(tmp_path)
+    spec, want = [], []
+    for seed in SEEDS:
+        info, payload = _draw(seed)[:2]
+        P, L, total = info.n_pieces, info.piece_length, info.length
+        rng = _random.Random(seed)
+        unreadable = sorted(rng.sample(range(P), min(2, P)))
+        wrong = sorted(rng.sample(range(P), 1))
+        spec.append({"info": _info_json(L, total, info.pieces_raw), "payload": _b64(payload[:total]),
+                     "unreadable": unreadable, "wrong": wrong, "chunk": rng.choice([0, 64, 4096])})
+        bits = ""
+        for i in range(P):
+            n = piece_length(i, info)
+            d = info.pieces_raw[20 * i:20 * i + 20]
+            ok = (i not in unreadable and i not in wrong and i * L + n <= total and len(d) == 20 and
+                  hashlib.sha1(payload[i * L:i * L + n]).digest() == d)
+            bits += "1" if ok else "0"
+        want.append(bits)
+    (tmp_path / "spec.json").write_text(json.dumps(spec))
+    out = run_node(tmp_path, f"""
+import {{ createRequire }} from "module";
+const require = createRequire("{HARNESS}/");
+const Deno = require("./fake_deno.js");
+const fs = require("fs");
+import("{mod}").then(async (m) => {{
+  const spec = JSON.parse(fs.readFileSync("{tmp_path}/spec.json", "utf8"));
+  const res = [];
+  for (const d of spec) {{
+    const raw = Buffer.from(d.info.pieces, "base64");
+    const pieces = [];
+    for (let i = 0; i < raw.length; i += 20) pieces.push(new Uint8Array(raw.subarray(i, Math.min(raw.length, i + 20))));
+    const info = {{ pieceLength: d.info.pieceLength, length: d.info.length, pieces, name: "t", private: 0 }};
+    const payload = new Uint8Array(Buffer.from(d.payload, "base64"));
+    const L = info.pieceLength, bad = new Set(d.unreadable), wrong = new Set(d.wrong);
+    const storage = {{
+      async get(offset, length) {{
+        await new Promise((r) => setImmediate(r));
+        const i = Math.floor(offset / L);
+        if (bad.has(i) || offset + length > payload.length) return null;
+        const b = payload.slice(offset, offset + length);
+        if (!wrong.has(i)) return b;
+        const longer = new Uint8Array(length + 1);
+        longer.set(b);
+        return longer;
+      }},
+    }};
+    const per = [];
+    for (const n of [1, 3]) {{
+      await m.releaseContexts();
+      Deno.fakeReset();
+      const bf = await m.verifyStream(info, storage, {{ devices: Array(n).fill(0), chunk: d.chunk }});
+      let bits = "";
+      for (let i = 0; i < pieces.length; i++) bits += (bf[i >> 3] >> (7 - (i % 8))) & 1;
+      per.push(bits);
+    }}
+    res.push(per);
+  }}
+  console.log(JSON.stringify(res));
+}}).catch((e) => {{ console.error(e); process.exit(1); }});
+""")
+    got = json.loads(out)
+    for seed, g, w in zip(SEEDS, got, want):
+        assert g == [w, w], (seed, g, w)

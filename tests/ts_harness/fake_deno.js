@@ -3,7 +3,8 @@
 // calls PieceVerifier makes (tv_create / tv_set_layout / tv_set_digests / tv_stage / tv_verify_list /
 // tv_destroy / tv_last_error / tv_abi_version), with SHA-1 from node's crypto as the checker, and the
 // calls verifyFiles makes (tv_set_option, tv_stage_files recording the host's segment plan, tv_verify
-// returning the host's availability bits); every other symbol throws if called.  Pointers are BigInt
+// returning the host's availability bits) and verifyStream makes (the tv_stream_* protocol, modelled with
+// several requests per column); every other symbol throws if called.  Pointers are BigInt
 // addresses of registered typed arrays.  `nonblocking` symbols resolve on a
 // later turn of the event loop, as Deno's do, so the verifier's timer and its block handler interleave.
 "use strict";
@@ -69,7 +70,78 @@ const impl = {
     });
     return 0;
   },
-  tv_set_option: () => 0,
+  tv_set_option(ctx, key, value) {
+    const c = contexts.get(ctx);
+    c.options = c.options || {};
+    c.options[Number(key)] = Number(value);
+    return 0;
+  },
+  // the stream protocol (tv_stream_*): columns of width C (TV_OPT_STREAM_CHUNK, else the piece length),
+  // requests of at most 7 rows so a shard takes several, rows appended per piece and hashed at the end
+  tv_stream_begin(ctx, availp) {
+    const c = contexts.get(ctx);
+    const C = (c.options && c.options[3]) || c.L;
+    const reqs = [];
+    for (let off = 0; off < c.L; off += C) {
+      for (let j = 0; j < c.count; j += 7) reqs.push({ piece: c.first + j, rows: Math.min(7, c.count - j), offset: off, width: C });
+    }
+    const avail = availp === null ? null : Buffer.from(bytesOf(availp).slice(0, Math.ceil(c.count / 8)));
+    c.stream = { reqs, k: 0, data: new Map(), unreadable: new Set(), avail };
+    return 0;
+  },
+  tv_stream_next(ctx, reqp) {
+    const c = contexts.get(ctx);
+    const st = c.stream;
+    const out = new BigUint64Array(bytesOf(reqp).buffer, bytesOf(reqp).byteOffset, 6);
+    if (st.k >= st.reqs.length) {
+      out.fill(0n);
+      return 0;
+    }
+    const r = st.reqs[st.k];
+    const slot = new ArrayBuffer(r.rows * r.width);
+    const addr = Deno.UnsafePointer.of(new Uint8Array(slot));
+    st.slot = slot;
+    out.set([BigInt(r.piece), BigInt(r.rows), BigInt(r.offset), BigInt(r.width), addr, BigInt(st.k)]);
+    return 0;
+  },
+  tv_stream_unreadable(ctx, piece) {
+    contexts.get(ctx).stream.unreadable.add(Number(piece));
+    return 0;
+  },
+  tv_stream_commit(ctx) {
+    const c = contexts.get(ctx);
+    const st = c.stream;
+    const r = st.reqs[st.k++];
+    const slot = new Uint8Array(st.slot);
+    for (let q = 0; q < r.rows; q++) {
+      const i = r.piece + q;
+      const plen = i === c.P - 1 && c.total % c.L ? c.total % c.L : c.L;
+      const n = Math.max(0, Math.min(r.width, plen - r.offset));
+      const prev = st.data.get(i) || Buffer.alloc(0);
+      st.data.set(i, Buffer.concat([prev, Buffer.from(slot.subarray(q * r.width, q * r.width + n))]));
+    }
+    return 0;
+  },
+  tv_stream_end(ctx, outp) {
+    const c = contexts.get(ctx);
+    const st = c.stream;
+    const out = bytesOf(outp);
+    out.fill(0, 0, Math.ceil(c.count / 8));
+    for (let j = 0; j < c.count; j++) {
+      const i = c.first + j;
+      const d = c.digests.slice(20 * i, 20 * i + 20);
+      const okAvail = !st.avail || (st.avail[j >> 3] >> (7 - (j % 8))) & 1;
+      const ok = okAvail && !st.unreadable.has(i) && d.length === 20 &&
+        crypto.createHash("sha1").update(st.data.get(i) || Buffer.alloc(0)).digest().equals(d);
+      if (ok) out[j >> 3] |= 0x80 >> (j % 8);
+    }
+    c.stream = null;
+    return 0;
+  },
+  tv_stream_abort(ctx) {
+    contexts.get(ctx).stream = null;
+    return 0;
+  },
   // tv_stage_files records the segments it is given (the host's plan) and reports them all readable
   tv_stage_files(ctx, n, pathsp, fop, linp, lenp, statusp) {
     const k = Number(n);
@@ -124,7 +196,13 @@ const Deno = {
     create: (v) => (v === 0n ? null : v),
     value: (p) => (p === null ? 0n : p),
   },
-  UnsafePointerView: {},
+  UnsafePointerView: {
+    getArrayBuffer(p, len) {
+      const ta = memory.get(p);
+      if (!ta || ta.byteLength < len) throw new Error("fake_deno: getArrayBuffer of an unknown or short pointer");
+      return ta.buffer;
+    },
+  },
   fakeContexts: contexts,
   fakeReset() {
     contexts.clear();
