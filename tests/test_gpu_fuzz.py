@@ -14,7 +14,7 @@ import random
 
 import pytest
 
-SEEDS = list(range(24))
+SEEDS = list(range(48))
 
 
 def _draw(seed):

@@ -342,7 +342,7 @@ class _PlanCtx:
 
 def test_verify_files_plan_equals_the_python_host(tmp_path):
     """verifyFiles (ts/verify.ts) and verify_files (torrent_amd/verify.py) walk the file table on their own;
-    for the 24 seeded random layouts of tests/test_gpu_fuzz.py, on 1 and 3 shards, both hand the library the
+    for the 48 seeded random layouts of tests/test_gpu_fuzz.py, on 1 and 3 shards, both hand the library the
     same segments (path, file offset, linear offset, length; zero-length ones included) and the same
     availability bits -- checked on CPU with the JS model of the library recording the TS plan."""
     from tests.test_gpu_fuzz import SEEDS, _draw
@@ -415,7 +415,7 @@ import("{mod}").then(async (m) => {{
 def test_verify_stream_host_logic_on_cpu(tmp_path):
     """verifyStream's host side (ts/verify.ts: request loop, row lengths, unreadable rows, the worker pool of
     reads, shard concatenation) on CPU against the JS model of the tv_stream_* protocol (several requests per
-    column; column widths L, 64 B and 4 KiB) for the 24 seeded fuzz layouts on 1 and 3 shards, with
+    column; column widths L, 64 B and 4 KiB) for the 48 seeded fuzz layouts on 1 and 3 shards, with
     unreadable pieces and rows one byte too long: the bits equal hashlib over Storage.get's bytes."""
     from tests.test_gpu_fuzz import SEEDS, _draw
     from torrent_amd.piece import piece_length
