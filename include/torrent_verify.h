@@ -272,6 +272,11 @@ int tv_host_unregister(void *ptr);
 #define TV_OPT_TWIN_FILL_READS 14 /* companion workgroups' loads: 0 (default) = every lane of a companion reads its
                                     main workgroup's first piece (the same instruction stream, 1/32 of the bytes);
                                     1 = the main workgroup's 32 pieces (round 2; 1.14-1.42 x payload of HBM reads) */
+#define TV_OPT_NUMA_BIND 15 /* 1 (default) = the library's host threads (file readers, ring copies, the staging
+                               helper lane) run on the CPUs of the GPU's NUMA node, and the pinned ring is
+                               allocated on that node (slots allocated after the option is set); 0 = unpinned,
+                               default placement.  An MI355X node has two sockets with four GPUs each: a copy
+                               from the far socket crosses the inter-socket link twice (read, then DMA). */
 int tv_set_option(tv_ctx *ctx, int key, int64_t value);
 int tv_get_option(tv_ctx *ctx, int key, int64_t *value);
 
@@ -292,6 +297,10 @@ int tv_last_kernel(tv_ctx *ctx, int *kernel, int *launches);
 #define TV_COUNTER_DEVICE_BYTES 4   /* bytes of device memory held now */
 #define TV_COUNTER_LAST_WORKGROUPS 5 /* workgroups of the last verify / hash / list launch (companion
                                         workgroups of TV_OPT_TWIN_FILL included) */
+#define TV_COUNTER_NUMA_NODE 6       /* the GPU's NUMA node (sysfs numa_node of its PCI function); UINT64_MAX if
+                                        unknown */
+#define TV_COUNTER_RING_NODE 7       /* the NUMA node holding the first pinned ring slot's first page; UINT64_MAX
+                                        if the ring is not allocated yet or the node is unknown */
 int tv_get_counter(tv_ctx *ctx, int key, uint64_t *value);
 
 /* Block until all work queued by the ctx is complete. */

@@ -254,3 +254,40 @@ def test_hash_files_refuses_a_short_or_missing_file(native, tmp_path):
     (tmp_path / "f2").unlink()
     with pytest.raises(FileNotFoundError):
         hash_files(info, str(tmp_path), devices=[0, 0])
+
+
+def test_numa_binding_places_the_ring_and_keeps_results(native, tmp_path):
+    """TV_OPT_NUMA_BIND (default on): the ctx knows its GPU's NUMA node (sysfs numa_node of the GPU's PCI
+    function), allocates its pinned ring there, and the bits of a files staging are the same bound and
+    unbound (the binding moves the library's threads, nothing else)."""
+    import ctypes
+    L, P = 65536, 40
+    payload = bytes((k * 11 + 3) & 0xFF for k in range(L * P - 777))
+    digests = b"".join(hashlib.sha1(payload[i * L:(i + 1) * L]).digest() for i in range(P))
+    f = tmp_path / "t.bin"
+    f.write_bytes(payload)
+    hip = ctypes.CDLL("libamdhip64.so")
+    buf = ctypes.create_string_buffer(64)
+    assert hip.hipDeviceGetPCIBusId(buf, 64, 0) == 0
+    try:
+        sys_node = int(open(f"/sys/bus/pci/devices/{buf.value.decode().lower()}/numa_node").read())
+    except OSError:
+        sys_node = -1
+    results = []
+    for bind in (1, 0):
+        with native.Context(0) as ctx:
+            assert ctx.get_option(native.TV_OPT_NUMA_BIND) == 1
+            node = ctx.counter(native.TV_COUNTER_NUMA_NODE)
+            assert node == (sys_node if sys_node >= 0 else 2 ** 64 - 1)
+            ctx.set_option(native.TV_OPT_NUMA_BIND, bind)
+            ctx.set_option(native.TV_OPT_FILE_DIRECT_MIN, 1 << 62)          # every segment via the readers
+            ctx.set_layout(len(payload), L, P)
+            ctx.set_digests(digests)
+            assert ctx.counter(native.TV_COUNTER_RING_NODE) == 2 ** 64 - 1    # no ring yet
+            segs = [(0, 5 * L + 9), (5 * L + 9, 17 * L), (22 * L + 9, len(payload) - 22 * L - 9)]
+            st = ctx.stage_files([str(f)] * 3, [a for a, _ in segs], [a for a, _ in segs], [n for _, n in segs])
+            assert st == [0, 0, 0]
+            if bind and sys_node >= 0:
+                assert ctx.counter(native.TV_COUNTER_RING_NODE) == sys_node
+            results.append(bytes(ctx.verify()))
+    assert results[0] == results[1] and _bits(results[0], P) == [1] * P

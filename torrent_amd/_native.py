@@ -35,12 +35,15 @@ TV_OPT_DEBUG_REBOUNCE = 11
 TV_OPT_TWIN_PACK = 12
 TV_OPT_TWIN_FILL = 13
 TV_OPT_TWIN_FILL_READS = 14
+TV_OPT_NUMA_BIND = 15
 
 TV_COUNTER_PAYLOAD_ALLOCS = 1
 TV_COUNTER_DEVICE_ALLOCS = 2
 TV_COUNTER_PAYLOAD_BYTES = 3
 TV_COUNTER_DEVICE_BYTES = 4
 TV_COUNTER_LAST_WORKGROUPS = 5
+TV_COUNTER_NUMA_NODE = 6
+TV_COUNTER_RING_NODE = 7
 
 TV_STREAM_RING_SLOTS = 3
 TV_STREAM_SLOT_BYTES = 64 << 20

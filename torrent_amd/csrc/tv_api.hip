@@ -6,12 +6,16 @@
 // runs).
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <pthread.h>
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
+#include <cctype>
 #include <cerrno>
 #include <condition_variable>
 #include <cstdarg>
@@ -35,11 +39,101 @@ constexpr uint64_t kSlack = 256;                          // bytes past the last
 constexpr int kRingSlots = TV_STREAM_RING_SLOTS;          // pinned staging buffers per lane
 constexpr size_t kRingSlotBytes = TV_STREAM_SLOT_BYTES;
 
+// Pin the calling thread to `cpus` (nullptr: leave it).  Used for the library's own threads only.
+void pin_thread(const cpu_set_t* cpus) {
+    if (cpus) (void)pthread_setaffinity_np(pthread_self(), sizeof(cpu_set_t), cpus);
+}
+
+// The NUMA node of GPU `device` (its PCI function's numa_node in sysfs), or -1.
+int gpu_numa_node(int device) {
+    char bdf[64] = {0};
+    if (hipDeviceGetPCIBusId(bdf, (int)sizeof bdf, device) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    for (char* p = bdf; *p; p++) *p = (char)tolower((unsigned char)*p);
+    const std::string path = std::string("/sys/bus/pci/devices/") + bdf + "/numa_node";
+    FILE* f = fopen(path.c_str(), "r");
+    if (!f) return -1;
+    int node = -1;
+    if (fscanf(f, "%d", &node) != 1) node = -1;
+    fclose(f);
+    return node;
+}
+
+// The CPUs of NUMA node `node` that this process may run on (sysfs cpulist & sched_getaffinity).
+bool node_cpus(int node, cpu_set_t* out) {
+    CPU_ZERO(out);
+    if (node < 0) return false;
+    char path[96];
+    snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+    FILE* f = fopen(path, "r");
+    if (!f) return false;
+    char list[4096] = {0};
+    const bool got = fgets(list, sizeof list, f) != nullptr;
+    fclose(f);
+    if (!got) return false;
+    for (char* p = list; *p && *p != '\n';) {
+        char* end = nullptr;
+        const long a = strtol(p, &end, 10);
+        if (end == p) break;
+        long b = a;
+        p = end;
+        if (*p == '-') {
+            b = strtol(p + 1, &end, 10);
+            p = end;
+        }
+        for (long cpu = a; cpu <= b && cpu < CPU_SETSIZE; cpu++) CPU_SET((int)cpu, out);
+        if (*p == ',') p++;
+    }
+    cpu_set_t allowed;
+    if (sched_getaffinity(0, sizeof allowed, &allowed) == 0) CPU_AND(out, out, &allowed);
+    return CPU_COUNT(out) > 0;
+}
+
+// hipHostMalloc with the pages placed on NUMA node `node` (>= 0): the calling thread's memory policy is set
+// to prefer that node around the allocation (hipHostMallocNumaUser makes HIP follow it) and restored.
+hipError_t host_malloc_on_node(void** p, size_t bytes, int node) {
+    if (node < 0 || node >= 1024) return hipHostMalloc(p, bytes, hipHostMallocDefault);
+    int old_mode = 0;
+    unsigned long old_mask[16] = {0};
+    if (syscall(SYS_get_mempolicy, &old_mode, old_mask, 1024ul, nullptr, 0ul) != 0)
+        return hipHostMalloc(p, bytes, hipHostMallocDefault);
+    unsigned long mask[16] = {0};
+    mask[node / 64] = 1ul << (node % 64);
+    constexpr int kMpolPreferred = 1;
+    if (syscall(SYS_set_mempolicy, kMpolPreferred, mask, 1024ul) != 0)
+        return hipHostMalloc(p, bytes, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(p, bytes, hipHostMallocNumaUser);
+    (void)syscall(SYS_set_mempolicy, old_mode, old_mode ? old_mask : nullptr, old_mode ? 1024ul : 0ul);
+    if (e != hipSuccess) {  // a runtime without the flag: default placement
+        (void)hipGetLastError();
+        e = hipHostMalloc(p, bytes, hipHostMallocDefault);
+    }
+    return e;
+}
+
+// The NUMA node holding the page at `p` (get_mempolicy MPOL_F_NODE | MPOL_F_ADDR), or -1.
+int page_node(const void* p) {
+    int node = -1;
+    constexpr unsigned long kFNode = 1, kFAddr = 2;
+    if (!p || syscall(SYS_get_mempolicy, &node, nullptr, 0ul, p, kFNode | kFAddr) != 0) return -1;
+    return node;
+}
+
 // Persistent host workers (one pool per staging lane): run(threads, tasks, fn) calls fn(0..tasks-1) on up
 // to `threads` threads, the caller included, and returns when every task is done.  Spawning threads for
-// every 64 MiB staging slot cost ~0.3 ms a slot, a quarter of the slot's PCIe time.
+// every 64 MiB staging slot cost ~0.3 ms a slot, a quarter of the slot's PCIe time.  With an affinity set
+// (the GPU's NUMA node, TV_OPT_NUMA_BIND) the workers run on those CPUs and the caller only waits, so every
+// copy into the pinned ring runs next to the ring's memory and the GPU.
 class Pool {
   public:
+    void set_affinity(const cpu_set_t* cpus) {
+        std::lock_guard<std::mutex> g(mu_);
+        has_aff_ = cpus != nullptr;
+        if (cpus) aff_ = *cpus;
+        aff_gen_++;
+    }
     ~Pool() {
         {
             std::lock_guard<std::mutex> g(mu_);
@@ -55,16 +149,19 @@ class Pool {
             return;
         }
         std::unique_lock<std::mutex> lk(mu_);
-        while (th_.size() < t - 1) th_.emplace_back([this] { loop(); });
+        const bool caller_works = !has_aff_;
+        const uint64_t workers = caller_works ? t - 1 : t;
+        while (th_.size() < workers) th_.emplace_back([this] { loop(); });
         fn_ = &fn;
         tasks_ = tasks;
         next_ = 0;
-        open_ = (int)t - 1;
+        open_ = (int)workers;
         gen_++;
         lk.unlock();
         cv_.notify_all();
-        work();
+        if (caller_works) work();
         lk.lock();
+        done_.wait(lk, [&] { return next_ >= tasks_; });  // (unpinned caller: every task claimed)
         open_ = 0;  // no late joiner may start on this run once the caller has seen every task claimed
         done_.wait(lk, [&] { return running_ == 0; });
     }
@@ -74,7 +171,9 @@ class Pool {
         for (uint64_t q = next_++; q < tasks_; q = next_++) (*fn_)(q);
     }
     void loop() {
-        uint64_t seen = 0;
+        uint64_t seen = 0, aff_seen = 0;
+        cpu_set_t all;
+        const bool have_all = sched_getaffinity(0, sizeof all, &all) == 0;  // the process's CPUs, to unpin
         std::unique_lock<std::mutex> lk(mu_);
         for (;;) {
             cv_.wait(lk, [&] { return stop_ || (gen_ != seen && open_ > 0); });
@@ -82,6 +181,11 @@ class Pool {
             seen = gen_;
             open_--;
             running_++;
+            if (aff_seen != aff_gen_) {
+                aff_seen = aff_gen_;
+                if (has_aff_) pin_thread(&aff_);
+                else if (have_all) pin_thread(&all);
+            }
             lk.unlock();
             work();
             lk.lock();
@@ -97,6 +201,9 @@ class Pool {
     int open_ = 0, running_ = 0;
     uint64_t gen_ = 0;
     bool stop_ = false;
+    bool has_aff_ = false;
+    cpu_set_t aff_;
+    uint64_t aff_gen_ = 0;
 };
 
 // One streamed verify (tv_stream_*): columns of C bytes of every shard piece flow host -> pinned ring
@@ -192,6 +299,12 @@ struct tv_ctx {
     bool ring2_lent[kRingSlots] = {false, false, false};
     int ring2_next = 0;
     Pool pool[2];                     // host workers of lane 0 / lane 1
+    // the GPU's NUMA node (-1: unknown) and its CPUs the process may use; with numa_bind the library's
+    // threads run there and the pinned ring is allocated there (TV_OPT_NUMA_BIND)
+    int numa_node = -1;
+    bool numa_cpus_ok = false;
+    cpu_set_t numa_cpus;
+    bool numa_bind = true;
     std::mutex err_mu;                // fail() may run on a tv_stage_files helper thread
     uint8_t* h_bits = nullptr;        // pinned bitfield bounce buffer
     size_t h_bits_cap = 0;
@@ -246,6 +359,17 @@ inline bool get_bit(const uint8_t* bf, uint64_t i) { return (bf[i >> 3] >> (7 - 
 // {read: true, write: true, create: true}, storage.ts:28-32,158)?  0, or the errno that open would fail with.
 int rw_access(const char* path) {
     return faccessat(AT_FDCWD, path, R_OK | W_OK, AT_EACCESS) == 0 ? 0 : errno;
+}
+
+
+// Open an existing file for reading the way fsStorage.get opens it, read + write (storage.ts:28-32,158):
+// -1 and *err = errno where that open fails (no write permission, a directory, a read-only filesystem).
+// One open(O_RDWR) walks the path once; an access(R_OK | W_OK) check before an O_RDONLY open walked it
+// twice and was 4-5 % slower on 10,000 small files (profiles/r03/f2_numa_ab.jsonl).  Nothing is written.
+int open_rw(const char* path, int* err) {
+    const int fd = open(path, O_RDWR | O_CLOEXEC);
+    *err = fd < 0 ? errno : 0;
+    return fd;
 }
 
 // Would fsStorage.get's Deno.open(path, {read, write, create}) succeed (storage.ts:28-32,158)?  Checked
@@ -327,10 +451,18 @@ RingRef ring_ref(tv_ctx* c, int which) {
 
 hipStream_t lane_stream(const tv_ctx* c, int which) { return which ? c->copy_stream2 : c->copy_stream; }
 
+// The CPUs the context's library threads run on: the GPU's NUMA node when bound, else none (unpinned).
+const cpu_set_t* numa_cpus(const tv_ctx* c) { return (c->numa_bind && c->numa_cpus_ok) ? &c->numa_cpus : nullptr; }
+
+void apply_numa(tv_ctx* c) {
+    for (auto& p : c->pool) p.set_affinity(numa_cpus(c));
+}
+
 int ensure_ring(tv_ctx* c, int which = 0) {
     RingRef r = ring_ref(c, which);
     for (int s = 0; s < kRingSlots; s++) {
-        if (!r.buf[s]) TV_HIP(c, hipHostMalloc((void**)&r.buf[s], kRingSlotBytes, hipHostMallocDefault));
+        if (!r.buf[s])
+            TV_HIP(c, host_malloc_on_node((void**)&r.buf[s], kRingSlotBytes, c->numa_bind ? c->numa_node : -1));
         if (!r.ev[s]) TV_HIP(c, hipEventCreateWithFlags(&r.ev[s], hipEventDisableTiming));
     }
     return TV_OK;
@@ -735,7 +867,7 @@ double resident_fraction(void* m, uint64_t n, uint64_t page) {
 // Read file bytes [fo, fo + n) into dst with parallel preads (4 MiB parts on up to max_threads threads,
 // TV_OPT_FILE_THREADS: a cold file is read with many large requests in flight).  Returns 0 or an
 // errno value (EIO for a short read).
-int pread_parallel(int fd, uint8_t* dst, uint64_t fo, uint64_t n, int max_threads) {
+int pread_parallel(int fd, uint8_t* dst, uint64_t fo, uint64_t n, int max_threads, const cpu_set_t* cpus) {
     const uint64_t part = 4ull << 20;
     const uint64_t nparts = (n + part - 1) / part;
     const int threads = (int)std::min<uint64_t>((uint64_t)std::max(1, max_threads), nparts);
@@ -756,7 +888,11 @@ int pread_parallel(int fd, uint8_t* dst, uint64_t fo, uint64_t n, int max_thread
         }
     };
     std::vector<std::thread> th;
-    for (int t = 1; t < threads; t++) th.emplace_back(work, t);
+    for (int t = 1; t < threads; t++)
+        th.emplace_back([&work, cpus, t] {
+            pin_thread(cpus);
+            work(t);
+        });
     if (threads > 0) work(0);
     for (auto& t : th) t.join();
     for (int e : err)
@@ -1023,6 +1159,10 @@ int tv_create(tv_ctx** out, int device) {
         tv_destroy(c);
         return TV_ERR_HIP;
     }
+    // the GPU's NUMA node: the library's threads and pinned ring go there (TV_OPT_NUMA_BIND, default on)
+    c->numa_node = gpu_numa_node(device);
+    c->numa_cpus_ok = node_cpus(c->numa_node, &c->numa_cpus);
+    apply_numa(c);
     *out = c;
     return TV_OK;
 }
@@ -1130,6 +1270,11 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
             if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_TWIN_FILL_READS must be 0 or 1");
             c->fill_all = value != 0;
             return TV_OK;
+        case TV_OPT_NUMA_BIND:
+            if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_NUMA_BIND must be 0 or 1");
+            c->numa_bind = value != 0;
+            apply_numa(c);
+            return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
@@ -1152,6 +1297,7 @@ int tv_get_option(tv_ctx* c, int key, int64_t* value) {
         case TV_OPT_TWIN_PACK: *value = c->twin_pack ? 1 : 0; return TV_OK;
         case TV_OPT_TWIN_FILL: *value = c->twin_fill; return TV_OK;
         case TV_OPT_TWIN_FILL_READS: *value = c->fill_all ? 1 : 0; return TV_OK;
+        case TV_OPT_NUMA_BIND: *value = c->numa_bind ? 1 : 0; return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
@@ -1302,10 +1448,10 @@ int stage_file_locked(tv_ctx* c, const char* path, uint64_t file_offset, uint64_
         const int e = fs_openable(path);
         return e ? fail(c, TV_ERR_IO, "open %s: %s", path, strerror(e)) : TV_OK;
     }
-    if (const int e = rw_access(path)) return fail(c, TV_ERR_IO, "open %s for read and write: %s", path, strerror(e));
     FileWindows win;  // before `drain`: destroyed after the streams are drained
-    win.fd = open(path, O_RDONLY | O_CLOEXEC);
-    if (win.fd < 0) return fail(c, TV_ERR_IO, "open %s: %s", path, strerror(errno));
+    int oe = 0;
+    win.fd = open_rw(path, &oe);
+    if (win.fd < 0) return fail(c, TV_ERR_IO, "open %s for read and write: %s", path, strerror(oe));
     struct stat st;
     if (fstat(win.fd, &st) != 0) return fail(c, TV_ERR_IO, "fstat %s: %s", path, strerror(errno));
     if ((uint64_t)st.st_size < file_offset + len)
@@ -1356,7 +1502,7 @@ int stage_file_locked(tv_ctx* c, const char* path, uint64_t file_offset, uint64_
                 rc = slot.take();
                 if (rc) return rc;
                 uint8_t* at = slot.ptr() + ((p + q) & 3);  // at the resident bytes' alignment mod 4
-                const int e = pread_parallel(win.fd, at, fo + q, kq, c->file_threads);
+                const int e = pread_parallel(win.fd, at, fo + q, kq, c->file_threads, numa_cpus(c));
                 if (e) return fail(c, TV_ERR_IO, "read %s at %llu: %s", path, (unsigned long long)(fo + q), strerror(e));
                 rc = stage_range(c, p + q, p + q + kq, at, p + q, true, lane, /*src_in_ring=*/true);
                 if (rc) return rc;
@@ -1388,11 +1534,9 @@ void read_segments(Pool& pool, const std::vector<SmallSeg>& segs, size_t lo, siz
         const SmallSeg& sg = segs[items[it].first];
         const uint64_t part0 = items[it].second, part1 = std::min(sg.len, part0 + kPart);
         const char* path = paths[sg.k];
-        int e = rw_access(path);  // opened as fsStorage.get opens it: read + write (storage.ts:28-32)
-        const int fd = e ? -1 : open(path, O_RDONLY | O_CLOEXEC);
-        if (fd < 0) {
-            if (!e) e = errno;
-        } else {
+        int e = 0;
+        const int fd = open_rw(path, &e);  // opened as fsStorage.get opens it: read + write (storage.ts:28-32)
+        if (fd >= 0) {
             uint64_t o = part0;
             while (o < part1) {
                 const ssize_t got = pread(fd, slot + sg.packed + o, part1 - o, (off_t)(sg.file_offset + o));
@@ -1556,6 +1700,7 @@ int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64
     } joiner{helper};  // every exit joins the helper before the ctx lock is released
     if (!lane_segs[1].empty()) {
         helper = std::thread([&]() {
+            pin_thread(numa_cpus(c));  // next to its ring and the GPU (TV_OPT_NUMA_BIND)
             if (hipSetDevice(c->device) != hipSuccess) {
                 helper_rc = fail(c, TV_ERR_HIP, "tv_stage_files: hipSetDevice(%d) failed", c->device);
                 return;
@@ -2001,6 +2146,12 @@ int tv_get_counter(tv_ctx* c, int key, uint64_t* value) {
                      2 * c->chunk_bytes + c->list_cap * 5;
             return TV_OK;
         case TV_COUNTER_LAST_WORKGROUPS: *value = c->last_workgroups; return TV_OK;
+        case TV_COUNTER_NUMA_NODE: *value = c->numa_node < 0 ? UINT64_MAX : (uint64_t)c->numa_node; return TV_OK;
+        case TV_COUNTER_RING_NODE: {
+            const int node = page_node(c->ring[0]);
+            *value = node < 0 ? UINT64_MAX : (uint64_t)node;
+            return TV_OK;
+        }
     }
     return fail(c, TV_ERR_ARG, "unknown counter %d", key);
 }
