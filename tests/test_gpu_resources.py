@@ -291,3 +291,42 @@ def test_numa_binding_places_the_ring_and_keeps_results(native, tmp_path):
                 assert ctx.counter(native.TV_COUNTER_RING_NODE) == sys_node
             results.append(bytes(ctx.verify()))
     assert results[0] == results[1] and _bits(results[0], P) == [1] * P
+
+
+def test_contexts_release_threads_and_memory(native, tmp_path):
+    """tv_destroy releases everything a ctx took: 30 create / stage-from-files / verify / destroy cycles (each
+    ctx spins up two pinned rings, its reader pool and the staging helper lane) leave the process's thread
+    count, the device's free memory and the resident set where they started."""
+    import ctypes
+    L, P = 65536, 64
+    payload = bytes((k * 7 + 1) & 0xFF for k in range(L * P))
+    digests = b"".join(hashlib.sha1(payload[i * L:(i + 1) * L]).digest() for i in range(P))
+    files = []
+    for k in range(4):
+        f = tmp_path / f"f{k}"
+        f.write_bytes(payload[k * 16 * L:(k + 1) * 16 * L])
+        files.append(str(f))
+    hip = ctypes.CDLL("libamdhip64.so")
+    free, total = ctypes.c_size_t(), ctypes.c_size_t()
+
+    def state():
+        assert hip.hipMemGetInfo(ctypes.byref(free), ctypes.byref(total)) == 0
+        rss = next(int(line.split()[1]) for line in open("/proc/self/status") if line.startswith("VmRSS:")) << 10
+        return len(os.listdir("/proc/self/task")), free.value, rss
+
+    def cycle():
+        with native.Context(0) as ctx:
+            ctx.set_option(native.TV_OPT_FILE_DIRECT_MIN, 8 * L)       # two lanes: helper thread + readers
+            ctx.set_layout(L * P, L, P)
+            ctx.set_digests(digests)
+            assert ctx.stage_files(files, [0] * 4, [k * 16 * L for k in range(4)], [16 * L] * 4) == [0] * 4
+            assert _bits(ctx.verify(), P) == [1] * P
+
+    cycle()                                                          # runtime-level first-use allocations
+    threads0, free0, rss0 = state()
+    for _ in range(30):
+        cycle()
+    threads1, free1, rss1 = state()
+    assert threads1 <= threads0, (threads0, threads1)
+    assert free1 >= free0 - (64 << 20), (free0, free1)               # no device memory left behind
+    assert rss1 <= rss0 + (256 << 20), (rss0, rss1)                  # nor pinned rings (384 MiB a ctx)
