@@ -259,3 +259,32 @@ def test_random_layouts_incremental_hash_and_piece(native, seed):
         assert not any(got[i] for i in range(P) if i not in truth)
     finally:
         v.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", SEEDS[:12])
+def test_random_layouts_wrong_length_reads(native, seed):
+    """A storage whose get returns one byte too many for a piece (the reference's Storage.get never does:
+    exactly the length asked, or null) makes that piece unreadable in verify_pieces and verify_stream, and
+    no other piece moves: the batch buffer keeps every later piece at its place."""
+    from torrent_amd import MemoryStorage, Storage, verify_pieces, verify_stream
+    info, payload, sizes, missing, short, single = _draw(seed)
+    P = info.n_pieces
+    mem = MemoryStorage()
+    st = Storage(mem, info, "/dl")
+    mem.files = {tuple(st.dir_path) + k: bytearray(v) for k, v in _disk(info, payload, sizes, missing, short,
+                                                                         single).items()}
+    want = _expected(info, st)
+    rng = random.Random(seed)
+    wrong = rng.randrange(P)
+    L = info.piece_length
+
+    class Longer:
+        def get(self, offset, length):
+            data = st.get(offset, length)
+            return None if data is None else (bytes(data) + b"\x5a" if offset // L == wrong else data)
+
+    want[wrong] = 0
+    for devices in ([0], [0, 0, 0]):
+        assert _bits(verify_pieces(info, Longer(), devices=devices), P) == want, (seed, devices)
+        assert _bits(verify_stream(info, Longer().get, devices=devices), P) == want, (seed, devices)

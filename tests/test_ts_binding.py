@@ -374,6 +374,7 @@ def test_verify_files_plan_equals_the_python_host(tmp_path):
 import {{ createRequire }} from "module";
 const require = createRequire("{HARNESS}/");
 const Deno = require("./fake_deno.js");
+Deno.fakeAvailOnly = true;
 const fs = require("fs");
 import("{mod}").then(async (m) => {{
   const spec = JSON.parse(fs.readFileSync("{tmp_path}/spec.json", "utf8"));
@@ -471,6 +472,80 @@ import("{mod}").then(async (m) => {{
       await m.releaseContexts();
       Deno.fakeReset();
       const bf = await m.verifyStream(info, storage, {{ devices: Array(n).fill(0), chunk: d.chunk }});
+      let bits = "";
+      for (let i = 0; i < pieces.length; i++) bits += (bf[i >> 3] >> (7 - (i % 8))) & 1;
+      per.push(bits);
+    }}
+    res.push(per);
+  }}
+  console.log(JSON.stringify(res));
+}}).catch((e) => {{ console.error(e); process.exit(1); }});
+""")
+    got = json.loads(out)
+    for seed, g, w in zip(SEEDS, got, want):
+        assert g == [w, w], (seed, g, w)
+
+
+def test_verify_pieces_host_logic_on_cpu(tmp_path):
+    """verifyPieces' host side (batches of storage.get, the availability bits, the staged ranges, shard
+    concatenation) on CPU against the JS model of the library for the 48 seeded fuzz layouts on 1 and 3
+    shards, with batches of 3 pieces, unreadable pieces and reads one byte too long (unreadable, never
+    shifting a later piece): the bits equal hashlib over Storage.get's bytes."""
+    from tests.test_gpu_fuzz import SEEDS, _draw
+    from torrent_amd.piece import piece_length
+    import random as _random
+    mod = erased_module(tmp_path)
+    spec, want = [], []
+    for seed in SEEDS:
+        info, payload = _draw(seed)[:2]
+        P, L, total = info.n_pieces, info.piece_length, info.length
+        rng = _random.Random(seed + 7)
+        unreadable = sorted(rng.sample(range(P), min(2, P)))
+        wrong = sorted(rng.sample(range(P), 1))
+        spec.append({"info": _info_json(L, total, info.pieces_raw), "payload": _b64(payload[:total]),
+                     "unreadable": unreadable, "wrong": wrong})
+        bits = ""
+        for i in range(P):
+            n = piece_length(i, info)
+            d = info.pieces_raw[20 * i:20 * i + 20]
+            ok = (i not in unreadable and i not in wrong and i * L + n <= total and len(d) == 20 and
+                  hashlib.sha1(payload[i * L:i * L + n]).digest() == d)
+            bits += "1" if ok else "0"
+        want.append(bits)
+    (tmp_path / "spec.json").write_text(json.dumps(spec))
+    out = run_node(tmp_path, f"""
+import {{ createRequire }} from "module";
+const require = createRequire("{HARNESS}/");
+const Deno = require("./fake_deno.js");
+const fs = require("fs");
+import("{mod}").then(async (m) => {{
+  const spec = JSON.parse(fs.readFileSync("{tmp_path}/spec.json", "utf8"));
+  const res = [];
+  for (const d of spec) {{
+    const raw = Buffer.from(d.info.pieces, "base64");
+    const pieces = [];
+    for (let i = 0; i < raw.length; i += 20) pieces.push(new Uint8Array(raw.subarray(i, Math.min(raw.length, i + 20))));
+    const info = {{ pieceLength: d.info.pieceLength, length: d.info.length, pieces, name: "t", private: 0 }};
+    const payload = new Uint8Array(Buffer.from(d.payload, "base64"));
+    const L = info.pieceLength, bad = new Set(d.unreadable), wrong = new Set(d.wrong);
+    const storage = {{
+      async get(offset, length) {{
+        await new Promise((r) => setImmediate(r));
+        const i = Math.floor(offset / L);
+        if (bad.has(i) || offset + length > payload.length) return null;
+        const b = payload.slice(offset, offset + length);
+        if (!wrong.has(i)) return b;
+        const longer = new Uint8Array(length + 1);
+        longer.set(b);
+        longer[length] = 0x5a;
+        return longer;
+      }},
+    }};
+    const per = [];
+    for (const n of [1, 3]) {{
+      await m.releaseContexts();
+      Deno.fakeReset();
+      const bf = await m.verifyPieces(info, storage, {{ devices: Array(n).fill(0), batchBytes: 3 * L }});
       let bits = "";
       for (let i = 0; i < pieces.length; i++) bits += (bf[i >> 3] >> (7 - (i % 8))) & 1;
       per.push(bits);

@@ -50,10 +50,20 @@ const impl = {
     contexts.get(ctx).digests = Buffer.from(bytesOf(p).slice(0, Number(n)));
     return 0;
   },
+  // tv_stage: linear bytes [off, off + n) into the staged pieces (a piece's buffer is its pieceLength)
   tv_stage(ctx, off, p, n) {
     const c = contexts.get(ctx);
-    const i = Number(off) / c.L;
-    c.staged.set(i, Buffer.from(bytesOf(p).slice(0, Number(n))));
+    const src = bytesOf(p);
+    for (let pos = Number(off), q = 0; q < Number(n);) {
+      const i = Math.floor(pos / c.L), within = pos % c.L;
+      const plen = i === c.P - 1 && c.total % c.L ? c.total % c.L : c.L;
+      if (within >= plen) break;
+      const k = Math.min(plen - within, Number(n) - q);
+      if (!c.staged.has(i)) c.staged.set(i, Buffer.alloc(plen));
+      c.staged.get(i).set(src.subarray(q, q + k), within);
+      pos += k;
+      q += k;
+    }
     return 0;
   },
   tv_verify_list(ctx, idxp, n, okp) {
@@ -152,13 +162,22 @@ const impl = {
     new Int32Array(bytesOf(statusp).buffer, bytesOf(statusp).byteOffset, k).fill(0);
     return 0;
   },
-  // tv_verify hands back the host's availability bits (shard-relative), so the host's own clearing shows
+  // tv_verify: the host's availability bits (shard-relative) and, unless Deno.fakeAvailOnly (the files plan
+  // check), the SHA-1 of every staged piece against its digest
   tv_verify(ctx, availp, outp) {
     const c = contexts.get(ctx);
     const out = bytesOf(outp);
     const n = Math.ceil(c.count / 8);
     if (availp === null) out.fill(0xff, 0, n);
     else out.set(bytesOf(availp).subarray(0, n));
+    if (Deno.fakeAvailOnly) return 0;
+    for (let j = 0; j < c.count; j++) {
+      const i = c.first + j;
+      const d = c.digests.slice(20 * i, 20 * i + 20);
+      const data = c.staged.get(i);
+      const ok = data && d.length === 20 && crypto.createHash("sha1").update(data).digest().equals(d);
+      if (!ok) out[j >> 3] &= ~(0x80 >> (j % 8));
+    }
     return 0;
   },
   tv_destroy(ctx) {

@@ -156,7 +156,10 @@ def verify_pieces(info: InfoDict, storage, devices=None, threads: int = 16) -> b
         per_batch = max(1, _STAGE_BATCH_BYTES // max(1, L))
 
         def get(i: int):
-            return storage.get(i * L, piece_length(i, info))  # storage.ts:50-65; None => bit 0
+            data = storage.get(i * L, piece_length(i, info))  # storage.ts:50-65; None => bit 0
+            # (Storage.get returns exactly the length asked or null; any other length is unreadable too,
+            # as in verify_stream -- it must not shift the batch buffer's later pieces)
+            return data if data is not None and len(data) == piece_length(i, info) else None
 
         with ThreadPoolExecutor(max(1, threads)) as pool:
             j = 0

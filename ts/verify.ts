@@ -187,7 +187,9 @@ export async function verifyPieces(
           Array.from({ length: k }, (_, q) => storage.get((first + j + q) * L, pieceLength(first + j + q, info))),
         );
         got.forEach((bytes, q) => {
-          if (!bytes) return;
+          // Storage.get returns exactly the length asked or null; any other length is unreadable too (as in
+          // verifyStream): a longer one would run into the next piece's place in the batch buffer
+          if (!bytes || bytes.length !== pieceLength(first + j + q, info)) return;
           buf.set(bytes, q * L);
           hi = q * L + bytes.length;
           avail[(j + q) >> 3] |= 128 >> ((j + q) % 8);
