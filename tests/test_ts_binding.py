@@ -558,3 +558,60 @@ import("{mod}").then(async (m) => {{
     got = json.loads(out)
     for seed, g, w in zip(SEEDS, got, want):
         assert g == [w, w], (seed, g, w)
+
+
+def test_reads_in_flight_are_bounded_and_resends_during_a_stage_are_ignored(tmp_path):
+    """verifyPieces with its default 256 MiB batch over 600 pieces of 16 KiB, and verifyStream over the same
+    torrent, keep at most 32 storage.get calls pending (each fsStorage.get is a Deno.open: a whole batch at once
+    would hit EMFILE, and fsStorage.get turns that into null, a valid piece reported 0), and still return every
+    piece's bit.  PieceVerifier: a re-sent block of a piece that arrives while the piece's completing stage is
+    still pending (nonblocking tv_stage) neither writes into the bytes being copied nor queues the piece twice.
+    CPU, against the JS model of the library (tests/ts_harness/fake_deno.js)."""
+    mod = erased_module(tmp_path)
+    out = run_node(tmp_path, f"""
+import {{ createRequire }} from "module";
+const require = createRequire("{HARNESS}/");
+const Deno = require("./fake_deno.js");
+const crypto = require("crypto");
+import("{mod}").then(async (m) => {{
+  const L = 16384, P = 600, total = L * (P - 1) + 77;
+  const payload = crypto.randomBytes(total);
+  const pieces = [];
+  for (let i = 0; i < P; i++) pieces.push(crypto.createHash("sha1").update(payload.slice(i * L, (i + 1) * L)).digest());
+  const info = {{ pieceLength: L, length: total, pieces, name: "t", private: 0 }};
+  let inFlight = 0, maxInFlight = 0, calls = 0;
+  const storage = {{
+    async get(offset, length) {{
+      inFlight++; calls++;
+      maxInFlight = Math.max(maxInFlight, inFlight);
+      await new Promise((r) => setTimeout(r, 1));
+      inFlight--;
+      return offset + length > payload.length ? null : payload.slice(offset, offset + length);
+    }},
+  }};
+  const ones = (bf) => Array.from({{ length: P }}, (_, i) => (bf[i >> 3] >> (7 - (i % 8))) & 1).join("");
+  const res = {{}};
+  Deno.fakeReset();
+  res.pieces = {{ bits: ones(await m.verifyPieces(info, storage)), max: maxInFlight, calls }};
+  maxInFlight = 0; calls = 0;
+  await m.releaseContexts();
+  Deno.fakeReset();
+  res.stream = {{ bits: ones(await m.verifyStream(info, storage, {{ chunk: 4096 }})), max: maxInFlight, calls }};
+  // PieceVerifier: the completing block of piece 5 and a corrupted re-send of its first block, concurrently
+  const L2 = 32768, info2 = {{ pieceLength: L2, length: 8 * L2, name: "t2", private: 0, pieces: [] }};
+  for (let i = 0; i < 8; i++) info2.pieces.push(crypto.createHash("sha1").update(payload.slice(i * L2, (i + 1) * L2)).digest());
+  const pv = new m.PieceVerifier(info2, {{ flushPieces: null, flushAgeMs: null }});
+  await pv.onBlock(5, 0, payload.slice(5 * L2, 5 * L2 + 16384));
+  const done = pv.onBlock(5, 16384, payload.slice(5 * L2 + 16384, 6 * L2));
+  const resend = pv.onBlock(5, 0, Buffer.alloc(16384));
+  res.verifier = {{ done: await done, resend: await resend, flush: await pv.flush() }};
+  pv.close();
+  console.log(JSON.stringify(res));
+}}).catch((e) => {{ console.error(e); process.exit(1); }});
+""")
+    res = json.loads(out)
+    assert res["pieces"]["bits"] == "1" * 600 and res["pieces"]["calls"] == 600
+    assert 1 < res["pieces"]["max"] <= 32, res["pieces"]
+    assert res["stream"]["bits"] == "1" * 600
+    assert 1 < res["stream"]["max"] <= 32, res["stream"]
+    assert res["verifier"] == {"done": True, "resend": False, "flush": [[5, True]]}

@@ -7,8 +7,9 @@
 // crypto.subtle.digest("SHA-1", content) (tools/make_torrent.ts:28-31) runs on the GPU here.
 //
 // Requires: deno run --unstable --allow-ffi (Deno 1.x, as the reference CI: .github/workflows/main.yml:14).
-// NOTE: Deno is not installed in the build container, so this file is exercised only through the
-// identical C ABI from Python (torrent_amd/_native.py, tests/test_gpu_parity.py).
+// Deno is not installed in the build container: tests/test_ts_binding.py runs this file under Node 12 with an
+// N-API shim of Deno's FFI on the GPU (tests/ts_harness/deno_shim.js) and against a JS model of the library
+// on CPU (tests/ts_harness/fake_deno.js).
 
 import type { InfoDict } from "../metainfo.ts";
 import type { Storage } from "../storage.ts";
@@ -153,6 +154,18 @@ function piecesRaw(info: InfoDict): Uint8Array {
   return out;
 }
 
+/** storage.get calls a bulk verify keeps outstanding (file descriptors, not bandwidth, bound it) */
+const READS_IN_FLIGHT = 32;
+
+/** fn(0..n-1), at most READS_IN_FLIGHT of them pending at a time. */
+async function eachLimited(n: number, fn: (q: number) => Promise<void>): Promise<void> {
+  let next = 0;
+  const worker = async () => {
+    for (let q = next++; q < n; q = next++) await fn(q);
+  };
+  await Promise.all(Array.from({ length: Math.min(READS_IN_FLIGHT, n) }, worker));
+}
+
 /**
  * verifyPieces(info, storage) -> have-bitfield (Uint8Array of ceil(P/8) bytes, MSB-first:
  * torrent.ts:53,60,147-149).  Piece i's bit is set iff storage.get(i*pieceLength, len_i) is
@@ -182,16 +195,17 @@ export async function verifyPieces(
         const k = Math.min(batch, count - j);
         const buf = new Uint8Array(k * L);
         let hi = 0;
-        // all reads outstanding at once, like make_torrent.ts:96,111 keeps its digests in flight
-        const got = await Promise.all(
-          Array.from({ length: k }, (_, q) => storage.get((first + j + q) * L, pieceLength(first + j + q, info))),
-        );
-        got.forEach((bytes, q) => {
+        // READS_IN_FLIGHT reads outstanding at a time (make_torrent.ts:96,111 keeps its work in flight too, but
+        // each fsStorage.get is a Deno.open: a batch of 16 KiB pieces at once would hit EMFILE, which
+        // fsStorage.get turns into null -- a valid piece reported 0)
+        await eachLimited(k, async (q) => {
+          const n = pieceLength(first + j + q, info);
+          const bytes = await storage.get((first + j + q) * L, n);
           // Storage.get returns exactly the length asked or null; any other length is unreadable too (as in
           // verifyStream): a longer one would run into the next piece's place in the batch buffer
-          if (!bytes || bytes.length !== pieceLength(first + j + q, info)) return;
+          if (!bytes || bytes.length !== n) return;
           buf.set(bytes, q * L);
-          hi = q * L + bytes.length;
+          hi = Math.max(hi, q * L + n);
           avail[(j + q) >> 3] |= 128 >> ((j + q) % 8);
         });
         if (hi) check(l, ctx, await l.symbols.tv_stage(ctx, BigInt((first + j) * L), ptr(buf), BigInt(hi)));
@@ -204,8 +218,6 @@ export async function verifyPieces(
   return bitfield;
 }
 
-/** storage.get calls a streamed verify keeps outstanding (file descriptors, not bandwidth, bound it) */
-const READS_IN_FLIGHT = 32;
 const TV_OPT_STREAM_CHUNK = 3;
 const TV_OPT_RESIDENT = 10;
 
@@ -249,18 +261,14 @@ export async function verifyStream(info: InfoDict, storage: Storage, opts: Verif
           const slot = new Uint8Array(Deno.UnsafePointerView.getArrayBuffer(Deno.UnsafePointer.create(req[4])!, rows * width));
           // READS_IN_FLIGHT reads of the request outstanding at a time: each fsStorage.get is a Deno.open, and
           // an EMFILE from a thousand opens at once would come back as null -- a valid piece reported 0
-          let next = 0;
-          const worker = async () => {
-            for (let q = next++; q < rows; q = next++) {
-              const n = Math.max(0, Math.min(width, pieceLength(piece + q, info) - offset));
-              if (n === 0) continue;
-              const bytes = await storage.get((piece + q) * L + offset, n);
-              // a row must be exactly n bytes: more would spill into the next row (Python: unreadable too)
-              if (bytes && bytes.length === n) slot.set(bytes, q * width);
-              else check(l, ctx, l.symbols.tv_stream_unreadable(ctx, BigInt(piece + q)));
-            }
-          };
-          await Promise.all(Array.from({ length: Math.min(READS_IN_FLIGHT, rows) }, worker));
+          await eachLimited(rows, async (q) => {
+            const n = Math.max(0, Math.min(width, pieceLength(piece + q, info) - offset));
+            if (n === 0) return;
+            const bytes = await storage.get((piece + q) * L + offset, n);
+            // a row must be exactly n bytes: more would spill into the next row (Python: unreadable too)
+            if (bytes && bytes.length === n) slot.set(bytes, q * width);
+            else check(l, ctx, l.symbols.tv_stream_unreadable(ctx, BigInt(piece + q)));
+          });
           check(l, ctx, await l.symbols.tv_stream_commit(ctx, reqp));
         }
         const out = new Uint8Array(Math.ceil(count / 8));
@@ -428,6 +436,7 @@ export class PieceVerifier {
   #bufs = new Map<number, { bytes: Uint8Array; blocks: Set<number> }>();
   #pending: number[] = [];
   #pendingSet = new Set<number>();
+  #staging = new Set<number>();
   #oldest = 0;
   #timer: number | undefined;
   #results: [number, boolean][] = [];
@@ -461,6 +470,7 @@ export class PieceVerifier {
     await this._autoFlush();                                  // the age bound, checked on every block
     if (this.bitfield[index >> 3] & (128 >> (index % 8))) return false;
     if (this.#pendingSet.has(index)) return false; // complete, waiting for a flush: ignore re-sends
+    if (this.#staging.has(index)) return false;    // its completing block is being staged right now
     const len = pieceLength(index, this.info);
     if (offset >= len) return false;
     if (offset + block.length > len) block = block.subarray(0, len - offset); // never into the next piece
@@ -469,7 +479,13 @@ export class PieceVerifier {
     e.bytes.set(block, offset);
     e.blocks.add(Math.floor(offset / 16384));
     if (e.blocks.size < Math.ceil(len / 16384)) return false;
-    check(this.#l, this.#ctx, await this.#l.symbols.tv_stage(this.#ctx, BigInt(index * this.info.pieceLength), ptr(e.bytes), BigInt(len)));
+    // a re-sent block of this piece arriving while the stage is pending must not stage (and queue) it twice
+    this.#staging.add(index);
+    try {
+      check(this.#l, this.#ctx, await this.#l.symbols.tv_stage(this.#ctx, BigInt(index * this.info.pieceLength), ptr(e.bytes), BigInt(len)));
+    } finally {
+      this.#staging.delete(index);
+    }
     this.#bufs.delete(index);
     if (this.#pending.length === 0) {
       this.#oldest = performance.now();
