@@ -369,7 +369,10 @@ export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptio
 
 /** verifyPiece(info, index, bytes): one piece (e.g. on completion of its last 16 KiB block). */
 export async function verifyPiece(info: InfoDict, index: number, bytes: Uint8Array, opts: VerifyOptions = {}): Promise<boolean> {
-  if (index >= info.pieces.length) throw new Error(`verifyPiece: invalid piece index ${index}`);
+  // piece.ts:22 rejects index >= pieces.length; a negative or fractional index is no piece either (as verify.py)
+  if (!Number.isInteger(index) || index < 0 || index >= info.pieces.length) {
+    throw new Error(`verifyPiece: invalid piece index ${index}`);
+  }
   if (bytes.length !== pieceLength(index, info) || info.pieces[index].length !== 20) return false;
   const l = load(opts.libPath);
   // its own cached context (slot -1): a one-piece layout on a bulk call's context would free that context's
