@@ -173,3 +173,27 @@ def test_c_consumer_error_paths(native, tmp_path):
     exe = build_c_consumer(tmp_path)
     r = subprocess.run([exe, "cpu"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_buffer_addresses_are_never_copies():
+    """_native._addr hands the library the caller's own bytes: a read-only source (a slice of a `bytes`
+    payload, as verify_payload stages it) is not duplicated -- a 16 GiB `bytes` payload would otherwise be
+    copied whole per shard -- and a read-only output is refused instead of written into a temporary."""
+    import ctypes
+    import pytest
+    from torrent_amd import _native
+    b = bytes(range(256)) * 16
+    base = ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p).value
+    a, keep = _native._addr(b)
+    assert a == base
+    a, keep = _native._addr(memoryview(b)[100:900])
+    assert a == base + 100 and ctypes.string_at(a, 800) == b[100:900]
+    ba = bytearray(b)
+    a, keep = _native._addr(memoryview(ba)[7:], writable=True)
+    ctypes.memset(a, 0xAB, 1)
+    assert ba[7] == 0xAB
+    with pytest.raises(TypeError):
+        _native._addr(memoryview(b)[1:], writable=True)
+    with pytest.raises(TypeError):
+        _native._addr(b, writable=True)
+    assert _native._addr(None) == (None, None) and _native._addr(bytearray())[0] is None

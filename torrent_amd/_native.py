@@ -125,18 +125,24 @@ def lib() -> ctypes.CDLL:
     return _lib
 
 
-def _addr(buf) -> tuple:
-    """(void* address, keepalive) of a bytes-like object or None."""
+def _addr(buf, writable: bool = False) -> tuple:
+    """(void* address, keepalive) of a bytes-like object or None, never a copy: the library reads sources
+    in place (a read-only buffer such as a slice of a 16 GiB `bytes` payload is not duplicated), and writes
+    outputs in place, so a read-only buffer given as an output (`writable`) is a TypeError rather than a
+    silent write into a temporary."""
     if buf is None:
         return None, None
-    if isinstance(buf, bytes):
+    if isinstance(buf, bytes) and not writable:
         return ctypes.cast(ctypes.c_char_p(buf), _p).value, buf
     mv = memoryview(buf).cast("B")
     if mv.nbytes == 0:
         return None, None
     if mv.readonly:
-        b = bytes(mv)
-        return ctypes.cast(ctypes.c_char_p(b), _p).value, b
+        if writable:
+            raise TypeError("the output buffer is read-only")
+        import numpy as np
+        a = np.frombuffer(mv, dtype=np.uint8)   # a view: the exporter's own bytes
+        return a.ctypes.data, a
     c = (ctypes.c_char * mv.nbytes).from_buffer(mv)
     return ctypes.addressof(c), c
 
@@ -302,7 +308,7 @@ class Context:
 
     def read(self, linear_offset: int, out) -> None:
         """Copy resident bytes at linear_offset into the writable buffer `out` (tv_read)."""
-        a, keep = _addr(out)
+        a, keep = _addr(out, writable=True)
         n = memoryview(out).nbytes
         self._check(self._L.tv_read(self._h, linear_offset, a, n))
         del keep
