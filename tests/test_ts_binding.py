@@ -209,6 +209,11 @@ def test_ts_binding_on_the_gpu(native, tmp_path, monkeypatch):
         expect[f"piece{i}"] = want
     cases.append({"name": "hash", "kind": "hash", "payload": _b64(blob), "pieceLength": L})
     expect["hash"] = digests.hex()
+    # hashPieces sharded over three contexts (21 pieces: shards of 8, 8 and 5, the last one short)
+    L2 = 16384
+    blob2 = bytes(rng.getrandbits(8) for _ in range(20 * L2 + 999))
+    cases.append({"name": "hash3", "kind": "hash", "payload": _b64(blob2), "pieceLength": L2, "devices": [0, 0, 0]})
+    expect["hash3"] = b"".join(hashlib.sha1(blob2[i * L2:(i + 1) * L2]).digest() for i in range(21)).hex()
 
     # PieceVerifier: blocks in random order, one corrupted, automatic flushes at 8 pending pieces
     L, P = 2 * BLOCK_SIZE, 37
@@ -615,3 +620,33 @@ import("{mod}").then(async (m) => {{
     assert res["stream"]["bits"] == "1" * 600
     assert 1 < res["stream"]["max"] <= 32, res["stream"]
     assert res["verifier"] == {"done": True, "resend": False, "flush": [[5, True]]}
+
+
+def test_hash_pieces_shards_like_the_python_host(tmp_path):
+    """hashPieces shards the pieces over opts.devices as verifyPieces does (and torrent_amd.hash_pieces): each
+    shard stages only its own bytes and its digests land at 20 * first -- on 1, 2 and 3 shards, with a short
+    last piece and shard boundaries inside the payload, the `pieces` string equals hashlib's.  CPU, against
+    the JS model of the library."""
+    mod = erased_module(tmp_path)
+    L, P = 4096, 37
+    payload = random.Random(11).randbytes(L * (P - 1) + 1234)
+    want = b"".join(hashlib.sha1(payload[i * L:(i + 1) * L]).digest() for i in range(P))
+    (tmp_path / "payload.bin").write_bytes(payload)
+    out = run_node(tmp_path, f"""
+import {{ createRequire }} from "module";
+const require = createRequire("{HARNESS}/");
+const Deno = require("./fake_deno.js");
+const fs = require("fs");
+import("{mod}").then(async (m) => {{
+  const payload = new Uint8Array(fs.readFileSync("{tmp_path}/payload.bin"));
+  const res = {{}};
+  for (const n of [1, 2, 3]) {{
+    await m.releaseContexts();
+    Deno.fakeReset();
+    res[n] = Buffer.from(await m.hashPieces(payload, {L}, {{ devices: Array(n).fill(0) }})).toString("hex");
+  }}
+  console.log(JSON.stringify(res));
+}}).catch((e) => {{ console.error(e); process.exit(1); }});
+""")
+    res = json.loads(out)
+    assert res == {"1": want.hex(), "2": want.hex(), "3": want.hex()}

@@ -1,7 +1,7 @@
 // fake_deno.js -- a CPU model of the library behind the Deno FFI, for the TS host logic on CPU (test
 // infrastructure only; tests/test_ts_binding.py).  Deno.dlopen returns JavaScript implementations of the
 // calls PieceVerifier makes (tv_create / tv_set_layout / tv_set_digests / tv_stage / tv_verify_list /
-// tv_destroy / tv_last_error / tv_abi_version), with SHA-1 from node's crypto as the checker, and the
+// tv_destroy / tv_last_error / tv_abi_version) and hashPieces makes (tv_hash), with SHA-1 from node's crypto as the checker, and the
 // calls verifyFiles makes (tv_set_option, tv_stage_files recording the host's segment plan, tv_verify
 // returning the host's availability bits) and verifyStream makes (the tv_stream_* protocol, modelled with
 // several requests per column); every other symbol throws if called.  Pointers are BigInt
@@ -177,6 +177,17 @@ const impl = {
       const data = c.staged.get(i);
       const ok = data && d.length === 20 && crypto.createHash("sha1").update(data).digest().equals(d);
       if (!ok) out[j >> 3] &= ~(0x80 >> (j % 8));
+    }
+    return 0;
+  },
+  // tv_hash: the SHA-1 of every staged shard piece (an unstaged piece hashes as its zero bytes)
+  tv_hash(ctx, outp) {
+    const c = contexts.get(ctx);
+    const out = bytesOf(outp);
+    for (let j = 0; j < c.count; j++) {
+      const i = c.first + j;
+      const plen = i === c.P - 1 && c.total % c.L ? c.total % c.L : c.L;
+      out.set(crypto.createHash("sha1").update(c.staged.get(i) || Buffer.alloc(plen)).digest(), 20 * j);
     }
     return 0;
   },

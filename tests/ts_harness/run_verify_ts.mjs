@@ -63,7 +63,7 @@ async function main() {
       } else if (c.kind === "piece") {
         r.ok = await v.verifyPiece(makeInfo(c.info), c.index, b64(c.bytes), opts);
       } else if (c.kind === "hash") {
-        r.pieces = hex(await v.hashPieces(b64(c.payload), c.pieceLength, opts));
+        r.pieces = hex(await v.hashPieces(b64(c.payload), c.pieceLength, { ...opts, devices: c.devices }));
       } else if (c.kind === "verifier") {
         const got = [];
         const pv = new v.PieceVerifier(makeInfo(c.info), {

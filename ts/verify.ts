@@ -391,20 +391,27 @@ export async function verifyPiece(info: InfoDict, index: number, bytes: Uint8Arr
 /**
  * hashPieces(payload, pieceLength) -> the `pieces` string (20 B per piece) of a linear payload:
  * creation mode (SURVEY 8f row f3), the GPU form of make_torrent.ts:147-173 (single file) and
- * :62-113 (files concatenated in order).
+ * :62-113 (files concatenated in order).  Pieces are sharded over `opts.devices` as verifyPieces shards
+ * them; each shard's digests land at 20 * first.  Same behaviour as torrent_amd.hash_pieces.
  */
 export async function hashPieces(payload: Uint8Array, pieceLength: number, opts: VerifyOptions = {}): Promise<Uint8Array> {
   const P = Math.ceil(payload.length / pieceLength);
   if (P === 0) return new Uint8Array(0);
   const l = load(opts.libPath);
-  return await withContext(l, (opts.devices || [0])[0], 0, async (ctx) => {
-    check(l, ctx, l.symbols.tv_set_layout(ctx, BigInt(payload.length), BigInt(pieceLength), BigInt(P), 0n, BigInt(P)));
-    check(l, ctx, l.symbols.tv_set_digests(ctx, null, 0n));
-    check(l, ctx, await l.symbols.tv_stage(ctx, 0n, ptr(payload), BigInt(payload.length)));
-    const out = new Uint8Array(20 * P);
-    check(l, ctx, await l.symbols.tv_hash(ctx, ptr(out)));
-    return out;
-  });
+  const devices = opts.devices || [0];
+  const out = new Uint8Array(20 * P);
+  await Promise.all(shardRanges(P, devices.length).map(async ([first, count], s) => {
+    if (count === 0) return;
+    await withContext(l, devices[s], s, async (ctx) => {
+      check(l, ctx, l.symbols.tv_set_layout(ctx, BigInt(payload.length), BigInt(pieceLength), BigInt(P), BigInt(first), BigInt(count)));
+      const lo = first * pieceLength, hi = Math.min(payload.length, (first + count) * pieceLength);
+      if (hi > lo) check(l, ctx, await l.symbols.tv_stage(ctx, BigInt(lo), ptr(payload.subarray(lo, hi)), BigInt(hi - lo)));
+      const digests = new Uint8Array(20 * count);
+      check(l, ctx, await l.symbols.tv_hash(ctx, ptr(digests)));
+      out.set(digests, 20 * first);
+    });
+  }));
+  return out;
 }
 
 /** Options of PieceVerifier's flush policy (same defaults as torrent_amd/incremental.py). */
