@@ -62,6 +62,23 @@ int tv_last_error(const tv_ctx *ctx, char *buf, size_t n);
 
 /*
  * Geometry of the torrent and of this ctx's shard; allocates the resident payload.
+ *
+ * Device budget.  The payload (shard_count padded pieces) is allocated whole when it fits
+ * TV_OPT_RESIDENT_BUDGET (default: the GPU's free memory at this call less a margin).  A larger shard gets a
+ * WINDOWED layout instead, so no shard fails for its size: the allocation holds two buffers (one when the
+ * budget holds only one) of W pieces (TV_COUNTER_WINDOW_PIECES), staging fills window k's buffer, and when
+ * staging reaches window k + 1 the library hashes window k (kernels into the shard's digest rows) while k + 1
+ * stages into the other buffer.  tv_verify / tv_hash end the pass (the open window is hashed, windows never
+ * staged get zero digests: bit 0) and compare / return the whole shard.  Rules of a windowed layout: staging
+ * (tv_stage, tv_stage_file, tv_fill_synthetic) must ascend window by window -- bytes of a window already
+ * hashed this pass are TV_ERR_STATE; tv_stage_files sorts its segments itself; tv_read reads the open window
+ * only; tv_verify_list is TV_ERR_STATE; repeated tv_verify / tv_hash reuse the pass's digests, and staging
+ * after them starts a new pass.  TV_COUNTER_PAYLOAD_BYTES <= the budget (unless one piece exceeds it).
+ * Slot pool.  With TV_OPT_LIST_SLOTS = K the payload holds K piece slots instead of the shard (incremental
+ * verify: only the pieces awaiting verification need device memory).  A piece takes a free slot when its
+ * first byte is staged and keeps it until tv_verify_list lists it; staging a piece when all K slots are
+ * taken is TV_ERR_STATE.  tv_verify / tv_hash / tv_fill_synthetic are TV_ERR_STATE on a slot pool.
+ *
  *   total_length : InfoDict.length (metainfo.ts:21,40 / :125 sum of file lengths)
  *   piece_length : InfoDict.pieceLength (metainfo.ts:14)
  *   n_pieces     : InfoDict.pieces.length, the DIGEST count (metainfo.ts:16,111);
@@ -167,7 +184,9 @@ int tv_verify(tv_ctx *ctx, const uint8_t *avail_bits, uint8_t *bitfield_out);
  * piece-message handler torrent.ts:183-193 is where a completed piece is checked).  pieces[k] are
  * GLOBAL piece indices inside this ctx's shard (any order, duplicates allowed); ok_out[k] = 1 iff
  * SHA-1 of the resident bytes of piece pieces[k] equals info.pieces[pieces[k]], else 0.  Only pieces
- * whose bytes were staged should be listed.
+ * whose bytes were staged should be listed.  On a slot pool (TV_OPT_LIST_SLOTS) a listed piece without a
+ * slot (never staged) is 0, and every listed piece's slot is free again when the call returns.
+ * TV_ERR_STATE on a windowed layout.
  */
 int tv_verify_list(tv_ctx *ctx, const uint64_t *pieces, uint64_t n, uint8_t *ok_out);
 
@@ -277,6 +296,16 @@ int tv_host_unregister(void *ptr);
                                allocated on that node (slots allocated after the option is set); 0 = unpinned,
                                default placement.  An MI355X node has two sockets with four GPUs each: a copy
                                from the far socket crosses the inter-socket link twice (read, then DMA). */
+#define TV_OPT_RESIDENT_BUDGET 16 /* bytes of device memory the resident payload may take (0, default: the GPU's free
+                                     memory at tv_set_layout less 4 GiB and 64 B per piece).  A shard larger than it
+                                     gets a windowed layout (tv_set_layout).  Takes effect at the next tv_set_layout */
+#define TV_OPT_LIST_SLOTS 17      /* K > 0: tv_set_layout allocates a pool of K piece slots instead of the shard (see
+                                     tv_set_layout; incremental verify, tv_verify_list).  0 (default) = off.  Takes
+                                     effect at the next tv_set_layout */
+#define TV_OPT_OPEN_RW 18         /* how tv_stage_file(s) open files: 1 (default) = read + write, as fsStorage.get
+                                     opens every segment (storage.ts:28-32,158; an unwritable file reads as null);
+                                     0 = read-only, as make_torrent.ts:78 opens its sources (creation mode from files
+                                     the process may not write).  Zero-length segments' open check follows it */
 int tv_set_option(tv_ctx *ctx, int key, int64_t value);
 int tv_get_option(tv_ctx *ctx, int key, int64_t *value);
 
@@ -301,6 +330,11 @@ int tv_last_kernel(tv_ctx *ctx, int *kernel, int *launches);
                                         unknown */
 #define TV_COUNTER_RING_NODE 7       /* the NUMA node holding the first pinned ring slot's first page; UINT64_MAX
                                         if the ring is not allocated yet or the node is unknown */
+#define TV_COUNTER_WINDOW_PIECES 8   /* pieces per window of a windowed layout (0: the shard is resident whole) */
+#define TV_COUNTER_WINDOWS 9         /* windows hashed by the current (or last) pass of a windowed layout */
+#define TV_COUNTER_BUDGET 10         /* the device budget the last tv_set_layout applied, bytes (0: no resident payload
+                                        or a slot pool) */
+#define TV_COUNTER_SLOTS_USED 11     /* slots of a slot pool holding a staged piece not yet listed */
 int tv_get_counter(tv_ctx *ctx, int key, uint64_t *value);
 
 /* Block until all work queued by the ctx is complete. */

@@ -197,3 +197,18 @@ def test_buffer_addresses_are_never_copies():
     with pytest.raises(TypeError):
         _native._addr(b, writable=True)
     assert _native._addr(None) == (None, None) and _native._addr(bytearray())[0] is None
+
+
+def test_option_and_counter_constants_match_header():
+    """Every TV_OPT_* / TV_COUNTER_* / TV_ERR_* value of include/torrent_verify.h is the same in the ctypes
+    binding (torrent_amd/_native.py) and in every constant ts/verify.ts declares."""
+    from torrent_amd import _native
+    txt = open(os.path.join(ROOT, "include", "torrent_verify.h")).read()
+    defs = {m.group(1): int(m.group(2)) for m in
+            re.finditer(r"^#define\s+(TV_(?:OPT|COUNTER|ERR)_\w+)\s+\(?(-?\d+)\)?", txt, re.M)}
+    assert len(defs) >= 30
+    for name, v in defs.items():
+        assert getattr(_native, name) == v, name
+    ts = open(os.path.join(ROOT, "ts", "verify.ts")).read()
+    for m in re.finditer(r"const\s+(TV_\w+)\s*=\s*(-?\d+)\s*;", ts):
+        assert defs[m.group(1)] == int(m.group(2)), m.group(1)

@@ -15,11 +15,20 @@ from torrent_amd.piece import BLOCK_SIZE, PieceMsg
 
 
 class _ListCtx:
-    """tv_ctx stand-in: stage() keeps the bytes, verify_list() hashes them (one call = one flush)."""
+    """tv_ctx stand-in: stage() keeps the bytes, verify_list() hashes them (one call = one flush).  It models
+    the library's slot pool (TV_OPT_LIST_SLOTS): a staged piece holds a slot until a flush lists it, and staging
+    with every slot taken is an error (TV_ERR_STATE in the library)."""
 
     def __init__(self, device=0):
         self.bytes = {}
         self.flushes = []
+        self.slots = 0
+        self.max_held = 0
+
+    def set_option(self, key, value):
+        from torrent_amd import _native
+        if key == _native.TV_OPT_LIST_SLOTS:
+            self.slots = value
 
     def set_layout(self, total, L, P, first, count):
         self.L = L
@@ -28,11 +37,19 @@ class _ListCtx:
         self.raw = raw
 
     def stage(self, off, data):
-        self.bytes[off // self.L] = bytes(data)
+        i = off // self.L
+        if self.slots and i not in self.bytes and len(self.bytes) >= self.slots:
+            raise RuntimeError("every slot holds a staged piece not yet listed")
+        self.bytes[i] = bytes(data)
+        self.max_held = max(self.max_held, len(self.bytes))
 
     def verify_list(self, pieces):
         self.flushes.append(list(pieces))
-        return bytes(int(hashlib.sha1(self.bytes[i]).digest() == self.raw[20 * i:20 * i + 20]) for i in pieces)
+        out = bytes(int(i in self.bytes and hashlib.sha1(self.bytes[i]).digest() == self.raw[20 * i:20 * i + 20])
+                    for i in pieces)
+        for i in pieces:
+            self.bytes.pop(i, None)
+        return out
 
     def close(self):
         pass
@@ -122,3 +139,22 @@ def test_corrupt_piece_is_reported_by_an_automatic_flush(fake):
     for m in _blocks(info, payload, 5):                          # re-received correctly
         v.on_block(m)
     assert got == {5: True} and v.bitfield[0] & 0x04
+
+
+def test_slot_pool_bounds_the_pending_pieces(fake):
+    """slots=3 with the caller flushing (no count or age bound): the verifier never holds more than 3 staged
+    pieces; the 4th completed piece first flushes the 3 pending ones (a forced flush), and every piece's result
+    is delivered exactly once, in completion order."""
+    info, payload = _torrent(P=10)
+    seen = []
+    v = incremental.IncrementalVerifier(info, flush_pieces=None, flush_age_ms=None, slots=3,
+                                        on_verified=lambda i, ok: seen.append((i, ok)))
+    for i in range(10):
+        for m in _blocks(info, payload, i):
+            v.on_block(m)
+    seen += v.flush()
+    ctx = fake[-1]
+    assert ctx.max_held == 3 and v.forced_flushes == 3
+    assert [len(f) for f in ctx.flushes] == [3, 3, 3, 1]
+    assert seen == [(i, True) for i in range(10)]
+    assert v.slots == 3

@@ -1,0 +1,230 @@
+"""Windowed layouts: every bulk path on a shard larger than the device budget (TV_OPT_RESIDENT_BUDGET).
+
+The budget is forced down to a few MiB (a few pieces per window) and every result must equal the one the
+reference's semantics give, exactly as without a budget: the reference's test_data fixtures (all 1706 / 1855
+digests), the seeded golden layouts incl. BASELINE config 3 (10,000 files), the 48 seeded fuzz layouts on
+one and three shards, and BASELINE config 2 at full size against the oracle.  The payload the context holds
+(TV_COUNTER_PAYLOAD_BYTES) stays within the budget, and a shard that fits is not windowed.
+"""
+import hashlib
+import json
+import os
+import random
+
+import pytest
+
+from tests.test_gpu_fuzz import SEEDS, _bits, _disk, _draw, _expected
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _stride(L):
+    return -(-L // 64) * 64 + 256
+
+
+def _budget(L, pieces_per_window):
+    """A budget whose windows hold `pieces_per_window` pieces (two buffers of them)."""
+    return 2 * (pieces_per_window * _stride(L) + 256)
+
+
+def _check_windowed(budget, expect_windowed=True):
+    """Every cached bulk context (slot >= 0) last laid out under `budget` holds at most `budget` bytes of
+    payload, and (expect_windowed) at least one of them is windowed."""
+    from torrent_amd import context_counters
+    seen = [c for (dev, slot), c in context_counters().items() if slot >= 0 and c["budget"] == budget]
+    assert seen
+    for c in seen:
+        assert c["payload_bytes"] <= budget, c
+    if expect_windowed:
+        assert any(c["window_pieces"] >= 1 for c in seen), seen
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["singlefile", "multifile"])
+def test_reference_fixtures_windowed(native, name):
+    """The reference's test_data torrents (digests produced by its own SHA-1 path, make_torrent.ts:28-31) with
+    8 MiB budgets: 447 / 972 MB payloads in windows of 15 / 7 pieces, resident staging, Storage reads and
+    creation mode; the three flipped pieces (#0, the file-spanning #852, the short last) and nothing else fail."""
+    from torrent_amd import MemoryStorage, Storage, hash_pieces, parse_metainfo, verify_payload, verify_pieces
+    from tests.test_gpu_paths import _all_ones, _load, _ref_payload
+    info = parse_metainfo(_load(f"{name}.torrent")).info
+    payload = bytearray(_ref_payload(name))
+    P, L = info.n_pieces, info.piece_length
+    budget = 8 << 20
+    assert bytes(verify_payload(info, payload, budget=budget)) == _all_ones(P)
+    _check_windowed(budget)
+    assert hash_pieces(bytes(payload), L, budget=budget) == info.pieces_raw
+    flips = [0, 852, P - 1]
+    for i in flips:
+        payload[i * L + 3] ^= 0x01
+    want = bytearray(_all_ones(P))
+    for i in flips:
+        want[i >> 3] &= ~(0x80 >> (i & 7)) & 0xFF
+    for devices in ([0], [0, 0, 0]):
+        assert bytes(verify_payload(info, payload, devices=devices, budget=budget)) == bytes(want), devices
+    if name == "multifile":
+        n0 = info.files[0].length
+        mem = MemoryStorage({tuple(info.files[0].path): bytes(payload[:n0]),
+                             tuple(info.files[1].path): bytes(payload[n0:])})
+        assert bytes(verify_pieces(info, Storage(mem, info, os.getcwd()), budget=budget)) == bytes(want)
+        _check_windowed(budget)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["single_short_last", "multi_zero_tiny", "many_tiny_span", "missing_and_short",
+                                    "exact_multiple", "cfg1", "cfg3"])
+def test_golden_layouts_windowed(native, layout, tmp_path, monkeypatch):
+    """The committed expected bitfields of the seeded layouts (hashlib-computed), windowed: resident staging
+    (verify_payload), file staging (verify_files over the files on disk, 10,000 of them for cfg3) and
+    creation mode (hash_pieces), with windows of 1-16 pieces, on one and three shards."""
+    from tests.layouts import build_layout, by_name
+    from torrent_amd import hash_pieces, verify_files, verify_payload
+    rec = {r["name"]: r for r in json.load(open(os.path.join(GOLDEN, "layouts.json")))}[layout]
+    lay = build_layout(by_name(layout))
+    info, L = lay["info"], lay["info"].piece_length
+    rng = random.Random(layout)
+    sizes = [1, 3, 16] if info.n_pieces < 1000 else [16, 64]    # (a window kernel costs one piece's SHA-1)
+    for devices in ([0], [0, 0, 0]):
+        budget = _budget(L, rng.choice(sizes))
+        assert bytes(verify_payload(info, lay["payload"], avail=lay["avail"], devices=devices,
+                                    budget=budget)).hex() == rec["expected_bitfield"], (devices, budget)
+        _check_windowed(budget, expect_windowed=devices == [0] and info.n_pieces > 16)
+    monkeypatch.chdir(tmp_path)
+    for path, data in lay["disk_files"]().items():
+        p = tmp_path.joinpath("dl", *path)
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_bytes(data)
+    for devices in ([0], [0, 0, 0]):
+        budget = _budget(L, rng.choice([2, 5, 16] if info.n_pieces < 1000 else [16, 64]))
+        assert bytes(verify_files(info, str(tmp_path / "dl"), devices=devices, threads=4,
+                                  budget=budget)).hex() == rec["expected_bitfield"], (devices, budget)
+        _check_windowed(budget, expect_windowed=devices == [0] and info.n_pieces > 16)
+    clean = hashlib.sha1(lay["pieces_raw"]).hexdigest()
+    assert clean == rec["pieces_sha1"]
+    if not lay["corrupted"]:
+        assert hash_pieces(bytes(lay["payload"]), L, budget=_budget(L, 2)) == lay["pieces_raw"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", SEEDS)
+def test_random_layouts_windowed(native, tmp_path, monkeypatch, seed):
+    """The 48 seeded fuzz layouts (tests/test_gpu_fuzz.py: odd piece lengths, zero-length / tiny / boundary
+    files, missing and short files, ragged digests, extra digests) through verify_pieces, verify_payload and
+    verify_files with windows of 1-5 pieces, on one and three shards: the bits equal Storage.get + hashlib's."""
+    from torrent_amd import MemoryStorage, Storage, verify_files, verify_payload, verify_pieces
+    from torrent_amd.piece import piece_length
+    from torrent_amd.storage import fs_storage
+    import shutil
+    info, payload, sizes, missing, short, single = _draw(seed)
+    P, L = info.n_pieces, info.piece_length
+    monkeypatch.chdir(tmp_path)
+    disk = _disk(info, payload, sizes, missing, short, single)
+    mem = MemoryStorage()
+    st = Storage(mem, info, str(tmp_path / "dl"))
+    mem.files = {tuple(st.dir_path) + k: bytearray(v) for k, v in disk.items()}
+    want = _expected(info, st)
+    for root in ("dl", "ref"):
+        for k, data in disk.items():
+            p = tmp_path.joinpath(root, *k)
+            p.parent.mkdir(parents=True, exist_ok=True)
+            p.write_bytes(data)
+    want_fs = _expected(info, Storage(fs_storage, info, str(tmp_path / "ref")))
+    shutil.rmtree(tmp_path / "ref", ignore_errors=True)
+    avail = bytearray((P + 7) // 8)
+    for i in range(P):
+        if st.get(i * L, piece_length(i, info)) is not None:
+            avail[i >> 3] |= 0x80 >> (i & 7)
+    rng = random.Random(seed)
+    for devices in ([0], [0, 0, 0]):
+        budget = _budget(L, rng.choice([1, 2, 3, 5]))
+        assert _bits(verify_pieces(info, st, devices=devices, budget=budget), P) == want, ("pieces", devices, budget)
+        assert _bits(verify_payload(info, payload[:info.length], devices=devices, avail=bytes(avail),
+                                    budget=budget), P) == want, ("payload", devices, budget)
+        assert _bits(verify_files(info, str(tmp_path / "dl"), devices=devices, threads=3, budget=budget),
+                     P) == want_fs, ("files", devices, budget)
+        _check_windowed(budget, expect_windowed=False)
+
+
+@pytest.mark.gpu
+def test_full_size_cfg2_windowed_against_the_oracle(native, oracle):
+    """BASELINE config 2 at full size (16 GiB, 16,384 x 1 MiB) under a 3 GiB budget: windows of 1,472 pieces,
+    filled on the device; creation mode equals the ORACLE's digests of every piece and verify (1 % corrupted
+    digests) gives exactly the oracle's bitfield, with every kernel choice; the payload held is <= the budget."""
+    from tests.test_gpu_paths import _threads
+    L, P = 1 << 20, 16384
+    total = L * P
+    truth = oracle.synth_piece_digests(2, total, L, P, threads=_threads())
+    bad = set(range(7, P, 101)) | {P - 1}
+    d2 = bytearray(truth)
+    for i in bad:
+        d2[20 * i + 7] ^= 0x10
+    budget = 3 << 30
+    with native.Context(0) as ctx:
+        ctx.set_option(native.TV_OPT_RESIDENT_BUDGET, budget)
+        for k in (0, 1, 2, 4):
+            ctx.set_option(native.TV_OPT_KERNEL, k)
+            ctx.set_layout(total, L, P)
+            W = ctx.counter(native.TV_COUNTER_WINDOW_PIECES)
+            assert 0 < W < P and ctx.counter(native.TV_COUNTER_PAYLOAD_BYTES) <= budget
+            ctx.fill_synthetic(2)
+            assert ctx.hash() == truth, k
+            assert ctx.counter(native.TV_COUNTER_WINDOWS) == -(-P // W)
+            ctx.set_digests(bytes(d2))
+            ctx.fill_synthetic(2)                       # a second pass over the same layout
+            bf = ctx.verify()
+            got = {i for i in range(P) if not (bf[i >> 3] >> (7 - (i & 7))) & 1}
+            assert got == bad, (k, sorted(got ^ bad)[:10])
+            assert ctx.last_timing()[0] > 0
+
+
+@pytest.mark.gpu
+def test_windowed_rules(native, oracle):
+    """The windowed layout's contract (include/torrent_verify.h, tv_set_layout): staging ascends (bytes of a
+    window already hashed this pass are TV_ERR_STATE and change nothing), pieces never staged are 0 / zero
+    digests, tv_read reads the open window only, tv_verify_list is refused, a repeated verify reuses the pass,
+    staging after it starts a new pass; and a shard that fits the budget stays whole (window counter 0)."""
+    L, P = 4096, 100
+    total = L * (P - 1) + 1234
+    payload = bytes(oracle.synth_fill(77, 0, total))
+    pieces = oracle.hash_pieces(bytearray(payload), total, L, P)
+    stride = _stride(L)
+    with native.Context(0) as ctx:
+        ctx.set_option(native.TV_OPT_RESIDENT_BUDGET, P * stride + 256)      # fits exactly: not windowed
+        ctx.set_layout(total, L, P)
+        assert ctx.counter(native.TV_COUNTER_WINDOW_PIECES) == 0
+        ctx.set_option(native.TV_OPT_RESIDENT_BUDGET, 2 * (7 * stride + 256))
+        ctx.set_layout(total, L, P)
+        assert ctx.counter(native.TV_COUNTER_WINDOW_PIECES) == 7
+        assert ctx.counter(native.TV_COUNTER_PAYLOAD_BYTES) == 2 * (7 * stride + 256)
+        ctx.set_digests(pieces)
+        ctx.stage(0, payload[:30 * L])                  # windows 0-4 (pieces 0-29)
+        out = bytearray(L)
+        ctx.read(28 * L, out)                           # window 4 is open
+        assert bytes(out) == payload[28 * L:29 * L]
+        with pytest.raises(native.NativeError) as e:
+            ctx.read(0, out)                            # window 0 was hashed
+        assert e.value.code == native.TV_ERR_STATE
+        with pytest.raises(native.NativeError) as e:
+            ctx.stage(3 * L, payload[3 * L:4 * L])      # descending: refused
+        assert e.value.code == native.TV_ERR_STATE and "ascending" in str(e.value)
+        with pytest.raises(native.NativeError) as e:
+            ctx.verify_list([0])
+        assert e.value.code == native.TV_ERR_STATE
+        ctx.stage(56 * L, payload[56 * L:])             # windows 8.. (pieces 35-55 never staged)
+        bf = ctx.verify()
+        want = [0 if 30 <= i < 56 else 1 for i in range(P)]
+        assert _bits(bf, P) == want
+        assert ctx.counter(native.TV_COUNTER_WINDOWS) == 5 + 7       # windows 0-4 and 8-14
+        assert ctx.verify() == bf                       # the same pass
+        digests = ctx.hash()
+        for i in range(P):
+            d = digests[20 * i:20 * i + 20]
+            if 35 <= i < 56:                            # windows 5-7: never opened, zero digests
+                assert d == bytes(20), i
+            elif 30 <= i < 35:                          # window 4's unstaged pieces: a stale buffer's bytes
+                assert d != pieces[20 * i:20 * i + 20], i
+            else:
+                assert d == pieces[20 * i:20 * i + 20], i
+        ctx.stage(0, payload)                           # a new pass: everything
+        assert _bits(ctx.verify(), P) == [1] * P
+        assert _bits(ctx.verify(bytes([0x7F]) + b"\xff" * ((P + 7) // 8 - 1)), P) == [0] + [1] * (P - 1)

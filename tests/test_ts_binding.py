@@ -650,3 +650,72 @@ import("{mod}").then(async (m) => {{
 """)
     res = json.loads(out)
     assert res == {"1": want.hex(), "2": want.hex(), "3": want.hex()}
+
+
+def test_piece_verifier_slots_shard_and_flush_ordering_on_cpu(tmp_path):
+    """PieceVerifier on CPU against the JS model of the library:
+    * slot pool: slots = 3 with the caller flushing holds at most 3 staged pieces, forces a flush when a 4th
+      completes, and delivers every result once;
+    * shard: a verifier over pieces [8, 16) takes only their blocks (a block of piece 3 throws) and lays out
+      that shard;
+    * flush() called while an automatic (timer) flush is still in its tv_verify_list (a slow call) returns that
+      flush's results too (they used to stay behind for a later flush), and poll() hands out what
+      automatic flushes returned."""
+    mod = erased_module(tmp_path)
+    out = run_node(tmp_path, f"""
+import {{ createRequire }} from "module";
+const require = createRequire("{HARNESS}/");
+const Deno = require("./fake_deno.js");
+const crypto = require("crypto");
+const sleep = (ms) => new Promise((r) => setTimeout(r, ms));
+import("{mod}").then(async (m) => {{
+  const L = 32768, P = 20, total = L * P;
+  const payload = crypto.randomBytes(total);
+  const pieces = [];
+  for (let i = 0; i < P; i++) pieces.push(crypto.createHash("sha1").update(payload.slice(i * L, (i + 1) * L)).digest());
+  const info = {{ pieceLength: L, length: total, pieces, name: "t", private: 0 }};
+  const blocksOf = (i) => [0, 16384].map((o) => [i, o, payload.slice(i * L + o, i * L + o + 16384)]);
+  const res = {{}};
+  {{
+    const got = [];
+    const pv = new m.PieceVerifier(info, {{ flushPieces: null, flushAgeMs: null, slots: 3, onVerified: (i, ok) => got.push([i, ok]) }});
+    for (let i = 0; i < 10; i++) for (const [x, o, b] of blocksOf(i)) await pv.onBlock(x, o, b);
+    const fin = await pv.flush();
+    const c = [...Deno.fakeContexts.values()].pop();
+    res.slots = {{ forced: pv.forcedFlushes, slots: pv.slots, max: c.maxStaged, opt: c.options[17], all: [...got, ...fin] }};
+    pv.close();
+  }}
+  {{
+    const pv = new m.PieceVerifier(info, {{ shard: [8, 8], flushPieces: 2, flushAgeMs: null }});
+    const c = [...Deno.fakeContexts.values()].pop();
+    let threw = false;
+    try {{ await pv.onBlock(3, 0, payload.slice(3 * L, 3 * L + 16384)); }} catch (e) {{ threw = true; }}
+    for (let i = 8; i < 12; i++) for (const [x, o, b] of blocksOf(i)) await pv.onBlock(x, o, b);
+    const polled = await pv.poll();
+    res.shard = {{ threw, first: c.first, count: c.count, polled, fin: await pv.flush(), slots: pv.slots }};
+    let bad = false;
+    try {{ new m.PieceVerifier(info, {{ shard: [4, 8] }}); }} catch (e) {{ bad = true; }}
+    res.shard.badShardThrows = bad;
+    pv.close();
+  }}
+  {{
+    Deno.fakeDelayMs = 20;
+    const pv = new m.PieceVerifier(info, {{ flushPieces: null, flushAgeMs: 1 }});
+    for (const [x, o, b] of blocksOf(0)) await pv.onBlock(x, o, b);   // staged by ~20 ms; timer 1 ms later
+    await sleep(8);                                                    // the timer's flush is in tv_verify_list
+    const fin = await pv.flush();
+    res.order = {{ fin, autoFlushes: pv.autoFlushes }};
+    Deno.fakeDelayMs = 0;
+    pv.close();
+  }}
+  console.log(JSON.stringify(res));
+}}).catch((e) => {{ console.error(e); process.exit(1); }});
+""")
+    res = json.loads(out)
+    assert res["slots"]["forced"] == 3 and res["slots"]["max"] == 3 and res["slots"]["slots"] == 3
+    assert res["slots"]["opt"] == 3
+    assert res["slots"]["all"] == [[i, True] for i in range(10)]
+    assert res["shard"]["threw"] and res["shard"]["first"] == 8 and res["shard"]["count"] == 8
+    assert res["shard"]["polled"] == [[8, True], [9, True], [10, True], [11, True]] and res["shard"]["fin"] == []
+    assert res["shard"]["slots"] == 2 and res["shard"]["badShardThrows"]
+    assert res["order"] == {"fin": [[0, True]], "autoFlushes": 1}

@@ -6,7 +6,10 @@
 // returning the host's availability bits) and verifyStream makes (the tv_stream_* protocol, modelled with
 // several requests per column); every other symbol throws if called.  Pointers are BigInt
 // addresses of registered typed arrays.  `nonblocking` symbols resolve on a
-// later turn of the event loop, as Deno's do, so the verifier's timer and its block handler interleave.
+// later turn of the event loop, as Deno's do, so the verifier's timer and its block handler interleave
+// (Deno.fakeDelayMs > 0: that many milliseconds later, a slow call).  The slot pool (TV_OPT_LIST_SLOTS) is
+// modelled: a staged piece holds a slot until tv_verify_list lists it; staging a new piece with every slot
+// taken returns TV_ERR_STATE (-3), as the library does.
 "use strict";
 const crypto = require("crypto");
 
@@ -54,12 +57,15 @@ const impl = {
   tv_stage(ctx, off, p, n) {
     const c = contexts.get(ctx);
     const src = bytesOf(p);
+    const slots = (c.options && c.options[17]) || 0;
     for (let pos = Number(off), q = 0; q < Number(n);) {
       const i = Math.floor(pos / c.L), within = pos % c.L;
       const plen = i === c.P - 1 && c.total % c.L ? c.total % c.L : c.L;
       if (within >= plen) break;
       const k = Math.min(plen - within, Number(n) - q);
+      if (slots && !c.staged.has(i) && c.staged.size >= slots) return -3;
       if (!c.staged.has(i)) c.staged.set(i, Buffer.alloc(plen));
+      c.maxStaged = Math.max(c.maxStaged || 0, c.staged.size);
       c.staged.get(i).set(src.subarray(q, q + k), within);
       pos += k;
       q += k;
@@ -78,6 +84,7 @@ const impl = {
       const d = c.digests.slice(20 * i, 20 * i + 20);
       ok[k] = data && d.length === 20 && crypto.createHash("sha1").update(data).digest().equals(d) ? 1 : 0;
     });
+    if ((c.options && c.options[17]) || 0) idx.forEach((v) => c.staged.delete(Number(v)));   // slots freed
     return 0;
   },
   tv_set_option(ctx, key, value) {
@@ -205,13 +212,17 @@ const Deno = {
         throw new Error(`fake_deno: ${name} is not modelled`);
       });
       out[name] = symbols[name].nonblocking
-        ? (...a) => new Promise((res, rej) => setImmediate(() => {
-          try {
-            res(f(...a));
-          } catch (e) {
-            rej(e);
-          }
-        }))
+        ? (...a) => new Promise((res, rej) => {
+          const run = () => {
+            try {
+              res(f(...a));
+            } catch (e) {
+              rej(e);
+            }
+          };
+          if (Deno.fakeDelayMs > 0) setTimeout(run, Deno.fakeDelayMs);
+          else setImmediate(run);
+        })
         : f;
     }
     return { symbols: out, close() {} };
@@ -234,6 +245,7 @@ const Deno = {
     },
   },
   fakeContexts: contexts,
+  fakeDelayMs: 0,
   fakeReset() {
     contexts.clear();
     memory.clear();

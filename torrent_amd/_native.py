@@ -36,6 +36,9 @@ TV_OPT_TWIN_PACK = 12
 TV_OPT_TWIN_FILL = 13
 TV_OPT_TWIN_FILL_READS = 14
 TV_OPT_NUMA_BIND = 15
+TV_OPT_RESIDENT_BUDGET = 16
+TV_OPT_LIST_SLOTS = 17
+TV_OPT_OPEN_RW = 18
 
 TV_COUNTER_PAYLOAD_ALLOCS = 1
 TV_COUNTER_DEVICE_ALLOCS = 2
@@ -44,6 +47,10 @@ TV_COUNTER_DEVICE_BYTES = 4
 TV_COUNTER_LAST_WORKGROUPS = 5
 TV_COUNTER_NUMA_NODE = 6
 TV_COUNTER_RING_NODE = 7
+TV_COUNTER_WINDOW_PIECES = 8
+TV_COUNTER_WINDOWS = 9
+TV_COUNTER_BUDGET = 10
+TV_COUNTER_SLOTS_USED = 11
 
 TV_STREAM_RING_SLOTS = 3
 TV_STREAM_SLOT_BYTES = 64 << 20

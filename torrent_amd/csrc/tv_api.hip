@@ -25,6 +25,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/torrent_verify.h"
@@ -128,10 +129,15 @@ int page_node(const void* p) {
 // copy into the pinned ring runs next to the ring's memory and the GPU.
 class Pool {
   public:
-    void set_affinity(const cpu_set_t* cpus) {
+    // cpus: where the workers run (nullptr: unpinned, i.e. on `process`, the process's CPUs recorded once at
+    // tv_create -- not a worker's own mask, which a thread inherits from its creator: lane 1's workers are
+    // created by the staging helper thread, itself pinned to the GPU's node)
+    void set_affinity(const cpu_set_t* cpus, const cpu_set_t* process) {
         std::lock_guard<std::mutex> g(mu_);
         has_aff_ = cpus != nullptr;
         if (cpus) aff_ = *cpus;
+        has_all_ = process != nullptr;
+        if (process) all_ = *process;
         aff_gen_++;
     }
     ~Pool() {
@@ -172,8 +178,6 @@ class Pool {
     }
     void loop() {
         uint64_t seen = 0, aff_seen = 0;
-        cpu_set_t all;
-        const bool have_all = sched_getaffinity(0, sizeof all, &all) == 0;  // the process's CPUs, to unpin
         std::unique_lock<std::mutex> lk(mu_);
         for (;;) {
             cv_.wait(lk, [&] { return stop_ || (gen_ != seen && open_ > 0); });
@@ -184,7 +188,7 @@ class Pool {
             if (aff_seen != aff_gen_) {
                 aff_seen = aff_gen_;
                 if (has_aff_) pin_thread(&aff_);
-                else if (have_all) pin_thread(&all);
+                else if (has_all_) pin_thread(&all_);
             }
             lk.unlock();
             work();
@@ -201,8 +205,8 @@ class Pool {
     int open_ = 0, running_ = 0;
     uint64_t gen_ = 0;
     bool stop_ = false;
-    bool has_aff_ = false;
-    cpu_set_t aff_;
+    bool has_aff_ = false, has_all_ = false;
+    cpu_set_t aff_, all_;
     uint64_t aff_gen_ = 0;
 };
 
@@ -321,6 +325,37 @@ struct tv_ctx {
     float kernel_ms = 0.f, total_ms = 0.f;
     int last_kernel = 0, last_launches = 0;
     uint32_t last_workgroups = 0;      // grid of the last verify / hash / list launch, companions included
+
+    // Device budget (TV_OPT_RESIDENT_BUDGET).  A shard whose padded payload exceeds it gets a WINDOWED layout:
+    // the payload allocation holds win_bufs buffers of win_n pieces, each window is hashed (HASH kernels into
+    // d_hash) as soon as staging moves past it, while the next window stages into the other buffer, and
+    // tv_verify compares d_hash with the digests at the end.  Staging must then ascend window by window.
+    uint64_t budget_opt = 0;           // bytes; 0 = automatic (free HBM at tv_set_layout - a margin)
+    uint64_t budget = 0;               // the budget the last tv_set_layout applied (0: no resident payload)
+    bool win = false;                  // the layout is windowed
+    uint64_t win_n = 0;                // pieces per window
+    int win_bufs = 0;                  // buffers in d_payload (2: window k + 1 stages while k hashes; 1)
+    uint64_t win_buf_bytes = 0;        // bytes per buffer (win_n * stride + kSlack)
+    uint64_t win_cur = UINT64_MAX;     // window open for staging (UINT64_MAX: none)
+    int win_buf = 1;                   // its buffer
+    uint64_t win_valid = 0;            // shard pieces [0, win_valid) are hashed (or zeroed: never staged) this pass
+    bool win_done = false;             // the pass is finalized: d_hash holds every shard piece's digest
+    bool win_timing = false;           // ev_call0 / ev_k0 recorded for this pass
+    uint64_t win_launched = 0;         // windows hashed this pass
+    uint64_t win_passes = 0;           // passes finalized since tv_set_layout
+    hipEvent_t win_ev[2] = {nullptr, nullptr};  // the last kernel reading buffer k
+    hipEvent_t win_cp[2] = {nullptr, nullptr};  // copies into the window queued on lane k (kernel waits on them)
+
+    // Slot pool (TV_OPT_LIST_SLOTS = K): the payload holds K piece slots instead of the shard; a staged piece
+    // takes a slot until tv_verify_list lists it (incremental verify).
+    uint64_t list_slots_opt = 0;
+    uint64_t slots = 0;                // slots of the current layout (0: not a slot layout)
+    std::unordered_map<uint64_t, uint32_t> slot_of;  // shard-relative piece -> slot
+    std::vector<uint32_t> slot_free;
+
+    bool open_rw = true;               // TV_OPT_OPEN_RW: files opened read + write (fsStorage.get) or read-only
+    cpu_set_t proc_cpus;               // the process's CPUs at tv_create (what "unpinned" workers run on)
+    bool proc_cpus_ok = false;
 };
 
 namespace {
@@ -355,19 +390,21 @@ uint64_t piece_len(const tv_ctx* c, uint64_t i) {  // piece.ts:16-19
 inline void set_bit(uint8_t* bf, uint64_t i) { bf[i >> 3] |= (uint8_t)(0x80u >> (i & 7)); }
 inline bool get_bit(const uint8_t* bf, uint64_t i) { return (bf[i >> 3] >> (7 - (i & 7))) & 1; }
 
-// May this process read and write the existing file `path` (fsStorage.get opens every segment with
-// {read: true, write: true, create: true}, storage.ts:28-32,158)?  0, or the errno that open would fail with.
-int rw_access(const char* path) {
-    return faccessat(AT_FDCWD, path, R_OK | W_OK, AT_EACCESS) == 0 ? 0 : errno;
+// May this process open the existing file `path` as the caller's reference path opens it?  rw (TV_OPT_OPEN_RW,
+// the default): read + write, as fsStorage.get opens every segment ({read, write, create}, storage.ts:28-32,158);
+// else read-only, as make_torrent.ts:78 opens its sources (Deno.open's default).  0, or the errno.
+int access_ok(const char* path, bool rw) {
+    return faccessat(AT_FDCWD, path, rw ? (R_OK | W_OK) : R_OK, AT_EACCESS) == 0 ? 0 : errno;
 }
 
 
-// Open an existing file for reading the way fsStorage.get opens it, read + write (storage.ts:28-32,158):
-// -1 and *err = errno where that open fails (no write permission, a directory, a read-only filesystem).
-// One open(O_RDWR) walks the path once; an access(R_OK | W_OK) check before an O_RDONLY open walked it
-// twice and was 4-5 % slower on 10,000 small files (profiles/r03/f2_numa_ab.jsonl).  Nothing is written.
-int open_rw(const char* path, int* err) {
-    const int fd = open(path, O_RDWR | O_CLOEXEC);
+// Open an existing file for reading the way the reference opens it: read + write for fsStorage.get
+// (storage.ts:28-32,158; -1 where that open fails: no write permission, a directory, a read-only filesystem),
+// read-only for make_torrent.ts:78 (creation from files the process may not write).  One open walks the path
+// once; an access(R_OK | W_OK) check before an O_RDONLY open walked it twice and was 4-5 % slower on 10,000
+// small files (profiles/r03/f2_numa_ab.jsonl).  Nothing is ever written.
+int open_file(const char* path, bool rw, int* err) {
+    const int fd = open(path, (rw ? O_RDWR : O_RDONLY) | O_CLOEXEC);
     *err = fd < 0 ? errno : 0;
     return fd;
 }
@@ -376,12 +413,14 @@ int open_rw(const char* path, int* err) {
 // without creating anything: an existing non-directory this process may read and write, or a missing file
 // whose parent directory exists and may be written.  A zero-length segment of Storage.get's walk
 // (storage.ts:109-110: a file ending where the piece starts, or a zero-length file inside the piece) reads
-// nothing, but its open still decides whether the piece is null.  0, or the errno.
-int fs_openable(const char* path) {
+// nothing, but its open still decides whether the piece is null.  Read-only mode (!rw, make_torrent.ts:78's
+// Deno.open(path)): an existing readable non-directory; a missing file fails (nothing would create it).
+// 0, or the errno.
+int fs_openable(const char* path, bool rw) {
     if (!path[0]) return ENOENT;
     struct stat st;
-    if (stat(path, &st) == 0) return S_ISDIR(st.st_mode) ? EISDIR : rw_access(path);
-    if (errno != ENOENT) return errno;
+    if (stat(path, &st) == 0) return S_ISDIR(st.st_mode) ? EISDIR : access_ok(path, rw);
+    if (errno != ENOENT || !rw) return errno;
     std::string parent(path);
     const size_t cut = parent.find_last_of('/');
     parent = cut == std::string::npos ? std::string(".") : (cut == 0 ? std::string("/") : parent.substr(0, cut));
@@ -455,7 +494,7 @@ hipStream_t lane_stream(const tv_ctx* c, int which) { return which ? c->copy_str
 const cpu_set_t* numa_cpus(const tv_ctx* c) { return (c->numa_bind && c->numa_cpus_ok) ? &c->numa_cpus : nullptr; }
 
 void apply_numa(tv_ctx* c) {
-    for (auto& p : c->pool) p.set_affinity(numa_cpus(c));
+    for (auto& p : c->pool) p.set_affinity(numa_cpus(c), c->proc_cpus_ok ? &c->proc_cpus : nullptr);
 }
 
 int ensure_ring(tv_ctx* c, int which = 0) {
@@ -564,8 +603,9 @@ int launch_avail(tv_ctx* c, const uint8_t* avail_bits, const uint64_t** out) {
     return TV_OK;
 }
 
-// Kernel of a launch over the whole shard (resident calls and streamed columns alike).
-int choose_kernel(const tv_ctx* c) {
+// Kernel of a launch over n consecutive pieces, one of them the torrent's short last piece when short_last
+// (resident calls, windows of a windowed layout and streamed columns alike).
+int choose_kernel_n(const tv_ctx* c, uint64_t n, bool short_last) {
     if (c->kernel_opt == TV_KERNEL_LANE || c->kernel_opt == TV_KERNEL_SPLIT || c->kernel_opt == TV_KERNEL_TWIN)
         return c->kernel_opt;
     // Twin (two lanes per piece, 2-wave workgroups over 32 pieces, 60 KiB of LDS: two per CU) while every
@@ -574,12 +614,17 @@ int choose_kernel(const tv_ctx* c) {
     // while every split pair (64 pieces, 2 waves) has SIMDs to itself: <= 32,768 pieces.  Beyond that rounds
     // waves share SIMDs and the lane kernel wins (measured 40,960 pieces split 1.62 vs lane 2.33 TB/s; 32,768
     // split 2.50 vs lane 1.87).
-    const uint64_t last = c->P - 1;
-    const bool short_last = last >= c->first && last < c->first + c->count && piece_len(c, last) != c->L;
-    const uint64_t n_main = c->count - (short_last ? 1 : 0);
+    const uint64_t n_main = n - (short_last ? 1 : 0);
     const uint64_t twin_wgs = (n_main + 31) / 32 + (short_last ? 1 : 0);   // as tv_launch_verify
     if (c->split_pairs != 2 && twin_wgs <= 2 * (uint64_t)c->cus) return TV_KERNEL_TWIN;
-    return c->count <= 32768 ? TV_KERNEL_SPLIT : TV_KERNEL_LANE;
+    return n <= 32768 ? TV_KERNEL_SPLIT : TV_KERNEL_LANE;
+}
+
+// Kernel of a launch over the whole shard.
+int choose_kernel(const tv_ctx* c) {
+    const uint64_t last = c->P - 1;
+    const bool short_last = last >= c->first && last < c->first + c->count && piece_len(c, last) != c->L;
+    return choose_kernel_n(c, c->count, short_last);
 }
 
 // One launch over the resident shard with the chosen kernel (TV_OPT_TWIN_PACK: on the CU-masked pack_stream,
@@ -644,6 +689,176 @@ TvPieces resident_launch(const tv_ctx* c) {
     p.out64 = c->d_out;
     p.out_digests = c->d_hash;
     return p;
+}
+
+// ---- what the resident payload holds: the whole shard, the open window, or a slot pool ---------------------
+
+// Shard-relative pieces [*j0, *j0 + *n) whose bytes the payload can take now: the shard; a windowed layout's
+// open window (n = 0 when none is open); a slot pool's whole shard (any piece may take a free slot).
+void resident_pieces(const tv_ctx* c, uint64_t* j0, uint64_t* n) {
+    *j0 = 0;
+    *n = c->count;
+    if (c->win) {
+        if (c->win_cur == UINT64_MAX) {
+            *n = 0;
+            return;
+        }
+        *j0 = c->win_cur * c->win_n;
+        *n = std::min(c->win_n, c->count - *j0);
+    }
+}
+
+uint8_t* win_base(const tv_ctx* c, int buf) { return c->d_payload + (uint64_t)buf * c->win_buf_bytes; }
+
+// Device address of GLOBAL piece i's byte 0 (i among the resident pieces).  A slot pool gives the piece its
+// slot, taking a free one the first time (TV_ERR_STATE when every slot holds a piece not yet listed).
+int piece_dst(tv_ctx* c, uint64_t i, uint8_t** out) {
+    const uint64_t j = i - c->first;
+    if (c->slots) {
+        auto it = c->slot_of.find(j);
+        if (it == c->slot_of.end()) {
+            if (c->slot_free.empty())
+                return fail(c, TV_ERR_STATE,
+                            "every one of the %llu slots (TV_OPT_LIST_SLOTS) holds a staged piece not yet listed: "
+                            "tv_verify_list them first", (unsigned long long)c->slots);
+            it = c->slot_of.emplace(j, c->slot_free.back()).first;
+            c->slot_free.pop_back();
+        }
+        *out = c->d_payload + (uint64_t)it->second * c->stride;
+    } else if (c->win) {
+        *out = win_base(c, c->win_buf) + (j - c->win_cur * c->win_n) * c->stride;
+    } else {
+        *out = c->d_payload + j * c->stride;
+    }
+    return TV_OK;
+}
+
+// The same for reading (tv_read): a slot pool's piece must hold a slot.
+int piece_src(tv_ctx* c, uint64_t i, const uint8_t** out) {
+    if (c->slots && !c->slot_of.count(i - c->first))
+        return fail(c, TV_ERR_STATE, "piece %llu holds no slot (it was never staged, or was listed since)",
+                    (unsigned long long)i);
+    uint8_t* p = nullptr;
+    const int rc = piece_dst(c, i, &p);
+    *out = p;
+    return rc;
+}
+
+// One launch over shard pieces [j0, j0 + n) whose bytes start at `data` (a window buffer): the resident
+// geometry narrowed to them; digest, state and hash rows are the shard's (dcount = count), offset by j0.
+TvPieces window_launch(const tv_ctx* c, uint64_t j0, uint64_t n, const uint8_t* data) {
+    TvPieces p = resident_launch(c);
+    p.data = data;
+    p.n = (uint32_t)n;
+    const uint64_t last = c->P - 1, g0 = c->first + j0;
+    p.last_idx = (last >= g0 && last < g0 + n) ? (uint32_t)(last - g0) : 0xFFFFFFFFu;
+    p.n_main = (p.last_idx != 0xFFFFFFFFu && p.last_len != c->L) ? p.n - 1 : p.n;
+    p.state = c->d_state + j0;
+    p.digests = c->d_digests + j0;
+    p.out_digests = c->d_hash + j0;
+    p.avail64 = nullptr;
+    p.out64 = nullptr;
+    return p;
+}
+
+// ---- windowed layouts (the shard's payload exceeds TV_OPT_RESIDENT_BUDGET) ----------------------------------
+//
+// Window w = shard pieces [w*win_n, (w+1)*win_n).  Staging opens the window of the bytes it stages (win_enter);
+// opening window w hashes the window open before it (win_seal: a HASH launch into the shard's digest rows d_hash,
+// after the copies queued into its buffer) and its buffer's next copies wait for the kernel that last read it, so
+// window w + 1 stages while window w hashes.  A pass ends at tv_verify / tv_hash (win_finalize), which then
+// compare / read d_hash for the whole shard; staging after that starts a new pass.  Windows a pass never opens
+// are never staged: their digests are zeroed (bit 0, zero digests), never a stale buffer's hash.
+
+int zero_hash(tv_ctx* c, uint64_t j0, uint64_t j1) {
+    if (j1 <= j0) return TV_OK;
+    for (int k = 0; k < 5; k++)
+        TV_HIP(c, hipMemsetAsync(c->d_hash + (uint64_t)k * c->count + j0, 0, (j1 - j0) * 4, c->stream));
+    return TV_OK;
+}
+
+int win_pass_timing(tv_ctx* c) {
+    if (!c->win_timing) {
+        TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
+        c->win_timing = true;
+    }
+    return TV_OK;
+}
+
+// Hash the open window (no-op when none is open).
+int win_seal(tv_ctx* c) {
+    if (c->win_cur == UINT64_MAX) return TV_OK;
+    const uint64_t j0 = c->win_cur * c->win_n, n = std::min(c->win_n, c->count - j0);
+    for (int l = 0; l < 2; l++) {  // after every copy queued into the buffer, on either staging lane
+        TV_HIP(c, hipEventRecord(c->win_cp[l], lane_stream(c, l)));
+        TV_HIP(c, hipStreamWaitEvent(c->stream, c->win_cp[l], 0));
+    }
+    if (c->win_launched == 0) TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
+    const TvPieces p = window_launch(c, j0, n, win_base(c, c->win_buf));
+    const int kernel = choose_kernel_n(c, n, p.n_main < p.n);
+    const int rc = launch_resident(c, p, kernel, /*hash=*/true);
+    if (rc) return rc;
+    TV_HIP(c, hipEventRecord(c->win_ev[c->win_buf], c->stream));
+    c->last_kernel = kernel;
+    c->win_launched++;
+    c->win_valid = j0 + n;
+    c->win_cur = UINT64_MAX;
+    return TV_OK;
+}
+
+// Open window w for staging.  A window of this pass already hashed is TV_ERR_STATE: staging ascends.
+int win_enter(tv_ctx* c, uint64_t w) {
+    if (c->win_done) {  // the last pass was finalized: this stage starts a new one
+        c->win_done = false;
+        c->win_valid = 0;
+        c->win_launched = 0;
+        c->win_timing = false;
+    }
+    if (w == c->win_cur) return TV_OK;
+    if ((c->win_cur != UINT64_MAX && w < c->win_cur) || w * c->win_n < c->win_valid)
+        return fail(c, TV_ERR_STATE,
+                    "windowed layout (the shard's %llu pieces exceed the device budget; windows of %llu pieces): "
+                    "pieces %llu.. were already hashed this pass -- stage in ascending piece order, or call "
+                    "tv_verify / tv_hash to end the pass first", (unsigned long long)c->count,
+                    (unsigned long long)c->win_n, (unsigned long long)(c->first + w * c->win_n));
+    int rc = win_pass_timing(c);
+    if (!rc) rc = win_seal(c);
+    if (!rc) rc = zero_hash(c, c->win_valid, w * c->win_n);   // windows skipped over: never staged
+    if (rc) return rc;
+    c->win_valid = w * c->win_n;
+    c->win_buf = (c->win_buf + 1) % c->win_bufs;
+    // the buffer is free once the kernel that last read it is done (copies on either lane wait for it; fills and
+    // kernels follow it on the compute stream)
+    TV_HIP(c, hipStreamWaitEvent(c->copy_stream, c->win_ev[c->win_buf], 0));
+    TV_HIP(c, hipStreamWaitEvent(c->copy_stream2, c->win_ev[c->win_buf], 0));
+    c->win_cur = w;
+    return TV_OK;
+}
+
+// End the pass: hash the open window, zero the windows never opened; d_hash then holds the whole shard.
+int win_finalize(tv_ctx* c) {
+    if (c->win_done) return TV_OK;
+    int rc = win_pass_timing(c);
+    if (!rc) rc = win_seal(c);
+    if (rc) return rc;
+    if (c->win_launched == 0) TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
+    rc = zero_hash(c, c->win_valid, c->count);
+    if (rc) return rc;
+    c->win_valid = c->count;
+    TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
+    c->win_done = true;
+    c->win_passes++;
+    return TV_OK;
+}
+
+// The window of shard-relative piece j.
+inline uint64_t win_of(const tv_ctx* c, uint64_t j) { return j / c->win_n; }
+
+// Linear byte where window w's pieces end (the next window's first byte; the shard's end for the last one).
+uint64_t win_end_linear(const tv_ctx* c, uint64_t w) {
+    const uint64_t j1 = std::min(c->count, (w + 1) * c->win_n);
+    const uint64_t last = c->first + j1 - 1;
+    return last * c->L + piece_len(c, last);
 }
 
 // The state every non-stream call needs.  need_resident: the call reads or writes the resident payload
@@ -729,7 +944,12 @@ int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n, bool pin
     while (n) {
         const uint64_t i = pos / c->L, within = pos % c->L;
         const uint64_t plen = piece_len(c, i);
-        uint8_t* dst = c->d_payload + (i - c->first) * c->stride + within;
+        uint8_t* dst = nullptr;
+        {
+            const int rc = piece_dst(c, i, &dst);  // (a slot pool gives piece i its slot here)
+            if (rc) return rc;
+        }
+        dst += within;
         const bool whole = within == 0 && plen == c->L && n >= c->L;
         // A pinned source whose alignment cannot match the destination's (mod 4; whole-piece rows need
         // it at 0 mod 4 and L % 4 == 0) goes through the ring instead: one memcpy, then aligned DMA.
@@ -750,6 +970,7 @@ int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n, bool pin
             uint64_t k = std::min<uint64_t>(n / c->L, cap / c->L);
             const uint64_t last_full = (c->total % c->L) ? c->P - 1 : c->P;  // first index that is not full
             k = std::min<uint64_t>(k, (last_full > i) ? last_full - i : 1);
+            if (c->slots) k = 1;  // a slot pool's rows are not consecutive pieces
             bytes = k * c->L;
             const uint8_t* from = via_ring ? slot.ptr() : src;
             if (via_ring) copy_into_ring(c->pool[lane], slot.ptr(), src, bytes, c->file_threads);
@@ -778,17 +999,20 @@ int stage_copy(tv_ctx* c, uint64_t pos, const uint8_t* src, uint64_t n, bool pin
     return TV_OK;
 }
 
-// Every exit of a call that queued copies from caller memory drains both streams, so no DMA
-// still reads the caller's buffer after the call returns (also on error paths), and destroys
-// the call's own events.
+// Every exit of a call that queued copies from caller memory drains its copy lane (and, unless `compute` is
+// false, the compute stream), so no DMA still reads the caller's buffer after the call returns (also on error
+// paths), and destroys the call's own events.  Staging calls leave the compute stream running: a windowed
+// layout's window kernel then hashes on while the caller reads the next bytes.
 struct DrainGuard {
     tv_ctx* c;
     int lane;
+    bool compute;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    explicit DrainGuard(tv_ctx* ctx, int copy_lane = 0) : c(ctx), lane(copy_lane) {}
+    explicit DrainGuard(tv_ctx* ctx, int copy_lane = 0, bool sync_compute = true)
+        : c(ctx), lane(copy_lane), compute(sync_compute) {}
     ~DrainGuard() {
         (void)hipStreamSynchronize(lane_stream(c, lane));
-        (void)hipStreamSynchronize(c->stream);
+        if (compute) (void)hipStreamSynchronize(c->stream);
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
         (void)hipGetLastError();
@@ -806,12 +1030,41 @@ bool is_pinned(const void* p) {
 }
 
 // Clip the LINEAR range [off, off + len) to this ctx's shard: [*a, *b) (empty when *a >= *b).
-void clip_to_shard(const tv_ctx* c, uint64_t off, uint64_t len, uint64_t* a, uint64_t* b) {
+void clip_to_whole_shard(const tv_ctx* c, uint64_t off, uint64_t len, uint64_t* a, uint64_t* b) {
     const uint64_t lo = c->first * c->L;
     const uint64_t last = c->first + c->count - 1;
     const uint64_t hi = last * c->L + piece_len(c, last);
     *a = std::max(off, lo);
     *b = std::min(off + len, hi);
+}
+
+// Clip it to the pieces the payload can take now (resident_pieces: the shard, or a windowed layout's open window).
+void clip_to_shard(const tv_ctx* c, uint64_t off, uint64_t len, uint64_t* a, uint64_t* b) {
+    uint64_t j0, n;
+    resident_pieces(c, &j0, &n);
+    if (n == 0) {
+        *a = *b = 0;
+        return;
+    }
+    const uint64_t lo = (c->first + j0) * c->L;
+    const uint64_t last = c->first + j0 + n - 1;
+    const uint64_t hi = last * c->L + piece_len(c, last);
+    *a = std::max(off, lo);
+    *b = std::min(off + len, hi);
+}
+
+// A later call that stages every byte of a piece clears its unreadable mark (recover_segment's), so a repaired
+// file re-staged into the same layout reads again: the whole pieces inside LINEAR [a, b).
+void clear_bad(tv_ctx* c, uint64_t a, uint64_t b) {
+    if (!c->any_file_bad || b <= a || c->count == 0) return;
+    const uint64_t lo = c->first * c->L;
+    if (b <= lo) return;
+    uint64_t i = std::max(a, lo);
+    i = (i + c->L - 1) / c->L;  // the first piece starting at or after a
+    for (; i < c->first + c->count && i * c->L + piece_len(c, i) <= b; i++) {
+        const uint64_t j = i - c->first;
+        c->file_bad[j >> 3] &= (uint8_t)~(0x80u >> (j & 7));
+    }
 }
 
 // Queue the copies of LINEAR bytes [a, b) (inside the shard) on the copy stream; byte `pos` is read
@@ -1153,13 +1406,18 @@ int tv_create(tv_ctx** out, int device) {
     for (int k = 0; k < 2; k++) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->col_ev[k], hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done_ev[k], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->win_ev[k], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->win_cp[k], hipEventDisableTiming);
     }
     if (e != hipSuccess) {
         fail(nullptr, TV_ERR_HIP, "tv_create: %s", hipGetErrorString(e));
         tv_destroy(c);
         return TV_ERR_HIP;
     }
-    // the GPU's NUMA node: the library's threads and pinned ring go there (TV_OPT_NUMA_BIND, default on)
+    // the GPU's NUMA node: the library's threads and pinned ring go there (TV_OPT_NUMA_BIND, default on); the
+    // process's CPUs, taken here on the creating thread before any library thread is pinned, are where the
+    // workers go back to when the binding is turned off
+    c->proc_cpus_ok = sched_getaffinity(0, sizeof c->proc_cpus, &c->proc_cpus) == 0;
     c->numa_node = gpu_numa_node(device);
     c->numa_cpus_ok = node_cpus(c->numa_node, &c->numa_cpus);
     apply_numa(c);
@@ -1183,7 +1441,8 @@ void tv_destroy(tv_ctx* c) {
     }
     if (c->h_bits) (void)hipHostFree(c->h_bits);
     for (hipEvent_t ev : {c->ev_call0, c->ev_k0, c->ev_k1, c->ev_call1, c->ev_avail, c->col_ev[0], c->col_ev[1],
-                          c->done_ev[0], c->done_ev[1], c->ev_fork, c->ev_join})
+                          c->done_ev[0], c->done_ev[1], c->ev_fork, c->ev_join, c->win_ev[0], c->win_ev[1],
+                          c->win_cp[0], c->win_cp[1]})
         if (ev) (void)hipEventDestroy(ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -1275,6 +1534,18 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
             c->numa_bind = value != 0;
             apply_numa(c);
             return TV_OK;
+        case TV_OPT_RESIDENT_BUDGET:
+            if (value < 0) return fail(c, TV_ERR_ARG, "TV_OPT_RESIDENT_BUDGET must be >= 0 (0 = automatic)");
+            c->budget_opt = (uint64_t)value;  // takes effect at the next tv_set_layout
+            return TV_OK;
+        case TV_OPT_LIST_SLOTS:
+            if (value < 0 || value >= 0xFFFFFFFFll) return fail(c, TV_ERR_ARG, "TV_OPT_LIST_SLOTS must be >= 0 (0 = off)");
+            c->list_slots_opt = (uint64_t)value;  // takes effect at the next tv_set_layout
+            return TV_OK;
+        case TV_OPT_OPEN_RW:
+            if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_OPEN_RW must be 0 or 1");
+            c->open_rw = value != 0;
+            return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
@@ -1298,6 +1569,9 @@ int tv_get_option(tv_ctx* c, int key, int64_t* value) {
         case TV_OPT_TWIN_FILL: *value = c->twin_fill; return TV_OK;
         case TV_OPT_TWIN_FILL_READS: *value = c->fill_all ? 1 : 0; return TV_OK;
         case TV_OPT_NUMA_BIND: *value = c->numa_bind ? 1 : 0; return TV_OK;
+        case TV_OPT_RESIDENT_BUDGET: *value = (int64_t)c->budget_opt; return TV_OK;
+        case TV_OPT_LIST_SLOTS: *value = (int64_t)c->list_slots_opt; return TV_OK;
+        case TV_OPT_OPEN_RW: *value = c->open_rw ? 1 : 0; return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
@@ -1340,6 +1614,21 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
     c->digest_ok.assign((shard_count + 7) / 8 + 8, 0);
     c->file_bad.assign((shard_count + 7) / 8 + 8, 0);
     c->any_file_bad = false;
+    c->win = false;
+    c->win_n = 0;
+    c->win_bufs = 0;
+    c->win_buf_bytes = 0;
+    c->win_cur = UINT64_MAX;
+    c->win_buf = 1;
+    c->win_valid = 0;
+    c->win_done = false;
+    c->win_timing = false;
+    c->win_launched = 0;
+    c->win_passes = 0;
+    c->slots = 0;
+    c->slot_of.clear();
+    c->slot_free.clear();
+    c->budget = 0;
     // Keep every allocation the new geometry fits (reuse_fits): a run of small layouts (verify_piece,
     // a flush of tv_verify_list) allocates once.  Everything else is released first, so a big payload
     // is never held beside its replacement.
@@ -1347,18 +1636,65 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
     // see no payload (TV_ERR_STATE), never a smaller buffer left by an earlier layout.  The streamed path's
     // chunk buffers are kept only for a streamed layout they fit (a resident payload must not be allocated
     // beside them), and the list buffers only while they are not far larger than the shard.
-    const uint64_t need_payload = (shard_count && c->resident) ? shard_count * c->stride + kSlack : 0;
-    if (!need_payload || !reuse_fits(need_payload, c->cap_payload)) free_payload(c);
+    uint64_t need_payload = (shard_count && c->resident) ? shard_count * c->stride + kSlack : 0;
+    uint64_t budget = 0;
+    if (need_payload && c->list_slots_opt) {
+        // a slot pool (incremental verify): K piece slots, whatever the shard's size
+        c->slots = std::min<uint64_t>(c->list_slots_opt, shard_count);
+        need_payload = c->slots * c->stride + kSlack;
+        for (uint64_t q = c->slots; q-- > 0;) c->slot_free.push_back((uint32_t)q);  // slot 0 is taken first
+    } else if (need_payload) {
+        // The device budget: TV_OPT_RESIDENT_BUDGET, or what HBM has free (plus what this ctx would release) less
+        // a margin for the per-piece rows and whatever else shares the GPU
+        budget = c->budget_opt;
+        if (!budget) {
+            size_t fr = 0, tot = 0;
+            TV_HIP(c, hipMemGetInfo(&fr, &tot));
+            const uint64_t avail = (uint64_t)fr + c->cap_payload + 2 * c->chunk_bytes;
+            const uint64_t margin = (4ull << 30) + 64 * shard_count;
+            budget = avail > margin ? avail - margin : 0;
+        }
+    }
+    // The payload: the whole shard when it fits the budget, else windows (a torrent of any size on a
+    // GPU of any free memory).  A failed allocation is retried at half the budget: only the windows shrink.
+    for (;;) {
+        if (need_payload && !c->slots && need_payload > budget) {
+            uint64_t bufs = 2, W = budget / 2 > kSlack ? (budget / 2 - kSlack) / c->stride : 0;
+            if (W == 0) {
+                bufs = 1;
+                W = budget > kSlack ? (budget - kSlack) / c->stride : 0;
+            }
+            W = std::max<uint64_t>(1, std::min(W, shard_count));  // (one piece larger than the budget: held anyway)
+            if (W >= 256) W = W / 64 * 64;                        // whole 64-piece waves per window
+            c->win = true;
+            c->win_n = W;
+            c->win_bufs = (int)bufs;
+            c->win_buf_bytes = W * c->stride + kSlack;
+            need_payload = bufs * c->win_buf_bytes;
+        }
+        if (!need_payload || !reuse_fits(need_payload, c->cap_payload)) free_payload(c);
+        if (!need_payload || c->d_payload) break;
+        const hipError_t e = hipMalloc((void**)&c->d_payload, need_payload);
+        if (e == hipSuccess) {
+            c->cap_payload = need_payload;
+            c->n_payload_allocs++;
+            c->n_device_allocs++;
+            break;
+        }
+        (void)hipGetLastError();
+        c->d_payload = nullptr;
+        if (e != hipErrorOutOfMemory || c->slots || need_payload <= (64ull << 20))
+            return fail(c, e == hipErrorOutOfMemory ? TV_ERR_NOMEM : TV_ERR_HIP, "hipMalloc(%llu) of the payload: %s",
+                        (unsigned long long)need_payload, hipGetErrorString(e));
+        budget = need_payload / 2;  // windows of half the size
+        need_payload = shard_count * c->stride + kSlack;
+        c->win = false;
+    }
+    c->budget = budget;
     if (!reuse_fits(shard_count, c->cap_count)) free_per_piece(c);
     if (!reuse_fits(c->bit_words, c->cap_words)) free_words(c);
     if (c->chunk_bytes && (need_payload || !reuse_fits(stream_chunk_need(c), c->chunk_bytes))) free_chunks(c);
     if (c->list_cap > std::max<uint64_t>(1024, 2 * shard_count)) free_list(c);
-    if (need_payload && !c->d_payload) {
-        TV_HIP(c, hipMalloc((void**)&c->d_payload, need_payload));
-        c->cap_payload = need_payload;
-        c->n_payload_allocs++;
-        c->n_device_allocs++;
-    }
     if (shard_count && !c->d_digests) {
         TV_HIP(c, hipMalloc((void**)&c->d_digests, 5 * shard_count * sizeof(uint32_t)));
         TV_HIP(c, hipMalloc((void**)&c->d_state, 5 * shard_count * sizeof(uint32_t)));
@@ -1374,8 +1710,11 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
         c->cap_words = c->bit_words;
         c->n_device_allocs += 3;
     }
-    if (need_payload) {  // the tail over-read slack past the last piece reads zeros
-        TV_HIP(c, hipMemsetAsync(c->d_payload + shard_count * c->stride, 0, kSlack, c->stream));
+    if (need_payload) {  // the tail over-read slack past the last piece (of each window buffer, of the slots) reads zeros
+        const uint64_t rows = c->win ? c->win_n : (c->slots ? c->slots : shard_count);
+        for (int k = 0; k < (c->win ? c->win_bufs : 1); k++)
+            TV_HIP(c, hipMemsetAsync(c->d_payload + (uint64_t)k * c->win_buf_bytes + rows * c->stride, 0, kSlack,
+                                     c->stream));
         TV_HIP(c, hipStreamSynchronize(c->stream));
     }
     c->has_layout = true;
@@ -1428,12 +1767,30 @@ int tv_stage(tv_ctx* c, uint64_t linear_offset, const uint8_t* src, uint64_t len
     if (c->count == 0 || len == 0) return TV_OK;
     TV_HIP(c, hipSetDevice(c->device));
     uint64_t a, b;
-    clip_to_shard(c, linear_offset, len, &a, &b);
+    clip_to_whole_shard(c, linear_offset, len, &a, &b);
     if (a >= b) return TV_OK;
-    DrainGuard drain(c);
-    rc = stage_range(c, a, b, src, linear_offset, is_pinned(src));
-    if (rc) return rc;
+    DrainGuard drain(c, 0, /*sync_compute=*/false);  // (a window kernel queued here hashes on after the call)
+    const bool pinned = is_pinned(src);
+    if (c->win) {
+        // window by window, ascending: opening the next window hashes the previous one (win_enter)
+        for (uint64_t pos = a; pos < b;) {
+            const uint64_t w = win_of(c, pos / c->L - c->first);
+            rc = win_enter(c, w);
+            if (rc) return rc;
+            uint64_t wa, wb;
+            clip_to_shard(c, pos, b - pos, &wa, &wb);
+            if (wa < wb) {
+                rc = stage_range(c, wa, wb, src, linear_offset, pinned);
+                if (rc) return rc;
+            }
+            pos = win_end_linear(c, w);
+        }
+    } else {
+        rc = stage_range(c, a, b, src, linear_offset, pinned);
+        if (rc) return rc;
+    }
     TV_HIP(c, hipStreamSynchronize(c->copy_stream));   // report a copy failure as this call's error
+    clear_bad(c, a, b);
     return TV_OK;
 }
 
@@ -1445,13 +1802,14 @@ int stage_file_locked(tv_ctx* c, const char* path, uint64_t file_offset, uint64_
     hipStream_t cs = lane_stream(c, lane);
     int rc = TV_OK;
     if (len == 0) {  // reads nothing, but fsStorage.get still opens the path (storage.ts:158)
-        const int e = fs_openable(path);
+        const int e = fs_openable(path, c->open_rw);
         return e ? fail(c, TV_ERR_IO, "open %s: %s", path, strerror(e)) : TV_OK;
     }
     FileWindows win;  // before `drain`: destroyed after the streams are drained
     int oe = 0;
-    win.fd = open_rw(path, &oe);
-    if (win.fd < 0) return fail(c, TV_ERR_IO, "open %s for read and write: %s", path, strerror(oe));
+    win.fd = open_file(path, c->open_rw, &oe);
+    if (win.fd < 0)
+        return fail(c, TV_ERR_IO, "open %s for %s: %s", path, c->open_rw ? "read and write" : "reading", strerror(oe));
     struct stat st;
     if (fstat(win.fd, &st) != 0) return fail(c, TV_ERR_IO, "fstat %s: %s", path, strerror(errno));
     if ((uint64_t)st.st_size < file_offset + len)
@@ -1462,7 +1820,7 @@ int stage_file_locked(tv_ctx* c, const char* path, uint64_t file_offset, uint64_
     clip_to_shard(c, linear_offset, len, &a, &b);
     if (a >= b) return TV_OK;
     TV_HIP(c, hipSetDevice(c->device));
-    DrainGuard drain(c, lane);
+    DrainGuard drain(c, lane, /*sync_compute=*/false);
     for (int k = 0; k < 2; k++) TV_HIP(c, hipEventCreateWithFlags(&drain.ev[k], hipEventDisableTiming));
     const uint64_t page = (uint64_t)sysconf(_SC_PAGESIZE);
     const uint64_t chunk = c->file_chunk;
@@ -1523,7 +1881,7 @@ struct SmallSeg {
 };
 
 void read_segments(Pool& pool, const std::vector<SmallSeg>& segs, size_t lo, size_t hi, const char* const* paths,
-                   uint8_t* slot, int32_t* status, int threads, std::string* first_err, std::mutex* err_mu) {
+                   uint8_t* slot, int32_t* status, int threads, bool rw, std::string* first_err, std::mutex* err_mu) {
     // work items: (segment, part) with parts of at most 4 MiB, so one long segment is read by many threads;
     // run on the lane's persistent workers (a thread spawn per 64 MiB slot cost ~15 x 20-50 us per slot)
     constexpr uint64_t kPart = 4ull << 20;
@@ -1535,7 +1893,7 @@ void read_segments(Pool& pool, const std::vector<SmallSeg>& segs, size_t lo, siz
         const uint64_t part0 = items[it].second, part1 = std::min(sg.len, part0 + kPart);
         const char* path = paths[sg.k];
         int e = 0;
-        const int fd = open_rw(path, &e);  // opened as fsStorage.get opens it: read + write (storage.ts:28-32)
+        const int fd = open_file(path, rw, &e);  // as fsStorage.get opens it, read + write (storage.ts:28-32)
         if (fd >= 0) {
             uint64_t o = part0;
             while (o < part1) {
@@ -1575,8 +1933,8 @@ void mark_bad(tv_ctx* c, uint64_t a, uint64_t b) {
 
 // Bytes of [file_offset, file_offset + len) that fsStorage.get's read of `path` would return: 0 when the
 // open (read + write, storage.ts:28-32,158) fails or the path is not a regular file, else what the file holds.
-uint64_t readable_prefix(const char* path, uint64_t file_offset, uint64_t len) {
-    if (rw_access(path)) return 0;
+uint64_t readable_prefix(const char* path, uint64_t file_offset, uint64_t len, bool rw) {
+    if (access_ok(path, rw)) return 0;
     struct stat st;
     if (stat(path, &st) != 0 || !S_ISREG(st.st_mode)) return 0;
     const uint64_t size = (uint64_t)st.st_size;
@@ -1591,7 +1949,7 @@ int recover_segment(tv_ctx* c, const char* path, uint64_t file_offset, uint64_t 
         mark_bad(c, linear_offset, linear_offset);
         return TV_OK;
     }
-    uint64_t r = readable_prefix(path, file_offset, len);
+    uint64_t r = readable_prefix(path, file_offset, len, c->open_rw);
     if (r == len) r = 0;  // readable by size yet the read failed (an I/O error): nothing of it counts
     // only the prefix's whole pieces are staged: the piece holding its first missing byte is marked below
     const uint64_t whole = (linear_offset + r) / c->L * c->L;
@@ -1615,32 +1973,55 @@ int tv_stage_file(tv_ctx* c, const char* path, uint64_t file_offset, uint64_t li
     if (!path) return fail(c, TV_ERR_ARG, "path is NULL");
     if (linear_offset + len < linear_offset || file_offset + len < file_offset)
         return fail(c, TV_ERR_ARG, "offset + len overflows");
-    rc = stage_file_locked(c, path, file_offset, linear_offset, len);
-    if (rc != TV_ERR_IO || c->count == 0) return rc;
-    const std::string err = c->err;
-    const int r = recover_segment(c, path, file_offset, linear_offset, len);
-    if (r) return r;
-    fail(c, TV_ERR_IO, "%s", err.c_str());  // the first failure stays the call's message
+    uint64_t a = 0, b = 0;
+    if (c->count) clip_to_whole_shard(c, linear_offset, len, &a, &b);
+    if (!c->win || len == 0 || a >= b) {
+        rc = stage_file_locked(c, path, file_offset, linear_offset, len);
+        if (rc == TV_OK) clear_bad(c, a, b);
+        if (rc != TV_ERR_IO || c->count == 0) return rc;
+        const std::string err = c->err;
+        const int r = recover_segment(c, path, file_offset, linear_offset, len);
+        if (r) return r;
+        fail(c, TV_ERR_IO, "%s", err.c_str());  // the first failure stays the call's message
+        return TV_ERR_IO;
+    }
+    // windowed layout: the segment window by window (each part is checked, staged and recovered on its own, so a
+    // short file still keeps its whole pieces before the first missing byte)
+    TV_HIP(c, hipSetDevice(c->device));
+    std::string first_err;
+    for (uint64_t pos = a; pos < b;) {
+        const uint64_t w = win_of(c, pos / c->L - c->first);
+        rc = win_enter(c, w);
+        if (rc) return rc;
+        const uint64_t e = std::min(b, win_end_linear(c, w));
+        const uint64_t fo = file_offset + (pos - linear_offset);
+        rc = stage_file_locked(c, path, fo, pos, e - pos);
+        if (rc == TV_OK) {
+            clear_bad(c, pos, e);
+        } else if (rc == TV_ERR_IO) {
+            if (first_err.empty()) first_err = c->err;
+            rc = recover_segment(c, path, fo, pos, e - pos);
+            if (rc) return rc;
+        } else {
+            return rc;
+        }
+        pos = e;
+    }
+    if (first_err.empty()) return TV_OK;
+    fail(c, TV_ERR_IO, "%s", first_err.c_str());
     return TV_ERR_IO;
 }
 
-int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64_t* file_offsets,
-                   const uint64_t* linear_offsets, const uint64_t* lens, int32_t* status_out) {
-    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
-    std::lock_guard<std::mutex> g(c->mu);
-    int rc = require_layout(c, false, true);
-    if (rc) return rc;
-    if (n == 0) return TV_OK;
-    if (!paths || !file_offsets || !linear_offsets || !lens || !status_out)
-        return fail(c, TV_ERR_ARG, "NULL argument");
-    for (uint64_t k = 0; k < n; k++) {
-        if (!paths[k]) return fail(c, TV_ERR_ARG, "paths[%llu] is NULL", (unsigned long long)k);
-        if (linear_offsets[k] + lens[k] < linear_offsets[k] || file_offsets[k] + lens[k] < file_offsets[k])
-            return fail(c, TV_ERR_ARG, "segment %llu: offset + len overflows", (unsigned long long)k);
-        status_out[k] = TV_OK;
-    }
-    if (c->count == 0) return TV_OK;
-    TV_HIP(c, hipSetDevice(c->device));
+}  // extern "C"
+
+namespace {
+
+// tv_stage_files with the lock held and the arguments checked: every segment's bytes among the resident pieces
+// (clip_to_shard: the shard, or a windowed layout's open window).  status_out[k] is set to TV_ERR_IO on a
+// failure and left alone otherwise.  check_zero: check the zero-length segments' opens (once per call).
+int stage_files_core(tv_ctx* c, uint64_t n, const char* const* paths, const uint64_t* file_offsets,
+                     const uint64_t* linear_offsets, const uint64_t* lens, int32_t* status_out, bool check_zero) {
+    int rc = TV_OK;
     // Long segments: the windowed page-cache path of tv_stage_file.  Short ones: packed into the pinned
     // ring's 64 MiB slots, read by the thread pool, DMA'd per run of linear-contiguous segments while the
     // next slot is read.  With TV_OPT_FILE_CONCURRENT the long segments are split by bytes between a
@@ -1656,7 +2037,8 @@ int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64
     std::string zero_err;
     for (uint64_t k = 0; k < n; k++) {
         if (lens[k] == 0) {  // Storage.get's zero-length segments: only the open decides (storage.ts:109-110,158)
-            if (const int e = fs_openable(paths[k])) {
+            if (!check_zero) continue;
+            if (const int e = fs_openable(paths[k], c->open_rw)) {
                 status_out[k] = TV_ERR_IO;
                 if (zero_err.empty()) zero_err = std::string(paths[k]) + ": " + strerror(e);
             }
@@ -1722,7 +2104,7 @@ int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64
     }
     std::string first_err = zero_err;
     std::mutex err_mu;
-    DrainGuard drain(c);
+    DrainGuard drain(c, 0, /*sync_compute=*/false);
     size_t i = 0;
     while (i < small.size()) {
         size_t j = i;
@@ -1738,7 +2120,8 @@ int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64
         SlotLease slot(c, 0);  // lent until every copy out of it is queued
         rc = slot.take();
         if (rc) return rc;
-        read_segments(c->pool[0], small, i, j, paths, slot.ptr(), status_out, c->file_threads, &first_err, &err_mu);
+        read_segments(c->pool[0], small, i, j, paths, slot.ptr(), status_out, c->file_threads, c->open_rw, &first_err,
+                      &err_mu);
         for (size_t q = i; q < j;) {  // one copy per run of readable, linear-contiguous segments
             if (status_out[small[q].k] != TV_OK) { q++; continue; }
             size_t r = q + 1;
@@ -1759,11 +2142,71 @@ int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64
     // the failed segments: their readable prefixes staged again, the rest of their pieces marked unreadable
     for (uint64_t k = 0; k < n; k++) {
         if (status_out[k] != TV_ERR_IO) continue;
+        if (lens[k] == 0 && !check_zero) continue;
         rc = recover_segment(c, paths[k], file_offsets[k], linear_offsets[k], lens[k]);
         if (rc) return rc;
     }
     if (!first_err.empty()) fail(c, TV_OK, "tv_stage_files: %s (and possibly more; see status_out)", first_err.c_str());
     return TV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64_t* file_offsets,
+                   const uint64_t* linear_offsets, const uint64_t* lens, int32_t* status_out) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = require_layout(c, false, true);
+    if (rc) return rc;
+    if (n == 0) return TV_OK;
+    if (!paths || !file_offsets || !linear_offsets || !lens || !status_out)
+        return fail(c, TV_ERR_ARG, "NULL argument");
+    for (uint64_t k = 0; k < n; k++) {
+        if (!paths[k]) return fail(c, TV_ERR_ARG, "paths[%llu] is NULL", (unsigned long long)k);
+        if (linear_offsets[k] + lens[k] < linear_offsets[k] || file_offsets[k] + lens[k] < file_offsets[k])
+            return fail(c, TV_ERR_ARG, "segment %llu: offset + len overflows", (unsigned long long)k);
+        status_out[k] = TV_OK;
+    }
+    if (c->count == 0) return TV_OK;
+    TV_HIP(c, hipSetDevice(c->device));
+    // the pieces whose every byte this call stages lose an earlier call's unreadable mark (the union of the
+    // segments, merged: a piece spanning files is covered by several)
+    if (c->any_file_bad) {
+        std::vector<std::pair<uint64_t, uint64_t>> iv;
+        for (uint64_t k = 0; k < n; k++)
+            if (lens[k]) iv.emplace_back(linear_offsets[k], linear_offsets[k] + lens[k]);
+        std::sort(iv.begin(), iv.end());
+        for (size_t q = 0; q < iv.size();) {
+            uint64_t a = iv[q].first, b = iv[q].second;
+            size_t r = q + 1;
+            for (; r < iv.size() && iv[r].first <= b; r++) b = std::max(b, iv[r].second);
+            clear_bad(c, a, b);
+            q = r;
+        }
+    }
+    if (!c->win) return stage_files_core(c, n, paths, file_offsets, linear_offsets, lens, status_out, true);
+    // windowed layout: the windows the segments touch, ascending; each is staged by one core pass (which skips
+    // every byte outside it) and hashed when the next one opens
+    const uint64_t nwin = (c->count + c->win_n - 1) / c->win_n;
+    std::vector<uint8_t> touched(nwin, 0);
+    for (uint64_t k = 0; k < n; k++) {
+        uint64_t a, b;
+        clip_to_whole_shard(c, linear_offsets[k], lens[k], &a, &b);
+        if (a >= b) continue;
+        const uint64_t w0 = win_of(c, a / c->L - c->first), w1 = win_of(c, (b - 1) / c->L - c->first);
+        std::fill(touched.begin() + (ptrdiff_t)w0, touched.begin() + (ptrdiff_t)w1 + 1, (uint8_t)1);
+    }
+    bool check_zero = true;  // (the zero-length segments' opens are checked in the first pass)
+    for (uint64_t w = 0; w < nwin; w++) {
+        if (!touched[w]) continue;
+        rc = win_enter(c, w);
+        if (!rc) rc = stage_files_core(c, n, paths, file_offsets, linear_offsets, lens, status_out, check_zero);
+        if (rc) return rc;
+        check_zero = false;
+    }
+    return check_zero ? stage_files_core(c, n, paths, file_offsets, linear_offsets, lens, status_out, true) : TV_OK;
 }
 
 int tv_read(tv_ctx* c, uint64_t linear_offset, uint8_t* dst, uint64_t len) {
@@ -1775,22 +2218,29 @@ int tv_read(tv_ctx* c, uint64_t linear_offset, uint8_t* dst, uint64_t len) {
     if (linear_offset + len < linear_offset) return fail(c, TV_ERR_ARG, "offset + len overflows");
     if (c->count == 0 || len == 0) return TV_OK;
     TV_HIP(c, hipSetDevice(c->device));
-    const uint64_t lo = c->first * c->L;
-    const uint64_t last = c->first + c->count - 1;
-    const uint64_t hi = last * c->L + piece_len(c, last);
-    uint64_t pos = std::max(linear_offset, lo);
-    const uint64_t b = std::min(linear_offset + len, hi);
+    uint64_t pos, b;
+    clip_to_whole_shard(c, linear_offset, len, &pos, &b);
+    if (c->win && pos < b) {  // a windowed layout holds the open window's bytes only
+        uint64_t wa, wb;
+        clip_to_shard(c, pos, b - pos, &wa, &wb);
+        if (wa != pos || wb != b)
+            return fail(c, TV_ERR_STATE, "windowed layout: tv_read reads only the open window's pieces");
+    }
     DrainGuard drain(c);  // no D2H copy into dst outlives the call, also on error paths
     while (pos < b) {
         const uint64_t i = pos / c->L, within = pos % c->L;
         const uint64_t plen = piece_len(c, i);
         if (within >= plen) { pos = (i + 1) * c->L; continue; }
-        const uint8_t* src = c->d_payload + (i - c->first) * c->stride + within;
+        const uint8_t* src = nullptr;
+        rc = piece_src(c, i, &src);
+        if (rc) return rc;
+        src += within;
         uint8_t* out = dst + (pos - linear_offset);
         if (within == 0 && plen == c->L && b - pos >= c->L) {
             uint64_t k = (b - pos) / c->L;
             const uint64_t last_full = (c->total % c->L) ? c->P - 1 : c->P;
             k = std::min<uint64_t>(k, last_full > i ? last_full - i : 1);
+            if (c->slots) k = 1;
             TV_HIP(c, hipMemcpy2DAsync(out, c->L, src, c->stride, c->L, k, hipMemcpyDeviceToHost, c->copy_stream));
             pos += k * c->L;
         } else {
@@ -1809,7 +2259,22 @@ int tv_fill_synthetic(tv_ctx* c, uint64_t seed) {
     int rc = require_layout(c, false, true);
     if (rc) return rc;
     if (!c->count) return TV_OK;
+    if (c->slots) return fail(c, TV_ERR_STATE, "tv_fill_synthetic: a slot pool (TV_OPT_LIST_SLOTS) holds no shard");
     TV_HIP(c, hipSetDevice(c->device));
+    if (c->win) {
+        // every window from the open one (or the next unhashed one; a new pass: the first) is filled in its buffer
+        // and hashed when the next opens, all on the compute stream
+        uint64_t w = c->win_done ? 0 : (c->win_cur != UINT64_MAX ? c->win_cur : (c->win_valid + c->win_n - 1) / c->win_n);
+        for (const uint64_t nwin = (c->count + c->win_n - 1) / c->win_n; w < nwin; w++) {
+            rc = win_enter(c, w);
+            if (rc) return rc;
+            const uint64_t j0 = w * c->win_n;
+            TV_HIP(c, tv_launch_fill(win_base(c, c->win_buf), c->stride, c->first + j0,
+                                     (uint32_t)std::min(c->win_n, c->count - j0), c->L, seed, c->stream));
+        }
+        TV_HIP(c, hipStreamSynchronize(c->stream));
+        return TV_OK;
+    }
     TV_HIP(c, tv_launch_fill(c->d_payload, c->stride, c->first, (uint32_t)c->count, c->L, seed, c->stream));
     TV_HIP(c, hipStreamSynchronize(c->stream));
     return TV_OK;
@@ -1822,9 +2287,22 @@ int tv_verify(tv_ctx* c, const uint8_t* avail_bits, uint8_t* bitfield_out) {
     if (rc) return rc;
     if (!bitfield_out && c->count) return fail(c, TV_ERR_ARG, "bitfield_out is NULL");
     if (!c->count) return TV_OK;
+    if (c->slots) return fail(c, TV_ERR_STATE, "tv_verify: a slot pool (TV_OPT_LIST_SLOTS) verifies with tv_verify_list");
     TV_HIP(c, hipSetDevice(c->device));
-    TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
     const uint64_t* av = nullptr;
+    if (c->win) {
+        // windowed: end the pass (its windows hashed into d_hash as they filled), then compare the whole shard
+        rc = win_finalize(c);
+        if (!rc) rc = launch_avail(c, avail_bits, &av);
+        if (rc) return rc;
+        TV_HIP(c, tv_launch_compare(c->d_hash, c->d_digests, (uint32_t)c->count, (uint32_t)c->count, av, c->d_out,
+                                    c->stream));
+        rc = read_bits(c, bitfield_out);
+        if (rc) return rc;
+        c->last_launches = (int)c->win_launched;
+        return finish_timing(c);
+    }
+    TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
     rc = launch_avail(c, avail_bits, &av);
     if (rc) return rc;
     const int kernel = choose_kernel(c);
@@ -1851,6 +2329,9 @@ int tv_verify_list(tv_ctx* c, const uint64_t* pieces, uint64_t n, uint8_t* ok_ou
     if (n == 0) return TV_OK;
     if (!pieces || !ok_out) return fail(c, TV_ERR_ARG, "NULL argument");
     if (n >= 0xFFFFFFFFull) return fail(c, TV_ERR_ARG, "list too long");
+    if (c->win)
+        return fail(c, TV_ERR_STATE, "tv_verify_list needs the shard resident or a slot pool (TV_OPT_LIST_SLOTS); "
+                                     "this layout is windowed (the shard exceeds the device budget)");
     std::vector<uint32_t> local(n);
     for (uint64_t k = 0; k < n; k++) {
         if (pieces[k] < c->first || pieces[k] >= c->first + c->count)
@@ -1859,75 +2340,101 @@ int tv_verify_list(tv_ctx* c, const uint64_t* pieces, uint64_t n, uint8_t* ok_ou
                         (unsigned long long)(c->first + c->count));
         local[k] = (uint32_t)(pieces[k] - c->first);
     }
-    // A short last piece (piece.ts:16-19) listed together with full pieces goes into waves of its own:
-    // the launch list is [full pieces..., padding to a multiple of 64, last-piece entries...], so no
+    // The entries launched: every listed piece, or, in a slot pool, the listed pieces that hold a slot (the others
+    // were never staged: 0).  A short last piece (piece.ts:16-19) listed together with full pieces goes into waves
+    // of its own: the launch list is [full pieces..., padding to a multiple of 64, last-piece entries...], so no
     // wave mixes the short piece's padding blocks with the others' raw blocks (the slow path).
+    std::vector<uint64_t> sel;
+    sel.reserve(n);
+    for (uint64_t k = 0; k < n; k++) {
+        if (!c->slots || c->slot_of.count(local[k])) sel.push_back(k);
+        else ok_out[k] = 0;
+    }
     const uint64_t lastj = c->first + c->count - 1 == c->P - 1 ? c->count - 1 : UINT64_MAX;
-    std::vector<uint32_t> launch;  // shard-relative pieces in launch order
+    uint64_t nlast = 0;
+    if (lastj != UINT64_MAX && piece_len(c, c->P - 1) != c->L)
+        for (uint64_t k : sel) nlast += local[k] == lastj;
+    std::vector<uint32_t> launch;  // shard-relative pieces in launch order (then, for a slot pool, their slots)
     std::vector<int64_t> origin;   // launch position -> index in `pieces` (-1 = padding)
-    bool reordered = false;
-    if (lastj != UINT64_MAX && piece_len(c, c->P - 1) != c->L) {
-        uint64_t nlast = 0;
-        for (uint64_t k = 0; k < n; k++) nlast += local[k] == lastj;
-        if (nlast && nlast < n) {
-            reordered = true;
-            for (uint64_t k = 0; k < n; k++)
-                if (local[k] != lastj) { launch.push_back(local[k]); origin.push_back((int64_t)k); }
-            while (launch.size() % 64) { launch.push_back(launch[0]); origin.push_back(-1); }
-            for (uint64_t k = 0; k < n; k++)
-                if (local[k] == lastj) { launch.push_back(local[k]); origin.push_back((int64_t)k); }
-        }
+    launch.reserve(sel.size() + 64);
+    origin.reserve(sel.size() + 64);
+    const bool separate = nlast && nlast < sel.size();
+    for (int part = 0; part < (separate ? 2 : 1); part++) {
+        for (uint64_t k : sel)
+            if (!separate || (local[k] == lastj) == (part == 1)) {
+                launch.push_back(local[k]);
+                origin.push_back((int64_t)k);
+            }
+        if (separate && part == 0)
+            while (launch.size() % 64) {
+                launch.push_back(launch[0]);
+                origin.push_back(-1);
+            }
     }
-    if (!reordered) launch.swap(local);
     const uint64_t m = launch.size();
-    std::vector<uint8_t> ok_launch(reordered ? m : 0);
+    if (c->slots)  // the rows: each entry's slot (the kernels read piece launch[j]'s bytes from slot rows[j])
+        for (uint64_t j = 0; j < m; j++) launch.push_back(c->slot_of.find(launch[j])->second);
+    std::vector<uint8_t> ok_launch(m);
     TV_HIP(c, hipSetDevice(c->device));
-    DrainGuard drain(c);  // after the host vectors: their H2D / D2H copies end before return
-    if (c->list_cap < m) {
-        free_list(c);
-        const uint64_t cap = std::max<uint64_t>(m, 1024);
-        TV_HIP(c, hipMalloc((void**)&c->d_list, cap * 4));
-        TV_HIP(c, hipMalloc((void**)&c->d_list_out, cap));
-        c->list_cap = cap;
-        c->n_device_allocs += 2;
+    int kernel = 0;
+    if (m) {
+        DrainGuard drain(c);  // after the host vectors: their H2D / D2H copies end before they go
+        if (c->list_cap < m) {
+            free_list(c);
+            const uint64_t cap = std::max<uint64_t>(m, 1024);
+            TV_HIP(c, hipMalloc((void**)&c->d_list, 2 * cap * 4));  // indices, then (slot pool) rows
+            TV_HIP(c, hipMalloc((void**)&c->d_list_out, cap));
+            c->list_cap = cap;
+            c->n_device_allocs += 2;
+        }
+        TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
+        TV_HIP(c, hipMemcpyAsync(c->d_list, launch.data(), launch.size() * 4, hipMemcpyHostToDevice, c->stream));
+        TvPieces p = resident_launch(c);
+        p.n = (uint32_t)m;
+        p.n_main = (uint32_t)m;
+        p.idx = c->d_list;
+        p.rows = c->slots ? c->d_list + m : nullptr;
+        p.out_bytes = c->d_list_out;
+        TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
+        // twin (two lanes per piece) while its 2-wave workgroups fit two per CU, then split (rounds + helper pair,
+        // ~30 % shorter serial stream per block than lane) while one pair per CU suffices, like choose_kernel;
+        // the lane list kernel for longer lists
+        kernel = (c->kernel_opt == TV_KERNEL_LANE || c->kernel_opt == TV_KERNEL_SPLIT ||
+                  c->kernel_opt == TV_KERNEL_TWIN)
+                     ? c->kernel_opt
+                     : (m <= 64 * (uint64_t)c->cus ? TV_KERNEL_TWIN : (m <= 256 * 64 ? TV_KERNEL_SPLIT : TV_KERNEL_LANE));
+        // Companions (as resident launches) only for a list that gives every CU a workgroup: a shorter one would
+        // fill 2 x CUs workgroups with copies re-hashing the same few pieces (a 1-piece flush: 512 copies) for a
+        // ~4 % shorter flush (r03 latency: tools/latency_probe.py)
+        const uint64_t list_wgs = (m + 31) / 32;
+        if (kernel == TV_KERNEL_TWIN && (c->twin_fill == 2 || (c->twin_fill == 1 && list_wgs >= (uint64_t)c->cus))) {
+            p.fill_to = 2u * (uint32_t)c->cus;
+            p.fill_all = c->fill_all ? 1u : 0u;
+        }
+        TV_HIP(c, tv_launch_verify_list(p, kernel, c->stream, &c->last_workgroups));
+        TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
+        TV_HIP(c, hipMemcpyAsync(ok_launch.data(), c->d_list_out, m, hipMemcpyDeviceToHost, c->stream));
+        TV_HIP(c, hipEventRecord(c->ev_call1, c->stream));
+        TV_HIP(c, hipEventSynchronize(c->ev_call1));
     }
-    TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
-    TV_HIP(c, hipMemcpyAsync(c->d_list, launch.data(), m * 4, hipMemcpyHostToDevice, c->stream));
-    TvPieces p = resident_launch(c);
-    p.n = (uint32_t)m;
-    p.n_main = (uint32_t)m;
-    p.idx = c->d_list;
-    p.out_bytes = c->d_list_out;
-    TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
-    // twin (two lanes per piece) while its 2-wave workgroups fit two per CU, then split (rounds + helper pair,
-    // ~30 % shorter serial stream per block than lane) while one pair per CU suffices, like choose_kernel;
-    // the lane list kernel for longer lists
-    const int kernel = (c->kernel_opt == TV_KERNEL_LANE || c->kernel_opt == TV_KERNEL_SPLIT ||
-                        c->kernel_opt == TV_KERNEL_TWIN)
-                           ? c->kernel_opt
-                           : (m <= 64 * (uint64_t)c->cus ? TV_KERNEL_TWIN
-                                                         : (m <= 256 * 64 ? TV_KERNEL_SPLIT : TV_KERNEL_LANE));
-    // Companions (as resident launches) only for a list that gives every CU a workgroup: a shorter one would
-    // fill 2 x CUs workgroups with copies re-hashing the same few pieces (a 1-piece flush: 512 copies) for a
-    // ~4 % shorter flush (r03 latency: tools/latency_probe.py)
-    const uint64_t list_wgs = (m + 31) / 32;
-    if (kernel == TV_KERNEL_TWIN && (c->twin_fill == 2 || (c->twin_fill == 1 && list_wgs >= (uint64_t)c->cus))) {
-        p.fill_to = 2u * (uint32_t)c->cus;
-        p.fill_all = c->fill_all ? 1u : 0u;
-    }
-    TV_HIP(c, tv_launch_verify_list(p, kernel, c->stream, &c->last_workgroups));
-    TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
-    TV_HIP(c, hipMemcpyAsync(reordered ? ok_launch.data() : ok_out, c->d_list_out, m, hipMemcpyDeviceToHost, c->stream));
-    TV_HIP(c, hipEventRecord(c->ev_call1, c->stream));
-    TV_HIP(c, hipEventSynchronize(c->ev_call1));
-    if (reordered)
-        for (uint64_t i = 0; i < m; i++)
-            if (origin[i] >= 0) ok_out[origin[i]] = ok_launch[i];
+    for (uint64_t i = 0; i < m; i++)
+        if (origin[i] >= 0) ok_out[origin[i]] = ok_launch[i];
     if (c->any_file_bad)  // pieces file staging could not read (recover_segment) are 0 here too
         for (uint64_t k = 0; k < n; k++)
-            if (get_bit(c->file_bad.data(), pieces[k] - c->first)) ok_out[k] = 0;
+            if (get_bit(c->file_bad.data(), local[k])) ok_out[k] = 0;
+    if (c->slots)  // a listed piece's slot is free again (a failed piece is staged anew when it is re-downloaded)
+        for (uint64_t k = 0; k < n; k++) {
+            auto it = c->slot_of.find(local[k]);
+            if (it == c->slot_of.end()) continue;
+            c->slot_free.push_back(it->second);
+            c->slot_of.erase(it);
+        }
     c->last_kernel = kernel;
-    c->last_launches = 1;
+    c->last_launches = m ? 1 : 0;
+    if (!m) {
+        c->kernel_ms = c->total_ms = 0.f;
+        return TV_OK;
+    }
     return finish_timing(c);
 }
 
@@ -1938,15 +2445,23 @@ int tv_hash(tv_ctx* c, uint8_t* digests_out) {
     if (rc) return rc;
     if (!digests_out && c->count) return fail(c, TV_ERR_ARG, "digests_out is NULL");
     if (!c->count) return TV_OK;
+    if (c->slots) return fail(c, TV_ERR_STATE, "tv_hash: a slot pool (TV_OPT_LIST_SLOTS) holds no shard");
     TV_HIP(c, hipSetDevice(c->device));
-    TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
-    const int kernel = choose_kernel(c);
-    TvPieces p = resident_launch(c);
-    p.avail64 = nullptr;
-    TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
-    rc = launch_resident(c, p, kernel, true);
-    if (rc) return rc;
-    TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
+    int kernel = 0;
+    if (c->win) {
+        rc = win_finalize(c);  // windowed: the windows were hashed into d_hash as they filled
+        if (rc) return rc;
+        kernel = c->last_kernel;
+    } else {
+        TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
+        kernel = choose_kernel(c);
+        TvPieces p = resident_launch(c);
+        p.avail64 = nullptr;
+        TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
+        rc = launch_resident(c, p, kernel, true);
+        if (rc) return rc;
+        TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
+    }
     std::vector<uint32_t> soa(5 * c->count);
     DrainGuard drain(c);  // declared after soa: drains before soa is freed, also on error paths
     TV_HIP(c, hipMemcpyAsync(soa.data(), c->d_hash, soa.size() * 4, hipMemcpyDeviceToHost, c->stream));
@@ -1959,7 +2474,7 @@ int tv_hash(tv_ctx* c, uint8_t* digests_out) {
             d[0] = (uint8_t)(v >> 24); d[1] = (uint8_t)(v >> 16); d[2] = (uint8_t)(v >> 8); d[3] = (uint8_t)v;
         }
     c->last_kernel = kernel;
-    c->last_launches = 1;
+    c->last_launches = c->win ? (int)c->win_launched : 1;
     return finish_timing(c);
 }
 
@@ -2143,7 +2658,7 @@ int tv_get_counter(tv_ctx* c, int key, uint64_t* value) {
         case TV_COUNTER_PAYLOAD_BYTES: *value = c->cap_payload; return TV_OK;
         case TV_COUNTER_DEVICE_BYTES:
             *value = c->cap_payload + c->cap_count * 3 * 5 * sizeof(uint32_t) + c->cap_words * 8 * 3 +
-                     2 * c->chunk_bytes + c->list_cap * 5;
+                     2 * c->chunk_bytes + c->list_cap * 9;
             return TV_OK;
         case TV_COUNTER_LAST_WORKGROUPS: *value = c->last_workgroups; return TV_OK;
         case TV_COUNTER_NUMA_NODE: *value = c->numa_node < 0 ? UINT64_MAX : (uint64_t)c->numa_node; return TV_OK;
@@ -2152,6 +2667,10 @@ int tv_get_counter(tv_ctx* c, int key, uint64_t* value) {
             *value = node < 0 ? UINT64_MAX : (uint64_t)node;
             return TV_OK;
         }
+        case TV_COUNTER_WINDOW_PIECES: *value = c->win ? c->win_n : 0; return TV_OK;
+        case TV_COUNTER_WINDOWS: *value = c->win_launched; return TV_OK;
+        case TV_COUNTER_BUDGET: *value = c->budget; return TV_OK;
+        case TV_COUNTER_SLOTS_USED: *value = c->slot_of.size(); return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown counter %d", key);
 }

@@ -38,6 +38,9 @@ struct TvPieces {
                              // the result (TV_OPT_TWIN_FILL)
     uint32_t fill_all;       // companions: 0 = every lane hashes the main workgroup's FIRST piece (the same
                              // instruction stream, 1/32 of the reads), 1 = its 32 pieces (TV_OPT_TWIN_FILL_READS)
+    const uint32_t* rows;    // list mode with a slot pool (TV_OPT_LIST_SLOTS): entry j's bytes are payload row
+                             // rows[j] (data + rows[j]*stride) while digests / length / availability stay those of
+                             // piece idx[j]; null = row idx[j]
 };
 
 // workgroups (optional): set to the launch's grid size, companions included.
@@ -46,3 +49,7 @@ hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_
 hipError_t tv_launch_verify_list(const TvPieces& p, int kernel, hipStream_t s, uint32_t* workgroups = nullptr);
 hipError_t tv_launch_fill(uint8_t* payload, uint64_t stride, uint64_t first, uint32_t n, uint64_t L,
                           uint64_t seed, hipStream_t s);
+// Windowed layouts: bit j of out64 (MSB-first bytes in 64-bit words, as the verify kernels write it) = the
+// digest hash[.][j] equals digests[.][j] ([5][dcount] SoA) and avail64 bit j (null: all); j < n, the rest 0.
+hipError_t tv_launch_compare(const uint32_t* hash, const uint32_t* digests, uint32_t dcount, uint32_t n,
+                             const uint64_t* avail64, uint64_t* out64, hipStream_t s);

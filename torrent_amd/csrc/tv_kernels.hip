@@ -328,7 +328,9 @@ __device__ __forceinline__ void split_group(const TvPieces& p, uint32_t wgi, uin
                             : last_grp ? wave_geom_flags(p, true, true) : wave_geom(p, wg0, span);
     const uint64_t len = lane_len(p, jj);
     const uint32_t nb = (uint32_t)nblocks(len);
-    const uint8_t* piece = p.data + (uint64_t)jj * p.stride - p.data_off;
+    // (list mode over a slot pool: the entry's bytes sit in payload row rows[jl], TV_OPT_LIST_SLOTS)
+    const uint32_t row = (LIST && p.rows) ? p.rows[jl] : jj;
+    const uint8_t* piece = p.data + (uint64_t)row * p.stride - p.data_off;
     const uint32_t b0 = g.fast_begin, end = g.end, fast_end = g.fast_end;
     uint4* const pring = ring + pair * kBufs * (kRingWords / 4);
 
@@ -492,7 +494,8 @@ __global__ __launch_bounds__(64 * kTwinWaves[SHAPE]) void tv_twin_kernel(TvPiece
                             : last_grp ? wave_geom_flags(p, true, true) : wave_geom(p, wg0, span);
     const uint64_t len = lane_len(p, jj);
     const uint32_t nb = (uint32_t)nblocks(len);
-    const uint8_t* piece = p.data + (uint64_t)jj * p.stride - p.data_off;
+    const uint32_t row = (LIST && p.rows) ? p.rows[jl] : jj;   // (slot pool: TV_OPT_LIST_SLOTS)
+    const uint8_t* piece = p.data + (uint64_t)row * p.stride - p.data_off;
     const uint32_t b0 = g.fast_begin, end = g.end, fast_end = g.fast_end;
     const uint32_t lds_lane = (uint32_t)(uintptr_t)(void*)ring + half * 1024u + lane * 16u;
 
@@ -566,12 +569,13 @@ __global__ __launch_bounds__(256) void tv_list_kernel(TvPieces p) {
     const uint32_t j0 = blockIdx.x * 256u + wave * 64u;
     if (j0 >= p.n) return;
     const uint32_t j = j0 + (threadIdx.x & 63u);
-    const uint32_t jj = p.idx[j < p.n ? j : p.n - 1];
+    const uint32_t jl = j < p.n ? j : p.n - 1;
+    const uint32_t jj = p.idx[jl];
     const bool is_last = jj == p.last_idx;
     const WaveGeom g = wave_geom_flags(p, __ballot(is_last) != 0, __ballot(!is_last) == 0);
     const uint64_t len = is_last ? p.last_len : p.L;
     const uint32_t nb = (uint32_t)nblocks(len);
-    const uint8_t* piece = p.data + (uint64_t)jj * p.stride;
+    const uint8_t* piece = p.data + (uint64_t)(p.rows ? p.rows[jl] : jj) * p.stride;   // (slot pool)
     uint32_t h[5];
     sha1_iv(h);
     uint32_t b = 0, w[16];
@@ -637,6 +641,27 @@ __global__ __launch_bounds__(256) void tv_fill_bytes_kernel(uint8_t* payload, ui
         const uint64_t j = g / L, k = g - j * L;
         const uint64_t o = (first + j) * L + k;
         payload[j * stride + k] = (uint8_t)(splitmix64(seed, o >> 3) >> (8 * (o & 7)));
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// windowed layouts (tv_api.hip): the windows are hashed (HASH kernels into the shard's digest rows) as they
+// fill, and tv_verify compares the whole shard at the end -- 40 B read per piece, one word written per 64.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void tv_compare_kernel(const uint32_t* hash, const uint32_t* digests,
+                                                         uint32_t dcount, uint32_t n, const uint64_t* avail64,
+                                                         uint64_t* out64) {
+    const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+    bool ok = j < n;
+    if (ok) {
+#pragma unroll
+        for (int k = 0; k < 5; k++) ok &= hash[(uint64_t)k * dcount + j] == digests[(uint64_t)k * dcount + j];
+    }
+    const uint64_t mask = __ballot(ok);
+    if ((threadIdx.x & 63u) == 0) {   // lane 0 of the wave: pieces j .. j + 63, word j >> 6
+        uint64_t bits = __builtin_bswap64(__builtin_bitreverse64(mask));   // ballot bit l -> MSB-first bytes
+        if (avail64) bits &= avail64[j >> 6];
+        out64[j >> 6] = bits;
     }
 }
 
@@ -718,5 +743,12 @@ hipError_t tv_launch_fill(uint8_t* payload, uint64_t stride, uint64_t first, uin
     const unsigned grid = 256 * 32;
     if (L % 8 == 0) hipLaunchKernelGGL(tv_fill_words_kernel, dim3(grid), dim3(256), 0, s, payload, stride, first, n, L, seed);
     else hipLaunchKernelGGL(tv_fill_bytes_kernel, dim3(grid), dim3(256), 0, s, payload, stride, first, n, L, seed);
+    return hipGetLastError();
+}
+
+hipError_t tv_launch_compare(const uint32_t* hash, const uint32_t* digests, uint32_t dcount, uint32_t n,
+                             const uint64_t* avail64, uint64_t* out64, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(tv_compare_kernel, dim3((n + 255) / 256), dim3(256), 0, s, hash, digests, dcount, n, avail64, out64);
     return hipGetLastError();
 }

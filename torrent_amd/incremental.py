@@ -14,6 +14,11 @@ A completed piece's bytes are staged into HBM as soon as its last block arrives;
 every pending piece in one list launch.  A piece that fails verification is forgotten (its blocks
 may be received again), as a client would re-request it.
 
+Device memory is bounded by the pieces AWAITING verification, not by the torrent: the context is a slot
+pool of K = `slots` pieces (TV_OPT_LIST_SLOTS; default the flush count, 4,096), a completed piece takes a
+slot when it is staged and gives it back when its flush returns, and when all K slots are taken the next
+completed piece first flushes the pending ones.  A 200 GiB torrent of 4 MiB pieces holds K x 4 MiB of HBM.
+
 Flush policy.  A list flush costs about one piece's serial SHA-1 whatever the list length, ~0.73 us per
 64-B block: 3.0 ms for 256 KiB pieces, whether 1 or 4,096 of them (3.00 / 3.01 / 3.15 ms for 1 / 64 /
 4,096; profiles/r02/latency_twin.json, r03 latency).  Flushing per piece therefore costs ~3 ms of GPU time
@@ -48,7 +53,7 @@ def flush_cost_ms(piece_len: int) -> float:
 class IncrementalVerifier:
     def __init__(self, info: InfoDict, storage=None, device: int = 0,
                  shard: Optional[Tuple[int, int]] = None, flush_pieces=_AUTO, flush_age_ms=_AUTO,
-                 on_verified: Optional[Callable[[int, bool], None]] = None):
+                 on_verified: Optional[Callable[[int, bool], None]] = None, slots: Optional[int] = None):
         self.info = info
         self.storage = storage
         self.flush_pieces = DEFAULT_FLUSH_PIECES if flush_pieces is _AUTO else flush_pieces
@@ -60,7 +65,14 @@ class IncrementalVerifier:
         self._results: List[Tuple[int, bool]] = []   # automatic flushes' results not yet handed out
         P = info.n_pieces
         self.first, self.count = shard if shard is not None else (0, P)
+        # the slot pool: K pieces of HBM awaiting verification (at least the count bound, so it never forces
+        # a flush the policy would not make)
+        if slots is None:
+            slots = self.flush_pieces if isinstance(self.flush_pieces, int) else DEFAULT_FLUSH_PIECES
+        self.slots = max(1, min(int(slots), max(1, self.count)))
+        self.forced_flushes = 0
         self.ctx = _native.Context(device)
+        self.ctx.set_option(_native.TV_OPT_LIST_SLOTS, self.slots)
         self.ctx.set_layout(info.length, info.piece_length, P, self.first, self.count)
         self.ctx.set_digests(info.pieces_raw)
         self.bitfield = bytearray((P + 7) // 8)        # torrent.ts:60
@@ -99,6 +111,9 @@ class IncrementalVerifier:
         blocks.add(msg.offset // BLOCK_SIZE)
         done = False
         if len(blocks) == self._blocks_in(i):
+            if len(self._pending) >= self.slots:          # every slot awaits a flush: make room
+                self.forced_flushes += 1
+                self._deliver(self._flush_pending())
             self.ctx.stage(i * self.info.piece_length, buf)
             del self._bufs[i], self._have_blocks[i]
             if not self._pending:
@@ -118,15 +133,17 @@ class IncrementalVerifier:
         return (self.flush_age_ms is not None and
                 (time.monotonic() - self._oldest) * 1e3 >= self.flush_age_ms)
 
+    def _deliver(self, res: List[Tuple[int, bool]]) -> None:
+        if self.on_verified is not None:
+            for i, ok in res:
+                self.on_verified(i, ok)
+        else:
+            self._results.extend(res)
+
     def _auto_flush(self) -> None:
         if self.due():
             self.auto_flushes += 1
-            res = self._flush_pending()
-            if self.on_verified is not None:
-                for i, ok in res:
-                    self.on_verified(i, ok)
-            else:
-                self._results.extend(res)
+            self._deliver(self._flush_pending())
 
     def poll(self) -> List[Tuple[int, bool]]:
         """For a client's event loop: flush if the policy says so, and hand out every result the automatic
@@ -153,6 +170,10 @@ class IncrementalVerifier:
         after those of earlier automatic flushes not yet handed out (none when on_verified is set)."""
         out, self._results = self._results, []
         return out + self._flush_pending()
+
+    def device_payload_bytes(self) -> int:
+        """HBM the verifier's payload holds (TV_COUNTER_PAYLOAD_BYTES): the K slots, whatever the torrent."""
+        return self.ctx.counter(_native.TV_COUNTER_PAYLOAD_BYTES)
 
     def close(self) -> None:
         self.ctx.close()

@@ -14,6 +14,10 @@ The SHA-1 work runs in libtorrent_verify.so (HIP, gfx950): the bytes are staged 
 one kernel verifies every piece (one lane per piece).  There is no CPU fallback: without the
 library or a GPU these functions raise.
 
+Device memory.  The bulk calls take `budget` (bytes of HBM the payload may use per device; None = the
+GPU's free memory less a margin).  A shard larger than it is verified in windows of pieces that fit, each
+hashed while the next one stages (tv_set_layout's windowed layout): no torrent is too large for a GPU.
+
 Public API (names follow the reference's camelCase surface, snake_cased):
     verify_pieces(info, storage, devices=None) -> bytearray         (verifyPieces)
     verify_piece(info, index, data) -> bool                         (verifyPiece)
@@ -102,7 +106,9 @@ def context_counters() -> dict:
         with lock:
             out[key] = {name: ctx.counter(k) for name, k in (
                 ("payload_allocs", _native.TV_COUNTER_PAYLOAD_ALLOCS), ("device_allocs", _native.TV_COUNTER_DEVICE_ALLOCS),
-                ("payload_bytes", _native.TV_COUNTER_PAYLOAD_BYTES), ("device_bytes", _native.TV_COUNTER_DEVICE_BYTES))}
+                ("payload_bytes", _native.TV_COUNTER_PAYLOAD_BYTES), ("device_bytes", _native.TV_COUNTER_DEVICE_BYTES),
+                ("window_pieces", _native.TV_COUNTER_WINDOW_PIECES), ("windows", _native.TV_COUNTER_WINDOWS),
+                ("budget", _native.TV_COUNTER_BUDGET))}
     return out
 
 
@@ -125,6 +131,13 @@ def _devices(devices) -> List[int]:
     return list(devices)
 
 
+def _layout(ctx, info_or_len, L: int, P: int, first: int, count: int, budget: Optional[int]) -> None:
+    """set_layout with this call's device budget (the contexts are cached: every call sets its own)."""
+    ctx.set_option(_native.TV_OPT_RESIDENT_BUDGET, int(budget or 0))
+    total = info_or_len if isinstance(info_or_len, int) else info_or_len.length
+    ctx.set_layout(total, L, P, first, count)
+
+
 def _run_shards(devs: List[int], n_pieces: int, fn):
     """fn(ctx, first, count) for each shard, one thread per shard (ctypes releases the GIL)."""
     ranges = shard_ranges(n_pieces, len(devs))
@@ -142,18 +155,21 @@ def _run_shards(devs: List[int], n_pieces: int, fn):
         return ranges, [f.result() for f in futs]
 
 
-def verify_pieces(info: InfoDict, storage, devices=None, threads: int = 16) -> bytearray:
+def verify_pieces(info: InfoDict, storage, devices=None, threads: int = 16,
+                  budget: Optional[int] = None) -> bytearray:
     """verifyPieces(info, storage): have-bitfield of every piece read through `storage`
     (a torrent_amd.storage.Storage, i.e. the reference's Storage over any StorageMethod).  The gets
     of a batch are in flight together on `threads` threads, as ts/verify.ts keeps them outstanding
-    with Promise.all (make_torrent.ts:96,111 does the same); threads=1 reads them one by one."""
+    with Promise.all (make_torrent.ts:96,111 does the same); threads=1 reads them one by one.
+    Reads and staging overlap: batch k + 1 is read (into the other of two buffers) while batch k is
+    copied to HBM (and, on a windowed layout, while the windows before it hash)."""
     P, L = info.n_pieces, info.piece_length
 
     def shard(ctx, first: int, count: int) -> bytes:
-        ctx.set_layout(info.length, L, P, first, count)
+        _layout(ctx, info, L, P, first, count, budget)
         ctx.set_digests(info.pieces_raw)
         avail = bytearray((count + 7) // 8)
-        per_batch = max(1, _STAGE_BATCH_BYTES // max(1, L))
+        per_batch = max(1, min(count, _STAGE_BATCH_BYTES // max(1, L)))
 
         def get(i: int):
             data = storage.get(i * L, piece_length(i, info))  # storage.ts:50-65; None => bit 0
@@ -161,21 +177,33 @@ def verify_pieces(info: InfoDict, storage, devices=None, threads: int = 16) -> b
             # as in verify_stream -- it must not shift the batch buffer's later pieces)
             return data if data is not None and len(data) == piece_length(i, info) else None
 
-        with ThreadPoolExecutor(max(1, threads)) as pool:
-            j = 0
-            while j < count:
-                k = min(per_batch, count - j)
-                buf = bytearray(k * L)
-                hi = 0
-                for q, data in enumerate(pool.map(get, range(first + j, first + j + k))):
-                    if data is None:
-                        continue
-                    buf[q * L:q * L + len(data)] = data
-                    hi = q * L + len(data)
-                    _set_bit(avail, j + q)
-                if hi:
-                    ctx.stage((first + j) * L, memoryview(buf)[:hi])
-                j += k
+        bufs = [bytearray(per_batch * L)]
+        with ThreadPoolExecutor(max(1, threads)) as pool, ThreadPoolExecutor(1) as stager:
+            staging = None              # the previous batch's stage (it reads the other buffer)
+            j, b = 0, 0
+            try:
+                while j < count:
+                    k = min(per_batch, count - j)
+                    if b == len(bufs):
+                        bufs.append(bytearray(per_batch * L))
+                    buf = bufs[b]       # its last stage (two batches ago) finished before `staging` began
+                    hi = 0
+                    for q, data in enumerate(pool.map(get, range(first + j, first + j + k))):
+                        if data is None:
+                            continue    # (the stale bytes left in the buffer there are never a readable piece)
+                        buf[q * L:q * L + len(data)] = data
+                        hi = q * L + len(data)
+                        _set_bit(avail, j + q)
+                    if staging is not None:
+                        staging.result()
+                        staging = None
+                    if hi:
+                        staging = stager.submit(ctx.stage, (first + j) * L, memoryview(buf)[:hi])
+                    j += k
+                    b ^= 1
+            finally:
+                if staging is not None:
+                    staging.result()
         return ctx.verify(avail)
 
     if P == 0:
@@ -185,10 +213,11 @@ def verify_pieces(info: InfoDict, storage, devices=None, threads: int = 16) -> b
 
 
 def verify_payload(info: InfoDict, payload, devices=None, resident: bool = True,
-                   avail: Optional[bytes] = None) -> bytearray:
+                   avail: Optional[bytes] = None, budget: Optional[int] = None) -> bytearray:
     """Verify a linear payload already in host memory (the concatenation of info.files in
-    order).  resident=True stages it into HBM and verifies there; resident=False streams it
-    column by column over PCIe (tv_verify_host, the end-to-end resume-check path)."""
+    order).  resident=True stages it into HBM and verifies there (in windows when the shard exceeds
+    `budget`); resident=False streams it column by column over PCIe (tv_verify_host, the end-to-end
+    resume-check path)."""
     P, L = info.n_pieces, info.piece_length
     mv = memoryview(payload).cast("B")
 
@@ -196,7 +225,7 @@ def verify_payload(info: InfoDict, payload, devices=None, resident: bool = True,
         if not resident:        # the streamed path needs no resident payload (tv_verify_host)
             ctx.set_option(_native.TV_OPT_RESIDENT, 0)
         try:
-            ctx.set_layout(info.length, L, P, first, count)
+            _layout(ctx, info, L, P, first, count, budget)
         finally:
             ctx.set_option(_native.TV_OPT_RESIDENT, 1)
         ctx.set_digests(info.pieces_raw)
@@ -299,7 +328,8 @@ def verify_stream(info: InfoDict, read, devices=None, avail: Optional[bytes] = N
 
 
 def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: int = 16,
-                 direct_min: Optional[int] = None, status_out: Optional[list] = None) -> bytearray:
+                 direct_min: Optional[int] = None, status_out: Optional[list] = None,
+                 open_rw: bool = True) -> bytearray:
     """Stage the shard's pieces from files into HBM and return the shard's readability bits.
 
     The shard's linear range is mapped to file segments exactly as Storage.get maps it
@@ -310,7 +340,9 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
     (storage.ts:50-65,150-172): a piece with a byte in a missing, unopenable or too-short part of a file,
     and a piece whose zero-length segment (storage.ts:109-110) names a path fsStorage.get could not open;
     a short file's pieces before its end stay readable.  Missing files are never created.  `status_out`, if
-    given, receives the per-segment statuses (hash_files raises on any failure)."""
+    given, receives the per-segment statuses (hash_files raises on any failure).  open_rw: files are opened
+    read + write as fsStorage.get opens them (storage.ts:28-32,158); False opens them read-only, as
+    make_torrent.ts:78 opens its sources (hash_files)."""
     L = info.piece_length
     avail = bytearray(b"\xff" * ((count + 7) // 8))
     if count % 8:
@@ -348,6 +380,7 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
         return avail
     paths = storage.file_paths()
     ctx.set_option(_native.TV_OPT_FILE_THREADS, max(1, threads))
+    ctx.set_option(_native.TV_OPT_OPEN_RW, 1 if open_rw else 0)
     ctx.set_option(_native.TV_OPT_FILE_DIRECT_MIN, _DIRECT_MIN_BYTES if direct_min is None else direct_min)
     # a failed segment's pieces are marked inside the library (tv_verify reports them 0): from the piece
     # holding its first unreadable byte on, as Storage.get reads piece by piece; the statuses are informational
@@ -358,7 +391,7 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
 
 
 def verify_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
-                 direct_min: Optional[int] = None) -> bytearray:
+                 direct_min: Optional[int] = None, budget: Optional[int] = None) -> bytearray:
     """Resume check from disk: the have-bitfield of the files under dir_path,
     laid out as Storage(fs_storage, info, dir_path) maps them (storage.ts:89-137; single-file
     torrents are [dir, name], multi-file [dir, *path] without info.name).
@@ -372,7 +405,7 @@ def verify_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
     storage = Storage(fs_storage, info, dir_path)
 
     def shard(ctx, first: int, count: int) -> bytes:
-        ctx.set_layout(info.length, L, P, first, count)
+        _layout(ctx, info, L, P, first, count, budget)
         ctx.set_digests(info.pieces_raw)
         if count == 0:
             return b""
@@ -385,9 +418,10 @@ def verify_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
 
 
 def hash_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
-               direct_min: Optional[int] = None) -> bytes:
+               direct_min: Optional[int] = None, budget: Optional[int] = None) -> bytes:
     """Creation mode from disk: the `pieces` string of the files info describes under dir_path
-    (info.pieces is ignored; only the geometry is used).  Raises if a file is missing or short."""
+    (info.pieces is ignored; only the geometry is used).  Raises if a file is missing or short.  Files are
+    opened read-only, as make_torrent.ts:78 opens its sources: the process need not be able to write them."""
     from .storage import Storage, fs_storage
 
     L = info.piece_length
@@ -395,11 +429,11 @@ def hash_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
     storage = Storage(fs_storage, info, dir_path)
 
     def shard(ctx, first: int, count: int) -> bytes:
-        ctx.set_layout(info.length, L, P, first, count)
+        _layout(ctx, info, L, P, first, count, budget)
         if count == 0:
             return b""
         status: list = []
-        avail = _files_shard(ctx, info, storage, first, count, threads, direct_min, status)
+        avail = _files_shard(ctx, info, storage, first, count, threads, direct_min, status, open_rw=False)
         full = bytearray(b"\xff" * ((count + 7) // 8))
         if count % 8:
             full[-1] = (0xFF00 >> (count % 8)) & 0xFF
@@ -422,13 +456,13 @@ def verify_piece(info: InfoDict, index: int, data) -> bool:
     if n != piece_length(index, info) or len(info.pieces[index]) != 20 or n == 0:
         return False
     with _context(0, _PIECE_SLOT) as ctx:      # its own context: never evicts a bulk call's payload
-        ctx.set_layout(n, n, 1, 0, 1)
+        _layout(ctx, n, n, 1, 0, 1, None)
         ctx.set_digests(bytes(info.pieces[index]))
         ctx.stage(0, data)
         return bool(ctx.verify()[0] & 0x80)
 
 
-def hash_pieces(payload, piece_length_: int, devices=None) -> bytes:
+def hash_pieces(payload, piece_length_: int, devices=None, budget: Optional[int] = None) -> bytes:
     """Creation mode: the `pieces` byte string for a linear payload (make_torrent.ts:147-173;
     multi-file payloads are the files concatenated in order, make_torrent.ts:62-113)."""
     mv = memoryview(payload).cast("B")
@@ -436,7 +470,7 @@ def hash_pieces(payload, piece_length_: int, devices=None) -> bytes:
     P = -(-total // piece_length_) if total else 0
 
     def shard(ctx, first: int, count: int) -> bytes:
-        ctx.set_layout(total, piece_length_, P, first, count)
+        _layout(ctx, total, piece_length_, P, first, count, budget)
         lo, hi = first * piece_length_, min(total, (first + count) * piece_length_)
         if hi > lo:
             ctx.stage(lo, mv[lo:hi])

@@ -66,7 +66,13 @@ export interface VerifyOptions {
   devices?: number[];
   /** pieces read through storage.get per staging batch */
   batchBytes?: number;
+  /** bytes of device memory the payload may take per device (default: the GPU's free memory less a margin); a
+   * shard larger than it is verified in windows of pieces that fit, each hashed while the next one stages */
+  budget?: number;
 }
+
+const TV_OPT_RESIDENT_BUDGET = 16;
+const TV_OPT_LIST_SLOTS = 17;
 
 type Lib = Deno.DynamicLibrary<typeof SYMBOLS>;
 let lib: Lib | null = null;
@@ -113,6 +119,13 @@ async function withContext<T>(l: Lib, device: number, slot: number, job: (ctx: D
   const run = entry.tail.then(() => job(entry.ctx));
   entry.tail = run.then(() => {}, () => {});
   return await run;
+}
+
+/** tv_set_layout under this call's device budget (contexts are cached: every call sets its own). */
+function setLayout(l: Lib, ctx: Deno.PointerValue, total: number, L: number, P: number, first: number, count: number,
+                   budget?: number): void {
+  check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_RESIDENT_BUDGET, BigInt(budget || 0)));
+  check(l, ctx, l.symbols.tv_set_layout(ctx, BigInt(total), BigInt(L), BigInt(P), BigInt(first), BigInt(count)));
 }
 
 /** Free every cached context (device payload, pinned ring); the next call creates new ones. */
@@ -170,7 +183,9 @@ async function eachLimited(n: number, fn: (q: number) => Promise<void>): Promise
  * verifyPieces(info, storage) -> have-bitfield (Uint8Array of ceil(P/8) bytes, MSB-first:
  * torrent.ts:53,60,147-149).  Piece i's bit is set iff storage.get(i*pieceLength, len_i) is
  * non-null (storage.ts:50-65) and its SHA-1 equals info.pieces[i].  Unreadable pieces are 0, not
- * errors (the reference swallows I/O failures into null); GPU / ABI failures throw Error.
+ * errors (the reference swallows I/O failures into null); GPU / ABI failures throw Error.  Reads and
+ * staging overlap: batch k + 1 is read into the other of two buffers while batch k's tv_stage (nonblocking)
+ * copies it to HBM.
  */
 export async function verifyPieces(
   info: InfoDict,
@@ -188,27 +203,39 @@ export async function verifyPieces(
   await Promise.all(shardRanges(P, devices.length).map(async ([first, count], s) => {
     if (count === 0) return;
     await withContext(l, devices[s], s, async (ctx) => {
-      check(l, ctx, l.symbols.tv_set_layout(ctx, BigInt(info.length), BigInt(L), BigInt(P), BigInt(first), BigInt(count)));
+      setLayout(l, ctx, info.length, L, P, first, count, opts.budget);
       check(l, ctx, l.symbols.tv_set_digests(ctx, ptr(raw), BigInt(raw.length)));
       const avail = new Uint8Array(Math.ceil(count / 8));
-      for (let j = 0; j < count; j += batch) {
-        const k = Math.min(batch, count - j);
-        const buf = new Uint8Array(k * L);
-        let hi = 0;
-        // READS_IN_FLIGHT reads outstanding at a time (make_torrent.ts:96,111 keeps its work in flight too, but
-        // each fsStorage.get is a Deno.open: a batch of 16 KiB pieces at once would hit EMFILE, which
-        // fsStorage.get turns into null -- a valid piece reported 0)
-        await eachLimited(k, async (q) => {
-          const n = pieceLength(first + j + q, info);
-          const bytes = await storage.get((first + j + q) * L, n);
-          // Storage.get returns exactly the length asked or null; any other length is unreadable too (as in
-          // verifyStream): a longer one would run into the next piece's place in the batch buffer
-          if (!bytes || bytes.length !== n) return;
-          buf.set(bytes, q * L);
-          hi = Math.max(hi, q * L + n);
-          avail[(j + q) >> 3] |= 128 >> ((j + q) % 8);
-        });
-        if (hi) check(l, ctx, await l.symbols.tv_stage(ctx, BigInt((first + j) * L), ptr(buf), BigInt(hi)));
+      const per = Math.min(batch, count);
+      const bufs: Uint8Array[] = [];
+      let staging: Promise<void> | null = null; // the previous batch's tv_stage (it reads the other buffer)
+      try {
+        for (let j = 0, b = 0; j < count; j += per, b ^= 1) {
+          const k = Math.min(per, count - j);
+          if (!bufs[b]) bufs[b] = new Uint8Array(per * L);
+          const buf = bufs[b]; // its last stage (two batches ago) settled before `staging` began
+          let hi = 0;
+          // READS_IN_FLIGHT reads outstanding at a time (make_torrent.ts:96,111 keeps its work in flight too, but
+          // each fsStorage.get is a Deno.open: a batch of 16 KiB pieces at once would hit EMFILE, which
+          // fsStorage.get turns into null -- a valid piece reported 0)
+          await eachLimited(k, async (q) => {
+            const n = pieceLength(first + j + q, info);
+            const bytes = await storage.get((first + j + q) * L, n);
+            // Storage.get returns exactly the length asked or null; any other length is unreadable too (as in
+            // verifyStream): a longer one would run into the next piece's place in the batch buffer
+            if (!bytes || bytes.length !== n) return; // (the stale bytes left there are never a readable piece)
+            buf.set(bytes, q * L);
+            hi = Math.max(hi, q * L + n);
+            avail[(j + q) >> 3] |= 128 >> ((j + q) % 8);
+          });
+          if (staging) await staging;
+          staging = null;
+          if (hi) {
+            staging = l.symbols.tv_stage(ctx, BigInt((first + j) * L), ptr(buf), BigInt(hi)).then((rc) => check(l, ctx, rc));
+          }
+        }
+      } finally {
+        if (staging) await staging;
       }
       const out = new Uint8Array(Math.ceil(count / 8));
       check(l, ctx, await l.symbols.tv_verify(ctx, ptr(avail), ptr(out)));
@@ -220,6 +247,7 @@ export async function verifyPieces(
 
 const TV_OPT_STREAM_CHUNK = 3;
 const TV_OPT_RESIDENT = 10;
+const TV_OPT_OPEN_RW = 18;
 
 /**
  * verifyStream(info, storage) -> have-bitfield: the end-to-end resume check through the library's
@@ -310,7 +338,8 @@ export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptio
   await Promise.all(shardRanges(P, devices.length).map(async ([first, count], s) => {
     if (count === 0) return;
     await withContext(l, devices[s], s, async (ctx) => {
-      check(l, ctx, l.symbols.tv_set_layout(ctx, BigInt(info.length), BigInt(L), BigInt(P), BigInt(first), BigInt(count)));
+      setLayout(l, ctx, info.length, L, P, first, count, opts.budget);
+      check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_OPEN_RW, 1n)); // fsStorage.get's read + write open
       check(l, ctx, l.symbols.tv_set_digests(ctx, ptr(raw), BigInt(raw.length)));
       const avail = new Uint8Array(Math.ceil(count / 8)).fill(0xff);
       if (count % 8) avail[avail.length - 1] = (0xff00 >> (count % 8)) & 0xff;
@@ -379,7 +408,7 @@ export async function verifyPiece(info: InfoDict, index: number, bytes: Uint8Arr
   // payload (tv_set_layout keeps an allocation only while the new geometry is at least half of it)
   return await withContext(l, (opts.devices || [0])[0], -1, async (ctx) => {
     const n = BigInt(bytes.length);
-    check(l, ctx, l.symbols.tv_set_layout(ctx, n, n, 1n, 0n, 1n)); // reuses the context's allocations
+    setLayout(l, ctx, bytes.length, bytes.length, 1, 0, 1); // reuses the context's allocations
     check(l, ctx, l.symbols.tv_set_digests(ctx, ptr(info.pieces[index]), 20n));
     check(l, ctx, await l.symbols.tv_stage(ctx, 0n, ptr(bytes), n));
     const out = new Uint8Array(1);
@@ -403,7 +432,7 @@ export async function hashPieces(payload: Uint8Array, pieceLength: number, opts:
   await Promise.all(shardRanges(P, devices.length).map(async ([first, count], s) => {
     if (count === 0) return;
     await withContext(l, devices[s], s, async (ctx) => {
-      check(l, ctx, l.symbols.tv_set_layout(ctx, BigInt(payload.length), BigInt(pieceLength), BigInt(P), BigInt(first), BigInt(count)));
+      setLayout(l, ctx, payload.length, pieceLength, P, first, count, opts.budget);
       const lo = first * pieceLength, hi = Math.min(payload.length, (first + count) * pieceLength);
       if (hi > lo) check(l, ctx, await l.symbols.tv_stage(ctx, BigInt(lo), ptr(payload.subarray(lo, hi)), BigInt(hi - lo)));
       const digests = new Uint8Array(20 * count);
@@ -436,11 +465,20 @@ export function flushCostMs(pieceLength: number): number {
  * storage.set); completed pieces are verified in ONE list launch (tv_verify_list) per flush, and their
  * have-bits set (torrent.ts:147-149).  The verifier flushes by itself when flushPieces are pending or the
  * oldest pending piece is flushAgeMs old (a timer is armed when the first piece becomes pending), so a
- * handler never pays a ~3 ms flush per piece.  Same behaviour as torrent_amd/incremental.py.
+ * handler never pays a ~3 ms flush per piece.  Device memory is a pool of `slots` pieces (TV_OPT_LIST_SLOTS;
+ * default flushPieces, else 4,096) -- the pieces awaiting verification, not the torrent -- and with every slot
+ * taken the next completed piece first flushes the pending ones.  `shard` limits the verifier to pieces
+ * [first, first + count) (first % 8 === 0) on opts.devices[0], as the Python verifier's shard.  The library
+ * calls (stages and flushes) run one at a time in order, so a flush() always returns the results of an
+ * automatic flush that was running when it was called.  Same behaviour as torrent_amd/incremental.py.
  */
 export class PieceVerifier {
   readonly bitfield: Uint8Array;
+  readonly first: number;
+  readonly count: number;
+  readonly slots: number;
   autoFlushes = 0;
+  forcedFlushes = 0;
   #l: Lib;
   #ctx: Deno.PointerValue;
   #bufs = new Map<number, { bytes: Uint8Array; blocks: Set<number> }>();
@@ -453,31 +491,52 @@ export class PieceVerifier {
   #flushPieces: number | null;
   #flushAgeMs: number | null;
   #onVerified?: (index: number, ok: boolean) => void;
-  #busy: Promise<unknown> = Promise.resolve();
+  #busy: Promise<unknown> = Promise.resolve(); // the verifier's library calls, one at a time, in order
   #timerError: unknown = null;   // a timer-driven flush that failed: rethrown by the next call
 
   readonly info: InfoDict;
 
-  constructor(info: InfoDict, opts: VerifyOptions & FlushPolicy = {}) {
+  constructor(info: InfoDict, opts: VerifyOptions & FlushPolicy & { shard?: [number, number]; slots?: number } = {}) {
     this.info = info;
     this.#l = load(opts.libPath);
     const P = info.pieces.length;
+    const [first, count] = opts.shard || [0, P];
+    if (!Number.isInteger(first) || !Number.isInteger(count) || first < 0 || count < 0 || first + count > P ||
+        (count > 0 && first % 8 !== 0)) {
+      throw new Error(`PieceVerifier: invalid shard [${first}, ${first} + ${count}) of ${P} pieces`);
+    }
+    this.first = first;
+    this.count = count;
+    this.#flushPieces = opts.flushPieces === undefined ? 4096 : opts.flushPieces;
+    this.#flushAgeMs = opts.flushAgeMs === undefined ? Math.max(5, 10 * flushCostMs(info.pieceLength)) : opts.flushAgeMs;
+    this.#onVerified = opts.onVerified;
+    const k = opts.slots !== undefined ? opts.slots : (this.#flushPieces !== null ? this.#flushPieces : 4096);
+    this.slots = Math.max(1, Math.min(Math.floor(k), Math.max(1, count)));
     const h = new BigUint64Array(1);
     check(this.#l, null, this.#l.symbols.tv_create(ptr(new Uint8Array(h.buffer)), (opts.devices || [0])[0]));
     this.#ctx = Deno.UnsafePointer.create(h[0]);
     const raw = piecesRaw(info);
-    check(this.#l, this.#ctx, this.#l.symbols.tv_set_layout(this.#ctx, BigInt(info.length), BigInt(info.pieceLength), BigInt(P), 0n, BigInt(P)));
+    check(this.#l, this.#ctx, this.#l.symbols.tv_set_option(this.#ctx, TV_OPT_LIST_SLOTS, BigInt(this.slots)));
+    check(this.#l, this.#ctx, this.#l.symbols.tv_set_layout(this.#ctx, BigInt(info.length), BigInt(info.pieceLength),
+                                                            BigInt(P), BigInt(first), BigInt(count)));
     check(this.#l, this.#ctx, this.#l.symbols.tv_set_digests(this.#ctx, ptr(raw), BigInt(raw.length)));
     this.bitfield = new Uint8Array(Math.ceil(P / 8));
-    this.#flushPieces = opts.flushPieces === undefined ? 4096 : opts.flushPieces;
-    this.#flushAgeMs = opts.flushAgeMs === undefined ? Math.max(5, 10 * flushCostMs(info.pieceLength)) : opts.flushAgeMs;
-    this.#onVerified = opts.onVerified;
+  }
+
+  /** `job` after every library call queued before it (stages and flushes run one at a time, in order). */
+  private _serial<T>(job: () => Promise<T>): Promise<T> {
+    const run = this.#busy.then(job);
+    this.#busy = run.catch(() => {});
+    return run;
   }
 
   /** One received block (already validated); true when it completed its piece. */
   async onBlock(index: number, offset: number, block: Uint8Array): Promise<boolean> {
     this._rethrow();
     await this._autoFlush();                                  // the age bound, checked on every block
+    if (index < this.first || index >= this.first + this.count) {
+      throw new Error(`PieceVerifier: piece ${index} is outside this verifier's shard`);
+    }
     if (this.bitfield[index >> 3] & (128 >> (index % 8))) return false;
     if (this.#pendingSet.has(index)) return false; // complete, waiting for a flush: ignore re-sends
     if (this.#staging.has(index)) return false;    // its completing block is being staged right now
@@ -491,24 +550,32 @@ export class PieceVerifier {
     if (e.blocks.size < Math.ceil(len / 16384)) return false;
     // a re-sent block of this piece arriving while the stage is pending must not stage (and queue) it twice
     this.#staging.add(index);
+    const bytes = e.bytes;
     try {
-      check(this.#l, this.#ctx, await this.#l.symbols.tv_stage(this.#ctx, BigInt(index * this.info.pieceLength), ptr(e.bytes), BigInt(len)));
+      await this._serial(async () => {
+        if (this.#pending.length >= this.slots) {            // every slot awaits a flush: make room
+          this.forcedFlushes++;
+          this._deliver(await this._flushLocked());
+        }
+        check(this.#l, this.#ctx, await this.#l.symbols.tv_stage(this.#ctx, BigInt(index * this.info.pieceLength), ptr(bytes), BigInt(len)));
+        if (this.#pending.length === 0) {
+          this.#oldest = performance.now();
+          // the age bound also holds when no further block arrives
+          if (this.#flushAgeMs !== null) this._armTimer(this.#flushAgeMs);
+        }
+        this.#pending.push(index);
+        this.#pendingSet.add(index);
+      });
     } finally {
       this.#staging.delete(index);
     }
     this.#bufs.delete(index);
-    if (this.#pending.length === 0) {
-      this.#oldest = performance.now();
-      // the age bound also holds when no further block arrives
-      if (this.#flushAgeMs !== null) this._armTimer(this.#flushAgeMs);
-    }
-    this.#pending.push(index);
-    this.#pendingSet.add(index);
     await this._autoFlush();                                  // the count bound
     return true;
   }
 
   private _armTimer(delayMs: number): void {
+    clearTimeout(this.#timer);
     this.#timer = setTimeout(() => {
       if (this.#pending.length === 0) return;
       // timers are millisecond-granular and may fire a little before the oldest piece is flushAgeMs old:
@@ -539,40 +606,54 @@ export class PieceVerifier {
     return this.#flushAgeMs !== null && performance.now() - this.#oldest >= this.#flushAgeMs;
   }
 
-  private async _autoFlush(): Promise<void> {
-    if (!this.due()) return;
-    this.autoFlushes++;
-    const res = await this._flushPending();
+  /** Results of an automatic or forced flush: to onVerified, else kept for flush() / poll(). */
+  private _deliver(res: [number, boolean][]): void {
     if (this.#onVerified) for (const [i, ok] of res) this.#onVerified(i, ok);
     else this.#results.push(...res);
   }
 
-  private async _flushPending(): Promise<[number, boolean][]> {
-    // one list launch at a time on the verifier's context (the timer and onBlock may both flush)
-    const run = this.#busy.then(async () => {
-      if (this.#pending.length === 0) return [] as [number, boolean][];
-      clearTimeout(this.#timer);
-      const pending = this.#pending;
-      this.#pending = [];
-      this.#pendingSet.clear();
-      const idx = BigUint64Array.from(pending.map(BigInt));
-      const ok = new Uint8Array(idx.length);
-      check(this.#l, this.#ctx, await this.#l.symbols.tv_verify_list(this.#ctx, ptr(new Uint8Array(idx.buffer)), BigInt(idx.length), ptr(ok)));
-      const out: [number, boolean][] = pending.map((i, k) => [i, ok[k] === 1]);
-      for (const [i, good] of out) if (good) this.bitfield[i >> 3] |= 128 >> (i % 8);
-      return out;
-    });
-    this.#busy = run.catch(() => {});
-    return await run;
+  private async _autoFlush(): Promise<void> {
+    if (!this.due()) return;
+    this.autoFlushes++;
+    await this._serial(async () => this._deliver(await this._flushLocked()));
+  }
+
+  /** One list launch over every pending piece (inside a _serial job); frees their slots. */
+  private async _flushLocked(): Promise<[number, boolean][]> {
+    if (this.#pending.length === 0) return [];
+    clearTimeout(this.#timer);
+    const pending = this.#pending;
+    this.#pending = [];
+    this.#pendingSet.clear();
+    const idx = BigUint64Array.from(pending.map(BigInt));
+    const ok = new Uint8Array(idx.length);
+    check(this.#l, this.#ctx, await this.#l.symbols.tv_verify_list(this.#ctx, ptr(new Uint8Array(idx.buffer)), BigInt(idx.length), ptr(ok)));
+    const out: [number, boolean][] = pending.map((i, k) => [i, ok[k] === 1]);
+    for (const [i, good] of out) if (good) this.bitfield[i >> 3] |= 128 >> (i % 8);
+    return out;
   }
 
   /** Verify all completed pieces in one launch; returns [index, ok] (after the results of automatic
-   * flushes not yet handed out) and sets the have-bits. */
+   * flushes not yet handed out, including one still running when flush() was called) and sets the have-bits. */
   async flush(): Promise<[number, boolean][]> {
     this._rethrow();
-    const earlier = this.#results;
-    this.#results = [];
-    return [...earlier, ...await this._flushPending()];
+    return await this._serial(async () => {
+      const earlier = this.#results;
+      this.#results = [];
+      return [...earlier, ...await this._flushLocked()];
+    });
+  }
+
+  /** For a client's event loop: flush if the policy says so, and hand out every result the automatic and
+   * forced flushes have not yet returned (none when onVerified is set).  As the Python verifier's poll(). */
+  async poll(): Promise<[number, boolean][]> {
+    this._rethrow();
+    await this._autoFlush();
+    return await this._serial(async () => {
+      const out = this.#results;
+      this.#results = [];
+      return out;
+    });
   }
 
   close(): void {
