@@ -206,7 +206,8 @@ def test_failed_segment_marks_last_until_the_next_layout(native, tmp_path):
     """A file segment the library could not read whole marks, inside the library, exactly the pieces
     Storage.get would return null for: a 10-piece file 3 pieces + 5 bytes long keeps pieces 0-2 (staged from
     the file's prefix) and loses 3-9.  The marks hold for tv_verify (no availability from the host) and for
-    tv_verify_list, survive a correct tv_stage of the same bytes, and end with the next tv_set_layout."""
+    tv_verify_list, end for the pieces a later call stages whole (the bytes were repaired: ADVICE r03), and
+    all end with the next tv_set_layout."""
     L, P = 4096, 10
     payload = bytes((k * 29 + 7) & 0xFF for k in range(L * P))
     digests = b"".join(hashlib.sha1(payload[i * L:(i + 1) * L]).digest() for i in range(P))
@@ -220,10 +221,10 @@ def test_failed_segment_marks_last_until_the_next_layout(native, tmp_path):
         want = [1, 1, 1] + [0] * 7
         assert _bits(ctx.verify(), P) == want
         assert list(ctx.verify_list(list(range(P)))) == want
-        ctx.stage(0, payload)                                       # marks are not undone by staging
-        assert _bits(ctx.verify(), P) == want
+        ctx.stage(0, payload[:5 * L + 7])                           # pieces 0-4 staged whole: unmarked
+        assert _bits(ctx.verify(), P) == [1] * 5 + [0] * 5
         assert not ctx.stage_file(str(tmp_path / "absent.bin"), 0, 0, L)   # a missing file marks piece 0
-        assert _bits(ctx.verify(), P) == [0, 1, 1] + [0] * 7
+        assert _bits(ctx.verify(), P) == [0] + [1] * 4 + [0] * 5
         ctx.set_layout(L * P, L, P)                                 # a new layout clears them
         ctx.set_digests(digests)
         ctx.stage(0, payload)

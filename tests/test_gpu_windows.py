@@ -30,7 +30,7 @@ def _budget(L, pieces_per_window):
 def _check_windowed(budget, expect_windowed=True):
     """Every cached bulk context (slot >= 0) last laid out under `budget` holds at most `budget` bytes of
     payload, and (expect_windowed) at least one of them is windowed."""
-    from torrent_amd import context_counters
+    from torrent_amd.verify import context_counters
     seen = [c for (dev, slot), c in context_counters().items() if slot >= 0 and c["budget"] == budget]
     assert seen
     for c in seen:

@@ -1672,7 +1672,9 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
             c->win_buf_bytes = W * c->stride + kSlack;
             need_payload = bufs * c->win_buf_bytes;
         }
-        if (!need_payload || !reuse_fits(need_payload, c->cap_payload)) free_payload(c);
+        // (an allocation larger than the budget is never kept: the budget bounds what the ctx holds)
+        if (!need_payload || !reuse_fits(need_payload, c->cap_payload) || (budget && c->cap_payload > budget))
+            free_payload(c);
         if (!need_payload || c->d_payload) break;
         const hipError_t e = hipMalloc((void**)&c->d_payload, need_payload);
         if (e == hipSuccess) {
