@@ -272,6 +272,11 @@ def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: b
     try:
         ctx.set_option(_native.TV_OPT_KERNEL, kernel_opt)
         ctx.set_layout(total, L, P, first, count)
+        # a resident step re-hashes the whole shard: the layout must hold it whole (a windowed layout, for a
+        # shard above the device budget, would hash once per pass and make repeated verifies compares)
+        if ctx.counter(_native.TV_COUNTER_WINDOW_PIECES):
+            raise RuntimeError(f"{workload}: the shard does not fit the device budget "
+                               f"({ctx.counter(_native.TV_COUNTER_BUDGET)} B); the resident bench needs it whole")
         ctx.fill_synthetic(seed)
         creation_exact = ctx.hash() == dig            # creation mode (make_torrent.ts:28-31) at full size
         d2 = bytearray(dig)

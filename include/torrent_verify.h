@@ -218,7 +218,8 @@ int tv_hash(tv_ctx *ctx, uint8_t *digests_out);
  *   tv_stream_end(ctx, bitfield_out)     ceil(shard_count/8) bytes, as tv_verify
  *
  * A request covers `rows` consecutive pieces starting at GLOBAL piece `piece`, and bytes
- * [offset, offset + width) of each (piece-relative; every request of one column has the same offset).
+ * [offset, offset + width) of each (piece-relative; every request of one column has the same offset; with
+ * TV_OPT_STREAM_ROWS the offset is 0 and the width the piece length).
  * Row q holds the LINEAR bytes [(piece+q)*piece_length + offset, ...) of length
  * row_bytes(q) = min(width, piece_len(piece+q) - offset), which is `width` for every row except
  * the short last piece's (0 past its end; piece.ts:16-19).  One request is outstanding at a time.  A piece whose bytes cannot be read
@@ -306,6 +307,13 @@ int tv_host_unregister(void *ptr);
                                      opens every segment (storage.ts:28-32,158; an unwritable file reads as null);
                                      0 = read-only, as make_torrent.ts:78 opens its sources (creation mode from files
                                      the process may not write).  Zero-length segments' open check follows it */
+#define TV_OPT_STREAM_ROWS 19     /* tv_stream_* request rows: 0 (default) = columns of TV_OPT_STREAM_CHUNK bytes of
+                                     every shard piece (one launch per column over the whole shard); 1 = whole
+                                     pieces (when a piece fits one ring slot), in windows of up to 4 GiB of pieces
+                                     per chunk buffer (a multiple of 64 pieces; TV_OPT_RESIDENT_BUDGET / 2 if set
+                                     and smaller), one launch per window: one Storage.get per piece for a reader
+                                     that opens a file per call (fsStorage.get, storage.ts:149-172).  Set it
+                                     before tv_stream_begin (TV_ERR_STATE during a stream) */
 int tv_set_option(tv_ctx *ctx, int key, int64_t value);
 int tv_get_option(tv_ctx *ctx, int key, int64_t *value);
 

@@ -252,3 +252,55 @@ def test_stream_state_errors_and_abort(native, oracle):
         ctx.stream_begin()
         assert ctx.stream_next().rows == 0
         assert ctx.stream_end() == b""
+
+
+@pytest.mark.parametrize("pieces_per_window", [64, 128])
+def test_stream_whole_piece_rows_in_windows(native, oracle, pieces_per_window):
+    """TV_OPT_STREAM_ROWS: every request row is a whole piece (offset 0, width = the piece length), so a
+    Storage reader is asked once per piece; the shard is hashed in windows of 64 / 128 pieces (the budget
+    halves bound each chunk buffer), 300 pieces of 16 KiB + 5 B (odd length) with a short last piece and
+    unreadable pieces: bit-exact against the oracle, and the reads equal the pieces."""
+    from torrent_amd import make_info, verify_stream
+    L, P = 16384 + 5, 300
+    total = L * (P - 1) + 777
+    payload = bytes(oracle.synth_fill(41, 0, total))
+    pieces = bytearray(oracle.hash_pieces(bytearray(payload), total, L, P))
+    for i in (3, 64, 200):
+        pieces[20 * i] ^= 1
+    expect = _bits(oracle.verify_linear(bytearray(payload), total, L, bytes(pieces)), P)
+    pitch = -(-L // 64) * 64 + 256
+    with native.Context(0) as ctx:
+        ctx.set_option(native.TV_OPT_RESIDENT, 0)
+        ctx.set_option(native.TV_OPT_STREAM_ROWS, 1)
+        ctx.set_option(native.TV_OPT_RESIDENT_BUDGET, 2 * pieces_per_window * pitch + 2 * 256)
+        ctx.set_layout(total, L, P)
+        ctx.set_digests(bytes(pieces))
+        seen, unreadable = [], {10, 299, 130}
+
+        def fill(req):
+            assert req.offset == 0 and req.width == L
+            slot = ctx.stream_slot(req)
+            for q in range(req.rows):
+                i = req.piece + q
+                n = ctx.row_bytes(req, q)
+                seen.append(i)
+                if i not in unreadable:
+                    slot[q * req.width:q * req.width + n] = payload[i * L:i * L + n]
+            slot.release()
+            ctx.stream_commit(req)
+
+        bf, reqs = _stream(native, ctx, fill, unreadable=unreadable)
+        assert sorted(seen) == list(range(P))
+        assert ctx.last_kernel()[1] == -(-P // pieces_per_window)      # one launch per window
+        want = [0 if i in unreadable else b for i, b in enumerate(expect)]
+        assert _bits(bf, P) == want
+    # the host function: one read per piece
+    info = make_info(L, bytes(pieces), "t", length=total)
+    calls = []
+
+    def read(off, n):
+        calls.append((off, n))
+        return payload[off:off + n]
+
+    assert _bits(verify_stream(info, read), P) == expect
+    assert len(calls) == P and all(off % L == 0 for off, _ in calls)

@@ -1,0 +1,213 @@
+"""The reference-shaped Storage paths against verify_files, warm and cold.
+
+Layouts written under <dir> (payload: the oracle's splitmix64 generator; digests: the CPU oracle, 1 % of them
+corrupted, so every result is checked against the oracle's bitfield):
+  cfg3      BASELINE config 3: 10,000 files of U[0, 512 KiB], 256 KiB pieces (tests/layouts.py; committed bits)
+  single16  one 16 GiB file, 1 MiB pieces (cfg2's geometry)
+  files64   16 GiB in 64 files, 1 MiB pieces (the round-1 resume-from-disk layout)
+
+Paths timed (each reads the files exactly as the reference would: Storage(fs_storage) = storage.ts's Storage over
+fsStorage, which opens the file once per get call, storage.ts:149-172):
+  verify_files                     one tv_stage_files call per shard (library readers / page-cache DMA)
+  verify_pieces(Storage(fs))       one Storage.get per piece (16 threads), double-buffered batches staged to HBM
+  verify_stream(Storage(fs).get)   the bounded ring, whole-piece rows (TV_OPT_STREAM_ROWS, the default)
+  verify_stream(..., chunk=L/4)    the bounded ring, columns: four gets per piece (the round-3 default)
+Warm = the files were just written (page cache); cold = posix_fadvise(DONTNEED) after fsync on every file
+(no root needed), then the same call.  `read_ceiling` = the files read cold by 16 threads of 4 MiB preads into
+host memory, nothing else: what the box's storage delivers.  Each line: GB/s, gets (= opens) per piece.
+
+usage: python tools/storage_paths_bench.py <dir> [layout ...] > out.jsonl
+"""
+import json
+import os
+import sys
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from oracle import oracle as O  # noqa: E402  (the checker and the generator)
+from torrent_amd import FileInfo, Storage, make_info, verify_files, verify_pieces, verify_stream  # noqa: E402
+from torrent_amd.storage import FsStorage  # noqa: E402
+
+MiB, GiB = 1 << 20, 1 << 30
+
+
+class CountingFs(FsStorage):
+    """fsStorage with a count of get calls (each one an open, storage.ts:158)."""
+
+    def __init__(self):
+        self.gets = 0
+        self._lock = threading.Lock()
+
+    def get(self, path, offset, length):
+        with self._lock:
+            self.gets += 1
+        return super().get(path, offset, length)
+
+
+def emit(rec):
+    print(json.dumps(rec), flush=True)
+
+
+def drop_cache(paths):
+    for p in paths:
+        fd = os.open(p, os.O_RDONLY)
+        try:
+            os.fsync(fd)
+            os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+        finally:
+            os.close(fd)
+
+
+def read_ceiling(paths, threads=16, part=4 * MiB):
+    """Bytes/s of reading every file with `threads` parallel preads of `part` bytes (nothing kept)."""
+    jobs = []
+    for p in paths:
+        n = os.path.getsize(p)
+        jobs += [(p, o, min(part, n - o)) for o in range(0, n, part)]
+    local = threading.local()
+
+    def one(j):
+        p, o, n = j
+        fd = os.open(p, os.O_RDONLY)
+        try:
+            buf = getattr(local, "buf", None)
+            if buf is None or len(buf) < part:
+                buf = local.buf = bytearray(part)
+            return os.preadv(fd, [memoryview(buf)[:n]], o)
+        finally:
+            os.close(fd)
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        total = sum(ex.map(one, jobs))
+    return total / (time.perf_counter() - t0)
+
+
+def write_layout(name, d):
+    """-> (info, expected bitfield bytes, file paths)."""
+    os.makedirs(d, exist_ok=True)
+    if name == "cfg3":
+        from tests.layouts import build_layout, by_name
+        lay = build_layout(by_name("cfg3"))
+        rec = {r["name"]: r for r in json.load(open(os.path.join(ROOT, "tests", "golden", "layouts.json")))}["cfg3"]
+        paths = []
+        for path, data in lay["disk_files"]().items():
+            p = os.path.join(d, *path)
+            os.makedirs(os.path.dirname(p), exist_ok=True)
+            with open(p, "wb") as f:
+                f.write(data)
+            paths.append(p)
+        return lay["info"], bytes.fromhex(rec["expected_bitfield"]), paths
+    L, total = MiB, 16 * GiB
+    P = total // L
+    nf = 1 if name == "single16" else 64
+    seed = 16 if nf == 1 else 64
+    digests = bytearray(O.synth_piece_digests(seed, total, L, P, threads=16))
+    for i in range(5, P, 100):
+        digests[20 * i + 3] ^= 0x08
+    bits = bytearray(b"\xff" * (P // 8))     # the oracle's digests of the written payload, 1 % corrupted
+    for i in range(5, P, 100):
+        bits[i >> 3] &= ~(0x80 >> (i & 7)) & 0xFF
+    expect = bytes(bits)
+    per = total // nf
+    if nf == 1:
+        files, paths = None, [os.path.join(d, "single16.bin")]
+        sizes = [total]
+    else:
+        sizes = [per] * nf
+        files = [FileInfo(s, [f"f{k:03d}.bin"]) for k, s in enumerate(sizes)]
+        paths = [os.path.join(d, f"f{k:03d}.bin") for k in range(nf)]
+    off = 0
+    chunk = 256 * MiB
+    for p, s in zip(paths, sizes):
+        with open(p, "wb") as f:
+            for o in range(0, s, chunk):
+                n = min(chunk, s - o)
+                f.write(O.synth_fill(seed, off + o, n))
+        off += s
+    info = make_info(L, bytes(digests), "single16.bin" if nf == 1 else "files64", files=files, length=total)
+    return info, expect, paths
+
+
+def timed(fn, reps):
+    best, out = None, None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out = fn()
+        el = time.perf_counter() - t0
+        best = el if best is None else min(best, el)
+    return best, out
+
+
+def main():
+    d = sys.argv[1]
+    names = sys.argv[2:] or ["cfg3", "single16", "files64"]
+    st = os.statvfs(d if os.path.exists(d) else os.path.dirname(d.rstrip("/")) or "/")
+    emit({"host": {"cpus_allowed": len(os.sched_getaffinity(0)), "free_disk_gib": round(st.f_bavail * st.f_frsize / GiB, 1)}})
+    for name in names:
+        root = os.path.join(d, name)
+        t0 = time.perf_counter()
+        info, expect, paths = write_layout(name, root)
+        P, L, total = info.n_pieces, info.piece_length, info.length
+        emit({"layout": name, "files": len(paths), "bytes": total, "pieces": P, "piece_length": L,
+              "write_s": round(time.perf_counter() - t0, 1)})
+        cwd = os.getcwd()
+        os.chdir(root)           # Storage(fs_storage) paths are relative to the working directory (storage.ts)
+        try:
+            for cold in (False, True):
+                legs = [("verify_files", lambda: verify_files(info, root), None)]
+                fs = CountingFs()
+                st_ = Storage(fs, info, root)
+                legs.append(("verify_pieces(Storage(fs))", lambda: verify_pieces(info, st_), fs))
+                fs2 = CountingFs()
+                st2 = Storage(fs2, info, root)
+                legs.append(("verify_stream(Storage(fs).get) rows", lambda: verify_stream(info, st2.get), fs2))
+                fs3 = CountingFs()
+                st3 = Storage(fs3, info, root)
+                legs.append((f"verify_stream(Storage(fs).get) columns chunk={L // 4}",
+                             lambda: verify_stream(info, st3.get, chunk=L // 4), fs3))
+                # the bound of the Storage paths: the gets alone (Storage(fs).get of every piece on the same 16
+                # threads, bytes dropped; no GPU), as verify_pieces issues them
+                fs4 = CountingFs()
+                st4 = Storage(fs4, info, root)
+                from torrent_amd.piece import piece_length as _plen
+
+                def gets_only(threads=16):
+                    with ThreadPoolExecutor(threads) as ex:
+                        return sum(ex.map(lambda i: st4.get(i * L, _plen(i, info)) is not None, range(P)))
+                if cold:
+                    drop_cache(paths)
+                el, n_ok = timed(gets_only, 1 if cold else 2)
+                emit({"layout": name, "cache": "cold" if cold else "warm", "path": "Storage(fs).get only, 16 threads",
+                      "best_s": round(el, 3), "gbps": round(total / el / 1e9, 2), "us_per_get_per_thread":
+                      round(el * 16 / max(1, fs4.gets / (1 if cold else 2)) * 1e6, 1),
+                      "gets_per_piece": round(fs4.gets / (1 if cold else 2) / P, 3)})
+                if cold:
+                    drop_cache(paths)
+                    ceil = read_ceiling(paths)
+                    emit({"layout": name, "cache": "cold", "read_ceiling_gbps": round(ceil / 1e9, 2),
+                          "how": "16 threads x 4 MiB preads of every file after fadvise DONTNEED"})
+                for leg, fn, counter in legs:
+                    if cold:
+                        drop_cache(paths)
+                    if counter is not None:
+                        counter.gets = 0
+                    reps = 1 if cold else (3 if leg == "verify_files" else 2)
+                    el, bf = timed(fn, reps)
+                    rec = {"layout": name, "cache": "cold" if cold else "warm", "path": leg,
+                           "best_s": round(el, 3), "gbps": round(total / el / 1e9, 2),
+                           "exact": bytes(bf) == expect}
+                    if counter is not None:
+                        rec["gets_per_piece"] = round(counter.gets / reps / P, 3)
+                    emit(rec)
+        finally:
+            os.chdir(cwd)
+        for p in paths:
+            os.unlink(p)
+
+
+if __name__ == "__main__":
+    main()

@@ -39,6 +39,7 @@ TV_OPT_NUMA_BIND = 15
 TV_OPT_RESIDENT_BUDGET = 16
 TV_OPT_LIST_SLOTS = 17
 TV_OPT_OPEN_RW = 18
+TV_OPT_STREAM_ROWS = 19
 
 TV_COUNTER_PAYLOAD_ALLOCS = 1
 TV_COUNTER_DEVICE_ALLOCS = 2
@@ -225,6 +226,9 @@ class Context:
             raise NativeError(rc, self._err())
 
     def close(self) -> None:
+        for b in getattr(self, "_batch_bufs", None) or ():   # verify_pieces' page-locked batch buffers
+            b.close()
+        self._batch_bufs = None
         if getattr(self, "_h", None):
             self._L.tv_destroy(self._h)
             self._h = None

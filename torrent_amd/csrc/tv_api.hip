@@ -210,17 +210,18 @@ class Pool {
     uint64_t aff_gen_ = 0;
 };
 
-// One streamed verify (tv_stream_*): columns of C bytes of every shard piece flow host -> pinned ring
-// slot -> device chunk buffer (two, ping-pong) -> one kernel launch per column.
+// One streamed verify (tv_stream_*): units of C bytes of every piece of a window of shard pieces flow host ->
+// pinned ring slot -> device chunk buffer (two, ping-pong) -> one kernel launch per unit.  Column mode: one
+// window (the shard), C-byte columns.  Row mode (TV_OPT_STREAM_ROWS): C = the whole piece, windows of wn pieces.
 struct StreamState {
     bool active = false;
     bool outstanding = false;  // a request (and its ring slot) is lent to the caller
     int slot = -1;             // the lent ring slot (lane 0)
     tv_stream_req req{};
-    uint64_t C = 0, row_pitch = 0, ncol = 0, col = 0, row = 0, rows_per_req = 0, seq = 0;
+    uint64_t C = 0, row_pitch = 0, ncol = 0, row = 0, rows_per_req = 0, seq = 0;
+    uint64_t wn = 0, nwin = 0, unit = 0, nunits = 0;  // pieces per window, windows; unit = window * ncol + column
     int kernel = 0;
     bool k0 = false;           // ev_k0 recorded (first launch queued)
-    TvPieces p{};
     std::vector<uint8_t> av;   // shard-relative availability bits, applied to the bitfield at the end
 };
 
@@ -354,6 +355,7 @@ struct tv_ctx {
     std::vector<uint32_t> slot_free;
 
     bool open_rw = true;               // TV_OPT_OPEN_RW: files opened read + write (fsStorage.get) or read-only
+    bool stream_rows = false;          // TV_OPT_STREAM_ROWS: stream requests carry whole pieces (windows of pieces)
     cpu_set_t proc_cpus;               // the process's CPUs at tv_create (what "unpinned" workers run on)
     bool proc_cpus_ok = false;
 };
@@ -1200,6 +1202,21 @@ void stream_abort_locked(tv_ctx* c) {
     st = StreamState{};
 }
 
+// Row mode (TV_OPT_STREAM_ROWS): each request row is a whole piece (one Storage.get per piece), which needs a
+// piece to fit one ring slot.
+bool stream_rows(const tv_ctx* c) { return c->stream_rows && c->L <= kRingSlotBytes; }
+
+// Row mode's window: whole pieces per chunk buffer, a multiple of 64 (bitfield words of their own), at most
+// kRowWindowBytes per buffer (TV_OPT_RESIDENT_BUDGET / 2 if smaller), the shard when it fits.
+constexpr uint64_t kRowWindowBytes = 4ull << 30;
+uint64_t stream_row_window(const tv_ctx* c) {
+    const uint64_t pitch = (c->L + 63) / 64 * 64 + 256;
+    uint64_t bytes = kRowWindowBytes;
+    if (c->budget_opt) bytes = std::min<uint64_t>(bytes, c->budget_opt / 2);
+    const uint64_t w = std::max<uint64_t>(64, bytes / pitch / 64 * 64);
+    return std::min<uint64_t>(w, c->count);
+}
+
 // Column width: TV_OPT_STREAM_CHUNK, or ~512 MiB columns (64 KiB .. L); a multiple of 64, at most one slot.
 uint64_t stream_column(const tv_ctx* c) {
     uint64_t C = c->stream_chunk;
@@ -1213,7 +1230,9 @@ uint64_t stream_column(const tv_ctx* c) {
 
 // Bytes of each of the two device chunk buffers a stream over the current geometry needs.
 uint64_t stream_chunk_need(const tv_ctx* c) {
-    return c->count ? (stream_column(c) + 256) * c->count + kSlack : 0;
+    if (!c->count) return 0;
+    if (stream_rows(c)) return ((c->L + 63) / 64 * 64 + 256) * stream_row_window(c) + kSlack;
+    return (stream_column(c) + 256) * c->count + kSlack;
 }
 
 int stream_begin_locked(tv_ctx* c, const uint8_t* avail_bits) {
@@ -1225,9 +1244,15 @@ int stream_begin_locked(tv_ctx* c, const uint8_t* avail_bits) {
         st.active = true;
         return TV_OK;
     }
-    st.C = stream_column(c);
+    if (stream_rows(c)) {  // whole pieces per row, windows of wn pieces
+        st.C = (c->L + 63) / 64 * 64;
+        st.wn = stream_row_window(c);
+    } else {               // columns across the whole shard
+        st.C = stream_column(c);
+        st.wn = c->count;
+    }
     st.row_pitch = st.C + 256;  // (tail over-read slack per row)
-    const uint64_t need = st.row_pitch * c->count + kSlack;
+    const uint64_t need = st.row_pitch * st.wn + kSlack;
     if (!reuse_fits(need, c->chunk_bytes)) {
         free_chunks(c);
         for (auto& p : c->d_chunk) {
@@ -1237,10 +1262,9 @@ int stream_begin_locked(tv_ctx* c, const uint8_t* avail_bits) {
         c->chunk_bytes = need;
     }
     st.ncol = (c->L + st.C - 1) / st.C;
+    st.nwin = (c->count + st.wn - 1) / st.wn;
+    st.nunits = st.nwin * st.ncol;
     st.rows_per_req = std::max<uint64_t>(1, kRingSlotBytes / st.C);
-    st.kernel = choose_kernel(c);
-    st.p = resident_launch(c);
-    st.p.stride = st.row_pitch;
     TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
     TV_HIP(c, hipMemsetAsync(c->d_out, 0, c->bit_words * 8, c->stream));  // fail closed, as tv_verify
     TV_HIP(c, hipEventRecord(c->done_ev[0], c->stream));
@@ -1255,15 +1279,16 @@ int stream_next_locked(tv_ctx* c, tv_stream_req* req) {
     if (st.outstanding)
         return fail(c, TV_ERR_STATE, "request %llu is still outstanding (commit it first)", (unsigned long long)st.req.seq);
     *req = tv_stream_req{};
-    if (st.col >= st.ncol) return TV_OK;  // rows == 0: every byte has been requested
-    const int buf = (int)(st.col & 1);
+    if (st.unit >= st.nunits) return TV_OK;  // rows == 0: every byte has been requested
+    const int buf = (int)(st.unit & 1);
+    const uint64_t j0 = st.unit / st.ncol * st.wn, wcount = std::min(st.wn, c->count - j0);
     // the first copy into chunk buffer `buf` waits for the kernel that last read it
     if (st.row == 0) TV_HIP(c, hipStreamWaitEvent(c->copy_stream, c->done_ev[buf], 0));
     int rc = take_slot(c, &st.slot, 0);
     if (rc) return rc;
-    req->piece = c->first + st.row;
-    req->rows = std::min<uint64_t>(st.rows_per_req, c->count - st.row);
-    req->offset = st.col * st.C;
+    req->piece = c->first + j0 + st.row;
+    req->rows = std::min<uint64_t>(st.rows_per_req, wcount - st.row);
+    req->offset = st.unit % st.ncol * st.C;
     req->width = std::min<uint64_t>(st.C, c->L - req->offset);
     req->slot = c->ring[st.slot];
     req->seq = ++st.seq;
@@ -1283,7 +1308,8 @@ int stream_commit_locked(tv_ctx* c, const tv_stream_req* req, const uint8_t* src
     if (!req || req->seq != st.req.seq || req->piece != st.req.piece || req->rows != st.req.rows)
         return fail(c, TV_ERR_ARG, "the request does not match outstanding request %llu", (unsigned long long)st.req.seq);
     const tv_stream_req r = st.req;
-    const int buf = (int)(st.col & 1);
+    const int buf = (int)(st.unit & 1);
+    const uint64_t j0 = st.unit / st.ncol * st.wn, wcount = std::min(st.wn, c->count - j0);
     uint8_t* dst = c->d_chunk[buf] + st.row * st.row_pitch;
     uint8_t* slot = c->ring[st.slot];
     const uint64_t n = std::min(rows_copy, r.rows);
@@ -1313,24 +1339,29 @@ int stream_commit_locked(tv_ctx* c, const tv_stream_req* req, const uint8_t* src
     int rc = release_slot(c, s, 0);  // its event follows the copies just queued
     if (rc) return rc;
     st.row += r.rows;
-    if (st.row < c->count) return TV_OK;
-    // the column is complete: hash it while the caller fills the next one
+    if (st.row < wcount) return TV_OK;
+    // the unit is complete: hash it while the caller fills the next one
     TV_HIP(c, hipEventRecord(c->col_ev[buf], c->copy_stream));
     TV_HIP(c, hipStreamWaitEvent(c->stream, c->col_ev[buf], 0));
     if (!st.k0) {
         TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
         st.k0 = true;
     }
-    const bool last = st.col + 1 == st.ncol;
-    TvPieces p = st.p;
-    p.data = c->d_chunk[buf];
+    const bool last = st.unit % st.ncol + 1 == st.ncol;
+    // the window's pieces (the shard's digest / state rows from j0; bitfield words from j0 / 64: a window of a
+    // multi-window stream is a multiple of 64 pieces)
+    TvPieces p = window_launch(c, j0, wcount, c->d_chunk[buf]);
+    p.stride = st.row_pitch;
+    p.avail64 = c->d_base_avail + j0 / 64;
+    p.out64 = c->d_out + j0 / 64;
     p.data_off = r.offset;
     p.blk_begin = r.offset / 64;
     p.blk_end = last ? UINT64_MAX : (r.offset + st.C) / 64;
     p.finalize = last ? 1 : 0;
+    st.kernel = choose_kernel_n(c, wcount, p.n_main < p.n);
     TV_HIP(c, tv_launch_verify(p, st.kernel, false, c->stream, c->split_pairs, &c->last_workgroups));
     TV_HIP(c, hipEventRecord(c->done_ev[buf], c->stream));
-    st.col++;
+    st.unit++;
     st.row = 0;
     return TV_OK;
 }
@@ -1338,8 +1369,8 @@ int stream_commit_locked(tv_ctx* c, const tv_stream_req* req, const uint8_t* src
 int stream_end_locked(tv_ctx* c, uint8_t* bitfield_out) {
     StreamState& st = c->st;
     if (!st.active) return fail(c, TV_ERR_STATE, "tv_stream_begin has not been called");
-    if (st.outstanding || st.col < st.ncol) {
-        const unsigned long long done = st.col, all = st.ncol;
+    if (st.outstanding || st.unit < st.nunits) {
+        const unsigned long long done = st.unit, all = st.nunits;
         stream_abort_locked(c);
         return fail(c, TV_ERR_STATE, "stream ended before its last column (%llu of %llu hashed); aborted", done, all);
     }
@@ -1356,7 +1387,7 @@ int stream_end_locked(tv_ctx* c, uint8_t* bitfield_out) {
         }
         for (size_t k = 0; k < st.av.size(); k++) bitfield_out[k] &= st.av[k];  // unreadable pieces: bit 0
         c->last_kernel = st.kernel;
-        c->last_launches = (int)st.ncol;
+        c->last_launches = (int)st.nunits;
         rc = finish_timing(c);
         st = StreamState{};
         return rc;
@@ -1546,6 +1577,11 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
             if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_OPEN_RW must be 0 or 1");
             c->open_rw = value != 0;
             return TV_OK;
+        case TV_OPT_STREAM_ROWS:
+            if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_STREAM_ROWS must be 0 or 1");
+            if (c->st.active) return fail(c, TV_ERR_STATE, "TV_OPT_STREAM_ROWS cannot change during a stream");
+            c->stream_rows = value != 0;
+            return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
@@ -1572,6 +1608,7 @@ int tv_get_option(tv_ctx* c, int key, int64_t* value) {
         case TV_OPT_RESIDENT_BUDGET: *value = (int64_t)c->budget_opt; return TV_OK;
         case TV_OPT_LIST_SLOTS: *value = (int64_t)c->list_slots_opt; return TV_OK;
         case TV_OPT_OPEN_RW: *value = c->open_rw ? 1 : 0; return TV_OK;
+        case TV_OPT_STREAM_ROWS: *value = c->stream_rows ? 1 : 0; return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }

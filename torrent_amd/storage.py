@@ -19,6 +19,7 @@ contiguous in HBM (see verify.py).
 from __future__ import annotations
 
 import bisect
+import ctypes
 import os
 from typing import Callable, List, Optional, Protocol, Tuple
 
@@ -185,17 +186,31 @@ class Storage:
             return False
 
     # -- reference API -----------------------------------------------------------------
-    def get(self, offset: int, length: int) -> Optional[bytearray]:
-        """storage.ts:50-65."""
-        out = bytearray(length)
-
-        def act(path, foff, sl):
-            got = self.method.get(path, foff, len(sl))
-            if got is not None:
-                sl[:] = got
-            return got is not None
-
-        return out if self._find_and_do(offset, out, act) else None
+    def get(self, offset: int, length: int):
+        """storage.ts:50-65: the bytes [offset, offset + length) read file segment by file segment through
+        the method, or None when a segment fails (or returns another length: the reference's copy into its
+        Uint8Array would throw, :61).  A range inside one file is the method's own bytes (no copy); the
+        segments of a range spanning files are copied into one buffer with the GIL released (memmove), so
+        many readers copy in parallel."""
+        try:
+            segs = self.segments(offset, length)
+            if segs is None:
+                return None
+            if len(segs) == 1:
+                path, foff, n, _ = segs[0]
+                got = self.method.get(path, foff, n)
+                return got if got is not None and len(got) == n else None
+            out = bytearray(length)
+            base = ctypes.addressof((ctypes.c_char * length).from_buffer(out)) if length else 0
+            for path, foff, n, start in segs:
+                got = self.method.get(path, foff, n)
+                if got is None or len(got) != n:
+                    return None
+                if n:
+                    copy_bytes(base + start, got, n)
+            return out
+        except Exception:
+            return None
 
     def set(self, offset: int, data: bytes) -> bool:
         """storage.ts:67-87 (blocks deduplicated by offset / BLOCK_SIZE)."""
@@ -207,6 +222,19 @@ class Storage:
         if ok:
             self._written[index] = True
         return ok
+
+
+def copy_bytes(dst: int, src, n: int) -> None:
+    """memmove n bytes of the bytes-like `src` to address dst, without the GIL (ctypes' C call) and without a
+    temporary copy of src."""
+    if isinstance(src, bytes):
+        ctypes.memmove(dst, src, n)                      # (a bytes argument is passed by its own address)
+        return
+    mv = memoryview(src).cast("B")
+    if mv.readonly:
+        ctypes.memmove(dst, bytes(mv[:n]), n)
+    else:
+        ctypes.memmove(dst, (ctypes.c_char * mv.nbytes).from_buffer(mv), n)
 
 
 class FsStorage:

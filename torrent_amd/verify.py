@@ -37,6 +37,7 @@ from typing import List, Optional, Sequence
 from . import _native
 from .metainfo import InfoDict
 from .piece import piece_length
+from .storage import copy_bytes
 
 # pieces gathered per tv_stage call when reading through a Storage
 _STAGE_BATCH_BYTES = 256 << 20
@@ -138,6 +139,18 @@ def _layout(ctx, info_or_len, L: int, P: int, first: int, count: int, budget: Op
     ctx.set_layout(total, L, P, first, count)
 
 
+def _batch_buffers(ctx, nbytes: int) -> list:
+    """Two page-locked batch buffers of `ctx` holding >= nbytes each (kept on the cached context and reused):
+    reads land in them and tv_stage DMAs them straight to HBM, with no copy through the staging ring."""
+    bufs = getattr(ctx, "_batch_bufs", None)
+    if bufs is None or bufs[0].nbytes < nbytes:
+        for b in bufs or ():
+            b.close()
+        ctx._batch_bufs = None
+        bufs = ctx._batch_bufs = [_native.PinnedBuffer(nbytes) for _ in range(2)]
+    return bufs
+
+
 def _run_shards(devs: List[int], n_pieces: int, fn):
     """fn(ctx, first, count) for each shard, one thread per shard (ctypes releases the GIL)."""
     ranges = shard_ranges(n_pieces, len(devs))
@@ -161,8 +174,9 @@ def verify_pieces(info: InfoDict, storage, devices=None, threads: int = 16,
     (a torrent_amd.storage.Storage, i.e. the reference's Storage over any StorageMethod).  The gets
     of a batch are in flight together on `threads` threads, as ts/verify.ts keeps them outstanding
     with Promise.all (make_torrent.ts:96,111 does the same); threads=1 reads them one by one.
-    Reads and staging overlap: batch k + 1 is read (into the other of two buffers) while batch k is
-    copied to HBM (and, on a windowed layout, while the windows before it hash)."""
+    Reads and staging overlap: batch k + 1 is read (into the other of two page-locked buffers) while batch
+    k is DMA'd to HBM (and, on a windowed layout, while the windows before it hash); each reader thread
+    copies its piece into the batch buffer itself, without the GIL."""
     P, L = info.n_pieces, info.piece_length
 
     def shard(ctx, first: int, count: int) -> bytes:
@@ -171,34 +185,36 @@ def verify_pieces(info: InfoDict, storage, devices=None, threads: int = 16,
         avail = bytearray((count + 7) // 8)
         per_batch = max(1, min(count, _STAGE_BATCH_BYTES // max(1, L)))
 
-        def get(i: int):
-            data = storage.get(i * L, piece_length(i, info))  # storage.ts:50-65; None => bit 0
+        def get(i: int, base: int) -> int:
+            """Piece i into the batch buffer at `base` (+ its slot); its length, or 0 when unreadable."""
+            n = piece_length(i, info)
+            data = storage.get(i * L, n)         # storage.ts:50-65; None => bit 0
             # (Storage.get returns exactly the length asked or null; any other length is unreadable too,
             # as in verify_stream -- it must not shift the batch buffer's later pieces)
-            return data if data is not None and len(data) == piece_length(i, info) else None
+            if data is None or len(data) != n:
+                return 0
+            copy_bytes(base, data, n)
+            return n
 
-        bufs = [bytearray(per_batch * L)]
+        bufs = _batch_buffers(ctx, per_batch * L)
         with ThreadPoolExecutor(max(1, threads)) as pool, ThreadPoolExecutor(1) as stager:
             staging = None              # the previous batch's stage (it reads the other buffer)
             j, b = 0, 0
             try:
                 while j < count:
                     k = min(per_batch, count - j)
-                    if b == len(bufs):
-                        bufs.append(bytearray(per_batch * L))
                     buf = bufs[b]       # its last stage (two batches ago) finished before `staging` began
                     hi = 0
-                    for q, data in enumerate(pool.map(get, range(first + j, first + j + k))):
-                        if data is None:
-                            continue    # (the stale bytes left in the buffer there are never a readable piece)
-                        buf[q * L:q * L + len(data)] = data
-                        hi = q * L + len(data)
-                        _set_bit(avail, j + q)
+                    got = pool.map(lambda q: get(first + j + q, buf.ptr + q * L), range(k))
+                    for q, n in enumerate(got):
+                        if n:           # (an unreadable piece's slot keeps stale bytes: never a readable piece)
+                            hi = q * L + n
+                            _set_bit(avail, j + q)
                     if staging is not None:
                         staging.result()
                         staging = None
                     if hi:
-                        staging = stager.submit(ctx.stage, (first + j) * L, memoryview(buf)[:hi])
+                        staging = stager.submit(ctx.stage, (first + j) * L, buf.mv[:hi])
                     j += k
                     b ^= 1
             finally:
@@ -268,19 +284,22 @@ def verify_stream(info: InfoDict, read, devices=None, avail: Optional[bytes] = N
                   threads: int = 16) -> bytearray:
     """End-to-end resume check through the library's BOUNDED pinned ring (tv_stream_*; SURVEY 8d config 5:
     the resume flow Client.add -> verify -> Torrent.bitfield -> sendBitfield, client.ts:53-67,
-    torrent.ts:56-60,101).  No resident payload and no whole-shard host buffer: the library asks for the
-    shard column by column (bytes [c*C, c*C + C) of every piece, C = `chunk` or automatic), and each row
-    is one read(linear_offset, length) -> bytes | None -- Storage.get's shape (storage.ts:50-65), so a
-    Storage's bound .get can be passed.  None makes that piece unreadable (bit 0); a piece is readable
-    iff every slice of it reads.  Host memory in flight: 3 x 64 MiB per device, whatever the size.  The reads
-    of a request are in flight together on `threads` threads (as verify_pieces; threads=1 reads them one by
-    one), each writing its own row of the slot."""
+    torrent.ts:56-60,101).  No resident payload and no whole-shard host buffer.  By default (chunk=0) each
+    request row is a WHOLE piece (TV_OPT_STREAM_ROWS; pieces of up to 64 MiB), so a piece costs one
+    read(linear_offset, length) -> bytes | None -- Storage.get's shape (storage.ts:50-65), so a Storage's
+    bound .get can be passed, and fsStorage.get opens each file once per piece; the library hashes windows of
+    up to 4 GiB of pieces as they arrive.  chunk=C > 0 asks for the shard column by column instead (bytes
+    [c*C, c*C + C) of every piece; all of the shard's pieces in each launch).  None makes that piece
+    unreadable (bit 0); a piece is readable iff every slice of it reads.  Host memory in flight: 3 x 64 MiB
+    per device, whatever the size.  The reads of a request are in flight together on `threads` threads (as
+    verify_pieces; threads=1 reads them one by one), each writing its own row of the slot."""
     P, L = info.n_pieces, info.piece_length
 
     def shard(ctx, first: int, count: int) -> bytes:
         ctx.set_option(_native.TV_OPT_RESIDENT, 0)       # no resident payload for a streamed check
         try:
             ctx.set_option(_native.TV_OPT_STREAM_CHUNK, chunk)
+            ctx.set_option(_native.TV_OPT_STREAM_ROWS, 0 if chunk else 1)
             ctx.set_layout(info.length, L, P, first, count)
             ctx.set_digests(info.pieces_raw)
         finally:
@@ -292,10 +311,10 @@ def verify_stream(info: InfoDict, read, devices=None, avail: Optional[bytes] = N
                 req = ctx.stream_next()
                 if not req.rows:
                     break
-                slot = ctx.stream_slot(req)
 
-                def fill(q: int, req=req, slot=slot):
-                    """Row q into the slot; returns the piece index when it is unreadable."""
+                def fill(q: int, req=req):
+                    """Row q into the slot (copied by this reader thread, without the GIL); returns the piece
+                    index when it is unreadable."""
                     n = ctx.row_bytes(req, q)
                     if n == 0:
                         return None
@@ -303,14 +322,13 @@ def verify_stream(info: InfoDict, read, devices=None, avail: Optional[bytes] = N
                     data = read(i * L + req.offset, n)
                     if data is None or len(data) != n:
                         return i
-                    slot[q * req.width:q * req.width + n] = data
+                    copy_bytes(req.slot + q * req.width, data, n)
                     return None
 
                 rows = range(req.rows)
                 for i in (pool.map(fill, rows) if pool is not None else map(fill, rows)):
                     if i is not None:
                         ctx.stream_unreadable(i)
-                slot.release()
                 ctx.stream_commit(req)
             return ctx.stream_end()
         except BaseException:
@@ -320,6 +338,7 @@ def verify_stream(info: InfoDict, read, devices=None, avail: Optional[bytes] = N
             if pool is not None:
                 pool.shutdown()
             ctx.set_option(_native.TV_OPT_STREAM_CHUNK, 0)
+            ctx.set_option(_native.TV_OPT_STREAM_ROWS, 0)
 
     if P == 0:
         return bytearray()

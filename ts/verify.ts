@@ -248,14 +248,16 @@ export async function verifyPieces(
 const TV_OPT_STREAM_CHUNK = 3;
 const TV_OPT_RESIDENT = 10;
 const TV_OPT_OPEN_RW = 18;
+const TV_OPT_STREAM_ROWS = 19;
 
 /**
  * verifyStream(info, storage) -> have-bitfield: the end-to-end resume check through the library's
  * BOUNDED pinned ring (tv_stream_*; SURVEY 8d config 5; the resume flow Client.add -> verify ->
  * Torrent.bitfield -> sendBitfield, client.ts:53-67, torrent.ts:56-60,101).  No resident payload and no
- * whole-shard buffer: the library requests the shard column by column (bytes [c*C, c*C + C) of every
- * piece), each row is one storage.get(offset, length) written straight into the library's pinned slot,
- * and the library DMAs the slot to HBM while the GPU hashes the previous column.  Host memory in flight:
+ * whole-shard buffer: the library requests the shard in rows of whole pieces (TV_OPT_STREAM_ROWS; with
+ * opts.chunk, column by column: bytes [c*C, c*C + C) of every piece), each row is one
+ * storage.get(offset, length) written straight into the library's pinned slot -- one fsStorage open per
+ * piece -- and the library DMAs the slot to HBM while the GPU hashes the previous window.  Host memory in flight:
  * 3 x 64 MiB per device.  null from storage.get makes that piece 0 (a piece is readable iff every slice
  * of it reads).  Same behaviour as torrent_amd.verify_stream.
  */
@@ -271,6 +273,8 @@ export async function verifyStream(info: InfoDict, storage: Storage, opts: Verif
     await withContext(l, devices[s], s, async (ctx) => {
       check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_RESIDENT, 0n));
       check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_STREAM_CHUNK, BigInt(opts.chunk || 0)));
+      // default: whole pieces per row (one storage.get, i.e. one fsStorage open, per piece); chunk: columns
+      check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_STREAM_ROWS, opts.chunk ? 0n : 1n));
       try {
         check(l, ctx, l.symbols.tv_set_layout(ctx, BigInt(info.length), BigInt(L), BigInt(P), BigInt(first), BigInt(count)));
       } finally {
@@ -307,6 +311,7 @@ export async function verifyStream(info: InfoDict, storage: Storage, opts: Verif
         throw err;
       } finally {
         l.symbols.tv_set_option(ctx, TV_OPT_STREAM_CHUNK, 0n);
+        l.symbols.tv_set_option(ctx, TV_OPT_STREAM_ROWS, 0n);
       }
     });
   }));
