@@ -253,6 +253,20 @@ def ground_truth(seed: int, total: int, L: int, P: int, first: int, count: int, 
     return d, time.perf_counter() - t0
 
 
+def _traffic(workload: str, bytes_per_launch: int):
+    """HBM bytes per launch from profiles/traffic_<workload>.json (PMC passes, corrected as the MI355X guide
+    prescribes), when it was measured on this launch geometry; else None."""
+    tpath = os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
+    if not os.path.exists(tpath):
+        return None
+    try:
+        rec = json.load(open(tpath))
+    except Exception:
+        return None
+    # a per-launch PMC figure applies only to the launch geometry it was measured on
+    return rec.get("hbm_bytes_per_launch") if rec.get("payload_bytes_per_launch") == bytes_per_launch else None
+
+
 def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: bool, steps: int, warmup: int,
                  kernel_opt: int, threads: int, want_digests: bool = False) -> dict:
     """One resident workload on every rank: synthetic payload filled in HBM by the device generator, oracle
@@ -271,6 +285,7 @@ def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: b
     ctx = _native.Context(device)
     try:
         ctx.set_option(_native.TV_OPT_KERNEL, kernel_opt)
+        ctx.set_option(_native.TV_OPT_CLOCK_PROBE, 1)   # workgroup 0 samples the shader clock it runs at
         ctx.set_layout(total, L, P, first, count)
         # a resident step re-hashes the whole shard: the layout must hold it whole (a windowed layout, for a
         # shard above the device budget, would hash once per pass and make repeated verifies compares)
@@ -303,6 +318,7 @@ def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: b
         t1 = time.perf_counter()
         _barrier(dist)
         kernel, _ = ctx.last_kernel()
+        clock_ghz = ctx.counter(_native.TV_COUNTER_LAST_CLOCK_KHZ) / 1e6   # (after the timed region: it syncs)
     finally:
         ctx.close()
     t_end = time.perf_counter()
@@ -321,6 +337,12 @@ def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: b
            "kernel_ms_max_over_ranks": round(_max(dist, avg), 3), "achieved": round(achieved, 1),
            "piece_parallelism_ceiling": round(ceiling, 1), "frac_of_piece_ceiling": round(achieved / ceiling, 4),
            "frac_of_valu_peak": round(achieved / VALU_PEAK_GBPS, 4),
+           "clock_ghz": round(clock_ghz, 3) if clock_ghz else None,
+           "frac_of_valu_peak_at_clock": round(achieved / (VALU_PEAK_GBPS * clock_ghz / (CLOCK_HZ / 1e9)), 4)
+           if clock_ghz else None,
+           "clock_note": "shader clock of the last timed launch (its workgroup 0's shader-counter ticks over 100 MHz "
+                         "real-time ticks, TV_OPT_CLOCK_PROBE); R_valu is quoted at 2.4 GHz, "
+                         "frac_of_valu_peak_at_clock rescales it to this clock",
            "bitfield_exact": exact, "expected": "oracle digests of every piece, 1 % corrupted",
            "ground_truth_s": round(gt_s, 2), "ground_truth_threads": threads,
            "phase_s": {"ground_truth": round(gt_s, 2), "setup": round(t_warm - t_setup, 2),
@@ -588,16 +610,13 @@ def main() -> int:
 
     if rank == 0:
         bytes_per_gpu = main_leg["bytes_per_gpu"]
-        traffic = None
-        tpath = os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
-        if os.path.exists(tpath):
-            try:
-                rec = json.load(open(tpath))
-                # a per-launch PMC figure applies only to the launch geometry it was measured on
-                if rec.get("payload_bytes_per_launch") == bytes_per_gpu:
-                    traffic = rec.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+        traffic = _traffic(workload, bytes_per_gpu)
+        tp = legs.get("piece_saturated")
+        if tp and "bytes_per_gpu" in tp:
+            tsat = _traffic("suppl", tp["bytes_per_gpu"])
+            if tsat:
+                tp["traffic_ratio"] = round(tsat / tp["bytes_per_gpu"], 5)
+                tp["traffic_source"] = "profiles/traffic_suppl.json (PMC passes of this geometry, tools/gpu_r04_pmc.sh)"
         achieved = main_leg["achieved"]
         out = {
             "metric": "verified GB/s (SHA-1 pieces, HBM-resident)",
@@ -627,6 +646,7 @@ def main() -> int:
                          "hbm_peak": HBM_PEAK_GBPS, "frac_hbm": round(achieved / HBM_PEAK_GBPS, 4),
                          "piece_parallelism_ceiling": main_leg["piece_parallelism_ceiling"],
                          "frac_of_piece_ceiling": main_leg["frac_of_piece_ceiling"],
+                         "clock_ghz": main_leg["clock_ghz"], "frac_at_clock": main_leg["frac_of_valu_peak_at_clock"],
                          "valu_peak_derivation": VALU_DERIVATION,
                          "note": "SHA-1 is serial per piece, so P pieces per GPU cap the rate at P x 64 B / "
                                  "(serial VALU instr x 4.07 cyc) (piece_parallelism_ceiling; 405 instr for the "

@@ -314,6 +314,9 @@ int tv_host_unregister(void *ptr);
                                      and smaller), one launch per window: one Storage.get per piece for a reader
                                      that opens a file per call (fsStorage.get, storage.ts:149-172).  Set it
                                      before tv_stream_begin (TV_ERR_STATE during a stream) */
+#define TV_OPT_CLOCK_PROBE 20     /* 1: verify / hash launches (resident, windows, stream units) record the shader clock
+                                     they ran at (workgroup 0 reads the shader and 100 MHz real-time counters at its
+                                     start and end; TV_COUNTER_LAST_CLOCK_KHZ).  0 (default) = off */
 int tv_set_option(tv_ctx *ctx, int key, int64_t value);
 int tv_get_option(tv_ctx *ctx, int key, int64_t *value);
 
@@ -343,6 +346,9 @@ int tv_last_kernel(tv_ctx *ctx, int *kernel, int *launches);
 #define TV_COUNTER_BUDGET 10         /* the device budget the last tv_set_layout applied, bytes (0: no resident payload
                                         or a slot pool) */
 #define TV_COUNTER_SLOTS_USED 11     /* slots of a slot pool holding a staged piece not yet listed */
+#define TV_COUNTER_LAST_CLOCK_KHZ 12 /* TV_OPT_CLOCK_PROBE: the shader clock of the last probed launch's workgroup 0, kHz
+                                        (shader-counter ticks / 100 MHz real-time ticks over its life); 0 = none.
+                                        Waits for the ctx's queued kernels */
 int tv_get_counter(tv_ctx *ctx, int key, uint64_t *value);
 
 /* Block until all work queued by the ctx is complete. */

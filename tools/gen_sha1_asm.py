@@ -63,6 +63,8 @@ ALIGN_FULL = os.environ.get("TV_GEN_ALIGN", "1") == "1"   # lane compression blo
 HELPER_PAIR = os.environ.get("TV_GEN_HPAIR", "0") == "1"  # split helper: schedule in pairs (4-byte ops paired)
 K_IN_ROUNDS = os.environ.get("TV_GEN_KROUNDS", "0") == "1"  # split: the rounds wave adds K (v_add3 with an SGPR)
 HELPER_X = os.environ.get("TV_GEN_HX", "")   # timing probes only: novalu / nowrite / noload (digests are wrong)
+ROUNDS_X = os.environ.get("TV_GEN_RX", "")   # timing probe only: nowait = the split rounds loop without its LDS-return
+                                             # waits (digests are wrong; barriers unchanged)
 LOOP_ALIGN = os.environ.get("TV_GEN_LALIGN", "1") == "1"  # split loops: .p2align 3 before every block body
 HELPER_AHEAD = LDS_BUFS - 1
 assert not PIPELINED or (LDS_BUFS >= 3 and RING_QUADS == 20), "the pipelined stream needs 3 buffers and a 20-quad ring"
@@ -469,7 +471,10 @@ def rounds_loop_text() -> str:
         else:   # per-block stream: its 15 reads issued at the block's start
             if LOOP_ALIGN:
                 L.append(".p2align 3")
-            L.extend(_emit_lines(gen_lds(k * RING_BYTES, lead_wait=False)))
+            body = _emit_lines(gen_lds(k * RING_BYTES, lead_wait=False))
+            if ROUNDS_X == "nowait":
+                body = [x for x in body if not x.startswith("s_waitcnt")]
+            L.extend(body)
             L.extend(f"v_add_u32 %[h{i}], %[h{i}], %[r{i}]" for i in range(5))
             L.append("s_barrier")
         L += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_eq_u32 %[cnt], 0",
@@ -616,12 +621,20 @@ def helper_loop_text(twin: bool = False) -> str:
     advance()
     loads(P1_BASE)
     advance()
-    # block 0 into buffer 0; with the helper two blocks ahead (HELPER_AHEAD = 2) no barrier follows it:
-    # its first barrier (the rounds wave's starting one) follows the write of block 1
+    # block 0 into buffer 0; with the helper A = HELPER_AHEAD blocks ahead no barrier follows its first A - 1
+    # writes: its first barrier (the rounds wave's starting one) follows the write of block A - 1, and block m
+    # (m >= A - 1) is followed by barrier m - A + 2 -- the C++ tail's rule (b - b0 + 1 >= kAhead) -- so the
+    # helper, whose A - 1 extra barriers end it, executes as many barriers as the rounds wave
     step(P0_BASE, 0, barrier=HELPER_AHEAD == 1)
     L.append("s_sub_u32 %[cnt], %[nraw], 1")
     L.append("s_cmp_eq_u32 %[cnt], 0")
     L.append("s_cbranch_scc1 L_hdone_%=")
+    first_loop_blk = max(1, HELPER_AHEAD - 1)
+    for m in range(1, first_loop_blk):   # blocks 1 .. A - 2 (A >= 3): written before the first barrier
+        step((P0_BASE, P1_BASE)[m % 2], (m % LDS_BUFS) * RING_BYTES, barrier=False)
+        L.append("s_sub_u32 %[cnt], %[cnt], 1")
+        L.append("s_cmp_eq_u32 %[cnt], 0")
+        L.append("s_cbranch_scc1 L_hdone_%=")
     if twin and TWIN_HALIGN is not None:
         L.append(".p2align 6")
         L.extend(["s_nop 0"] * int(TWIN_HALIGN))
@@ -631,7 +644,7 @@ def helper_loop_text(twin: bool = False) -> str:
     L.append("L_hloop_%=:")
     period = 2 * LDS_BUFS // (2 if LDS_BUFS % 2 == 0 else 1)   # lcm(prefetch register sets 2, LDS buffers)
     for k in range(period):
-        blk = k + 1                  # block index (mod period) of this step
+        blk = k + first_loop_blk     # block index (mod period) of this step
         step((P0_BASE, P1_BASE)[blk % 2], (blk % LDS_BUFS) * RING_BYTES)
         L.append("s_sub_u32 %[cnt], %[cnt], 1")
         L.append("s_cmp_eq_u32 %[cnt], 0")
@@ -995,7 +1008,8 @@ def _emit_lines(ins, full: bool = False):
         elif o == "ds_read_b128":
             q, off = op[1], op[2]
             lo = RING_BASE + 4 * (q % RING_QUADS)
-            lines.append(f"ds_read_b128 v[{lo}:{lo + 3}], %[addr] offset:{off}")
+            a, off = ("%[addr2]", off - 65536) if off >= 65536 else ("%[addr]", off)   # (16-bit DS offsets)
+            lines.append(f"ds_read_b128 v[{lo}:{lo + 3}], {a} offset:{off}")
         elif o == "v_bitop3_b32":
             lines.append(f"v_bitop3_b32 {_opnd(op[1], full)}, {_opnd(op[2], full)}, {_opnd(op[3], full)}, "
                          f"{_opnd(op[4], full)} bitop3:0x{op[5]:02x}")
@@ -1006,7 +1020,8 @@ def _emit_lines(ins, full: bool = False):
         elif o == "v_perm_b32":
             lines.append(f"v_perm_b32 {_opnd(op[1], full)}, {_opnd(op[2], full)}, {_opnd(op[3], full)}, {_opnd(op[4], full)}")
         elif o == "ds_write_b128":
-            lines.append(f"ds_write_b128 %[addr], v[{op[1]}:{op[1] + 3}] offset:{op[2]}")
+            a, off = ("%[addr2]", op[2] - 65536) if op[2] >= 65536 else ("%[addr]", op[2])
+            lines.append(f"ds_write_b128 {a}, v[{op[1]}:{op[1] + 3}] offset:{off}")
         elif o == "s_barrier":
             lines.append("s_barrier")
         elif o == "s_nop":
@@ -1070,7 +1085,7 @@ __device__ __forceinline__ void tv_sha1_lds(const uint32_t h[5], uint32_t r[5], 
 {lds}
     : [r0] "=&v"(r[0]), [r1] "=&v"(r[1]), [r2] "=&v"(r[2]), [r3] "=&v"(r[3]), [r4] "=&v"(r[4]),
       [t0] "=&v"(t0), [t1] "=&v"(t1)
-    : [h0] "v"(h[0]), [h1] "v"(h[1]), [h2] "v"(h[2]), [h3] "v"(h[3]), [h4] "v"(h[4]), [addr] "v"(addr),
+    : [h0] "v"(h[0]), [h1] "v"(h[1]), [h2] "v"(h[2]), [h3] "v"(h[3]), [h4] "v"(h[4]), [addr] "v"(addr){addr2},
       [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
     : {ring_clobbers}, "memory");
 }}
@@ -1085,7 +1100,7 @@ __device__ __forceinline__ void tv_sha1_helper_loop(const void* va, uint32_t nra
     asm volatile(
 {helper_loop}
     : [cnt] "=&s"(cnt), [adv] "=&s"(adv), [inc] "=&s"(inc)
-    : [va] "v"(va), [nraw] "s"(nraw), [addr] "v"(addr), [sel] "s"(0x00010203u),
+    : [va] "v"(va), [nraw] "s"(nraw), [addr] "v"(addr){addr2}, [sel] "s"(0x00010203u),
       [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
     : {loop_clobbers}, "scc", "memory");
 }}
@@ -1100,7 +1115,7 @@ __device__ __forceinline__ void tv_sha1_rounds_loop(uint32_t h[5], uint32_t addr
     : [h0] "+v"(h[0]), [h1] "+v"(h[1]), [h2] "+v"(h[2]), [h3] "+v"(h[3]), [h4] "+v"(h[4]),
       [r0] "=&v"(r[0]), [r1] "=&v"(r[1]), [r2] "=&v"(r[2]), [r3] "=&v"(r[3]), [r4] "=&v"(r[4]),
       [t0] "=&v"(t0), [t1] "=&v"(t1), [cnt] "=&s"(cnt)
-    : [addr] "v"(addr), [nsteps] "s"(nsteps), [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
+    : [addr] "v"(addr){addr2}, [nsteps] "s"(nsteps), [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
     : {ring_clobbers}, "scc", "memory");
 }}
 
@@ -1116,7 +1131,7 @@ __device__ __forceinline__ void tv_sha1_schedule_lds(const uint32_t raw[16], uin
       [raw4] "v"(raw[4]), [raw5] "v"(raw[5]), [raw6] "v"(raw[6]), [raw7] "v"(raw[7]),
       [raw8] "v"(raw[8]), [raw9] "v"(raw[9]), [raw10] "v"(raw[10]), [raw11] "v"(raw[11]),
       [raw12] "v"(raw[12]), [raw13] "v"(raw[13]), [raw14] "v"(raw[14]), [raw15] "v"(raw[15]),
-      [addr] "v"(addr), [sel] "s"(0x00010203u), [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
+      [addr] "v"(addr){addr2}, [sel] "s"(0x00010203u), [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
     : {helper_clobbers}, "memory");
 }}
 """
@@ -1134,7 +1149,7 @@ __device__ __forceinline__ void tv_sha1_twin_lds(const uint32_t h[5], uint32_t r
 {twin_lds}
     : [r0] "=&v"(r[0]), [r1] "=&v"(r[1]), [r2] "=&v"(r[2]), [r3] "=&v"(r[3]), [r4] "=&v"(r[4]),
       [t0] "=&v"(t0), [t1] "=&v"(t1)
-    : [h0] "v"(h[0]), [h1] "v"(h[1]), [h2] "v"(h[2]), [h3] "v"(h[3]), [h4] "v"(h[4]), [addr] "v"(addr)
+    : [h0] "v"(h[0]), [h1] "v"(h[1]), [h2] "v"(h[2]), [h3] "v"(h[3]), [h4] "v"(h[4]), [addr] "v"(addr){addr2}
     : {ring_clobbers}, "memory");
 }}
 
@@ -1146,7 +1161,7 @@ __device__ __forceinline__ void tv_sha1_twin_rounds_loop(uint32_t h[5], uint32_t
     : [h0] "+v"(h[0]), [h1] "+v"(h[1]), [h2] "+v"(h[2]), [h3] "+v"(h[3]), [h4] "+v"(h[4]),
       [r0] "=&v"(r[0]), [r1] "=&v"(r[1]), [r2] "=&v"(r[2]), [r3] "=&v"(r[3]), [r4] "=&v"(r[4]),
       [t0] "=&v"(t0), [t1] "=&v"(t1), [cnt] "=&s"(cnt)
-    : [addr] "v"(addr), [nsteps] "s"(nsteps)
+    : [addr] "v"(addr){addr2}, [nsteps] "s"(nsteps)
     : {ring_clobbers}, "scc", "memory");
 }}
 
@@ -1159,7 +1174,7 @@ __device__ __forceinline__ void tv_sha1_twin_helper_loop(const void* va, uint32_
     asm volatile(
 {twin_helper_loop}
     : [cnt] "=&s"(cnt), [adv] "=&s"(adv), [inc] "=&s"(inc)
-    : [va] "v"(va), [nraw] "s"(nraw), [addr] "v"(addr), [sel] "s"(0x00010203u), [psel] "v"(psel),
+    : [va] "v"(va), [nraw] "s"(nraw), [addr] "v"(addr){addr2}, [sel] "s"(0x00010203u), [psel] "v"(psel),
       [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
     : {twin_loop_clobbers}, "scc", "memory");
 }}
@@ -1174,7 +1189,7 @@ __device__ __forceinline__ void tv_sha1_twin_schedule_lds(const uint32_t raw[16]
       [raw4] "v"(raw[4]), [raw5] "v"(raw[5]), [raw6] "v"(raw[6]), [raw7] "v"(raw[7]),
       [raw8] "v"(raw[8]), [raw9] "v"(raw[9]), [raw10] "v"(raw[10]), [raw11] "v"(raw[11]),
       [raw12] "v"(raw[12]), [raw13] "v"(raw[13]), [raw14] "v"(raw[14]), [raw15] "v"(raw[15]),
-      [addr] "v"(addr), [sel] "s"(0x00010203u), [psel] "v"(psel), [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
+      [addr] "v"(addr){addr2}, [sel] "s"(0x00010203u), [psel] "v"(psel), [k0] "s"(k0), [k1] "s"(k1), [k2] "s"(k2), [k3] "s"(k3)
     : {twin_helper_clobbers}, "memory");
 }}
 """
@@ -1188,7 +1203,9 @@ def render() -> str:
     h2regs = list(range(H2_F, H2_O + 12))
     h2 = ", ".join(f'"v{i}"' for i in h2regs)
     h2loop = ", ".join(f'"v{i}"' for i in h2regs + list(range(P0_BASE, VL + 2)))
-    return HEADER.format(k_in_rounds=int(K_IN_ROUNDS), ring_base=RING_BASE, ring_quads=RING_QUADS, lds_bufs=LDS_BUFS, helper_ahead=HELPER_AHEAD,
+    # a K+W ring past 64 KiB (LDS_BUFS >= 4) addresses its upper buffers from a second register: DS offsets are 16-bit
+    addr2 = ', [addr2] "v"(addr + 65536u)' if LDS_BUFS * RING_BYTES > 65536 else ""
+    return HEADER.format(addr2=addr2, k_in_rounds=int(K_IN_ROUNDS), ring_base=RING_BASE, ring_quads=RING_QUADS, lds_bufs=LDS_BUFS, helper_ahead=HELPER_AHEAD,
                          full=('    ".p2align 3\\n"\n' if ALIGN_FULL else "") + emit(gen_full(), True),
                          lds=emit(gen_lds(), False), helper=emit(gen_helper(), False),
                          helper_loop=helper_loop_text(), rounds_loop=rounds_loop_text(),
@@ -1198,7 +1215,7 @@ def render() -> str:
                              twin_rounds_loop=twin_rounds_loop_text(),
                              twin_helper_loop=helper_loop_text(twin=True),
                              twin_helper=emit(gen_helper2(), False),
-                             ring_clobbers=ring, twin_helper_clobbers=h2, twin_loop_clobbers=h2loop))
+                             ring_clobbers=ring, twin_helper_clobbers=h2, twin_loop_clobbers=h2loop, addr2=addr2))
 
 
 def main():

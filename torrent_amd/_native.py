@@ -40,6 +40,7 @@ TV_OPT_RESIDENT_BUDGET = 16
 TV_OPT_LIST_SLOTS = 17
 TV_OPT_OPEN_RW = 18
 TV_OPT_STREAM_ROWS = 19
+TV_OPT_CLOCK_PROBE = 20
 
 TV_COUNTER_PAYLOAD_ALLOCS = 1
 TV_COUNTER_DEVICE_ALLOCS = 2
@@ -52,6 +53,7 @@ TV_COUNTER_WINDOW_PIECES = 8
 TV_COUNTER_WINDOWS = 9
 TV_COUNTER_BUDGET = 10
 TV_COUNTER_SLOTS_USED = 11
+TV_COUNTER_LAST_CLOCK_KHZ = 12
 
 TV_STREAM_RING_SLOTS = 3
 TV_STREAM_SLOT_BYTES = 64 << 20

@@ -356,6 +356,8 @@ struct tv_ctx {
 
     bool open_rw = true;               // TV_OPT_OPEN_RW: files opened read + write (fsStorage.get) or read-only
     bool stream_rows = false;          // TV_OPT_STREAM_ROWS: stream requests carry whole pieces (windows of pieces)
+    bool clock_probe = false;          // TV_OPT_CLOCK_PROBE: verify / hash launches stamp their clock into d_clock
+    uint64_t* d_clock = nullptr;       // {shader clock, real-time} counters at the start and end of workgroup 0
     cpu_set_t proc_cpus;               // the process's CPUs at tv_create (what "unpinned" workers run on)
     bool proc_cpus_ok = false;
 };
@@ -690,6 +692,7 @@ TvPieces resident_launch(const tv_ctx* c) {
     p.avail64 = c->d_base_avail;
     p.out64 = c->d_out;
     p.out_digests = c->d_hash;
+    p.clock = c->clock_probe ? c->d_clock : nullptr;
     return p;
 }
 
@@ -1471,6 +1474,7 @@ void tv_destroy(tv_ctx* c) {
         if (c->ring2_ev[s]) (void)hipEventDestroy(c->ring2_ev[s]);
     }
     if (c->h_bits) (void)hipHostFree(c->h_bits);
+    if (c->d_clock) (void)hipFree(c->d_clock);
     for (hipEvent_t ev : {c->ev_call0, c->ev_k0, c->ev_k1, c->ev_call1, c->ev_avail, c->col_ev[0], c->col_ev[1],
                           c->done_ev[0], c->done_ev[1], c->ev_fork, c->ev_join, c->win_ev[0], c->win_ev[1],
                           c->win_cp[0], c->win_cp[1]})
@@ -1577,6 +1581,15 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
             if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_OPEN_RW must be 0 or 1");
             c->open_rw = value != 0;
             return TV_OK;
+        case TV_OPT_CLOCK_PROBE:
+            if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_CLOCK_PROBE must be 0 or 1");
+            if (value && !c->d_clock) {
+                TV_HIP(c, hipSetDevice(c->device));
+                TV_HIP(c, hipMalloc((void**)&c->d_clock, 4 * sizeof(uint64_t)));
+                TV_HIP(c, hipMemset(c->d_clock, 0, 4 * sizeof(uint64_t)));
+            }
+            c->clock_probe = value != 0;
+            return TV_OK;
         case TV_OPT_STREAM_ROWS:
             if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_STREAM_ROWS must be 0 or 1");
             if (c->st.active) return fail(c, TV_ERR_STATE, "TV_OPT_STREAM_ROWS cannot change during a stream");
@@ -1609,6 +1622,7 @@ int tv_get_option(tv_ctx* c, int key, int64_t* value) {
         case TV_OPT_LIST_SLOTS: *value = (int64_t)c->list_slots_opt; return TV_OK;
         case TV_OPT_OPEN_RW: *value = c->open_rw ? 1 : 0; return TV_OK;
         case TV_OPT_STREAM_ROWS: *value = c->stream_rows ? 1 : 0; return TV_OK;
+        case TV_OPT_CLOCK_PROBE: *value = c->clock_probe ? 1 : 0; return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
@@ -2433,6 +2447,7 @@ int tv_verify_list(tv_ctx* c, const uint64_t* pieces, uint64_t n, uint8_t* ok_ou
         p.n_main = (uint32_t)m;
         p.idx = c->d_list;
         p.rows = c->slots ? c->d_list + m : nullptr;
+        p.clock = nullptr;
         p.out_bytes = c->d_list_out;
         TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
         // twin (two lanes per piece) while its 2-wave workgroups fit two per CU, then split (rounds + helper pair,
@@ -2710,6 +2725,17 @@ int tv_get_counter(tv_ctx* c, int key, uint64_t* value) {
         case TV_COUNTER_WINDOWS: *value = c->win_launched; return TV_OK;
         case TV_COUNTER_BUDGET: *value = c->budget; return TV_OK;
         case TV_COUNTER_SLOTS_USED: *value = c->slot_of.size(); return TV_OK;
+        case TV_COUNTER_LAST_CLOCK_KHZ: {
+            *value = 0;
+            if (!c->d_clock) return TV_OK;
+            uint64_t st[4] = {0, 0, 0, 0};
+            TV_HIP(c, hipSetDevice(c->device));
+            TV_HIP(c, hipStreamSynchronize(c->stream));
+            TV_HIP(c, hipMemcpy(st, c->d_clock, sizeof st, hipMemcpyDeviceToHost));
+            if (st[3] > st[1] && st[2] > st[0])   // shader cycles / real-time ticks x 100 MHz
+                *value = (uint64_t)((double)(st[2] - st[0]) / (double)(st[3] - st[1]) * 100000.0 + 0.5);
+            return TV_OK;
+        }
     }
     return fail(c, TV_ERR_ARG, "unknown counter %d", key);
 }

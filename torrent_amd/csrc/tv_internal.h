@@ -41,6 +41,8 @@ struct TvPieces {
     const uint32_t* rows;    // list mode with a slot pool (TV_OPT_LIST_SLOTS): entry j's bytes are payload row
                              // rows[j] (data + rows[j]*stride) while digests / length / availability stay those of
                              // piece idx[j]; null = row idx[j]
+    uint64_t* clock;         // TV_OPT_CLOCK_PROBE: lane 0 of workgroup 0's (rounds) wave stores {shader clock counter,
+                             // 100 MHz real-time counter} at its start and end here (4 words); null = off
 };
 
 // workgroups (optional): set to the launch's grid size, companions included.

@@ -185,6 +185,26 @@ __device__ __forceinline__ void finish(const TvPieces& p, bool writer, uint32_t 
     }
 }
 
+// Clock probe (TV_OPT_CLOCK_PROBE): workgroup 0 reads the shader clock counter (s_memtime) and the 100 MHz
+// real-time counter (s_memrealtime) when it starts; lane 0 of its first (rounds) wave writes both pairs with a
+// vector store when it ends.  The ratio of the two intervals is the shader clock the kernel actually ran at.
+struct ClockStamp {
+    uint64_t t0 = 0, r0 = 0;
+    __device__ __forceinline__ void start(const TvPieces& p) {
+        if (p.clock && blockIdx.x == 0) {   // (kernel argument and block index: a scalar branch)
+            t0 = __builtin_amdgcn_s_memtime();
+            r0 = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+    __device__ __forceinline__ void end(const TvPieces& p) const {
+        if (p.clock && blockIdx.x == 0 && threadIdx.x == 0) {
+            const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+            reinterpret_cast<ulonglong2*>(p.clock)[0] = make_ulonglong2(t0, r0);
+            reinterpret_cast<ulonglong2*>(p.clock)[1] = make_ulonglong2(t1, r1);
+        }
+    }
+};
+
 __device__ __forceinline__ void start_state(const TvPieces& p, uint32_t jj, uint32_t h[5]) {
     if (p.blk_begin == 0) {
         sha1_iv(h);
@@ -227,6 +247,29 @@ __device__ __forceinline__ void lane_group(const TvPieces& p, uint32_t gw) {
 
     uint32_t b = g.fast_begin;
     uint32_t w[16];
+#ifdef TV_LANE_PAIRS
+    if (b < g.fast_end) {
+        // (A/B variant, D_TV_LANE_PAIRS) a ring of 4 register blocks refilled in PAIRS: a lane's two 64-B blocks
+        // of one 128-B line are loaded back to back, so both halves reach L2 together
+        const uint32_t last = g.fast_end - 1;
+        uint4 R[4][4];
+#pragma unroll
+        for (int d = 0; d < 4; d++) load_block(piece, b + d < last ? b + d : last, R[d]);
+        for (;;) {
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                bswap_block(R[2 * q], w);
+                compress_full(h, w);
+                if (++b >= g.fast_end) goto raw_done;
+                bswap_block(R[2 * q + 1], w);
+                load_block(piece, b + 3 < last ? b + 3 : last, R[2 * q]);
+                load_block(piece, b + 4 < last ? b + 4 : last, R[2 * q + 1]);
+                compress_full(h, w);
+                if (++b >= g.fast_end) goto raw_done;
+            }
+        }
+    }
+#else
     if (b < g.fast_end) {
         // TV_LANE_DEPTH register blocks in flight.  Loads are unconditional (the block index is clamped
         // to the last raw block), so they are never predicated and stay in flight across a block.
@@ -245,6 +288,7 @@ __device__ __forceinline__ void lane_group(const TvPieces& p, uint32_t gw) {
             }
         }
     }
+#endif
 raw_done:
     for (; b < g.end; b++) {
         build_tail_block(piece, len, b, w);
@@ -267,7 +311,10 @@ __global__ __launch_bounds__(256) void tv_lane_kernel(TvPieces p) {
 #ifdef TV_LANE_PAD
     asm volatile(".p2align 6\n.rept " TV_STR(TV_LANE_PAD) "\ns_nop 0\n.endr\n" ::: "memory");
 #endif
+    ClockStamp clk;
+    clk.start(p);
     lane_group<HASH>(p, blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+    clk.end(p);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -401,7 +448,10 @@ __device__ __forceinline__ void split_group(const TvPieces& p, uint32_t wgi, uin
 template <bool HASH, int PAIRS, bool LIST = false>
 __global__ __launch_bounds__(128 * PAIRS) void tv_split_kernel(TvPieces p) {
     __shared__ __attribute__((aligned(16))) uint4 ring[kBufs * PAIRS * kRingWords / 4];
+    ClockStamp clk;
+    clk.start(p);
     split_group<HASH, PAIRS, LIST>(p, blockIdx.x, ring, [] { return true; });
+    clk.end(p);   // (the rounds wave, wave 0, returns from split_group last)
 }
 
 // ------------------------------------------------------------------------------------------
@@ -498,6 +548,8 @@ __global__ __launch_bounds__(64 * kTwinWaves[SHAPE]) void tv_twin_kernel(TvPiece
     const uint8_t* piece = p.data + (uint64_t)row * p.stride - p.data_off;
     const uint32_t b0 = g.fast_begin, end = g.end, fast_end = g.fast_end;
     const uint32_t lds_lane = (uint32_t)(uintptr_t)(void*)ring + half * 1024u + lane * 16u;
+    ClockStamp clk;
+    clk.start(p);
 
     if (role == 2) {   // idle wave: the same number of barriers as the others (end - b0 + 1)
         for (uint32_t b = b0; b <= end; b++) lds_barrier();
@@ -546,6 +598,7 @@ __global__ __launch_bounds__(64 * kTwinWaves[SHAPE]) void tv_twin_kernel(TvPiece
         }
         lds_barrier();
     }
+    clk.end(p);              // (wave 0 is a rounds wave in every shape)
     if (companion) return;   // its digests duplicate a main workgroup's: nothing to write
     if (LIST) {
         if (j < p.n && (lane & 1u) == 0) {
