@@ -317,6 +317,10 @@ int tv_host_unregister(void *ptr);
 #define TV_OPT_CLOCK_PROBE 20     /* 1: verify / hash launches (resident, windows, stream units) record the shader clock
                                      they ran at (workgroup 0 reads the shader and 100 MHz real-time counters at its
                                      start and end; TV_COUNTER_LAST_CLOCK_KHZ).  0 (default) = off */
+#define TV_OPT_LANE_PAIRS 21      /* lane kernel loads: 0 (default) = auto: a lane's two 64-B blocks of a 128-B line loaded
+                                     back to back when the launch has >= 256 x CUs pieces (>= 1 wave per SIMD; HBM reads
+                                     1.0004 instead of 1.023 x payload at 262,144 x 64 KiB), else a 3-deep ring of
+                                     single blocks; 1 = pairs always; 2 = never */
 int tv_set_option(tv_ctx *ctx, int key, int64_t value);
 int tv_get_option(tv_ctx *ctx, int key, int64_t *value);
 

@@ -10,12 +10,16 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = [1, 2, 4]  # lane, split, twin
+# lane (3-deep ring of single-block loads), split, twin, and 101 = the lane kernel with pair loads (TV_OPT_LANE_PAIRS:
+# the auto rule picks pairs only at >= 256 x CUs pieces, so both lane forms are forced here)
+KERNELS = [1, 2, 4, 101]
 
 
 def _ctx(native, kernel=0):
     c = native.Context(0)
-    c.set_option(native.TV_OPT_KERNEL, kernel)
+    c.set_option(native.TV_OPT_KERNEL, 1 if kernel == 101 else kernel)
+    if kernel in (1, 101):
+        c.set_option(native.TV_OPT_LANE_PAIRS, 1 if kernel == 101 else 2)
     return c
 
 

@@ -223,6 +223,11 @@ def test_full_size_cfg4_oracle_ground_truth(native, oracle):
             assert ctx.last_kernel()[0] == k
             got = {i for i in range(P) if not (bf[i >> 3] >> (7 - (i & 7))) & 1}
             assert got == bad, (k, sorted(got ^ bad)[:10])
+        ctx.set_option(native.TV_OPT_KERNEL, 1)
+        ctx.set_option(native.TV_OPT_LANE_PAIRS, 1)        # the lane kernel's pair loads (auto picks them >= 65,536)
+        bf = ctx.verify()
+        got = {i for i in range(P) if not (bf[i >> 3] >> (7 - (i & 7))) & 1}
+        assert got == bad, ("lane pairs", sorted(got ^ bad)[:10])
     first, count = shard_ranges(P, 8)[7]
     assert (first, count) == (44800, 6400)
     with native.Context(0) as ctx:

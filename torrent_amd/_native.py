@@ -41,6 +41,7 @@ TV_OPT_LIST_SLOTS = 17
 TV_OPT_OPEN_RW = 18
 TV_OPT_STREAM_ROWS = 19
 TV_OPT_CLOCK_PROBE = 20
+TV_OPT_LANE_PAIRS = 21
 
 TV_COUNTER_PAYLOAD_ALLOCS = 1
 TV_COUNTER_DEVICE_ALLOCS = 2

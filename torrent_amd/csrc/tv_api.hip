@@ -356,6 +356,7 @@ struct tv_ctx {
 
     bool open_rw = true;               // TV_OPT_OPEN_RW: files opened read + write (fsStorage.get) or read-only
     bool stream_rows = false;          // TV_OPT_STREAM_ROWS: stream requests carry whole pieces (windows of pieces)
+    int lane_pairs = 0;                // TV_OPT_LANE_PAIRS: 0 auto (>= 256 x CUs pieces in the launch), 1 on, 2 off
     bool clock_probe = false;          // TV_OPT_CLOCK_PROBE: verify / hash launches stamp their clock into d_clock
     uint64_t* d_clock = nullptr;       // {shader clock, real-time} counters at the start and end of workgroup 0
     cpu_set_t proc_cpus;               // the process's CPUs at tv_create (what "unpinned" workers run on)
@@ -631,10 +632,19 @@ int choose_kernel(const tv_ctx* c) {
     return choose_kernel_n(c, c->count, short_last);
 }
 
+// The lane kernel's loads for a launch of n pieces: pairs once every SIMD holds a wave (>= 64 lanes x 4 SIMDs x
+// CUs pieces; TV_OPT_LANE_PAIRS overrides).
+uint32_t lane_pairs_for(const tv_ctx* c, uint64_t n) {
+    if (c->lane_pairs == 1) return 1;
+    if (c->lane_pairs == 2) return 0;
+    return n >= 256ull * (uint64_t)c->cus ? 1u : 0u;
+}
+
 // One launch over the resident shard with the chosen kernel (TV_OPT_TWIN_PACK: on the CU-masked pack_stream,
 // forked after everything queued on c->stream and joined back into it).
 int launch_resident(tv_ctx* c, const TvPieces& p_in, int kernel, bool hash) {
     TvPieces p = p_in;
+    p.lane_pairs = lane_pairs_for(c, p.n);
     // A CU running ONE 2-wave twin workgroup spends ~80 more shader cycles per block than one running two
     // (PMC GRBM_GUI_ACTIVE: 1,806 vs 1,727; sleeping fillers do not help, working ones do: DESIGN.md section 5).
     // With fewer real workgroups than 2 per CU, companions fill the grid to 2 x CUs: they re-hash main
@@ -1362,6 +1372,7 @@ int stream_commit_locked(tv_ctx* c, const tv_stream_req* req, const uint8_t* src
     p.blk_end = last ? UINT64_MAX : (r.offset + st.C) / 64;
     p.finalize = last ? 1 : 0;
     st.kernel = choose_kernel_n(c, wcount, p.n_main < p.n);
+    p.lane_pairs = lane_pairs_for(c, p.n);
     TV_HIP(c, tv_launch_verify(p, st.kernel, false, c->stream, c->split_pairs, &c->last_workgroups));
     TV_HIP(c, hipEventRecord(c->done_ev[buf], c->stream));
     st.unit++;
@@ -1581,6 +1592,10 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
             if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_OPEN_RW must be 0 or 1");
             c->open_rw = value != 0;
             return TV_OK;
+        case TV_OPT_LANE_PAIRS:
+            if (value < 0 || value > 2) return fail(c, TV_ERR_ARG, "TV_OPT_LANE_PAIRS must be 0 (auto), 1 (on) or 2 (off)");
+            c->lane_pairs = (int)value;
+            return TV_OK;
         case TV_OPT_CLOCK_PROBE:
             if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_CLOCK_PROBE must be 0 or 1");
             if (value && !c->d_clock) {
@@ -1623,6 +1638,7 @@ int tv_get_option(tv_ctx* c, int key, int64_t* value) {
         case TV_OPT_OPEN_RW: *value = c->open_rw ? 1 : 0; return TV_OK;
         case TV_OPT_STREAM_ROWS: *value = c->stream_rows ? 1 : 0; return TV_OK;
         case TV_OPT_CLOCK_PROBE: *value = c->clock_probe ? 1 : 0; return TV_OK;
+        case TV_OPT_LANE_PAIRS: *value = c->lane_pairs; return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }

@@ -43,6 +43,8 @@ struct TvPieces {
                              // piece idx[j]; null = row idx[j]
     uint64_t* clock;         // TV_OPT_CLOCK_PROBE: lane 0 of workgroup 0's (rounds) wave stores {shader clock counter,
                              // 100 MHz real-time counter} at its start and end here (4 words); null = off
+    uint32_t lane_pairs;     // host-side choice for the lane kernel: 1 = the pair-load instantiation (a lane's two
+                             // 64-B blocks of a 128-B line loaded back to back; >= 1 wave per SIMD), 0 = 3-deep ring
 };
 
 // workgroups (optional): set to the launch's grid size, companions included.

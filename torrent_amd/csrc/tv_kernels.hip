@@ -226,7 +226,12 @@ __device__ __forceinline__ void start_state(const TvPieces& p, uint32_t jj, uint
 
 // Wave-group gw of a launch: pieces [64 gw, 64 gw + 64) (clamped to n_main), or, for gw == the first group
 // past n_main, the short last piece alone.  Blocks [blk_begin, blk_end) of p.
-template <bool HASH>
+// PAIRS: the raw-block loop's register ring holds 4 blocks refilled two at a time, so a lane's two 64-B blocks of
+// one 128-B line are requested back to back.  With >= 1 wave per SIMD (>= 65,536 pieces on 256 CUs) the single
+// loads of the 3-deep ring let ~2 % of the lines be evicted between their two halves (HBM reads 1.023 x payload
+// at 262,144 x 64 KiB, L2 hit 35 %); pairs read 1.0004 x and run 0.3-2.6 % faster there, but 0.4-0.8 % slower
+// below one wave per SIMD (profiles/r04/variants/ab_lane_pairs_sweep.jsonl), so the host picks (lane_pairs).
+template <bool HASH, bool PAIRS>
 __device__ __forceinline__ void lane_group(const TvPieces& p, uint32_t gw) {
     const uint32_t lane = threadIdx.x & 63u;
     // main waves cover [0, n_main); a short last piece (n_main < n) gets the wave after them alone
@@ -247,10 +252,9 @@ __device__ __forceinline__ void lane_group(const TvPieces& p, uint32_t gw) {
 
     uint32_t b = g.fast_begin;
     uint32_t w[16];
-#ifdef TV_LANE_PAIRS
-    if (b < g.fast_end) {
-        // (A/B variant, D_TV_LANE_PAIRS) a ring of 4 register blocks refilled in PAIRS: a lane's two 64-B blocks
-        // of one 128-B line are loaded back to back, so both halves reach L2 together
+    if (PAIRS && b < g.fast_end) {
+        // a ring of 4 register blocks refilled in pairs: a lane's two 64-B blocks of one 128-B line are loaded
+        // back to back, so both halves reach L2 together
         const uint32_t last = g.fast_end - 1;
         uint4 R[4][4];
 #pragma unroll
@@ -269,8 +273,7 @@ __device__ __forceinline__ void lane_group(const TvPieces& p, uint32_t gw) {
             }
         }
     }
-#else
-    if (b < g.fast_end) {
+    if (!PAIRS && b < g.fast_end) {
         // TV_LANE_DEPTH register blocks in flight.  Loads are unconditional (the block index is clamped
         // to the last raw block), so they are never predicated and stay in flight across a block.
         constexpr int D = TV_LANE_DEPTH;
@@ -288,7 +291,6 @@ __device__ __forceinline__ void lane_group(const TvPieces& p, uint32_t gw) {
             }
         }
     }
-#endif
 raw_done:
     for (; b < g.end; b++) {
         build_tail_block(piece, len, b, w);
@@ -306,14 +308,14 @@ raw_done:
 // moves the raw-block loop through the 16 word positions of a 64-byte line (tools/build_variants.py D_TV_LANE_PAD)
 #define TV_STR2(x) #x
 #define TV_STR(x) TV_STR2(x)
-template <bool HASH>
+template <bool HASH, bool PAIRS>
 __global__ __launch_bounds__(256) void tv_lane_kernel(TvPieces p) {
 #ifdef TV_LANE_PAD
     asm volatile(".p2align 6\n.rept " TV_STR(TV_LANE_PAD) "\ns_nop 0\n.endr\n" ::: "memory");
 #endif
     ClockStamp clk;
     clk.start(p);
-    lane_group<HASH>(p, blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+    lane_group<HASH, PAIRS>(p, blockIdx.x * 4u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
     clk.end(p);
 }
 
@@ -765,8 +767,13 @@ hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_
         const unsigned waves = (p.n_main + 63) / 64 + (p.n_main < p.n ? 1 : 0);
         const unsigned grid = (waves + 3) / 4;
         if (workgroups) *workgroups = grid;
-        if (hash) hipLaunchKernelGGL(tv_lane_kernel<true>, dim3(grid), dim3(256), 0, s, p);
-        else hipLaunchKernelGGL(tv_lane_kernel<false>, dim3(grid), dim3(256), 0, s, p);
+        if (p.lane_pairs) {
+            if (hash) hipLaunchKernelGGL((tv_lane_kernel<true, true>), dim3(grid), dim3(256), 0, s, p);
+            else hipLaunchKernelGGL((tv_lane_kernel<false, true>), dim3(grid), dim3(256), 0, s, p);
+        } else {
+            if (hash) hipLaunchKernelGGL((tv_lane_kernel<true, false>), dim3(grid), dim3(256), 0, s, p);
+            else hipLaunchKernelGGL((tv_lane_kernel<false, false>), dim3(grid), dim3(256), 0, s, p);
+        }
     }
     return hipGetLastError();
 }
