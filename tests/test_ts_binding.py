@@ -719,3 +719,94 @@ import("{mod}").then(async (m) => {{
     assert res["shard"]["polled"] == [[8, True], [9, True], [10, True], [11, True]] and res["shard"]["fin"] == []
     assert res["shard"]["slots"] == 2 and res["shard"]["badShardThrows"]
     assert res["order"] == {"fin": [[0, True]], "autoFlushes": 1}
+
+
+def test_binding_stays_within_its_minimum_deno(tmp_path):
+    """ts/verify.ts states its minimum Deno (1.31: pointer objects, UnsafePointer.create / value; nonblocking
+    symbols): its code uses no Deno member outside that version's FFI surface (tests/ts_harness/deno_api.js), its
+    whole symbol table passes the harness's 1.31 check (both shims apply it at dlopen), and a table using a newer
+    FFI feature -- a struct type (1.35), an `optional` symbol (1.36), a "bool" result -- is rejected."""
+    import re
+    src = open(os.path.join(ROOT, "ts", "verify.ts")).read()
+    assert "Deno 1.31" in src.split("\nimport ")[0]                              # the header states it
+    assert "1.31" in open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    code = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    code = "\n".join(line.split("//")[0] for line in code.splitlines())         # (no // inside strings here)
+    used = set(re.findall(r"Deno\.([A-Za-z]+(?:\.[A-Za-z]+)?)", code))
+    out = run_node(tmp_path, f"""
+import {{ createRequire }} from "module";
+const require = createRequire("{HARNESS}/");
+const Deno = require("./fake_deno.js");
+const api = require("./deno_api.js");
+const res = {{ surface: api.SURFACE, min: api.MIN_VERSION, rejected: [] }};
+const probes = {{
+  struct: {{ f: {{ parameters: [{{ struct: ["u8", "u32"] }}], result: "void" }} }},
+  optional: {{ f: {{ parameters: [], result: "i32", optional: true }} }},
+  bool: {{ f: {{ parameters: [], result: "bool" }} }},
+}};
+for (const [k, table] of Object.entries(probes)) {{
+  try {{ Deno.dlopen("x", table); }} catch (e) {{ res.rejected.push(k); }}
+}}
+import("{erased_module(tmp_path)}").then(async (m) => {{
+  // the binding's own table binds through the checked dlopen (a zero-piece call loads it)
+  const info = {{ pieceLength: 16384, length: 0, pieces: [], name: "t", private: 0 }};
+  res.bound = (await m.verifyPieces(info, {{ async get() {{ return null; }} }})).length === 0;
+  console.log(JSON.stringify(res));
+}}).catch((e) => {{ console.error(e); process.exit(1); }});
+""")
+    res = json.loads(out)
+    assert res["min"] == "1.31" and res["bound"]
+    assert sorted(res["rejected"]) == ["bool", "optional", "struct"]
+    assert used <= set(res["surface"]), used - set(res["surface"])
+
+
+def test_opt_in_cpu_path_on_cpu(tmp_path):
+    """The opt-in CPU path runs the reference's own crypto.subtle.digest("SHA-1", ...)
+    (tools/make_torrent.ts:28-31; here Node's SHA-1 stands in for WebCrypto, which Node 12 lacks): verifyPiece
+    with cpuFallback never loads the library (a missing libPath still answers) and gives hashlib's answer;
+    PieceVerifier with cpuFallbackMaxPieces = 3 hashes a flush of <= 3 pieces on the CPU (no list launch, nothing
+    staged) and sends a longer one to the library (staged at the flush, one tv_verify_list), with identical bits
+    either way, a corrupted piece included.  Off by default."""
+    mod = erased_module(tmp_path)
+    out = run_node(tmp_path, f"""
+import {{ createRequire }} from "module";
+const require = createRequire("{HARNESS}/");
+const Deno = require("./fake_deno.js");
+const nodeCrypto = require("crypto");
+globalThis.crypto = {{ subtle: {{ async digest(alg, data) {{
+  if (alg !== "SHA-1") throw new Error(alg);
+  const b = nodeCrypto.createHash("sha1").update(Buffer.from(data)).digest();
+  return b.buffer.slice(b.byteOffset, b.byteOffset + 20);
+}} }} }};
+import("{mod}").then(async (m) => {{
+  const L = 32768, P = 12, total = L * P;
+  const payload = nodeCrypto.randomBytes(total);
+  const pieces = [];
+  for (let i = 0; i < P; i++) pieces.push(nodeCrypto.createHash("sha1").update(payload.slice(i * L, (i + 1) * L)).digest());
+  const info = {{ pieceLength: L, length: total, pieces, name: "t", private: 0 }};
+  const res = {{}};
+  res.piece = [await m.verifyPiece(info, 3, payload.slice(3 * L, 4 * L), {{ cpuFallback: true, libPath: "/nonexistent.so" }}),
+               await m.verifyPiece(info, 3, Buffer.alloc(L), {{ cpuFallback: true, libPath: "/nonexistent.so" }})];
+  const pv = new m.PieceVerifier(info, {{ flushPieces: null, flushAgeMs: null, cpuFallbackMaxPieces: 3 }});
+  const c = [...Deno.fakeContexts.values()].pop();
+  const feed = async (i, bad) => {{
+    for (const o of [0, 16384]) {{
+      const b = Buffer.from(payload.slice(i * L + o, i * L + o + 16384));
+      if (bad && o === 0) b[7] ^= 1;
+      await pv.onBlock(i, o, b);
+    }}
+  }};
+  await feed(0); await feed(1, true);
+  res.short = {{ out: await pv.flush(), lists: c.lists || 0, staged: c.staged.size }};
+  for (let i = 2; i < 7; i++) await feed(i, i === 5);
+  res.long = {{ out: await pv.flush(), lists: c.lists || 0 }};
+  res.bits = Array.from({{ length: P }}, (_, i) => (pv.bitfield[i >> 3] >> (7 - (i % 8))) & 1).join("");
+  pv.close();
+  console.log(JSON.stringify(res));
+}}).catch((e) => {{ console.error(e); process.exit(1); }});
+""")
+    res = json.loads(out)
+    assert res["piece"] == [True, False]
+    assert res["short"] == {"out": [[0, True], [1, False]], "lists": 0, "staged": 0}
+    assert res["long"] == {"out": [[2, True], [3, True], [4, True], [5, False], [6, True]], "lists": 1}
+    assert res["bits"] == "101110100000"

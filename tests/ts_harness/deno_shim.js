@@ -10,6 +10,7 @@
 "use strict";
 const path = require("path");
 const native = require(path.join(__dirname, "deno_ffi.node"));
+const api = require("./deno_api.js");   // the FFI surface of the binding's minimum Deno (1.31)
 
 function arg(kind, v) {
   switch (kind) {
@@ -28,6 +29,7 @@ function arg(kind, v) {
 
 const Deno = {
   dlopen(file, symbols) {
+    api.checkSymbols(symbols);
     const h = native.open(file);
     const out = {};
     for (const name of Object.keys(symbols)) {

@@ -12,6 +12,7 @@
 // taken returns TV_ERR_STATE (-3), as the library does.
 "use strict";
 const crypto = require("crypto");
+const api = require("./deno_api.js");   // the FFI surface of the binding's minimum Deno (1.31)
 
 const contexts = new Map();
 let nextHandle = 1n;
@@ -206,6 +207,7 @@ const impl = {
 
 const Deno = {
   dlopen(_path, symbols) {
+    api.checkSymbols(symbols);
     const out = {};
     for (const name of Object.keys(symbols)) {
       const f = impl[name] || (() => {

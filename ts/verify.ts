@@ -6,7 +6,10 @@
 // Torrent are unaffected.  The SHA-1 arithmetic that the reference runs through
 // crypto.subtle.digest("SHA-1", content) (tools/make_torrent.ts:28-31) runs on the GPU here.
 //
-// Requires: deno run --unstable --allow-ffi (Deno 1.x, as the reference CI: .github/workflows/main.yml:14).
+// Requires: Deno 1.31 or newer (the pointer-object FFI: Deno.UnsafePointer.create / .value and Deno.PointerValue
+// objects; `nonblocking` symbols, 1.15), run as deno run --unstable --allow-ffi (Deno 1.x, as the reference CI:
+// .github/workflows/main.yml:13-14, deno-version v1.x).  tests/ts_harness/deno_api.js holds that version's FFI
+// surface, and both harness shims reject a symbol table that goes beyond it.
 // Deno is not installed in the build container: tests/test_ts_binding.py runs this file under Node 12 with an
 // N-API shim of Deno's FFI on the GPU (tests/ts_harness/deno_shim.js) and against a JS model of the library
 // on CPU (tests/ts_harness/fake_deno.js).
@@ -69,6 +72,17 @@ export interface VerifyOptions {
   /** bytes of device memory the payload may take per device (default: the GPU's free memory less a margin); a
    * shard larger than it is verified in windows of pieces that fit, each hashed while the next one stages */
   budget?: number;
+  /** verifyPiece only: hash on the CPU with the reference's own crypto.subtle.digest("SHA-1", bytes)
+   * (tools/make_torrent.ts:28-31) instead of a ~3 ms GPU launch.  Off by default */
+  cpuFallback?: boolean;
+}
+
+/** SHA-1(bytes) === digest through WebCrypto, the reference's SHA-1 path (make_torrent.ts:28-31). */
+async function cpuPieceOk(bytes: Uint8Array, digest: Uint8Array): Promise<boolean> {
+  if (digest.length !== 20) return false;
+  const d = new Uint8Array(await crypto.subtle.digest("SHA-1", bytes));
+  for (let k = 0; k < 20; k++) if (d[k] !== digest[k]) return false;
+  return true;
 }
 
 const TV_OPT_RESIDENT_BUDGET = 16;
@@ -408,6 +422,7 @@ export async function verifyPiece(info: InfoDict, index: number, bytes: Uint8Arr
     throw new Error(`verifyPiece: invalid piece index ${index}`);
   }
   if (bytes.length !== pieceLength(index, info) || info.pieces[index].length !== 20) return false;
+  if (opts.cpuFallback) return await cpuPieceOk(bytes, info.pieces[index]);
   const l = load(opts.libPath);
   // its own cached context (slot -1): a one-piece layout on a bulk call's context would free that context's
   // payload (tv_set_layout keeps an allocation only while the new geometry is at least half of it)
@@ -456,6 +471,12 @@ export interface FlushPolicy {
   flushAgeMs?: number | null;
   /** results of automatic flushes (else they are returned by the next flush()) */
   onVerified?: (index: number, ok: boolean) => void;
+  /** flushes of at most this many pieces are hashed on the CPU with crypto.subtle.digest (the reference's SHA-1,
+   * make_torrent.ts:28-31) instead of one GPU list launch; completed pieces then wait host-side and are staged
+   * at the flush that goes to the GPU.  0 (default) = off.  The crossover (a GPU flush costs ~one piece's serial
+   * SHA-1 whatever the count, 3.0 ms at 256 KiB; a CPU core hashes 256 KiB in 0.2 ms with SHA-NI) is measured
+   * by tools/cpu_crossover.py (profiles/r04/cpu_crossover.json) */
+  cpuFallbackMaxPieces?: number;
 }
 
 /** GPU time of one list flush of pieces of `pieceLength` bytes: one piece's serial SHA-1, ~0.73 us per 64-B
@@ -498,6 +519,8 @@ export class PieceVerifier {
   #onVerified?: (index: number, ok: boolean) => void;
   #busy: Promise<unknown> = Promise.resolve(); // the verifier's library calls, one at a time, in order
   #timerError: unknown = null;   // a timer-driven flush that failed: rethrown by the next call
+  #cpuMax: number;               // cpuFallbackMaxPieces
+  #held = new Map<number, Uint8Array>();   // (cpuMax > 0) completed pieces' bytes, staged only if the flush is GPU
 
   readonly info: InfoDict;
 
@@ -515,6 +538,7 @@ export class PieceVerifier {
     this.#flushPieces = opts.flushPieces === undefined ? 4096 : opts.flushPieces;
     this.#flushAgeMs = opts.flushAgeMs === undefined ? Math.max(5, 10 * flushCostMs(info.pieceLength)) : opts.flushAgeMs;
     this.#onVerified = opts.onVerified;
+    this.#cpuMax = Math.max(0, Math.floor(opts.cpuFallbackMaxPieces || 0));
     const k = opts.slots !== undefined ? opts.slots : (this.#flushPieces !== null ? this.#flushPieces : 4096);
     this.slots = Math.max(1, Math.min(Math.floor(k), Math.max(1, count)));
     const h = new BigUint64Array(1);
@@ -562,7 +586,8 @@ export class PieceVerifier {
           this.forcedFlushes++;
           this._deliver(await this._flushLocked());
         }
-        check(this.#l, this.#ctx, await this.#l.symbols.tv_stage(this.#ctx, BigInt(index * this.info.pieceLength), ptr(bytes), BigInt(len)));
+        if (this.#cpuMax > 0) this.#held.set(index, bytes);   // staged (or hashed on the CPU) by its flush
+        else check(this.#l, this.#ctx, await this.#l.symbols.tv_stage(this.#ctx, BigInt(index * this.info.pieceLength), ptr(bytes), BigInt(len)));
         if (this.#pending.length === 0) {
           this.#oldest = performance.now();
           // the age bound also holds when no further block arrives
@@ -630,6 +655,20 @@ export class PieceVerifier {
     const pending = this.#pending;
     this.#pending = [];
     this.#pendingSet.clear();
+    if (this.#cpuMax > 0) {
+      const held = pending.map((i) => this.#held.get(i)!);
+      for (const i of pending) this.#held.delete(i);
+      if (pending.length <= this.#cpuMax) {   // a short flush: the reference's WebCrypto SHA-1 on the CPU
+        const oks = await Promise.all(pending.map((i, k) => cpuPieceOk(held[k], this.info.pieces[i])));
+        const res: [number, boolean][] = pending.map((i, k) => [i, oks[k]]);
+        for (const [i, good] of res) if (good) this.bitfield[i >> 3] |= 128 >> (i % 8);
+        return res;
+      }
+      for (let k = 0; k < pending.length; k++) {   // a long one: stage the held pieces, one list launch
+        check(this.#l, this.#ctx, await this.#l.symbols.tv_stage(this.#ctx, BigInt(pending[k] * this.info.pieceLength),
+                                                                 ptr(held[k]), BigInt(held[k].length)));
+      }
+    }
     const idx = BigUint64Array.from(pending.map(BigInt));
     const ok = new Uint8Array(idx.length);
     check(this.#l, this.#ctx, await this.#l.symbols.tv_verify_list(this.#ctx, ptr(new Uint8Array(idx.buffer)), BigInt(idx.length), ptr(ok)));
