@@ -20,7 +20,7 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
-KERNELS = {"lane": "_Z14tv_lane_kernelILb0EEv8TvPieces", "split": "_Z15tv_split_kernelILb0ELi1ELb0EEv8TvPieces",
+KERNELS = {"lane": "_Z14tv_lane_kernelILb0ELb0EEv8TvPieces", "lane_pairs": "_Z14tv_lane_kernelILb0ELb1EEv8TvPieces", "split": "_Z15tv_split_kernelILb0ELi1ELb0EEv8TvPieces",
            "twin": "_Z14tv_twin_kernelILb0ELi1ELb0EEv8TvPieces"}
 _INS = re.compile(r"\s+(\S.*?)\s+//\s*([0-9A-Fa-f]+):\s*((?:[0-9A-Fa-f]{8}\s*)+)")
 

@@ -65,6 +65,25 @@ K_IN_ROUNDS = os.environ.get("TV_GEN_KROUNDS", "0") == "1"  # split: the rounds 
 HELPER_X = os.environ.get("TV_GEN_HX", "")   # timing probes only: novalu / nowrite / noload (digests are wrong)
 ROUNDS_X = os.environ.get("TV_GEN_RX", "")   # timing probe only: nowait = the split rounds loop without its LDS-return
                                              # waits (digests are wrong; barriers unchanged)
+# Diagnostic builds only (tools/split_stamps.py): STAMP = 1 brackets the split kernel's in-loop barriers (rounds and
+# helper waves) with shader-clock reads into SGPRs s[88:91] and accumulates the cycles spent at them in an SGPR
+# operand; the kernels then need -DTV_STAMPS=1.  The default header is unchanged.
+# STAMP = 2 also brackets the helper's two waits per block: for its prefetched global words (vmcnt) and for its
+# LDS writes before the barrier (lgkmcnt), into %[svm] and %[slg].
+STAMP = int(os.environ.get("TV_GEN_STAMP", "0"))
+
+
+def _stamped(line: str, acc: str) -> list:
+    return ["s_memtime s[88:89]", line, "s_memtime s[90:91]", "s_waitcnt lgkmcnt(0)",
+            "s_sub_u32 s90, s90, s88", f"s_add_u32 %[{acc}], %[{acc}], s90"]
+
+
+STAMP_SEQ = _stamped("s_barrier", "sbar")
+# Split helper: where it waits for its LDS writes.  "0": lgkmcnt(0) before every barrier (block m's writes done
+# before barrier m - 1).  "mid": lgkmcnt(10) before the 11th write of block m + 1 instead -- block m is read
+# only after barrier m, and the next block's first 10 writes (issued after block m's, LDS counts in order) may
+# still be in flight; nothing waits at the barrier.
+HELPER_WAIT = os.environ.get("TV_GEN_HWAIT", "mid")
 LOOP_ALIGN = os.environ.get("TV_GEN_LALIGN", "1") == "1"  # split loops: .p2align 3 before every block body
 HELPER_AHEAD = LDS_BUFS - 1
 assert not PIPELINED or (LDS_BUFS >= 3 and RING_QUADS == 20), "the pipelined stream needs 3 buffers and a 20-quad ring"
@@ -476,7 +495,7 @@ def rounds_loop_text() -> str:
                 body = [x for x in body if not x.startswith("s_waitcnt")]
             L.extend(body)
             L.extend(f"v_add_u32 %[h{i}], %[h{i}], %[r{i}]" for i in range(5))
-            L.append("s_barrier")
+            L.extend(STAMP_SEQ if STAMP else ["s_barrier"])   # (every LDS read of the block has been waited)
         L += ["s_sub_u32 %[cnt], %[cnt], 1", "s_cmp_eq_u32 %[cnt], 0",
               "s_cbranch_scc1 L_rdone_%=" if k < LDS_BUFS - 1 else "s_cbranch_scc0 L_rloop_%="]
     L += ["L_rdone_%=:", "s_waitcnt lgkmcnt(0)"]
@@ -594,7 +613,7 @@ def helper_loop_text(twin: bool = False) -> str:
         L.append(f"v_lshl_add_u64 v[{VL}:{VL + 1}], v[{VL}:{VL + 1}], 0, %[inc]")
 
     def step(pbase, off_base, barrier=True):
-        L.append("s_waitcnt vmcnt(4)")
+        L.extend(_stamped("s_waitcnt vmcnt(4)", "svm") if STAMP >= 2 and not twin else ["s_waitcnt vmcnt(4)"])
         body = (gen_helper2 if twin else gen_helper)([f"v{pbase + i}" for i in range(16)], off_base)
         perms, rest = body[:16], body[16:]
         # timing-only experiments (wrong digests): drop a class of the helper's work, keep its barriers
@@ -610,10 +629,16 @@ def helper_loop_text(twin: bool = False) -> str:
         advance()
         if LOOP_ALIGN:
             L.append(".p2align 3")
+        if HELPER_WAIT == "mid" and not twin:
+            assert HELPER_AHEAD >= 2
+            k = [i for i, op in enumerate(rest) if op[0] == "ds_write_b128"][10]
+            rest = rest[:k] + [("s_waitcnt_lgkm", 10)] + rest[k:]
         L.extend(_emit_lines(rest))
-        if barrier:
-            L.append("s_waitcnt lgkmcnt(0)")
-            L.append("s_barrier")
+        if barrier and HELPER_WAIT == "mid" and not twin:
+            L.extend(STAMP_SEQ if STAMP else ["s_barrier"])
+        elif barrier:
+            L.extend(_stamped("s_waitcnt lgkmcnt(0)", "slg") if STAMP >= 2 and not twin else ["s_waitcnt lgkmcnt(0)"])
+            L.extend(STAMP_SEQ if STAMP and not twin else ["s_barrier"])
 
     L.append("s_sub_u32 %[adv], %[nraw], 1")
     L.append(f"v_mov_b64 v[{VL}:{VL + 1}], %[va]")
@@ -650,6 +675,8 @@ def helper_loop_text(twin: bool = False) -> str:
         L.append("s_cmp_eq_u32 %[cnt], 0")
         L.append("s_cbranch_scc1 L_hdone_%=" if k < period - 1 else "s_cbranch_scc0 L_hloop_%=")
     L.append("L_hdone_%=:")
+    if HELPER_WAIT == "mid" and not twin:
+        L.append("s_waitcnt lgkmcnt(0)")   # (no write of this statement left in flight for the compiler's code)
     L.append("s_waitcnt vmcnt(0)")
     return "\n".join(f'    "{l}\\n"' for l in L)
 
@@ -1218,6 +1245,28 @@ def render() -> str:
                              ring_clobbers=ring, twin_helper_clobbers=h2, twin_loop_clobbers=h2loop, addr2=addr2))
 
 
+def _stamp_patch(txt: str) -> str:
+    """STAMP builds: give tv_sha1_rounds_loop and tv_sha1_helper_loop an accumulator argument `sbar` (cycles at
+    the in-loop barriers) and the SGPRs the stamps use as clobbers."""
+    assert not (PIPELINED or SPLIT_MID or SPLIT_PRE), "stamps are for the shipped per-block split rounds loop"
+    for fn, sig_old, out_old in (
+            ("tv_sha1_rounds_loop", "uint32_t nsteps,\n", '[cnt] "=&s"(cnt)\n'),
+            ("tv_sha1_helper_loop", "uint32_t nraw, uint32_t addr,\n", '[inc] "=&s"(inc)\n')):
+        extra = fn == "tv_sha1_helper_loop" and STAMP >= 2
+        i = txt.index(f"void {fn}(")
+        j = txt.index("\n}\n", i)
+        seg = txt[i:j]
+        for old, new in ((sig_old, sig_old[:-2] + (", uint32_t& sbar, uint32_t& svm, uint32_t& slg,\n" if extra
+                                                    else ", uint32_t& sbar,\n")),
+                         (out_old, out_old[:-1] + ', [sbar] "+s"(sbar)' + (', [svm] "+s"(svm), [slg] "+s"(slg)' if extra
+                                                                          else "") + "\n"),
+                         ('"scc", "memory");', '"s88", "s89", "s90", "s91", "scc", "memory");')):
+            assert seg.count(old) == 1, (fn, old)
+            seg = seg.replace(old, new)
+        txt = txt[:i] + seg + txt[j:]
+    return txt.replace("#define TV_SHA1_K_IN_ROUNDS", f"#define TV_SHA1_STAMP {STAMP}\n#define TV_SHA1_K_IN_ROUNDS", 1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "torrent_amd", "csrc", "sha1_asm.h"))
@@ -1228,6 +1277,8 @@ def main():
         print("emulator self-check: ok")
         return
     txt = render()
+    if STAMP:
+        txt = _stamp_patch(txt)
     with open(a.out, "w") as f:
         f.write(txt)
     print(f"wrote {a.out}: FULL {len(gen_full())} instr, LDS {len(gen_lds())} instr, "

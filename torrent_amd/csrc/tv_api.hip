@@ -1600,8 +1600,8 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
             if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_CLOCK_PROBE must be 0 or 1");
             if (value && !c->d_clock) {
                 TV_HIP(c, hipSetDevice(c->device));
-                TV_HIP(c, hipMalloc((void**)&c->d_clock, 4 * sizeof(uint64_t)));
-                TV_HIP(c, hipMemset(c->d_clock, 0, 4 * sizeof(uint64_t)));
+                TV_HIP(c, hipMalloc((void**)&c->d_clock, kClockWords * sizeof(uint64_t)));
+                TV_HIP(c, hipMemset(c->d_clock, 0, kClockWords * sizeof(uint64_t)));
             }
             c->clock_probe = value != 0;
             return TV_OK;
@@ -2755,6 +2755,18 @@ int tv_get_counter(tv_ctx* c, int key, uint64_t* value) {
     }
     return fail(c, TV_ERR_ARG, "unknown counter %d", key);
 }
+
+#if TV_STAMPS
+// Diagnostic builds only (not in include/torrent_verify.h): copy the clock buffer (probe + split loop stamps).
+int tv_debug_stamps(tv_ctx* c, void* out, uint64_t bytes) {
+    if (!c || !out || !c->d_clock) return fail(c, TV_ERR_ARG, "no clock buffer (set TV_OPT_CLOCK_PROBE)");
+    if (bytes > kClockWords * sizeof(uint64_t)) bytes = kClockWords * sizeof(uint64_t);
+    TV_HIP(c, hipSetDevice(c->device));
+    TV_HIP(c, hipStreamSynchronize(c->stream));
+    TV_HIP(c, hipMemcpy(out, c->d_clock, bytes, hipMemcpyDeviceToHost));
+    return TV_OK;
+}
+#endif
 
 int tv_last_kernel(tv_ctx* c, int* kernel, int* launches) {
     if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");

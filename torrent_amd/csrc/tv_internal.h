@@ -10,6 +10,13 @@
 //  chosen, removed in round 3; the value stays unused)
 #define TV_KERNEL_TWIN 4    // split with two lanes per piece in the rounds waves (half the K+W reads per block)
 
+#ifndef TV_STAMPS
+#define TV_STAMPS 0   // 1: diagnostic split-kernel loop stamps (tools/split_stamps.py), never the shipped library
+#endif
+// words of the device clock buffer (TV_OPT_CLOCK_PROBE): the probe's 4, plus in TV_STAMPS builds 8 per wave of up
+// to 4 waves in each of 65,536 workgroups
+constexpr size_t kClockWords = 4 + (TV_STAMPS ? 8 * 4 * 65536 : 0);
+
 // One launch over a contiguous run of n pieces.  Piece j's byte k (piece-relative) is at
 // data + j*stride + k - data_off.  Blocks [blk_begin, min(blk_end, nb_j)) are processed.
 struct TvPieces {

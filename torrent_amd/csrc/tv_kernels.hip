@@ -338,6 +338,29 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+#if TV_STAMPS
+// Diagnostic builds (tools/split_stamps.py; generator TV_GEN_STAMP=1 + -DTV_STAMPS=1): each split wave's asm loop
+// time and the cycles its in-loop barriers (and, TV_SHA1_STAMP 2, the helper's vmcnt / lgkmcnt waits) took, per
+// workgroup and wave, after the clock probe's 4 words: clock[4 + 8 (4 wg + wave) ..] = {loop cycles, barrier
+// cycles, loop blocks, 1, vmcnt-wait cycles, lgkmcnt-wait cycles, 0, 0} (lane 0, vector stores).
+static_assert(TV_SHA1_STAMP, "TV_STAMPS needs the generator's TV_GEN_STAMP header");
+constexpr uint32_t kStampGroups = 65536;
+struct LoopStamp {
+    uint32_t bar = 0, vm = 0, lg = 0;
+    uint64_t t0 = 0;
+    __device__ __forceinline__ void start() { t0 = __builtin_amdgcn_s_memtime(); }
+    __device__ __forceinline__ void end(const TvPieces& p, uint32_t wave, uint32_t blocks) const {
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();
+        if (p.clock && blockIdx.x < kStampGroups && (threadIdx.x & 63u) == 0) {
+            uint64_t* q = p.clock + 4 + 8 * (4 * (uint64_t)blockIdx.x + wave);
+            reinterpret_cast<ulonglong2*>(q)[0] = make_ulonglong2(t1 - t0, bar);
+            reinterpret_cast<ulonglong2*>(q)[1] = make_ulonglong2(blocks, 1);
+            reinterpret_cast<ulonglong2*>(q)[2] = make_ulonglong2(vm, lg);
+        }
+    }
+};
+#endif
+
 }  // namespace
 
 __device__ __forceinline__ bool avail_bit(const uint64_t* a, uint32_t i) {
@@ -394,7 +417,19 @@ __device__ __forceinline__ void split_group(const TvPieces& p, uint32_t wgi, uin
         const uint32_t lds_lane = (uint32_t)(uintptr_t)(void*)pring + lane * 16u;
         uint32_t b = b0;
         if (fast_end > b0) {
+#if TV_STAMPS
+            LoopStamp st;
+            st.start();
+#if TV_SHA1_STAMP >= 2
+            tv_sha1_helper_loop(piece + (uint64_t)b0 * 64, fast_end - b0, lds_lane, st.bar, st.vm, st.lg,
+                                TV_K0, TV_K1, TV_K2, TV_K3);
+#else
+            tv_sha1_helper_loop(piece + (uint64_t)b0 * 64, fast_end - b0, lds_lane, st.bar, TV_K0, TV_K1, TV_K2, TV_K3);
+#endif
+            st.end(p, wave, fast_end - b0);
+#else
             tv_sha1_helper_loop(piece + (uint64_t)b0 * 64, fast_end - b0, lds_lane, TV_K0, TV_K1, TV_K2, TV_K3);
+#endif
             b = fast_end;
         }
         for (; b <= end; b++) {
@@ -422,7 +457,14 @@ __device__ __forceinline__ void split_group(const TvPieces& p, uint32_t wgi, uin
     // blocks where every lane of the wave updates: one asm loop (rounds, h += r, barrier)
     const uint32_t full_end = end < nb_min ? end : nb_min;
     if (b < full_end) {
+#if TV_STAMPS
+        LoopStamp st;
+        st.start();
+        tv_sha1_rounds_loop(h, ring_base, full_end - b, st.bar, TV_K0, TV_K1, TV_K2, TV_K3);
+        st.end(p, wave, full_end - b);
+#else
         tv_sha1_rounds_loop(h, ring_base, full_end - b, TV_K0, TV_K1, TV_K2, TV_K3);
+#endif
         b = full_end;
     }
     // the short last piece's wave: lanes past their final block keep their digest
