@@ -297,7 +297,7 @@ import("{mod}").then(async (m) => {{
     const fin = await pv.flush();
     res.count = {{ auto: got.length, autoFlushes: pv.autoFlushes, final: fin.length,
                    all: [...got, ...fin].filter(([, ok]) => ok).length }};
-    pv.close();
+    await pv.close();
   }}
   // age bound only, bursts and gaps
   for (let trial = 0; trial < 40; trial++) {{
@@ -317,7 +317,7 @@ import("{mod}").then(async (m) => {{
     const fin = await pv.flush();
     const have = Array.from({{ length: P }}, (_, i) => (pv.bitfield[i >> 3] >> (7 - (i % 8))) & 1);
     res.age.push({{ auto: got.length, final: fin.length, autoFlushes: pv.autoFlushes, have: have.join("") }});
-    pv.close();
+    await pv.close();
   }}
   console.log(JSON.stringify(res));
 }}).catch((e) => {{ console.error(e); process.exit(1); }});
@@ -610,7 +610,7 @@ import("{mod}").then(async (m) => {{
   const done = pv.onBlock(5, 16384, payload.slice(5 * L2 + 16384, 6 * L2));
   const resend = pv.onBlock(5, 0, Buffer.alloc(16384));
   res.verifier = {{ done: await done, resend: await resend, flush: await pv.flush() }};
-  pv.close();
+  await pv.close();
   console.log(JSON.stringify(res));
 }}).catch((e) => {{ console.error(e); process.exit(1); }});
 """)
@@ -683,7 +683,7 @@ import("{mod}").then(async (m) => {{
     const fin = await pv.flush();
     const c = [...Deno.fakeContexts.values()].pop();
     res.slots = {{ forced: pv.forcedFlushes, slots: pv.slots, max: c.maxStaged, opt: c.options[17], all: [...got, ...fin] }};
-    pv.close();
+    await pv.close();
   }}
   {{
     const pv = new m.PieceVerifier(info, {{ shard: [8, 8], flushPieces: 2, flushAgeMs: null }});
@@ -696,7 +696,7 @@ import("{mod}").then(async (m) => {{
     let bad = false;
     try {{ new m.PieceVerifier(info, {{ shard: [4, 8] }}); }} catch (e) {{ bad = true; }}
     res.shard.badShardThrows = bad;
-    pv.close();
+    await pv.close();
   }}
   {{
     Deno.fakeDelayMs = 20;
@@ -706,7 +706,21 @@ import("{mod}").then(async (m) => {{
     const fin = await pv.flush();
     res.order = {{ fin, autoFlushes: pv.autoFlushes }};
     Deno.fakeDelayMs = 0;
-    pv.close();
+    await pv.close();
+  }}
+  {{
+    // close() while the age timer's flush is inside its (slow) tv_verify_list: the context is destroyed only after
+    // it returns, its results still reach onVerified, and the verifier refuses further use
+    Deno.fakeDelayMs = 20;
+    const got = [];
+    const pv = new m.PieceVerifier(info, {{ flushPieces: null, flushAgeMs: 1, onVerified: (i, ok) => got.push([i, ok]) }});
+    for (const [x, o, b] of blocksOf(1)) await pv.onBlock(x, o, b);
+    await sleep(8);
+    await pv.close();
+    let threw = false;
+    try {{ await pv.onBlock(2, 0, payload.slice(2 * L, 2 * L + 16384)); }} catch (e) {{ threw = /closed/.test(String(e)); }}
+    Deno.fakeDelayMs = 0;
+    res.close = {{ got, violations: Deno.fakeViolations.slice(), threw }};
   }}
   console.log(JSON.stringify(res));
 }}).catch((e) => {{ console.error(e); process.exit(1); }});
@@ -718,6 +732,7 @@ import("{mod}").then(async (m) => {{
     assert res["shard"]["threw"] and res["shard"]["first"] == 8 and res["shard"]["count"] == 8
     assert res["shard"]["polled"] == [[8, True], [9, True], [10, True], [11, True]] and res["shard"]["fin"] == []
     assert res["shard"]["slots"] == 2 and res["shard"]["badShardThrows"]
+    assert res["close"] == {"got": [[1, True]], "violations": [], "threw": True}
     assert res["order"] == {"fin": [[0, True]], "autoFlushes": 1}
 
 
@@ -801,7 +816,7 @@ import("{mod}").then(async (m) => {{
   for (let i = 2; i < 7; i++) await feed(i, i === 5);
   res.long = {{ out: await pv.flush(), lists: c.lists || 0 }};
   res.bits = Array.from({{ length: P }}, (_, i) => (pv.bitfield[i >> 3] >> (7 - (i % 8))) & 1).join("");
-  pv.close();
+  await pv.close();
   console.log(JSON.stringify(res));
 }}).catch((e) => {{ console.error(e); process.exit(1); }});
 """)

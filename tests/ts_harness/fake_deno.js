@@ -200,6 +200,9 @@ const impl = {
     return 0;
   },
   tv_destroy(ctx) {
+    // the real library must not be destroyed beside a call still running on another thread
+    const c = contexts.get(ctx);
+    if (c && c.inflight > 0) Deno.fakeViolations.push("tv_destroy while a nonblocking call runs on the context");
     contexts.delete(ctx);
   },
   tv_last_error: () => 0,
@@ -215,7 +218,10 @@ const Deno = {
       });
       out[name] = symbols[name].nonblocking
         ? (...a) => new Promise((res, rej) => {
+          const c = name === "tv_create" ? null : contexts.get(a[0]);
+          if (c) c.inflight = (c.inflight || 0) + 1;
           const run = () => {
+            if (c) c.inflight--;
             try {
               res(f(...a));
             } catch (e) {
@@ -248,6 +254,7 @@ const Deno = {
   },
   fakeContexts: contexts,
   fakeDelayMs: 0,
+  fakeViolations: [],
   fakeReset() {
     contexts.clear();
     memory.clear();

@@ -78,7 +78,7 @@ async function main() {
         r.final = await pv.flush();
         r.completed = completed;
         r.bitfield = hex(pv.bitfield);
-        pv.close();
+        await pv.close();
       } else {
         throw new Error("unknown case kind " + c.kind);
       }

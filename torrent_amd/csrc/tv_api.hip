@@ -2759,7 +2759,9 @@ int tv_get_counter(tv_ctx* c, int key, uint64_t* value) {
 #if TV_STAMPS
 // Diagnostic builds only (not in include/torrent_verify.h): copy the clock buffer (probe + split loop stamps).
 int tv_debug_stamps(tv_ctx* c, void* out, uint64_t bytes) {
-    if (!c || !out || !c->d_clock) return fail(c, TV_ERR_ARG, "no clock buffer (set TV_OPT_CLOCK_PROBE)");
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!out || !c->d_clock) return fail(c, TV_ERR_ARG, "no clock buffer (set TV_OPT_CLOCK_PROBE)");
     if (bytes > kClockWords * sizeof(uint64_t)) bytes = kClockWords * sizeof(uint64_t);
     TV_HIP(c, hipSetDevice(c->device));
     TV_HIP(c, hipStreamSynchronize(c->stream));

@@ -521,6 +521,7 @@ export class PieceVerifier {
   #timerError: unknown = null;   // a timer-driven flush that failed: rethrown by the next call
   #cpuMax: number;               // cpuFallbackMaxPieces
   #held = new Map<number, Uint8Array>();   // (cpuMax > 0) completed pieces' bytes, staged only if the flush is GPU
+  #closed = false;
 
   readonly info: InfoDict;
 
@@ -561,6 +562,7 @@ export class PieceVerifier {
 
   /** One received block (already validated); true when it completed its piece. */
   async onBlock(index: number, offset: number, block: Uint8Array): Promise<boolean> {
+    this._open();
     this._rethrow();
     await this._autoFlush();                                  // the age bound, checked on every block
     if (index < this.first || index >= this.first + this.count) {
@@ -607,7 +609,7 @@ export class PieceVerifier {
   private _armTimer(delayMs: number): void {
     clearTimeout(this.#timer);
     this.#timer = setTimeout(() => {
-      if (this.#pending.length === 0) return;
+      if (this.#closed || this.#pending.length === 0) return;
       // timers are millisecond-granular and may fire a little before the oldest piece is flushAgeMs old:
       // then wait out the rest instead of leaving the pending pieces to the next block
       const wait = (this.#flushAgeMs || 0) - (performance.now() - this.#oldest);
@@ -619,6 +621,10 @@ export class PieceVerifier {
         this.#timerError = e;
       });
     }, delayMs);
+  }
+
+  private _open(): void {
+    if (this.#closed) throw new Error("PieceVerifier: closed");
   }
 
   private _rethrow(): void {
@@ -680,6 +686,7 @@ export class PieceVerifier {
   /** Verify all completed pieces in one launch; returns [index, ok] (after the results of automatic
    * flushes not yet handed out, including one still running when flush() was called) and sets the have-bits. */
   async flush(): Promise<[number, boolean][]> {
+    this._open();
     this._rethrow();
     return await this._serial(async () => {
       const earlier = this.#results;
@@ -691,6 +698,7 @@ export class PieceVerifier {
   /** For a client's event loop: flush if the policy says so, and hand out every result the automatic and
    * forced flushes have not yet returned (none when onVerified is set).  As the Python verifier's poll(). */
   async poll(): Promise<[number, boolean][]> {
+    this._open();
     this._rethrow();
     await this._autoFlush();
     return await this._serial(async () => {
@@ -700,8 +708,14 @@ export class PieceVerifier {
     });
   }
 
-  close(): void {
+  /** Release the device context once every library call already queued -- an automatic flush the age timer
+   * started included -- has finished (tv_destroy must not run beside a nonblocking call on the same context).
+   * Pending pieces not yet flushed are dropped; the verifier cannot be used afterwards. */
+  async close(): Promise<void> {
+    if (this.#closed) return;
+    this.#closed = true;
     clearTimeout(this.#timer);
+    await this.#busy;
     this.#l.symbols.tv_destroy(this.#ctx);
   }
 }
