@@ -1,0 +1,76 @@
+"""What a windowed layout costs: verify_payload over a payload in page-locked host memory with the whole shard
+resident (one window) and under smaller device budgets (TV_OPT_RESIDENT_BUDGET: windows of pieces staged while the
+previous window hashes), beside the streamed path (verify_stream over the same memory).  Every bitfield is checked
+against the oracle's digests of the payload (1 % of them corrupted).
+
+    python tools/window_bench.py [--gib 16] [--piece-mib 1] [--budgets 0,8,2,0.5] [--reps 3]
+
+Prints one JSON line per leg: path, budget (GiB; 0 = automatic), windows and window pieces (the library's
+counters), best and median wall seconds of the call, GB/s (payload bytes / best wall, H2D included)."""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from oracle import oracle as O  # noqa: E402  (the generator and the checker)
+from torrent_amd import _native as N  # noqa: E402
+from torrent_amd.metainfo import make_info  # noqa: E402
+from torrent_amd.verify import context_counters, verify_payload, verify_stream  # noqa: E402
+
+GiB, MiB = 1 << 30, 1 << 20
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gib", type=float, default=16)
+    ap.add_argument("--piece-mib", type=float, default=1)
+    ap.add_argument("--budgets", default="0,8,2,0.5")
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    L = int(a.piece_mib * MiB)
+    total = int(a.gib * GiB) // L * L
+    P = total // L
+    seed = 7
+    buf = N.PinnedBuffer(total)
+    chunk = 256 * MiB
+    for o in range(0, total, chunk):
+        n = min(chunk, total - o)
+        ctypes.memmove(buf.ptr + o, bytes(O.synth_fill(seed, o, n)), n)
+    digests = bytearray(O.synth_piece_digests(seed, total, L, P, threads=16))
+    for i in range(5, P, 100):
+        digests[20 * i + 3] ^= 0x08
+    expect = bytearray(b"\xff" * ((P + 7) // 8))
+    for i in range(5, P, 100):
+        expect[i >> 3] &= ~(0x80 >> (i & 7)) & 0xFF
+    if P % 8:
+        expect[-1] &= (0xFF << (8 - P % 8)) & 0xFF
+    info = make_info(L, bytes(digests), "w", length=total)
+
+    def leg(name, fn, budget_gib):
+        walls, ok = [], True
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            bf = fn()
+            walls.append(time.perf_counter() - t0)
+            ok &= bytes(bf) == bytes(expect)
+        cnt = next(iter(context_counters().values()), {})
+        print(json.dumps({"path": name, "bytes": total, "piece_length": L, "pieces": P, "budget_gib": budget_gib,
+                          "windows": cnt.get("windows"), "window_pieces": cnt.get("window_pieces"),
+                          "payload_bytes": cnt.get("payload_bytes"), "best_s": round(min(walls), 4),
+                          "median_s": round(statistics.median(walls), 4),
+                          "gbps": round(total / min(walls) / 1e9, 2), "bitfield_exact": ok}), flush=True)
+
+    for b in [float(x) for x in a.budgets.split(",")]:
+        budget = int(b * GiB) if b else None
+        leg("verify_payload resident", lambda: verify_payload(info, buf.mv, budget=budget), b)
+    leg("verify_stream rows", lambda: verify_stream(info, lambda off, n: buf.mv[off:off + n]), None)
+    buf.close()
+
+
+if __name__ == "__main__":
+    main()
