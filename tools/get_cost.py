@@ -8,7 +8,7 @@ bytes:
 Prints one JSON line per (variant, threads): gets, wall seconds, microseconds per get (wall / gets, i.e. the
 aggregate rate), GB/s of piece bytes.
 
-    python tools/get_cost.py DIR"""
+    python tools/get_cost.py DIR [cfg3|single16|files64] [sweep]"""
 import json
 import os
 import sys
@@ -80,13 +80,17 @@ class Counting:
 
 def main():
     d = sys.argv[1]
-    root = os.path.join(d, "cfg3")
-    info, _, paths = write_layout("cfg3", root)
+    layout = sys.argv[2] if len(sys.argv) > 2 else "cfg3"
+    sweep = len(sys.argv) > 3 and sys.argv[3] == "sweep"   # the reference method over 1 .. 16 threads only
+    root = os.path.join(d, layout)
+    info, _, paths = write_layout(layout, root)
     P, L = info.n_pieces, info.piece_length
     os.chdir(root)
     gets = None
-    for name, method in (("ref", FsStorage()), ("nocreat", NoCreat()), ("rdonly", RdOnly()), ("openonly", OpenOnly())):
-        for threads in (1, 16):
+    variants = (("ref", FsStorage()),) if sweep else (("ref", FsStorage()), ("nocreat", NoCreat()), ("rdonly", RdOnly()),
+                                                       ("openonly", OpenOnly()))
+    for name, method in variants:
+        for threads in ((1, 2, 4, 8, 16) if sweep else (1, 16)):
             cm = Counting(method)
             st = Storage(cm, info, root)
             best = None
@@ -98,7 +102,7 @@ def main():
                 best = el if best is None else min(best, el)
             if gets is None:
                 gets = cm.gets // 2
-            print(json.dumps({"variant": name, "threads": threads, "gets": gets, "pieces_ok": n_ok,
+            print(json.dumps({"layout": layout, "variant": name, "threads": threads, "gets": gets, "pieces_ok": n_ok,
                               "best_s": round(best, 4), "us_per_get": round(best / gets * 1e6, 2),
                               "gbps": round(info.length / best / 1e9, 2)}), flush=True)
 

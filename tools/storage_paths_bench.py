@@ -9,7 +9,7 @@ corrupted, so every result is checked against the oracle's bitfield):
 Paths timed (each reads the files exactly as the reference would: Storage(fs_storage) = storage.ts's Storage over
 fsStorage, which opens the file once per get call, storage.ts:149-172):
   verify_files                     one tv_stage_files call per shard (library readers / page-cache DMA)
-  verify_pieces(Storage(fs))       one Storage.get per piece (16 threads), double-buffered batches staged to HBM
+  verify_pieces(Storage(fs))       one Storage.get per piece (default reader threads), double-buffered batches to HBM
   verify_stream(Storage(fs).get)   the bounded ring, whole-piece rows (TV_OPT_STREAM_ROWS, the default)
   verify_stream(..., chunk=L/4)    the bounded ring, columns: four gets per piece (the round-3 default)
 Warm = the files were just written (page cache); cold = posix_fadvise(DONTNEED) after fsync on every file

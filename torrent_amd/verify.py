@@ -151,6 +151,20 @@ def _batch_buffers(ctx, nbytes: int) -> list:
     return bufs
 
 
+def _chunked_map(pool, fn, n: int, parts: int) -> list:
+    """[fn(0), .., fn(n - 1)] with the indices split into `parts` contiguous runs, one pool task per run (pool None:
+    in this thread).  One task per index costs a Future, a queue hand-off and a thread wake-up each, which on
+    10,000 small files cost more than the reads (tools/threads_sweep.py)."""
+    if pool is None or parts <= 1 or n <= 1:
+        return [fn(q) for q in range(n)]
+    parts = min(parts, n)
+    bounds = [n * r // parts for r in range(parts + 1)]
+    out = []
+    for run in pool.map(lambda r: [fn(q) for q in range(bounds[r], bounds[r + 1])], range(parts)):
+        out.extend(run)
+    return out
+
+
 def _run_shards(devs: List[int], n_pieces: int, fn):
     """fn(ctx, first, count) for each shard, one thread per shard (ctypes releases the GIL)."""
     ranges = shard_ranges(n_pieces, len(devs))
@@ -168,7 +182,14 @@ def _run_shards(devs: List[int], n_pieces: int, fn):
         return ranges, [f.result() for f in futs]
 
 
-def verify_pieces(info: InfoDict, storage, devices=None, threads: int = 16,
+# Python reader threads of the Storage paths (verify_pieces, verify_stream): each Storage.get is Python work under
+# the GIL around its open / pread / copy, so past a few threads they contend more than they overlap -- 4 was the
+# fastest or within noise of it on cfg3's 10,000 files and on 16 GiB in one and in 64 files, warm, for both paths
+# (tools/threads_sweep.py, profiles/r04/threads_sweep.jsonl).  (verify_files reads in the library's own threads.)
+_STORAGE_THREADS = 4
+
+
+def verify_pieces(info: InfoDict, storage, devices=None, threads: int = _STORAGE_THREADS,
                   budget: Optional[int] = None) -> bytearray:
     """verifyPieces(info, storage): have-bitfield of every piece read through `storage`
     (a torrent_amd.storage.Storage, i.e. the reference's Storage over any StorageMethod).  The gets
@@ -205,7 +226,7 @@ def verify_pieces(info: InfoDict, storage, devices=None, threads: int = 16,
                     k = min(per_batch, count - j)
                     buf = bufs[b]       # its last stage (two batches ago) finished before `staging` began
                     hi = 0
-                    got = pool.map(lambda q: get(first + j + q, buf.ptr + q * L), range(k))
+                    got = _chunked_map(pool, lambda q: get(first + j + q, buf.ptr + q * L), k, threads)
                     for q, n in enumerate(got):
                         if n:           # (an unreadable piece's slot keeps stale bytes: never a readable piece)
                             hi = q * L + n
@@ -281,7 +302,7 @@ def _shard_avail(avail: Optional[bytes], first: int, count: int) -> Optional[byt
 
 
 def verify_stream(info: InfoDict, read, devices=None, avail: Optional[bytes] = None, chunk: int = 0,
-                  threads: int = 16) -> bytearray:
+                  threads: int = _STORAGE_THREADS) -> bytearray:
     """End-to-end resume check through the library's BOUNDED pinned ring (tv_stream_*; SURVEY 8d config 5:
     the resume flow Client.add -> verify -> Torrent.bitfield -> sendBitfield, client.ts:53-67,
     torrent.ts:56-60,101).  No resident payload and no whole-shard host buffer.  By default (chunk=0) each
@@ -325,8 +346,7 @@ def verify_stream(info: InfoDict, read, devices=None, avail: Optional[bytes] = N
                     copy_bytes(req.slot + q * req.width, data, n)
                     return None
 
-                rows = range(req.rows)
-                for i in (pool.map(fill, rows) if pool is not None else map(fill, rows)):
+                for i in _chunked_map(pool, fill, req.rows, threads):
                     if i is not None:
                         ctx.stream_unreadable(i)
                 ctx.stream_commit(req)
