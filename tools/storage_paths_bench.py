@@ -18,6 +18,8 @@ host memory, nothing else: what the box's storage delivers.  Each line: GB/s, ge
 
 usage: python tools/storage_paths_bench.py <dir> [layout ...] > out.jsonl
 """
+import copy
+import itertools
 import json
 import os
 import sys
@@ -38,12 +40,17 @@ class CountingFs(FsStorage):
     """fsStorage with a count of get calls (each one an open, storage.ts:158)."""
 
     def __init__(self):
-        self.gets = 0
-        self._lock = threading.Lock()
+        self.reset()
+
+    def reset(self) -> None:
+        self._n = itertools.count()      # (next() on it is atomic under the GIL: no lock on the hot path)
+
+    @property
+    def gets(self) -> int:
+        return next(copy.copy(self._n))  # (the count so far, without consuming it)
 
     def get(self, path, offset, length):
-        with self._lock:
-            self.gets += 1
+        next(self._n)
         return super().get(path, offset, length)
 
 
@@ -169,22 +176,25 @@ def main():
                 st3 = Storage(fs3, info, root)
                 legs.append((f"verify_stream(Storage(fs).get) columns chunk={L // 4}",
                              lambda: verify_stream(info, st3.get, chunk=L // 4), fs3))
-                # the bound of the Storage paths: the gets alone (Storage(fs).get of every piece on the same 16
-                # threads, bytes dropped; no GPU), as verify_pieces issues them
+                # the bound of the Storage paths: the gets alone (Storage(fs).get of every piece on the same reader
+                # threads as verify_pieces, in the same runs of pieces; bytes dropped; no GPU)
                 fs4 = CountingFs()
                 st4 = Storage(fs4, info, root)
                 from torrent_amd.piece import piece_length as _plen
+                from torrent_amd.verify import _STORAGE_THREADS, _chunked_map
 
-                def gets_only(threads=16):
+                def gets_only(threads=_STORAGE_THREADS):
                     with ThreadPoolExecutor(threads) as ex:
-                        return sum(ex.map(lambda i: st4.get(i * L, _plen(i, info)) is not None, range(P)))
+                        return sum(_chunked_map(ex, lambda i: st4.get(i * L, _plen(i, info)) is not None, P, threads))
                 if cold:
                     drop_cache(paths)
                 el, n_ok = timed(gets_only, 1 if cold else 2)
-                emit({"layout": name, "cache": "cold" if cold else "warm", "path": "Storage(fs).get only, 16 threads",
-                      "best_s": round(el, 3), "gbps": round(total / el / 1e9, 2), "us_per_get_per_thread":
-                      round(el * 16 / max(1, fs4.gets / (1 if cold else 2)) * 1e6, 1),
-                      "gets_per_piece": round(fs4.gets / (1 if cold else 2) / P, 3)})
+                ngets = fs4.gets
+                emit({"layout": name, "cache": "cold" if cold else "warm",
+                      "path": f"Storage(fs).get only, {_STORAGE_THREADS} threads",
+                      "best_s": round(el, 3), "gbps": round(total / el / 1e9, 2), "us_per_get":
+                      round(el / max(1, ngets / (1 if cold else 2)) * 1e6, 1),
+                      "gets_per_piece": round(ngets / (1 if cold else 2) / P, 3)})
                 if cold:
                     drop_cache(paths)
                     ceil = read_ceiling(paths)
@@ -194,7 +204,7 @@ def main():
                     if cold:
                         drop_cache(paths)
                     if counter is not None:
-                        counter.gets = 0
+                        counter.reset()
                     reps = 1 if cold else (3 if leg == "verify_files" else 2)
                     el, bf = timed(fn, reps)
                     rec = {"layout": name, "cache": "cold" if cold else "warm", "path": leg,
