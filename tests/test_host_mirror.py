@@ -503,3 +503,31 @@ def test_file_paths_equal_os_path_join():
         info = make_info(4096, bytes(20), "t", files=[FileInfo(1, c) for c in cases])
         st = Storage(FsStorage(), info, d)
         assert st.file_paths() == [os.path.join(*st.dir_path, *c) for c in cases], d
+
+
+def test_chunked_map_keeps_order_and_splits_into_runs():
+    """verify._chunked_map (the Storage paths' reader dispatch): results in index order for any run count, one pool
+    task per contiguous run (never per index), and in the calling thread without a pool."""
+    from concurrent.futures import ThreadPoolExecutor
+    import threading
+    from torrent_amd import verify
+
+    seen = []
+
+    def fn(q):
+        seen.append((q, threading.get_ident()))
+        return q * q
+
+    assert verify._chunked_map(None, fn, 5, 4) == [0, 1, 4, 9, 16]
+    assert {t for _, t in seen} == {threading.get_ident()}
+    with ThreadPoolExecutor(4) as pool:
+        for n, parts in [(0, 4), (1, 4), (3, 4), (10, 4), (17, 3), (100, 1), (7, 16)]:
+            seen.clear()
+            assert verify._chunked_map(pool, fn, n, parts) == [q * q for q in range(n)], (n, parts)
+            # each run is handled by one thread, in order: indices of one thread are consecutive and ascending
+            by_thread = {}
+            for q, t in seen:
+                by_thread.setdefault(t, []).append(q)
+            for qs in by_thread.values():
+                assert qs == sorted(qs)
+    assert verify._STORAGE_THREADS == 4
