@@ -67,6 +67,34 @@ def test_asm_generator_emulator_options(env):
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr
 
 
+@pytest.mark.parametrize("stamp", ["1", "2"])
+def test_asm_generator_stamp_headers(tmp_path, stamp):
+    """The diagnostic stamp headers (TV_GEN_STAMP, tools/split_stamps.py) still generate: both split loops get the
+    accumulator argument(s) and the stamp SGPRs as clobbers; level 2 also brackets the helper's prefetch wait, and its
+    LDS-write drain where the helper still drains before the barrier (TV_GEN_HWAIT=0);
+    the shipped header's helper waits mid-block (TV_GEN_HWAIT=mid) and the previous form stays available."""
+    out = tmp_path / "h.h"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_sha1_asm.py"), "--out", str(out)],
+                       capture_output=True, text=True, env=dict(os.environ, TV_GEN_STAMP=stamp))
+    assert r.returncode == 0, r.stderr
+    h = out.read_text()
+    assert f"#define TV_SHA1_STAMP {stamp}" in h
+    assert "tv_sha1_rounds_loop(uint32_t h[5], uint32_t addr, uint32_t nsteps, uint32_t& sbar," in h
+    assert ('uint32_t& sbar, uint32_t& svm, uint32_t& slg,' in h) == (stamp == "2")
+    assert h.count('"s88", "s89", "s90", "s91"') == 2
+    assert ("%[svm]" in h) == (stamp == "2") and "%[sbar]" in h
+    if stamp == "2":   # the drain stamp needs the drain: the pre-round-4 helper wait (TV_GEN_HWAIT=0)
+        assert "%[slg]" not in h
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_sha1_asm.py"), "--out", str(out)],
+                           capture_output=True, text=True, env=dict(os.environ, TV_GEN_STAMP="2", TV_GEN_HWAIT="0"))
+        assert r.returncode == 0 and "%[slg]" in out.read_text(), r.stderr
+    shipped = open(os.path.join(ROOT, "torrent_amd", "csrc", "sha1_asm.h")).read()
+    assert "TV_SHA1_STAMP" not in shipped and "s_memtime" not in shipped and "s_waitcnt lgkmcnt(10)" in shipped
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_sha1_asm.py"), "--out", str(out)],
+                       capture_output=True, text=True, env=dict(os.environ, TV_GEN_HWAIT="0"))
+    assert r.returncode == 0 and "s_waitcnt lgkmcnt(10)" not in out.read_text(), r.stderr
+
+
 def test_generated_header_is_current(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_sha1_asm.py"), "--out",
                         str(tmp_path / "h.h")], capture_output=True, text=True)
