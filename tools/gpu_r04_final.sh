@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-4 final check of the build: the whole -m gpu suite, smoke(), the default bench line, its rocprofv3 kernel
-# trace, and the split kernel on cfg4's N = 2 shard (tools/shard_probe.py) under rocprofv3.  Every GPU step has
+# trace, the split kernel on cfg4's N = 2 shard (tools/shard_probe.py) under rocprofv3, and the TS host's Storage
+# paths (tools/ts_storage_bench.py).  Every GPU step has
 # its own time limit; the chain stops at the first failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -13,7 +14,9 @@ timeout -k 10 400 python3 bench.py > $out/bench_n1.json 2> $out/bench_n1.err && 
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/prof -o run -- python3 bench.py --steps 10 --warmup 3 \
     > $out/bench_prof.json 2> $out/bench_prof.err && echo PROF_OK &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof_split -o run -- python3 tools/shard_probe.py --shards 2 \
-    > $out/split25600_under_rocprof.json 2> $out/split25600.err && echo SPLIT_PROF_OK
+    > $out/split25600_under_rocprof.json 2> $out/split25600.err && echo SPLIT_PROF_OK &&
+mkdir -p /tmp/tsb && UV_THREADPOOL_SIZE=16 timeout -k 10 400 python3 -u tools/ts_storage_bench.py /tmp/tsb single16 cfg3 \
+    > $out/ts_storage_bench.jsonl 2> $out/ts_storage_bench.err && echo TS_BENCH_OK
 rc=$?
 tail -3 $out/pytest_gpu.log; head -c 400 $out/bench_n1.json; echo
 exit $rc
