@@ -128,6 +128,11 @@ def test_random_layouts_every_host_path(native, tmp_path, monkeypatch, seed):
         assert _bits(verify_stream(info, st.get, devices=devices), P) == want, ("stream", seed, devices)
         assert _bits(verify_files(info, str(tmp_path / "dl"), devices=devices, threads=3), P) == want_fs, \
             ("files", seed, devices)
+    # the Storage paths' reader dispatch (runs of pieces per thread) at its extremes: in the calling thread, and
+    # more threads than a small batch has pieces
+    for devices, threads in (([0], 1), ([0, 0], 16)):
+        assert _bits(verify_pieces(info, st, devices=devices, threads=threads), P) == want, ("pieces", seed, threads)
+        assert _bits(verify_stream(info, st.get, devices=devices, threads=threads), P) == want, ("stream", seed, threads)
     assert sorted(str(x) for x in (tmp_path / "dl").rglob("*")) == before      # verify_files created nothing
 
 
