@@ -92,6 +92,31 @@ import(pathToFileURL("MODULE").href).then(async (v) => {
   if (spec.files) info.files = spec.files;
   const st = makeStorage(info, spec.dir);
   const opts = { libPath: spec.lib };
+  // the reads alone, as the binding issues them (32 in flight, bytes dropped): the Storage restatement, and for a
+  // single-file torrent fsStorage.get itself (no Storage copy)
+  const P = pieces.length, L = info.pieceLength;
+  const plen = (i) => (i === P - 1 && info.length % L ? info.length % L : L);
+  const readAll = async (get) => {
+    let next = 0;
+    const worker = async () => { while (next < P) { const i = next++; await get(i); } };
+    await Promise.all(Array.from({ length: 32 }, worker));
+    return new Uint8Array(0);
+  };
+  const readLegs = [["Storage.get only (32 in flight)", () => readAll((i) => st.get(i * L, plen(i)))]];
+  if (!info.files) {
+    readLegs.push(["fsStorage.get only (32 in flight)", () => readAll((i) => fsStorage.get([spec.dir, info.name], i * L, plen(i)))]);
+  }
+  for (const [name, fn] of readLegs) {
+    let best = Infinity;
+    for (let r = 0; r < 2; r++) {
+      const t0 = process.hrtime.bigint();
+      await fn();
+      best = Math.min(best, Number(process.hrtime.bigint() - t0) / 1e9);
+    }
+    console.log(JSON.stringify({ layout: spec.layout, path: name, best_s: +best.toFixed(4),
+                                 gbps: +(spec.length / best / 1e9).toFixed(2),
+                                 uv_threadpool: process.env.UV_THREADPOOL_SIZE || "4 (default)" }));
+  }
   const legs = [["verifyPieces", () => v.verifyPieces(info, st, opts)],
                 ["verifyStream rows", () => v.verifyStream(info, st, opts)],
                 ["verifyFiles", () => v.verifyFiles(info, spec.dir, opts)]];
