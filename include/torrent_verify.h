@@ -111,6 +111,17 @@ int tv_set_digests(tv_ctx *ctx, const uint8_t *pieces, uint64_t pieces_len);
 int tv_stage(tv_ctx *ctx, uint64_t linear_offset, const uint8_t *src, uint64_t len);
 
 /*
+ * n tv_stage calls in one: buffer k (srcs[k], lens[k] bytes) holds LINEAR bytes [linear_offsets[k],
+ * linear_offsets[k] + lens[k]).  The same clipping, windows (ascending, as consecutive tv_stage calls) and mark
+ * clearing apply, in order k = 0 .. n-1; every copy is complete when the call returns.  For a host that holds a
+ * batch of pieces as separate buffers (one Storage.get result per piece, storage.ts:50-65): the library copies
+ * them into its pinned ring on its own threads, so the caller does no gather copy.  Replaces: the same reads as
+ * tv_stage.
+ */
+int tv_stage_many(tv_ctx *ctx, uint64_t n, const uint64_t *linear_offsets, const uint8_t *const *srcs,
+                  const uint64_t *lens);
+
+/*
  * Stage `len` bytes of the file at `path` (a NUL-terminated path), starting at byte `file_offset`,
  * as LINEAR torrent bytes [linear_offset, linear_offset + len).  This is one file segment of
  * Storage.get's mapping (storage.ts:89-137: path, offset in the file, length) read the way

@@ -228,3 +228,53 @@ def test_windowed_rules(native, oracle):
         ctx.stage(0, payload)                           # a new pass: everything
         assert _bits(ctx.verify(), P) == [1] * P
         assert _bits(ctx.verify(bytes([0x7F]) + b"\xff" * ((P + 7) // 8 - 1)), P) == [0] + [1] * (P - 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("windowed", [False, True])
+def test_stage_many_equals_stage_calls(native, windowed):
+    """tv_stage_many (the TS verifyPieces' hand-over of a batch of separate piece buffers) stages exactly what the
+    same tv_stage calls in order stage: pieces of a ragged layout with a short last piece, some missing, each its
+    own buffer (pageable and page-locked, odd addresses), on a whole-shard and a windowed layout; the bitfield
+    equals hashlib's, a NULL source with bytes is TV_ERR_ARG, and n = 0 is a no-op."""
+    import ctypes
+    from torrent_amd import _native as N
+    L, P = 40000, 37
+    total = L * (P - 1) + 1234
+    rng = random.Random(11)
+    payload = bytes(rng.randrange(256) for _ in range(total))
+    digests = bytearray(b"".join(hashlib.sha1(payload[i * L:(i + 1) * L]).digest() for i in range(P)))
+    for i in (4, 20):
+        digests[20 * i] ^= 1
+    missing = {7, 8, 30}
+    with N.Context(0) as ctx, N.PinnedBuffer(2 * L + 8) as pin:
+        if windowed:
+            ctx.set_option(N.TV_OPT_RESIDENT_BUDGET, _budget(L, 5))
+        ctx.set_layout(total, L, P)
+        ctx.set_digests(bytes(digests))
+        parts = []
+        for i in range(P):
+            if i in missing:
+                continue
+            chunk = payload[i * L:min(total, (i + 1) * L)]
+            if i % 9 == 3:      # a page-locked source at an odd address
+                pin.mv[1:1 + len(chunk)] = chunk
+                parts.append((i * L, pin.mv[1:1 + len(chunk)]))
+                ctx.stage_many(parts)   # (the pinned buffer is reused: hand over what uses it now)
+                parts = []
+            else:
+                parts.append((i * L, bytearray(b"\x00" + chunk)[1:]))   # a pageable copy of its own
+        ctx.stage_many(parts)
+        ctx.stage_many([])
+        if windowed:
+            assert ctx.counter(N.TV_COUNTER_WINDOW_PIECES) >= 1
+        avail = bytearray((P + 7) // 8)
+        for i in range(P):
+            if i not in missing:
+                avail[i >> 3] |= 0x80 >> (i & 7)
+        bf = ctx.verify(bytes(avail))
+        want = [0 if (i in missing or i in (4, 20)) else 1 for i in range(P)]
+        assert _bits(bf, P) == want
+        L_ = ctx._L
+        offs, srcs, lens = (ctypes.c_uint64 * 1)(0), (ctypes.c_uint64 * 1)(0), (ctypes.c_uint64 * 1)(16)
+        assert L_.tv_stage_many(ctx._h, 1, offs, srcs, lens) == N.TV_ERR_ARG

@@ -1,6 +1,6 @@
 // fake_deno.js -- a CPU model of the library behind the Deno FFI, for the TS host logic on CPU (test
 // infrastructure only; tests/test_ts_binding.py).  Deno.dlopen returns JavaScript implementations of the
-// calls PieceVerifier makes (tv_create / tv_set_layout / tv_set_digests / tv_stage / tv_verify_list /
+// calls PieceVerifier makes (tv_create / tv_set_layout / tv_set_digests / tv_stage(_many) / tv_verify_list /
 // tv_destroy / tv_last_error / tv_abi_version) and hashPieces makes (tv_hash), with SHA-1 from node's crypto as the checker, and the
 // calls verifyFiles makes (tv_set_option, tv_stage_files recording the host's segment plan, tv_verify
 // returning the host's availability bits) and verifyStream makes (the tv_stream_* protocol, modelled with
@@ -158,6 +158,19 @@ const impl = {
   },
   tv_stream_abort(ctx) {
     contexts.get(ctx).stream = null;
+    return 0;
+  },
+  // tv_stage_many: tv_stage of each (offset, buffer address, length) in order
+  tv_stage_many(ctx, n, offsp, srcsp, lensp) {
+    const view = (p) => {
+      const b = bytesOf(p);
+      return new BigUint64Array(b.buffer, b.byteOffset, Number(n));
+    };
+    const offs = view(offsp), srcs = view(srcsp), lens = view(lensp);
+    for (let k = 0; k < Number(n); k++) {
+      const rc = impl.tv_stage(ctx, offs[k], srcs[k], lens[k]);
+      if (rc) return rc;
+    }
     return 0;
   },
   // tv_stage_files records the segments it is given (the host's plan) and reports them all readable

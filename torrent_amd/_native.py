@@ -81,6 +81,7 @@ SYMBOLS = [
     ("tv_set_layout", _int, [_p, _u64, _u64, _u64, _u64, _u64]),
     ("tv_set_digests", _int, [_p, _p, _u64]),
     ("tv_stage", _int, [_p, _u64, _p, _u64]),
+    ("tv_stage_many", _int, [_p, _u64, _p, _p, _p]),
     ("tv_stage_file", _int, [_p, ctypes.c_char_p, _u64, _u64, _u64]),
     ("tv_stage_files", _int, [_p, _u64, _p, _p, _p, _p, _p]),
     ("tv_read", _int, [_p, _u64, _p, _u64]),
@@ -275,6 +276,21 @@ class Context:
         n = memoryview(data).nbytes
         self._check(self._L.tv_stage(self._h, linear_offset, a, n))
         del keep
+
+    def stage_many(self, parts) -> None:
+        """tv_stage_many: [(linear_offset, data), ...] staged in order in one call (no gather copy here)."""
+        parts = list(parts)
+        if not parts:
+            return
+        n = len(parts)
+        offs, ptrs, lens = (ctypes.c_uint64 * n)(), (ctypes.c_uint64 * n)(), (ctypes.c_uint64 * n)()
+        keeps = []
+        for k, (off, data) in enumerate(parts):
+            a, keep = _addr(data)
+            keeps.append(keep)
+            offs[k], ptrs[k], lens[k] = off, a or 0, memoryview(data).nbytes
+        self._check(self._L.tv_stage_many(self._h, n, offs, ptrs, lens))
+        del keeps
 
     def stage_file(self, path, file_offset: int, linear_offset: int, length: int) -> bool:
         """tv_stage_file: stage `length` bytes of file `path` from `file_offset` as linear bytes

@@ -1826,6 +1826,45 @@ int tv_set_digests(tv_ctx* c, const uint8_t* pieces, uint64_t pieces_len) {
     return TV_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// tv_stage's work with the lock held and the arguments checked: LINEAR [linear_offset, linear_offset + len) from
+// src queued on the copy lane (window by window on a windowed layout).  The caller drains the lane (DrainGuard),
+// synchronises it to see copy failures and then clears the staged pieces' marks (clear_staged).
+int stage_locked(tv_ctx* c, uint64_t linear_offset, const uint8_t* src, uint64_t len) {
+    uint64_t a, b;
+    clip_to_whole_shard(c, linear_offset, len, &a, &b);
+    if (a >= b) return TV_OK;
+    const bool pinned = is_pinned(src);
+    if (!c->win) return stage_range(c, a, b, src, linear_offset, pinned);
+    // window by window, ascending: opening the next window hashes the previous one (win_enter)
+    for (uint64_t pos = a; pos < b;) {
+        const uint64_t w = win_of(c, pos / c->L - c->first);
+        int rc = win_enter(c, w);
+        if (rc) return rc;
+        uint64_t wa, wb;
+        clip_to_shard(c, pos, b - pos, &wa, &wb);
+        if (wa < wb) {
+            rc = stage_range(c, wa, wb, src, linear_offset, pinned);
+            if (rc) return rc;
+        }
+        pos = win_end_linear(c, w);
+    }
+    return TV_OK;
+}
+
+void clear_staged(tv_ctx* c, uint64_t linear_offset, uint64_t len) {
+    uint64_t a, b;
+    clip_to_whole_shard(c, linear_offset, len, &a, &b);
+    clear_bad(c, a, b);
+}
+
+}  // namespace
+
+extern "C" {
+
 int tv_stage(tv_ctx* c, uint64_t linear_offset, const uint8_t* src, uint64_t len) {
     if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
     std::lock_guard<std::mutex> g(c->mu);
@@ -1835,31 +1874,38 @@ int tv_stage(tv_ctx* c, uint64_t linear_offset, const uint8_t* src, uint64_t len
     if (linear_offset + len < linear_offset) return fail(c, TV_ERR_ARG, "offset + len overflows");
     if (c->count == 0 || len == 0) return TV_OK;
     TV_HIP(c, hipSetDevice(c->device));
-    uint64_t a, b;
-    clip_to_whole_shard(c, linear_offset, len, &a, &b);
-    if (a >= b) return TV_OK;
     DrainGuard drain(c, 0, /*sync_compute=*/false);  // (a window kernel queued here hashes on after the call)
-    const bool pinned = is_pinned(src);
-    if (c->win) {
-        // window by window, ascending: opening the next window hashes the previous one (win_enter)
-        for (uint64_t pos = a; pos < b;) {
-            const uint64_t w = win_of(c, pos / c->L - c->first);
-            rc = win_enter(c, w);
-            if (rc) return rc;
-            uint64_t wa, wb;
-            clip_to_shard(c, pos, b - pos, &wa, &wb);
-            if (wa < wb) {
-                rc = stage_range(c, wa, wb, src, linear_offset, pinned);
-                if (rc) return rc;
-            }
-            pos = win_end_linear(c, w);
-        }
-    } else {
-        rc = stage_range(c, a, b, src, linear_offset, pinned);
+    rc = stage_locked(c, linear_offset, src, len);
+    if (rc) return rc;
+    TV_HIP(c, hipStreamSynchronize(c->copy_stream));   // report a copy failure as this call's error
+    clear_staged(c, linear_offset, len);
+    return TV_OK;
+}
+
+int tv_stage_many(tv_ctx* c, uint64_t n, const uint64_t* linear_offsets, const uint8_t* const* srcs,
+                  const uint64_t* lens) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = require_layout(c, false, true);
+    if (rc) return rc;
+    if (n == 0) return TV_OK;
+    if (!linear_offsets || !srcs || !lens) return fail(c, TV_ERR_ARG, "NULL argument");
+    for (uint64_t k = 0; k < n; k++) {
+        if (!srcs[k] && lens[k]) return fail(c, TV_ERR_ARG, "srcs[%llu] is NULL", (unsigned long long)k);
+        if (linear_offsets[k] + lens[k] < linear_offsets[k])
+            return fail(c, TV_ERR_ARG, "buffer %llu: offset + len overflows", (unsigned long long)k);
+    }
+    if (c->count == 0) return TV_OK;
+    TV_HIP(c, hipSetDevice(c->device));
+    DrainGuard drain(c, 0, /*sync_compute=*/false);  // no DMA reads a caller buffer after the call
+    for (uint64_t k = 0; k < n; k++) {
+        if (!lens[k]) continue;
+        rc = stage_locked(c, linear_offsets[k], srcs[k], lens[k]);
         if (rc) return rc;
     }
-    TV_HIP(c, hipStreamSynchronize(c->copy_stream));   // report a copy failure as this call's error
-    clear_bad(c, a, b);
+    TV_HIP(c, hipStreamSynchronize(c->copy_stream));
+    for (uint64_t k = 0; k < n; k++)
+        if (lens[k]) clear_staged(c, linear_offsets[k], lens[k]);
     return TV_OK;
 }
 

@@ -26,6 +26,7 @@ const SYMBOLS = {
   tv_set_layout: { parameters: ["pointer", "u64", "u64", "u64", "u64", "u64"], result: "i32" },
   tv_set_digests: { parameters: ["pointer", "pointer", "u64"], result: "i32" },
   tv_stage: { parameters: ["pointer", "u64", "pointer", "u64"], result: "i32", nonblocking: true },
+  tv_stage_many: { parameters: ["pointer", "u64", "pointer", "pointer", "pointer"], result: "i32", nonblocking: true },
   tv_stage_file: { parameters: ["pointer", "pointer", "u64", "u64", "u64"], result: "i32", nonblocking: true },
   tv_stage_files: {
     parameters: ["pointer", "u64", "pointer", "pointer", "pointer", "pointer", "pointer"],
@@ -198,8 +199,8 @@ async function eachLimited(n: number, fn: (q: number) => Promise<void>): Promise
  * torrent.ts:53,60,147-149).  Piece i's bit is set iff storage.get(i*pieceLength, len_i) is
  * non-null (storage.ts:50-65) and its SHA-1 equals info.pieces[i].  Unreadable pieces are 0, not
  * errors (the reference swallows I/O failures into null); GPU / ABI failures throw Error.  Reads and
- * staging overlap: batch k + 1 is read into the other of two buffers while batch k's tv_stage (nonblocking)
- * copies it to HBM.
+ * staging overlap: batch k + 1 is read while batch k's pieces -- the Uint8Arrays storage.get returned, never
+ * gathered on this thread -- are copied into the library's pinned ring and DMA'd (tv_stage_many, nonblocking).
  */
 export async function verifyPieces(
   info: InfoDict,
@@ -221,14 +222,12 @@ export async function verifyPieces(
       check(l, ctx, l.symbols.tv_set_digests(ctx, ptr(raw), BigInt(raw.length)));
       const avail = new Uint8Array(Math.ceil(count / 8));
       const per = Math.min(batch, count);
-      const bufs: Uint8Array[] = [];
-      let staging: Promise<void> | null = null; // the previous batch's tv_stage (it reads the other buffer)
+      const u8 = (a: ArrayBufferView) => new Uint8Array(a.buffer, a.byteOffset, a.byteLength);
+      let staging: Promise<void> | null = null; // the previous batch's tv_stage_many (it still reads its buffers)
       try {
-        for (let j = 0, b = 0; j < count; j += per, b ^= 1) {
+        for (let j = 0; j < count; j += per) {
           const k = Math.min(per, count - j);
-          if (!bufs[b]) bufs[b] = new Uint8Array(per * L);
-          const buf = bufs[b]; // its last stage (two batches ago) settled before `staging` began
-          let hi = 0;
+          const got: (Uint8Array | null)[] = new Array(k).fill(null);
           // READS_IN_FLIGHT reads outstanding at a time (make_torrent.ts:96,111 keeps its work in flight too, but
           // each fsStorage.get is a Deno.open: a batch of 16 KiB pieces at once would hit EMFILE, which
           // fsStorage.get turns into null -- a valid piece reported 0)
@@ -236,16 +235,31 @@ export async function verifyPieces(
             const n = pieceLength(first + j + q, info);
             const bytes = await storage.get((first + j + q) * L, n);
             // Storage.get returns exactly the length asked or null; any other length is unreadable too (as in
-            // verifyStream): a longer one would run into the next piece's place in the batch buffer
-            if (!bytes || bytes.length !== n) return; // (the stale bytes left there are never a readable piece)
-            buf.set(bytes, q * L);
-            hi = Math.max(hi, q * L + n);
+            // verifyStream)
+            if (!bytes || bytes.length !== n) return;
+            got[q] = bytes;
             avail[(j + q) >> 3] |= 128 >> ((j + q) % 8);
           });
           if (staging) await staging;
           staging = null;
-          if (hi) {
-            staging = l.symbols.tv_stage(ctx, BigInt((first + j) * L), ptr(buf), BigInt(hi)).then((rc) => check(l, ctx, rc));
+          // the batch's readable pieces, ascending, handed over as they are: the library copies them into its
+          // pinned ring on its own threads (tv_stage_many), so this thread does no gather copy
+          const qs = got.map((b, q) => (b ? q : -1)).filter((q) => q >= 0);
+          if (qs.length) {
+            const offs = new BigUint64Array(qs.length), srcs = new BigUint64Array(qs.length);
+            const lens = new BigUint64Array(qs.length);
+            qs.forEach((q, t) => {
+              const b = got[q] as Uint8Array;
+              offs[t] = BigInt((first + j + q) * L);
+              srcs[t] = BigInt(Deno.UnsafePointer.value(Deno.UnsafePointer.of(b)));
+              lens[t] = BigInt(b.length);
+            });
+            const keep = [got, offs, srcs, lens]; // alive until the library has read them
+            staging = l.symbols.tv_stage_many(ctx, BigInt(qs.length), ptr(u8(offs)), ptr(u8(srcs)), ptr(u8(lens)))
+              .then((rc) => {
+                keep.length = 0;
+                check(l, ctx, rc);
+              });
           }
         }
       } finally {
