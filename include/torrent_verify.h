@@ -257,14 +257,6 @@ int tv_stream_commit(tv_ctx *ctx, const tv_stream_req *req);
  * tv_stream_abort returns; pageable memory is copied into the request's slot before the call returns. */
 int tv_stream_commit_from(tv_ctx *ctx, const tv_stream_req *req, const uint8_t *src, uint64_t src_pitch);
 /* Piece `piece` (GLOBAL, inside the shard) is unreadable: its bit will be 0. */
-/*
- * tv_stream_commit with the rows given as separate buffers: rows[q] (lens[q] bytes, exactly the row's valid length
- * min(width, piece length - offset)) is copied into row q of the lent slot on the library's threads, then the
- * request is committed.  rows[q] == NULL leaves row q as it is (a row the host reported with tv_stream_unreadable,
- * or one with no bytes).  For a host whose reads return one buffer per row (Storage.get, storage.ts:50-65): its own
- * thread copies nothing.
- */
-int tv_stream_commit_rows(tv_ctx *ctx, const tv_stream_req *req, const uint8_t *const *rows, const uint64_t *lens);
 int tv_stream_unreadable(tv_ctx *ctx, uint64_t piece);
 int tv_stream_end(tv_ctx *ctx, uint8_t *bitfield_out);
 /* Drop an active stream (a reader failed part-way); the ctx is usable again.  No-op when idle. */

@@ -65,11 +65,10 @@ def cfg5_small(oracle):
 
 
 @pytest.mark.parametrize("chunk", [0, MiB, 3 * 65536])   # auto (one 4 MiB column, 16-row requests), 4 and 22 columns
-@pytest.mark.parametrize("source", ["slot", "pageable", "pinned", "rows"])
+@pytest.mark.parametrize("source", ["slot", "pageable", "pinned"])
 def test_stream_4mib_pieces(native, oracle, cfg5_small, source, chunk):
-    """Rows filled by the caller into the lent pinned slot, copied from pageable memory, DMA'd straight
-    from a page-locked buffer (tv_stream_commit_from, src pitch L), or given as one buffer per row
-    (tv_stream_commit_rows, a row of the wrong length refused first): the bitfield equals the oracle's."""
+    """Rows filled by the caller into the lent pinned slot, copied from pageable memory, or DMA'd straight
+    from a page-locked buffer (tv_stream_commit_from, src pitch L): the bitfield equals the oracle's."""
     d = cfg5_small
     L, P, total, payload = d["L"], d["P"], d["total"], d["payload"]
     pb = None
@@ -92,12 +91,6 @@ def test_stream_4mib_pieces(native, oracle, cfg5_small, source, chunk):
                     slot[q * req.width:q * req.width + n] = payload[base + q * L:base + q * L + n]
                 slot.release()
                 ctx.stream_commit(req)
-            elif source == "rows":
-                rows = [bytes(payload[base + q * L:base + q * L + ctx.row_bytes(req, q)]) for q in range(req.rows)]
-                if req.seq == 1:
-                    with pytest.raises(native.NativeError, match="bytes; the request asks"):
-                        ctx.stream_commit_rows(req, [rows[0] + b"x"] + rows[1:])
-                ctx.stream_commit_rows(req, rows)
             else:
                 ctx.stream_commit_from(req, src, L, base)
 

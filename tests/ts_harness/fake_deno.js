@@ -140,24 +140,6 @@ const impl = {
     }
     return 0;
   },
-  // tv_stream_commit_rows: each given row (its exact valid length, else -1 like the library) into the slot, then
-  // the commit
-  tv_stream_commit_rows(ctx, reqp, rowsp, lensp) {
-    const c = contexts.get(ctx);
-    const st = c.stream;
-    const r = st.reqs[st.k];
-    const rows = u64s(rowsp, r.rows), lens = u64s(lensp, r.rows);
-    const slot = new Uint8Array(st.slot);
-    for (let q = 0; q < r.rows; q++) {
-      if (rows[q] === 0n) continue;
-      const i = r.piece + q;
-      const plen = i === c.P - 1 && c.total % c.L ? c.total % c.L : c.L;
-      const n = Math.max(0, Math.min(r.width, plen - r.offset));
-      if (Number(lens[q]) !== n) return -1;
-      slot.set(bytesOf(rows[q]).subarray(0, n), q * r.width);
-    }
-    return impl.tv_stream_commit(ctx, reqp);
-  },
   tv_stream_end(ctx, outp) {
     const c = contexts.get(ctx);
     const st = c.stream;

@@ -94,7 +94,6 @@ SYMBOLS = [
     ("tv_stream_next", _int, [_p, _REQ]),
     ("tv_stream_commit", _int, [_p, _REQ]),
     ("tv_stream_commit_from", _int, [_p, _REQ, _p, _u64]),
-    ("tv_stream_commit_rows", _int, [_p, _REQ, _p, _p]),
     ("tv_stream_unreadable", _int, [_p, _u64]),
     ("tv_stream_end", _int, [_p, _p]),
     ("tv_stream_abort", _int, [_p]),
@@ -416,21 +415,6 @@ class Context:
         a, keep = _addr(src)
         self._check(self._L.tv_stream_commit_from(self._h, ctypes.byref(req), (a or 0) + src_offset, pitch))
         del keep
-
-    def stream_commit_rows(self, req: StreamReq, rows) -> None:
-        """tv_stream_commit_rows: rows[q] is row q's bytes (exactly row_bytes(q)) or None (left as is)."""
-        n = req.rows
-        ptrs, lens = (ctypes.c_uint64 * max(1, n))(), (ctypes.c_uint64 * max(1, n))()
-        keeps = []
-        for q in range(n):
-            data = rows[q] if q < len(rows) else None
-            if data is None:
-                continue
-            a, keep = _addr(data)
-            keeps.append(keep)
-            ptrs[q], lens[q] = a or 0, memoryview(data).nbytes
-        self._check(self._L.tv_stream_commit_rows(self._h, ctypes.byref(req), ptrs, lens))
-        del keeps
 
     def stream_unreadable(self, piece: int) -> None:
         self._check(self._L.tv_stream_unreadable(self._h, piece))

@@ -2684,33 +2684,6 @@ int tv_stream_commit_from(tv_ctx* c, const tv_stream_req* req, const uint8_t* sr
     return stream_result(c, stream_commit_locked(c, req, src, src_pitch, is_pinned(src), req ? req->rows : 0));
 }
 
-int tv_stream_commit_rows(tv_ctx* c, const tv_stream_req* req, const uint8_t* const* rows, const uint64_t* lens) {
-    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
-    if (!rows || !lens) return fail(c, TV_ERR_ARG, "NULL argument");
-    std::lock_guard<std::mutex> g(c->mu);
-    StreamState& st = c->st;
-    if (!st.active) return fail(c, TV_ERR_STATE, "tv_stream_begin has not been called");
-    if (!st.outstanding) return fail(c, TV_ERR_STATE, "no outstanding request (call tv_stream_next)");
-    const tv_stream_req r = st.req;
-    if (!req || req->seq != r.seq || req->piece != r.piece || req->rows != r.rows)
-        return fail(c, TV_ERR_ARG, "the request does not match outstanding request %llu", (unsigned long long)r.seq);
-    for (uint64_t q = 0; q < r.rows; q++) {
-        const uint64_t want = row_bytes(c, r.piece + q, r.offset, r.width);
-        if (rows[q] && lens[q] != want)
-            return fail(c, TV_ERR_ARG, "row %llu holds %llu bytes; the request asks %llu", (unsigned long long)q,
-                        (unsigned long long)lens[q], (unsigned long long)want);
-    }
-    TV_HIP(c, hipSetDevice(c->device));
-    // the rows into the lent slot on the lane's workers (the caller's thread copies nothing), then the commit
-    uint8_t* slot = c->ring[st.slot];
-    const uint64_t per = std::max<uint64_t>(1, (4ull << 20) / std::max<uint64_t>(1, r.width));  // rows per task
-    c->pool[0].run(c->file_threads, (r.rows + per - 1) / per, [&](uint64_t t) {
-        for (uint64_t q = t * per; q < std::min(r.rows, (t + 1) * per); q++)
-            if (rows[q] && lens[q]) tv_copy_host(slot + q * r.width, rows[q], lens[q]);
-    });
-    return stream_result(c, stream_commit_locked(c, req, nullptr, 0, true, r.rows));
-}
-
 int tv_stream_unreadable(tv_ctx* c, uint64_t piece) {
     if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
     std::lock_guard<std::mutex> g(c->mu);

@@ -46,7 +46,6 @@ const SYMBOLS = {
   tv_stream_begin: { parameters: ["pointer", "pointer"], result: "i32" },
   tv_stream_next: { parameters: ["pointer", "pointer"], result: "i32", nonblocking: true },
   tv_stream_commit: { parameters: ["pointer", "pointer"], result: "i32", nonblocking: true },
-  tv_stream_commit_rows: { parameters: ["pointer", "pointer", "pointer", "pointer"], result: "i32", nonblocking: true },
   tv_stream_commit_from: { parameters: ["pointer", "pointer", "pointer", "u64"], result: "i32", nonblocking: true },
   tv_stream_unreadable: { parameters: ["pointer", "u64"], result: "i32" },
   tv_stream_end: { parameters: ["pointer", "pointer"], result: "i32", nonblocking: true },
@@ -285,11 +284,10 @@ const TV_OPT_STREAM_ROWS = 19;
  * Torrent.bitfield -> sendBitfield, client.ts:53-67, torrent.ts:56-60,101).  No resident payload and no
  * whole-shard buffer: the library requests the shard in rows of whole pieces (TV_OPT_STREAM_ROWS; with
  * opts.chunk, column by column: bytes [c*C, c*C + C) of every piece), each row is one
- * storage.get(offset, length) -- one fsStorage open per piece -- whose buffer the library copies into its pinned
- * slot on its own threads (tv_stream_commit_rows) and DMAs to HBM while the GPU hashes the previous window.
- * Host memory in flight: 3 x 64 MiB per device, plus the rows of the request being read.  null from
- * storage.get makes that piece 0 (a piece is readable iff every slice of it reads).  Same behaviour as
- * torrent_amd.verify_stream.
+ * storage.get(offset, length) written straight into the library's pinned slot -- one fsStorage open per
+ * piece -- and the library DMAs the slot to HBM while the GPU hashes the previous window.  Host memory in flight:
+ * 3 x 64 MiB per device.  null from storage.get makes that piece 0 (a piece is readable iff every slice
+ * of it reads).  Same behaviour as torrent_amd.verify_stream.
  */
 export async function verifyStream(info: InfoDict, storage: Storage, opts: VerifyOptions & { chunk?: number } = {}): Promise<Uint8Array> {
   const l = load(opts.libPath);
@@ -320,9 +318,7 @@ export async function verifyStream(info: InfoDict, storage: Storage, opts: Verif
           const rows = Number(req[1]);
           if (rows === 0) break;
           const piece = Number(req[0]), offset = Number(req[2]), width = Number(req[3]);
-          // the rows as storage.get returns them, handed to the library as they are (tv_stream_commit_rows: its
-          // threads copy them into the pinned slot), so this thread copies nothing
-          const got: (Uint8Array | null)[] = new Array(rows).fill(null);
+          const slot = new Uint8Array(Deno.UnsafePointerView.getArrayBuffer(Deno.UnsafePointer.create(req[4])!, rows * width));
           // READS_IN_FLIGHT reads of the request outstanding at a time: each fsStorage.get is a Deno.open, and
           // an EMFILE from a thousand opens at once would come back as null -- a valid piece reported 0
           await eachLimited(rows, async (q) => {
@@ -330,19 +326,10 @@ export async function verifyStream(info: InfoDict, storage: Storage, opts: Verif
             if (n === 0) return;
             const bytes = await storage.get((piece + q) * L + offset, n);
             // a row must be exactly n bytes: more would spill into the next row (Python: unreadable too)
-            if (bytes && bytes.length === n) got[q] = bytes;
+            if (bytes && bytes.length === n) slot.set(bytes, q * width);
             else check(l, ctx, l.symbols.tv_stream_unreadable(ctx, BigInt(piece + q)));
           });
-          const srcs = new BigUint64Array(rows), lens = new BigUint64Array(rows);
-          got.forEach((b, q) => {
-            if (b && b.length) {
-              srcs[q] = BigInt(Deno.UnsafePointer.value(Deno.UnsafePointer.of(b)));
-              lens[q] = BigInt(b.length);
-            }
-          });
-          check(l, ctx, await l.symbols.tv_stream_commit_rows(ctx, reqp, ptr(new Uint8Array(srcs.buffer)),
-                                                              ptr(new Uint8Array(lens.buffer))));
-          got.length = 0; // (the buffers were alive until the library had copied them)
+          check(l, ctx, await l.symbols.tv_stream_commit(ctx, reqp));
         }
         const out = new Uint8Array(Math.ceil(count / 8));
         check(l, ctx, await l.symbols.tv_stream_end(ctx, ptr(out)));
