@@ -4,7 +4,8 @@ tests/ts_harness, on the GPU) runs verifyPieces / verifyStream over a JS restate
 Node's fs, whose work runs on libuv's thread pool as Deno's ops run on its blocking pool) and verifyFiles over the
 same directory.  Every bitfield is compared with the oracle's / the committed bits.
 
-    python tools/ts_storage_bench.py DIR [single16|files64|cfg3 ...]      (env UV_THREADPOOL_SIZE: libuv's pool)
+    python tools/ts_storage_bench.py DIR [single16|files64|cfg3 ...]      (env UV_THREADPOOL_SIZE: libuv's pool;
+                                                                           TS_SRC: another verify.ts, for A/Bs)
 
 One JSON line per (layout, path): best wall seconds of 2 runs, GB/s, exact."""
 import base64
@@ -144,7 +145,7 @@ def main():
     mod = os.path.join(d, "verify.mjs")
     os.makedirs(d, exist_ok=True)
     with open(mod, "w") as f:
-        f.write(erase(open(os.path.join(ROOT, "ts", "verify.ts")).read()))
+        f.write(erase(open(os.environ.get("TS_SRC") or os.path.join(ROOT, "ts", "verify.ts")).read()))
     for layout in sys.argv[2:] or ["single16"]:
         root = os.path.join(d, layout)
         info, expect, _ = write_layout(layout, root)
