@@ -571,7 +571,7 @@ def twin_rounds_loop_text() -> str:
             L.extend(body)
             L.append("v_add_u32_e64 %[h0], %[h0], %[r0]")
             L.extend(f"v_add_u32 %[h{i}], %[h{i}], %[r{i}]" for i in range(1, 5))
-            L += ["s_barrier", "s_cmp_eq_u32 %[cnt], 0",
+            L += (STAMP_SEQ if STAMP else ["s_barrier"]) + ["s_cmp_eq_u32 %[cnt], 0",
                   "s_cbranch_scc1 L_rdone_%=" if k < LDS_BUFS - 1 else "s_cbranch_scc0 L_rloop_%="]
         L += ["L_rdone_%=:", "s_waitcnt lgkmcnt(0)"]
         return "\n".join(f'    "{l}\\n"' for l in L)
@@ -613,7 +613,7 @@ def helper_loop_text(twin: bool = False) -> str:
         L.append(f"v_lshl_add_u64 v[{VL}:{VL + 1}], v[{VL}:{VL + 1}], 0, %[inc]")
 
     def step(pbase, off_base, barrier=True):
-        L.extend(_stamped("s_waitcnt vmcnt(4)", "svm") if STAMP >= 2 and not twin else ["s_waitcnt vmcnt(4)"])
+        L.extend(_stamped("s_waitcnt vmcnt(4)", "svm") if STAMP >= 2 else ["s_waitcnt vmcnt(4)"])
         body = (gen_helper2 if twin else gen_helper)([f"v{pbase + i}" for i in range(16)], off_base)
         perms, rest = body[:16], body[16:]
         # timing-only experiments (wrong digests): drop a class of the helper's work, keep its barriers
@@ -637,8 +637,8 @@ def helper_loop_text(twin: bool = False) -> str:
         if barrier and HELPER_WAIT == "mid" and not twin:
             L.extend(STAMP_SEQ if STAMP else ["s_barrier"])
         elif barrier:
-            L.extend(_stamped("s_waitcnt lgkmcnt(0)", "slg") if STAMP >= 2 and not twin else ["s_waitcnt lgkmcnt(0)"])
-            L.extend(STAMP_SEQ if STAMP and not twin else ["s_barrier"])
+            L.extend(_stamped("s_waitcnt lgkmcnt(0)", "slg") if STAMP >= 2 else ["s_waitcnt lgkmcnt(0)"])
+            L.extend(STAMP_SEQ if STAMP else ["s_barrier"])
 
     L.append("s_sub_u32 %[adv], %[nraw], 1")
     L.append(f"v_mov_b64 v[{VL}:{VL + 1}], %[va]")
@@ -1251,13 +1251,18 @@ def _stamp_patch(txt: str) -> str:
     assert not (PIPELINED or SPLIT_MID or SPLIT_PRE), "stamps are for the shipped per-block split rounds loop"
     for fn, sig_old, out_old in (
             ("tv_sha1_rounds_loop", "uint32_t nsteps,\n", '[cnt] "=&s"(cnt)\n'),
-            ("tv_sha1_helper_loop", "uint32_t nraw, uint32_t addr,\n", '[inc] "=&s"(inc)\n')):
-        extra = fn == "tv_sha1_helper_loop" and STAMP >= 2
+            ("tv_sha1_helper_loop", "uint32_t nraw, uint32_t addr,\n", '[inc] "=&s"(inc)\n'),
+            ("tv_sha1_twin_rounds_loop", "uint32_t nsteps) {\n", '[cnt] "=&s"(cnt)\n'),
+            ("tv_sha1_twin_helper_loop", "uint32_t addr, uint32_t psel,\n", '[inc] "=&s"(inc)\n')):
+        extra = fn in ("tv_sha1_helper_loop", "tv_sha1_twin_helper_loop") and STAMP >= 2
         i = txt.index(f"void {fn}(")
         j = txt.index("\n}\n", i)
         seg = txt[i:j]
-        for old, new in ((sig_old, sig_old[:-2] + (", uint32_t& sbar, uint32_t& svm, uint32_t& slg,\n" if extra
-                                                    else ", uint32_t& sbar,\n")),
+        if sig_old.endswith(") {\n"):   # (a signature ending the parameter list: add before the parenthesis)
+            sig_new = sig_old[:-4] + ", uint32_t& sbar) {\n"
+        else:
+            sig_new = sig_old[:-2] + (", uint32_t& sbar, uint32_t& svm, uint32_t& slg,\n" if extra else ", uint32_t& sbar,\n")
+        for old, new in ((sig_old, sig_new),
                          (out_old, out_old[:-1] + ', [sbar] "+s"(sbar)' + (', [svm] "+s"(svm), [slg] "+s"(slg)' if extra
                                                                           else "") + "\n"),
                          ('"scc", "memory");', '"s88", "s89", "s90", "s91", "scc", "memory");')):

@@ -1,4 +1,5 @@
-"""Where the split kernel's waves spend their cycles, from in-kernel clock stamps.
+"""Where the split (and twin, --kernel 4) kernel's waves spend their cycles, from in-kernel clock stamps (VERDICT r03
+item 5).
 
 A diagnostic library (tools/build_variants.py stamps:STAMP=1,D_TV_STAMPS=1 -> build/variants/libtv_stamps.so)
 brackets every in-loop workgroup barrier of the split kernel's rounds and helper waves with `s_memtime` reads and
@@ -41,14 +42,15 @@ def main():
     ap.add_argument("--shards", type=int, default=2)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--kernel", type=int, default=2, help="2 split, 4 twin (the 2-wave shape: wave 0 rounds, 1 helper)")
     a = ap.parse_args()
     L = a.piece_mib << 20
     P = a.pieces
     first, count = shard_ranges(P, a.shards)[0]
     stamped = hasattr(N.lib(), "tv_debug_stamps")
-    out = {"pieces_per_gpu": count, "piece_length": L, "lib": os.path.relpath(N.LIB_PATH, ROOT), "stamped": stamped}
+    out = {"kernel": a.kernel, "pieces_per_gpu": count, "piece_length": L, "lib": os.path.relpath(N.LIB_PATH, ROOT), "stamped": stamped}
     with N.Context(0) as ctx:
-        ctx.set_option(N.TV_OPT_KERNEL, 2)
+        ctx.set_option(N.TV_OPT_KERNEL, a.kernel)
         ctx.set_option(N.TV_OPT_CLOCK_PROBE, 1)
         ctx.set_layout(L * P, L, P, first, count)
         ctx.fill_synthetic(4)
@@ -77,7 +79,7 @@ def main():
                 fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
                 ctx._check(fn(ctx._h, buf, ctypes.sizeof(buf)))
                 reps.append([tuple(buf[4 + 8 * i:12 + 8 * i]) for i in range(4 * wgs)])
-        assert ctx.last_kernel()[0] == 2, "the split kernel did not run"
+        assert ctx.last_kernel()[0] == a.kernel, "the requested kernel did not run"
     out.update({"workgroups": wgs, "kernel_ms": [round(x, 3) for x in ms], "kernel_ms_median": round(statistics.median(ms), 3),
                 "gbps": round(L * count / (statistics.median(ms) / 1e3) / 1e9, 1),
                 "clock_ghz": [round(c, 3) for c in clocks]})

@@ -604,7 +604,20 @@ __global__ __launch_bounds__(64 * kTwinWaves[SHAPE]) void tv_twin_kernel(TvPiece
         const uint32_t psel = (lane & 1u) ? 0x07060504u : 0x03020100u;
         uint32_t b = b0;
         if (fast_end > b0) {
+#if TV_STAMPS
+            LoopStamp st;
+            st.start();
+#if TV_SHA1_STAMP >= 2
+            tv_sha1_twin_helper_loop(piece + (uint64_t)b0 * 64, fast_end - b0, lds_lane, psel, st.bar, st.vm, st.lg,
+                                     TV_K0, TV_K1, TV_K2, TV_K3);
+#else
+            tv_sha1_twin_helper_loop(piece + (uint64_t)b0 * 64, fast_end - b0, lds_lane, psel, st.bar,
+                                     TV_K0, TV_K1, TV_K2, TV_K3);
+#endif
+            st.end(p, wave, fast_end - b0);
+#else
             tv_sha1_twin_helper_loop(piece + (uint64_t)b0 * 64, fast_end - b0, lds_lane, psel, TV_K0, TV_K1, TV_K2, TV_K3);
+#endif
             b = fast_end;
         }
         for (; b <= end; b++) {
@@ -628,7 +641,14 @@ __global__ __launch_bounds__(64 * kTwinWaves[SHAPE]) void tv_twin_kernel(TvPiece
     uint32_t b = b0;
     const uint32_t full_end = end < g.nb_min ? end : g.nb_min;
     if (b < full_end) {
+#if TV_STAMPS
+        LoopStamp st;
+        st.start();
+        tv_sha1_twin_rounds_loop(h, ring_base, full_end - b, st.bar);
+        st.end(p, wave, full_end - b);
+#else
         tv_sha1_twin_rounds_loop(h, ring_base, full_end - b);
+#endif
         b = full_end;
     }
     // the short last piece's workgroup: lanes past their final block keep their digest (both lanes of a
