@@ -81,7 +81,8 @@ def test_asm_generator_stamp_headers(tmp_path, stamp):
     assert f"#define TV_SHA1_STAMP {stamp}" in h
     assert "tv_sha1_rounds_loop(uint32_t h[5], uint32_t addr, uint32_t nsteps, uint32_t& sbar," in h
     assert ('uint32_t& sbar, uint32_t& svm, uint32_t& slg,' in h) == (stamp == "2")
-    assert h.count('"s88", "s89", "s90", "s91"') == 2
+    assert h.count('"s88", "s89", "s90", "s91"') == 4      # split and twin: rounds and helper loops
+    assert "tv_sha1_twin_rounds_loop(uint32_t h[5], uint32_t addr, uint32_t nsteps, uint32_t& sbar) {" in h
     assert ("%[svm]" in h) == (stamp == "2") and "%[sbar]" in h
     if stamp == "2":   # the drain stamp needs the drain: the pre-round-4 helper wait (TV_GEN_HWAIT=0)
         assert "%[slg]" not in h
