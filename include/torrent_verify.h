@@ -115,8 +115,8 @@ int tv_stage(tv_ctx *ctx, uint64_t linear_offset, const uint8_t *src, uint64_t l
  * linear_offsets[k] + lens[k]).  The same clipping, windows (ascending, as consecutive tv_stage calls) and mark
  * clearing apply, in order k = 0 .. n-1; every copy is complete when the call returns.  For a host that holds a
  * batch of pieces as separate buffers (one Storage.get result per piece, storage.ts:50-65): the library copies
- * them into its pinned ring on its own threads, so the caller does no gather copy.  Replaces: the same reads as
- * tv_stage.
+ * them into its pinned ring on its own threads, so the caller does no gather copy.  Replaces: a batch of
+ * Storage.get results (storage.ts:50-65), one per piece, as verifyPieces collects them.
  */
 int tv_stage_many(tv_ctx *ctx, uint64_t n, const uint64_t *linear_offsets, const uint8_t *const *srcs,
                   const uint64_t *lens);
