@@ -19,7 +19,7 @@ def _bits(bf, n):
 
 
 def _column(L, count, chunk):
-    """The library's column width (tv_api.hip stream_column): TV_OPT_STREAM_CHUNK, or the widest power of
+    """The library's column width (tv_stream.hip stream_column): TV_OPT_STREAM_CHUNK, or the widest power of
     two from 64 KiB up to L whose column of every piece stays <= 512 MiB; at most one 64 MiB slot."""
     C = chunk
     if not C:

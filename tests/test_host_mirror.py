@@ -327,7 +327,7 @@ def test_info_hash_is_sha1_of_the_original_info_bytes(name):
 def _fs_openable(path: str) -> bool:
     """Would fsStorage.get's Deno.open(path, {read, write, create}) succeed (storage.ts:28-32,158)?  Without
     creating anything: an existing non-directory with read + write access, or a missing file in an existing,
-    writable directory.  (The CPU stand-in's copy of tv_api.hip fs_openable.)"""
+    writable directory.  (The CPU stand-in's copy of tv_core.hip fs_openable.)"""
     import stat
     try:
         st = os.stat(path)
@@ -342,7 +342,7 @@ def _fs_openable(path: str) -> bool:
 class _ImageCtx:
     """Stand-in for a tv_ctx on CPU: tv_stage_files writes into a linear image of the shard, so
     verify_files' staging plan (the storage.ts segment mapping, one batched call) is checked without a GPU.
-    Files are read the way the library reads them, and a failed segment is handled as tv_api.hip
+    Files are read the way the library reads them, and a failed segment is handled as tv_files.hip
     recover_segment does (restated): the whole pieces of the file's readable prefix are staged, the pieces
     from the first unreadable byte to the segment's end are marked (`bad`, linear piece indices), and a
     failed zero-length segment marks its piece."""
@@ -382,7 +382,7 @@ class _ImageCtx:
         out = []
         for path, foff, off, n in zip(paths, file_offsets, linear_offsets, lens):
             foff, off, n = int(foff), int(off), int(n)
-            if n == 0:   # the library's zero-length rule (tv_api.hip fs_openable), restated
+            if n == 0:   # the library's zero-length rule (tv_core.hip fs_openable), restated
                 ok = _fs_openable(path)
                 out.append(0 if ok else -5)
                 if not ok:

@@ -12,6 +12,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 CSRC = os.path.join(ROOT, "torrent_amd", "csrc")
 OUT = os.path.join(ROOT, "build", "variants")
 HIPCC = "/opt/rocm/bin/hipcc"
@@ -25,7 +26,8 @@ def build(name, env):
                            os.path.join(CSRC, "sha1_asm.h")], env=e, stdout=subprocess.DEVNULL)
     os.makedirs(OUT, exist_ok=True)
     objs = []
-    for src in ("tv_kernels.hip", "tv_api.hip"):
+    from torrent_amd._build import SOURCES, EXPORTS
+    for src in SOURCES:
         o = os.path.join(OUT, f"{name}_{src}.o")
         subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I",
                                os.path.join(ROOT, "include")] + defs + ["-c", os.path.join(CSRC, src), "-o", o])
@@ -34,7 +36,7 @@ def build(name, env):
     subprocess.check_call(["g++", "-O3", "-std=c++17", "-fPIC", "-c", os.path.join(CSRC, "tv_host.cpp"), "-o", o])
     objs.append(o)
     lib = os.path.join(OUT, f"libtv_{name}.so")
-    subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib] + objs)
+    subprocess.check_call([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", f"-Wl,--version-script={EXPORTS}", "-o", lib] + objs)
     for x in objs:
         os.remove(x)
     print(lib)

@@ -1,6 +1,6 @@
 """Piece-count sweep: HBM-resident verify throughput of every kernel variant vs pieces per GPU
 (16 GiB payload per point, piece length = 16 GiB / P rounded to 64 B).  Substantiates the
-auto kernel choice (tv_api.hip choose_kernel) and the piece-parallelism ceiling of DESIGN.md 4.
+auto kernel choice (tv_core.hip choose_kernel) and the piece-parallelism ceiling of DESIGN.md 4.
 usage: python tools/sweep_pieces.py [out.jsonl]"""
 import json
 import os

@@ -15,8 +15,10 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libtorrent_verify.so")
-SOURCES = ["tv_kernels.hip", "tv_api.hip"]
+SOURCES = ["tv_kernels.hip", "tv_core.hip", "tv_context.hip", "tv_stage.hip", "tv_files.hip",
+           "tv_stream.hip", "tv_verify.hip"]
 HOST_SOURCES = ["tv_host.cpp"]          # host-only C++ (no device code): the host compiler
+EXPORTS = os.path.join(CSRC, "exports.map")   # the link exports tv_* only
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 ARCH = os.environ.get("TV_OFFLOAD_ARCH", "gfx950")
@@ -37,18 +39,25 @@ def build(force: bool = False, verbose: bool = False) -> str:
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     host_srcs = [os.path.join(CSRC, s) for s in HOST_SOURCES]
     deps = srcs + host_srcs + [header, os.path.join(CSRC, "tv_internal.h"), os.path.join(CSRC, "tv_host.h"),
+                               os.path.join(CSRC, "tv_ctx.h"), os.path.join(CSRC, "tv_options_internal.h"), EXPORTS,
                                os.path.join(ROOT, "include", "torrent_verify.h")]
     if not (force or _newer(LIB, deps)):
         return LIB
     objs = []
+    cmds = []
     for s in srcs:
         o = os.path.join(CSRC, os.path.basename(s) + ".o")
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-               "-I", os.path.join(ROOT, "include"), "-c", s, "-o", o]
+        cmds.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+                     "-I", os.path.join(ROOT, "include"), "-c", s, "-o", o])
+        objs.append(o)
+    procs = []
+    for cmd in cmds:                       # (the translation units compile side by side)
         if verbose:
             print(" ".join(cmd))
-        subprocess.check_call(cmd)
-        objs.append(o)
+        procs.append(subprocess.Popen(cmd))
+    bad = [cmd for cmd, p in zip(cmds, procs) if p.wait() != 0]
+    if bad:
+        raise subprocess.CalledProcessError(1, bad[0])
     for s in host_srcs:
         o = os.path.join(CSRC, os.path.basename(s) + ".o")
         cmd = [CXX, "-O3", "-std=c++17", "-fPIC", "-Wall", "-c", s, "-o", o]
@@ -56,7 +65,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
             print(" ".join(cmd))
         subprocess.check_call(cmd)
         objs.append(o)
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", f"-Wl,--version-script={EXPORTS}", "-o", LIB] + objs
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

@@ -1,4 +1,4 @@
-// tv_internal.h -- shared between the kernels (tv_kernels.hip) and the C ABI (tv_api.hip).
+// tv_internal.h -- shared between the kernels (tv_kernels.hip) and the C ABI (tv_core.hip, tv_context.hip, ...: see tv_ctx.h).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

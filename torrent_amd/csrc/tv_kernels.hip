@@ -762,7 +762,7 @@ __global__ __launch_bounds__(256) void tv_fill_bytes_kernel(uint8_t* payload, ui
 }
 
 // ------------------------------------------------------------------------------------------
-// windowed layouts (tv_api.hip): the windows are hashed (HASH kernels into the shard's digest rows) as they
+// windowed layouts (tv_core.hip): the windows are hashed (HASH kernels into the shard's digest rows) as they
 // fill, and tv_verify compares the whole shard at the end -- 40 B read per piece, one word written per 64.
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void tv_compare_kernel(const uint32_t* hash, const uint32_t* digests,
@@ -783,7 +783,7 @@ __global__ __launch_bounds__(256) void tv_compare_kernel(const uint32_t* hash, c
 }
 
 // ------------------------------------------------------------------------------------------
-// host-side launchers (called by tv_api.hip)
+// host-side launchers (called by tv_core.hip, tv_stream.hip, tv_verify.hip)
 // ------------------------------------------------------------------------------------------
 hipError_t tv_launch_verify(const TvPieces& p, int kernel, bool hash, hipStream_t s, int split_pairs,
                             uint32_t* workgroups) {

@@ -1,0 +1,363 @@
+// tv_stream.hip -- the streamed verify engine (tv_stream_*; tv_verify_host runs on it): a bounded pinned ring
+// between the caller's bytes and two device chunk buffers, one kernel launch per column / window of pieces.
+#include <cstring>
+
+#include "tv_ctx.h"
+
+namespace tvi {
+
+// ---- streamed verify (tv_stream_*; tv_verify_host runs on it too) ------------------------------------
+//
+// Column `col` carries bytes [col*C, col*C + C) of every shard piece.  Its rows arrive as requests of up to
+// one ring slot (64 MiB) each, filled by the caller, and are DMA'd from the slot into device chunk buffer
+// col & 1 (row pitch C + 256).  When a column's last request is committed, one kernel launch hashes it on the
+// compute stream (chaining values persist in d_state; the last column pads, compares and writes the
+// bitfield) while the next column's requests fill the other buffer.  Host memory in flight: the ring.
+
+uint64_t row_bytes(const tv_ctx* c, uint64_t piece, uint64_t offset, uint64_t width) {  // piece.ts:16-19
+    const uint64_t plen = piece_len(c, piece);
+    return plen > offset ? std::min(width, plen - offset) : 0;
+}
+
+// Drop an active stream: give its lent slot back and let the queued copies and kernels drain.
+void stream_abort_locked(tv_ctx* c) {
+    StreamState& st = c->st;
+    if (!st.active) return;
+    if (st.outstanding && st.slot >= 0) (void)release_slot(c, st.slot, 0);
+    (void)hipStreamSynchronize(c->copy_stream);
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipGetLastError();
+    st = StreamState{};
+}
+
+// Row mode (TV_OPT_STREAM_ROWS): each request row is a whole piece (one Storage.get per piece), which needs a
+// piece to fit one ring slot.
+bool stream_rows(const tv_ctx* c) { return c->stream_rows && c->L <= kRingSlotBytes; }
+
+// Row mode's window: whole pieces per chunk buffer, a multiple of 64 (bitfield words of their own), at most
+// kRowWindowBytes per buffer (TV_OPT_RESIDENT_BUDGET / 2 if smaller), the shard when it fits.
+constexpr uint64_t kRowWindowBytes = 4ull << 30;
+uint64_t stream_row_window(const tv_ctx* c) {
+    const uint64_t pitch = (c->L + 63) / 64 * 64 + 256;
+    uint64_t bytes = kRowWindowBytes;
+    if (c->budget_opt) bytes = std::min<uint64_t>(bytes, c->budget_opt / 2);
+    const uint64_t w = std::max<uint64_t>(64, bytes / pitch / 64 * 64);
+    return std::min<uint64_t>(w, c->count);
+}
+
+// Column width: TV_OPT_STREAM_CHUNK, or ~512 MiB columns (64 KiB .. L); a multiple of 64, at most one slot.
+uint64_t stream_column(const tv_ctx* c) {
+    uint64_t C = c->stream_chunk;
+    if (!C) {
+        C = 64ull << 10;
+        while (C * 2 <= c->L && C * 2 * c->count <= (512ull << 20)) C *= 2;
+    }
+    C = std::min<uint64_t>((C / 64) * 64, ((c->L + 63) / 64) * 64);
+    return std::max<uint64_t>(64, std::min<uint64_t>(C, kRingSlotBytes));
+}
+
+// Bytes of each of the two device chunk buffers a stream over the current geometry needs.
+uint64_t stream_chunk_need(const tv_ctx* c) {
+    if (!c->count) return 0;
+    if (stream_rows(c)) return ((c->L + 63) / 64 * 64 + 256) * stream_row_window(c) + kSlack;
+    return (stream_column(c) + 256) * c->count + kSlack;
+}
+
+int stream_begin_locked(tv_ctx* c, const uint8_t* avail_bits) {
+    StreamState& st = c->st;
+    st = StreamState{};
+    st.av.assign((c->count + 7) / 8, 0xFF);
+    if (avail_bits) memcpy(st.av.data(), avail_bits, st.av.size());
+    if (c->count == 0) {  // nothing to hash: the first tv_stream_next reports completion
+        st.active = true;
+        return TV_OK;
+    }
+    if (stream_rows(c)) {  // whole pieces per row, windows of wn pieces
+        st.C = (c->L + 63) / 64 * 64;
+        st.wn = stream_row_window(c);
+    } else {               // columns across the whole shard
+        st.C = stream_column(c);
+        st.wn = c->count;
+    }
+    st.row_pitch = st.C + 256;  // (tail over-read slack per row)
+    const uint64_t need = st.row_pitch * st.wn + kSlack;
+    if (!reuse_fits(need, c->chunk_bytes)) {
+        free_chunks(c);
+        for (auto& p : c->d_chunk) {
+            TV_HIP(c, hipMalloc((void**)&p, need));
+            c->n_device_allocs++;
+        }
+        c->chunk_bytes = need;
+    }
+    st.ncol = (c->L + st.C - 1) / st.C;
+    st.nwin = (c->count + st.wn - 1) / st.wn;
+    st.nunits = st.nwin * st.ncol;
+    st.rows_per_req = std::max<uint64_t>(1, kRingSlotBytes / st.C);
+    TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
+    TV_HIP(c, hipMemsetAsync(c->d_out, 0, c->bit_words * 8, c->stream));  // fail closed, as tv_verify
+    TV_HIP(c, hipEventRecord(c->done_ev[0], c->stream));
+    TV_HIP(c, hipEventRecord(c->done_ev[1], c->stream));
+    st.active = true;
+    return TV_OK;
+}
+
+int stream_next_locked(tv_ctx* c, tv_stream_req* req) {
+    StreamState& st = c->st;
+    if (!st.active) return fail(c, TV_ERR_STATE, "tv_stream_begin has not been called");
+    if (st.outstanding)
+        return fail(c, TV_ERR_STATE, "request %llu is still outstanding (commit it first)", (unsigned long long)st.req.seq);
+    *req = tv_stream_req{};
+    if (st.unit >= st.nunits) return TV_OK;  // rows == 0: every byte has been requested
+    const int buf = (int)(st.unit & 1);
+    const uint64_t j0 = st.unit / st.ncol * st.wn, wcount = std::min(st.wn, c->count - j0);
+    // the first copy into chunk buffer `buf` waits for the kernel that last read it
+    if (st.row == 0) TV_HIP(c, hipStreamWaitEvent(c->copy_stream, c->done_ev[buf], 0));
+    int rc = take_slot(c, &st.slot, 0);
+    if (rc) return rc;
+    req->piece = c->first + j0 + st.row;
+    req->rows = std::min<uint64_t>(st.rows_per_req, wcount - st.row);
+    req->offset = st.unit % st.ncol * st.C;
+    req->width = std::min<uint64_t>(st.C, c->L - req->offset);
+    req->slot = c->ring[st.slot];
+    req->seq = ++st.seq;
+    st.req = *req;
+    st.outstanding = true;
+    return TV_OK;
+}
+
+// Queue the outstanding request's rows [0, rows_copy) (the others are unreadable and not copied).  Source:
+// the request's slot (src == nullptr), or caller memory at src (row q at src + q*pitch), DMA'd directly when
+// page-locked and gathered into the slot otherwise.  Completes the column: one kernel launch.
+int stream_commit_locked(tv_ctx* c, const tv_stream_req* req, const uint8_t* src, uint64_t pitch, bool pinned,
+                         uint64_t rows_copy) {
+    StreamState& st = c->st;
+    if (!st.active) return fail(c, TV_ERR_STATE, "tv_stream_begin has not been called");
+    if (!st.outstanding) return fail(c, TV_ERR_STATE, "no outstanding request (call tv_stream_next)");
+    if (!req || req->seq != st.req.seq || req->piece != st.req.piece || req->rows != st.req.rows)
+        return fail(c, TV_ERR_ARG, "the request does not match outstanding request %llu", (unsigned long long)st.req.seq);
+    const tv_stream_req r = st.req;
+    const int buf = (int)(st.unit & 1);
+    const uint64_t j0 = st.unit / st.ncol * st.wn, wcount = std::min(st.wn, c->count - j0);
+    uint8_t* dst = c->d_chunk[buf] + st.row * st.row_pitch;
+    uint8_t* slot = c->ring[st.slot];
+    const uint64_t n = std::min(rows_copy, r.rows);
+    uint64_t full = n;  // rows [0, full) carry `width` bytes; only the torrent's short last piece has fewer
+    if (full && row_bytes(c, r.piece + full - 1, r.offset, r.width) < r.width) full--;
+    const uint64_t tail = full < n ? row_bytes(c, r.piece + full, r.offset, r.width) : 0;
+    const uint8_t* from = slot;
+    uint64_t from_pitch = r.width;
+    if (src) {
+        if (pinned) {
+            from = src;
+            from_pitch = pitch;
+        } else {
+            gather_rows(c->pool[0], slot, src, r.width, pitch, full, c->file_threads);
+            if (tail) memcpy(slot + full * r.width, src + full * pitch, tail);
+        }
+    }
+    if (full)
+        TV_HIP(c, hipMemcpy2DAsync(dst, st.row_pitch, from, from_pitch, r.width, full, hipMemcpyHostToDevice,
+                                   c->copy_stream));
+    if (tail)
+        TV_HIP(c, hipMemcpyAsync(dst + full * st.row_pitch, from + full * from_pitch, tail, hipMemcpyHostToDevice,
+                                 c->copy_stream));
+    st.outstanding = false;
+    const int s = st.slot;
+    st.slot = -1;
+    int rc = release_slot(c, s, 0);  // its event follows the copies just queued
+    if (rc) return rc;
+    st.row += r.rows;
+    if (st.row < wcount) return TV_OK;
+    // the unit is complete: hash it while the caller fills the next one
+    TV_HIP(c, hipEventRecord(c->col_ev[buf], c->copy_stream));
+    TV_HIP(c, hipStreamWaitEvent(c->stream, c->col_ev[buf], 0));
+    if (!st.k0) {
+        TV_HIP(c, hipEventRecord(c->ev_k0, c->stream));
+        st.k0 = true;
+    }
+    const bool last = st.unit % st.ncol + 1 == st.ncol;
+    // the window's pieces (the shard's digest / state rows from j0; bitfield words from j0 / 64: a window of a
+    // multi-window stream is a multiple of 64 pieces)
+    TvPieces p = window_launch(c, j0, wcount, c->d_chunk[buf]);
+    p.stride = st.row_pitch;
+    p.avail64 = c->d_base_avail + j0 / 64;
+    p.out64 = c->d_out + j0 / 64;
+    p.data_off = r.offset;
+    p.blk_begin = r.offset / 64;
+    p.blk_end = last ? UINT64_MAX : (r.offset + st.C) / 64;
+    p.finalize = last ? 1 : 0;
+    st.kernel = choose_kernel_n(c, wcount, p.n_main < p.n);
+    p.lane_pairs = lane_pairs_for(c, p.n);
+    TV_HIP(c, tv_launch_verify(p, st.kernel, false, c->stream, c->split_pairs, &c->last_workgroups));
+    TV_HIP(c, hipEventRecord(c->done_ev[buf], c->stream));
+    st.unit++;
+    st.row = 0;
+    return TV_OK;
+}
+
+int stream_end_locked(tv_ctx* c, uint8_t* bitfield_out) {
+    StreamState& st = c->st;
+    if (!st.active) return fail(c, TV_ERR_STATE, "tv_stream_begin has not been called");
+    if (st.outstanding || st.unit < st.nunits) {
+        const unsigned long long done = st.unit, all = st.nunits;
+        stream_abort_locked(c);
+        return fail(c, TV_ERR_STATE, "stream ended before its last column (%llu of %llu hashed); aborted", done, all);
+    }
+    if (c->count) {
+        if (!bitfield_out) {
+            stream_abort_locked(c);
+            return fail(c, TV_ERR_ARG, "bitfield_out is NULL");
+        }
+        TV_HIP(c, hipEventRecord(c->ev_k1, c->stream));
+        int rc = read_bits(c, bitfield_out);
+        if (rc) {
+            stream_abort_locked(c);
+            return rc;
+        }
+        for (size_t k = 0; k < st.av.size(); k++) bitfield_out[k] &= st.av[k];  // unreadable pieces: bit 0
+        c->last_kernel = st.kernel;
+        c->last_launches = (int)st.nunits;
+        rc = finish_timing(c);
+        st = StreamState{};
+        return rc;
+    }
+    st = StreamState{};
+    return TV_OK;
+}
+
+
+// Public stream calls: a HIP failure leaves the stream unusable, so it is aborted (the ctx stays usable).
+int stream_result(tv_ctx* c, int rc) {
+    if (rc == TV_ERR_HIP || rc == TV_ERR_NOMEM) stream_abort_locked(c);
+    return rc;
+}
+
+
+}  // namespace tvi
+
+using namespace tvi;
+
+extern "C" {
+
+// End-to-end verification from a host buffer holding the whole shard (tv_verify_host): the stream engine
+// with the caller's buffer as the producer.  Each request's rows are one 2D DMA straight from a page-locked
+// source (src pitch L) or are gathered into the request's ring slot first.  Rows past src_len are not
+// copied; their pieces are unreadable.
+int tv_verify_host(tv_ctx* c, const uint8_t* src, uint64_t src_len, const uint8_t* avail_bits,
+                   uint8_t* bitfield_out) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = require_layout(c, true);
+    if (rc) return rc;
+    if (!bitfield_out && c->count) return fail(c, TV_ERR_ARG, "bitfield_out is NULL");
+    if (!src && src_len) return fail(c, TV_ERR_ARG, "src is NULL");
+    if (!c->count) return TV_OK;
+    TV_HIP(c, hipSetDevice(c->device));
+    // pieces whose bytes extend past src_len are unreadable
+    std::vector<uint8_t> av((c->count + 7) / 8, 0);
+    for (uint64_t j = 0; j < c->count; j++) {
+        const uint64_t end = j * c->L + piece_len(c, c->first + j);
+        if (end <= src_len && (!avail_bits || get_bit(avail_bits, j))) set_bit(av.data(), j);
+    }
+    const bool pinned = is_pinned(src);
+    DrainGuard drain(c);  // no DMA reads the caller's buffer after the call returns, also on error paths
+    rc = stream_begin_locked(c, av.data());
+    if (rc) {
+        stream_abort_locked(c);
+        return rc;
+    }
+    for (;;) {
+        tv_stream_req req;
+        rc = stream_next_locked(c, &req);
+        if (rc || !req.rows) break;
+        // rows wholly inside src: a prefix of the request (its rows ascend in linear offset)
+        const uint64_t base = (req.piece - c->first) * c->L + req.offset;
+        uint64_t k = 0;
+        while (k < req.rows && base + k * c->L + row_bytes(c, req.piece + k, req.offset, req.width) <= src_len) k++;
+        rc = stream_commit_locked(c, &req, k ? src + base : nullptr, c->L, pinned, k);
+        if (rc) break;
+    }
+    if (rc) {
+        stream_abort_locked(c);
+        return rc;
+    }
+    return stream_end_locked(c, bitfield_out);
+}
+
+int tv_stream_begin(tv_ctx* c, const uint8_t* avail_bits) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = require_layout(c, true);
+    if (rc) return rc;
+    TV_HIP(c, hipSetDevice(c->device));
+    return stream_result(c, stream_begin_locked(c, avail_bits));
+}
+
+int tv_stream_next(tv_ctx* c, tv_stream_req* req) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    if (!req) return fail(c, TV_ERR_ARG, "req is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    TV_HIP(c, hipSetDevice(c->device));
+    return stream_result(c, stream_next_locked(c, req));
+}
+
+int tv_stream_commit(tv_ctx* c, const tv_stream_req* req) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    TV_HIP(c, hipSetDevice(c->device));
+    return stream_result(c, stream_commit_locked(c, req, nullptr, 0, true, req ? req->rows : 0));
+}
+
+int tv_stream_commit_from(tv_ctx* c, const tv_stream_req* req, const uint8_t* src, uint64_t src_pitch) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    if (!src) return fail(c, TV_ERR_ARG, "src is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (req && req->rows > 1 && src_pitch < req->width)
+        return fail(c, TV_ERR_ARG, "src_pitch %llu is shorter than the row width %llu", (unsigned long long)src_pitch,
+                    (unsigned long long)req->width);
+    TV_HIP(c, hipSetDevice(c->device));
+    return stream_result(c, stream_commit_locked(c, req, src, src_pitch, is_pinned(src), req ? req->rows : 0));
+}
+
+int tv_stream_unreadable(tv_ctx* c, uint64_t piece) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->st.active) return fail(c, TV_ERR_STATE, "tv_stream_begin has not been called");
+    if (piece < c->first || piece >= c->first + c->count)
+        return fail(c, TV_ERR_ARG, "piece %llu is not in this context's shard", (unsigned long long)piece);
+    const uint64_t j = piece - c->first;
+    c->st.av[j >> 3] &= (uint8_t)~(0x80u >> (j & 7));
+    return TV_OK;
+}
+
+int tv_stream_end(tv_ctx* c, uint8_t* bitfield_out) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    TV_HIP(c, hipSetDevice(c->device));
+    return stream_end_locked(c, bitfield_out);
+}
+
+int tv_stream_abort(tv_ctx* c) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    TV_HIP(c, hipSetDevice(c->device));
+    stream_abort_locked(c);
+    return TV_OK;
+}
+
+int tv_stream_fill_synthetic(tv_ctx* c, const tv_stream_req* req, uint64_t seed) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    const StreamState& st = c->st;
+    if (!st.active || !st.outstanding) return fail(c, TV_ERR_STATE, "no outstanding request (call tv_stream_next)");
+    if (!req || req->seq != st.req.seq) return fail(c, TV_ERR_ARG, "the request does not match the outstanding one");
+    const tv_stream_req r = st.req;
+    uint8_t* slot = c->ring[st.slot];
+    c->pool[0].run(c->file_threads, r.rows, [&](uint64_t q) {
+        const uint64_t i = r.piece + q;
+        tv_synth_fill_host(seed, i * c->L + r.offset, row_bytes(c, i, r.offset, r.width), slot + q * r.width);
+    });
+    return TV_OK;
+}
+
+}  // extern "C"
