@@ -201,6 +201,9 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
             }
             c->clock_probe = value != 0;
             return TV_OK;
+        case TV_OPT_FILE_CLOCK_RESET:
+            for (auto& v : c->file_ns) v.store(0);
+            return TV_OK;
         case TV_OPT_STREAM_ROWS:
             if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_STREAM_ROWS must be 0 or 1");
             if (c->st.active) return fail(c, TV_ERR_STATE, "TV_OPT_STREAM_ROWS cannot change during a stream");
@@ -485,6 +488,9 @@ int tv_get_counter(tv_ctx* c, int key, uint64_t* value) {
         case TV_COUNTER_WINDOWS: *value = c->win_launched; return TV_OK;
         case TV_COUNTER_BUDGET: *value = c->budget; return TV_OK;
         case TV_COUNTER_SLOTS_USED: *value = c->slot_of.size(); return TV_OK;
+        case TV_COUNTER_FILE_CLOCK + TV_FILE_PHASE_OPEN ... TV_COUNTER_FILE_CLOCK + TV_FILE_CLOCK_N - 1:
+            *value = c->file_ns[key - TV_COUNTER_FILE_CLOCK].load();
+            return TV_OK;
         case TV_COUNTER_LAST_CLOCK_KHZ: {
             *value = 0;
             if (!c->d_clock) return TV_OK;

@@ -427,6 +427,7 @@ uint8_t* win_base(const tv_ctx* c, int buf) { return c->d_payload + (uint64_t)bu
 int piece_dst(tv_ctx* c, uint64_t i, uint8_t** out) {
     const uint64_t j = i - c->first;
     if (c->slots) {
+        std::lock_guard<std::mutex> g(c->slot_mu);  // (a tv_stage_files helper may stage on lane 1 meanwhile)
         auto it = c->slot_of.find(j);
         if (it == c->slot_of.end()) {
             if (c->slot_free.empty())

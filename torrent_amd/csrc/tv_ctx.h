@@ -268,6 +268,7 @@ struct tv_ctx {
     uint64_t slots = 0;                // slots of the current layout (0: not a slot layout)
     std::unordered_map<uint64_t, uint32_t> slot_of;  // shard-relative piece -> slot
     std::vector<uint32_t> slot_free;
+    std::mutex slot_mu;                // piece_dst's slot path: tv_stage_files' lane-1 helper stages beside the caller
 
     bool open_rw = true;               // TV_OPT_OPEN_RW: files opened read + write (fsStorage.get) or read-only
     bool stream_rows = false;          // TV_OPT_STREAM_ROWS: stream requests carry whole pieces (windows of pieces)
@@ -275,6 +276,7 @@ struct tv_ctx {
     bool clock_probe = false;          // TV_OPT_CLOCK_PROBE: verify / hash launches stamp their clock into d_clock
     uint64_t* d_clock = nullptr;       // {shader clock, real-time} counters at the start and end of workgroup 0
     cpu_set_t proc_cpus;               // the process's CPUs at tv_create (what "unpinned" workers run on)
+    std::atomic<uint64_t> file_ns[TV_FILE_CLOCK_N] = {};  // the file staging phase clock (tv_options_internal.h)
     bool proc_cpus_ok = false;
 };
 

@@ -7,6 +7,7 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <chrono>
 #include <cstring>
 
 #include "tv_ctx.h"
@@ -38,142 +39,239 @@ double resident_fraction(void* m, uint64_t n, uint64_t page) {
     return vec.empty() ? 1.0 : (double)r / (double)vec.size();
 }
 
-// Read file bytes [fo, fo + n) into dst with parallel preads (4 MiB parts on up to max_threads threads,
-// TV_OPT_FILE_THREADS: a cold file is read with many large requests in flight).  Returns 0 or an
-// errno value (EIO for a short read).
-int pread_parallel(int fd, uint8_t* dst, uint64_t fo, uint64_t n, int max_threads, const cpu_set_t* cpus) {
-    const uint64_t part = 4ull << 20;
+// Read file bytes [fo, fo + n) into dst with parallel preads on the lane's persistent workers (`threads` of
+// them; parts of 1-4 MiB, at least two per thread so the slowest part ends the slot early).  Returns 0 or an errno
+// value (EIO for a short read).  The round-1..4 form spawned `threads` std::threads per 64 MiB slot.
+int pread_pool(Pool& pool, int threads, int fd, uint8_t* dst, uint64_t fo, uint64_t n) {
+    threads = std::max(1, threads);
+    uint64_t part = n / (2 * (uint64_t)threads);
+    part = std::min<uint64_t>(4ull << 20, std::max<uint64_t>(1ull << 20, (part + 65535) / 65536 * 65536));
     const uint64_t nparts = (n + part - 1) / part;
-    const int threads = (int)std::min<uint64_t>((uint64_t)std::max(1, max_threads), nparts);
-    std::vector<int> err(threads, 0);
-    auto work = [&](int t) {
-        for (uint64_t q = t; q < nparts; q += threads) {
-            uint64_t o = q * part;
-            const uint64_t e = std::min(n, o + part);
-            while (o < e) {
-                const ssize_t got = pread(fd, dst + o, e - o, (off_t)(fo + o));
-                if (got < 0 && errno == EINTR) continue;
-                if (got <= 0) {
-                    err[t] = got < 0 ? errno : EIO;
-                    return;
-                }
-                o += (uint64_t)got;
+    std::atomic<int> err{0};
+    pool.run(threads, nparts, [&](uint64_t q) {
+        uint64_t o = q * part;
+        const uint64_t e = std::min(n, o + part);
+        while (o < e && !err.load(std::memory_order_relaxed)) {
+            const ssize_t got = pread(fd, dst + o, e - o, (off_t)(fo + o));
+            if (got < 0 && errno == EINTR) continue;
+            if (got <= 0) {
+                int expect = 0;
+                err.compare_exchange_strong(expect, got < 0 ? errno : EIO);
+                return;
             }
+            o += (uint64_t)got;
         }
-    };
-    std::vector<std::thread> th;
-    for (int t = 1; t < threads; t++)
-        th.emplace_back([&work, cpus, t] {
-            pin_thread(cpus);
-            work(t);
-        });
-    if (threads > 0) work(0);
-    for (auto& t : th) t.join();
-    for (int e : err)
-        if (e) return e;
-    return 0;
+    });
+    return err.load();
 }
 
-// Memory-mapped windows of a file for tv_stage_file; released (unregistered, unmapped) on every exit.
-// Declared BEFORE the call's DrainGuard, so the streams are drained before any window goes away.
+// The phase clock of file staging (internal counters TV_COUNTER_FILE_NS_*, tv_options_internal.h): nanoseconds a
+// scope spent, added to the ctx's total for its phase (both lanes add; a lane's phases do not overlap each other).
+struct FileClock {
+    tv_ctx* c;
+    int phase;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    FileClock(tv_ctx* ctx, int ph) : c(ctx), phase(ph) {}
+    ~FileClock() {
+        const auto ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+        c->file_ns[phase].fetch_add((uint64_t)ns, std::memory_order_relaxed);
+    }
+};
+
+// Memory-mapped windows of a file (the direct path), released (unregistered, unmapped) on every exit, and the open
+// file.  Declared BEFORE the lane's DrainGuard, so the stream is drained before any window goes away.
 struct FileWindows {
     struct W {
         void* ptr = nullptr;
         size_t len = 0;
         bool registered = false;
     };
+    tv_ctx* c;
     W w[2];
     int fd = -1;
+    const char* path = nullptr;   // the open file (units of one segment on one lane share the open)
+    uint64_t size = 0;
+    explicit FileWindows(tv_ctx* ctx) : c(ctx) {}
     void release(int k) {
-        if (w[k].registered) (void)hipHostUnregister(w[k].ptr);
-        if (w[k].ptr) munmap(w[k].ptr, w[k].len);
+        if (w[k].ptr) {
+            FileClock t(c, TV_FILE_PHASE_RELEASE);
+            if (w[k].registered) (void)hipHostUnregister(w[k].ptr);
+            munmap(w[k].ptr, w[k].len);
+            (void)hipGetLastError();
+        }
         w[k] = W{};
-        (void)hipGetLastError();
+    }
+    void close_file() {
+        if (fd >= 0) close(fd);
+        fd = -1;
+        path = nullptr;
     }
     ~FileWindows() {
         release(0);
         release(1);
-        if (fd >= 0) close(fd);
+        close_file();
     }
 };
 
+// One part of a long file segment: file bytes [fo, fo + len) -> LINEAR [a, a + len) (inside the resident pieces),
+// segment k of the call.
+struct FileUnit {
+    uint64_t k, fo, a, len;
+    const char* path;
+};
 
-// tv_stage_file with the context lock held and the arguments checked.
-int stage_file_locked(tv_ctx* c, const char* path, uint64_t file_offset, uint64_t linear_offset, uint64_t len,
-                      int lane = 0) {
+// Open the unit's file as the reference opens it (unless this lane has it open already) and check it holds the
+// unit's bytes.  TV_ERR_IO (message set) when it cannot be read.
+int unit_open(tv_ctx* c, FileWindows& win, const FileUnit& u) {
+    FileClock t(c, TV_FILE_PHASE_OPEN);
+    if (win.fd < 0 || win.path != u.path) {
+        win.close_file();
+        int oe = 0;
+        win.fd = open_file(u.path, c->open_rw, &oe);
+        if (win.fd < 0)
+            return fail(c, TV_ERR_IO, "open %s for %s: %s", u.path, c->open_rw ? "read and write" : "reading",
+                        strerror(oe));
+        struct stat st;
+        if (fstat(win.fd, &st) != 0) {
+            const int e = errno;
+            win.close_file();
+            return fail(c, TV_ERR_IO, "fstat %s: %s", u.path, strerror(e));
+        }
+        win.path = u.path;
+        win.size = (uint64_t)st.st_size;
+    }
+    if (win.size < u.fo + u.len)
+        return fail(c, TV_ERR_IO, "%s has %llu bytes, the read needs %llu", u.path, (unsigned long long)win.size,
+                    (unsigned long long)(u.fo + u.len));
+    return TV_OK;
+}
+
+// Stage the units (each lane's in ascending linear order) on staging lane `lane` with `threads` reader threads.
+// Per chunk of the unit: with TV_OPT_FILE_DIRECT a window of TV_OPT_FILE_CHUNK bytes whose pages are mostly in the
+// page cache is mapped, registered read-only and DMA'd to HBM from the page cache; otherwise (and for cold windows)
+// slot-sized chunks are read by parallel preads into the lane's pinned ring and DMA'd from there.  The ring's slot
+// leases order the reads behind the DMAs that last read the slot, so consecutive units stream with no drain between
+// them.  A unit whose file cannot be read sets status[k] = TV_ERR_IO (the caller recovers the segment); a HIP or
+// state error ends the lane with that status.
+int stage_units(tv_ctx* c, const std::vector<FileUnit>& units, int lane, int threads, int32_t* status) {
+    if (units.empty()) return TV_OK;
     hipStream_t cs = lane_stream(c, lane);
+    FileWindows win(c);  // before `drain`: unmapped after the stream is drained
+    DrainGuard drain(c, lane, /*sync_compute=*/false);
+    for (int k = 0; k < 2; k++) TV_HIP(c, hipEventCreateWithFlags(&drain.ev[k], hipEventDisableTiming));
+    const uint64_t page = (uint64_t)sysconf(_SC_PAGESIZE);
+    int idx = 0;
     int rc = TV_OK;
+    for (const FileUnit& u : units) {
+        if (unit_open(c, win, u)) {
+            __atomic_store_n(&status[u.k], TV_ERR_IO, __ATOMIC_RELAXED);
+            continue;
+        }
+        const uint64_t chunk = c->file_direct ? c->file_chunk : (uint64_t)kRingSlotBytes - 4;
+        bool unit_ok = true;
+        for (uint64_t p = u.a; p < u.a + u.len && unit_ok; p += chunk, idx++) {
+            const int k = idx & 1;
+            const uint64_t n = std::min(chunk, u.a + u.len - p);
+            const uint64_t fo = u.fo + (p - u.a);
+            bool direct = false;
+            void* m = MAP_FAILED;
+            uint64_t delta = 0;
+            if (c->file_direct) {
+                // the window used two chunks ago must be DMA-complete before it is unmapped
+                if (win.w[k].ptr) {
+                    {
+                        FileClock t(c, TV_FILE_PHASE_WAIT);
+                        TV_HIP(c, hipEventSynchronize(drain.ev[k]));
+                    }
+                    win.release(k);
+                }
+                const uint64_t map_off = fo / page * page;
+                delta = fo - map_off;
+                {
+                    FileClock t(c, TV_FILE_PHASE_MAP);
+                    // (a file that cannot be mapped, e.g. on a filesystem without mmap, takes the pread path)
+                    m = mmap(nullptr, delta + n, PROT_READ, MAP_SHARED, win.fd, (off_t)map_off);
+                    if (m != MAP_FAILED) {
+                        win.w[k].ptr = m;
+                        win.w[k].len = delta + n;
+                    }
+                    // direct only when the file bytes and the resident bytes agree mod 4 (else the DMA is unaligned)
+                    direct = m != MAP_FAILED && ((fo ^ p) & 3) == 0 && resident_fraction(m, delta + n, page) >= 0.5;
+                }
+                if (direct) {
+                    // warm window: register its page-cache pages read-only and DMA them to HBM directly
+                    {
+                        FileClock t(c, TV_FILE_PHASE_POPULATE);
+                        populate_window(m, delta + n);
+                    }
+                    FileClock t(c, TV_FILE_PHASE_REGISTER);
+                    win.w[k].registered = hipHostRegister(m, delta + n, hipHostRegisterReadOnly) == hipSuccess;
+                    (void)hipGetLastError();
+                    direct = win.w[k].registered;
+                }
+            }
+            if (direct) {
+                FileClock t(c, TV_FILE_PHASE_QUEUE);
+                rc = stage_range(c, p, p + n, (const uint8_t*)m + delta, p, true, lane);
+                if (rc) return rc;
+                c->file_ns[TV_FILE_BYTES_DIRECT].fetch_add(n, std::memory_order_relaxed);
+            } else {
+                // cold window (or direct DMA off / refused): parallel preads into the pinned ring, then DMA
+                win.release(k);
+                for (uint64_t q = 0; q < n; q += kRingSlotBytes - 4) {
+                    const uint64_t kq = std::min<uint64_t>(kRingSlotBytes - 4, n - q);
+                    SlotLease slot(c, lane);  // lent until every copy out of it is queued
+                    {
+                        FileClock t(c, TV_FILE_PHASE_WAIT);
+                        rc = slot.take();
+                        if (rc) return rc;
+                    }
+                    uint8_t* at = slot.ptr() + ((p + q) & 3);  // at the resident bytes' alignment mod 4
+                    int e;
+                    {
+                        FileClock t(c, TV_FILE_PHASE_READ);
+                        e = pread_pool(c->pool[lane], threads, win.fd, at, fo + q, kq);
+                    }
+                    if (e) {
+                        fail(c, TV_ERR_IO, "read %s at %llu: %s", u.path, (unsigned long long)(fo + q), strerror(e));
+                        __atomic_store_n(&status[u.k], TV_ERR_IO, __ATOMIC_RELAXED);
+                        unit_ok = false;
+                        break;
+                    }
+                    FileClock t(c, TV_FILE_PHASE_QUEUE);
+                    rc = stage_range(c, p + q, p + q + kq, at, p + q, true, lane, /*src_in_ring=*/true);
+                    if (rc) return rc;
+                    rc = slot.release();
+                    if (rc) return rc;
+                    c->file_ns[TV_FILE_BYTES_READ].fetch_add(kq, std::memory_order_relaxed);
+                }
+            }
+            if (c->file_direct) TV_HIP(c, hipEventRecord(drain.ev[k], cs));
+        }
+    }
+    FileClock t(c, TV_FILE_PHASE_DRAIN);
+    TV_HIP(c, hipStreamSynchronize(cs));
+    return TV_OK;
+}
+
+// tv_stage_file's work with the context lock held and the arguments checked: one segment on lane 0.
+int stage_file_locked(tv_ctx* c, const char* path, uint64_t file_offset, uint64_t linear_offset, uint64_t len) {
     if (len == 0) {  // reads nothing, but fsStorage.get still opens the path (storage.ts:158)
         const int e = fs_openable(path, c->open_rw);
         return e ? fail(c, TV_ERR_IO, "open %s: %s", path, strerror(e)) : TV_OK;
     }
-    FileWindows win;  // before `drain`: destroyed after the streams are drained
-    int oe = 0;
-    win.fd = open_file(path, c->open_rw, &oe);
-    if (win.fd < 0)
-        return fail(c, TV_ERR_IO, "open %s for %s: %s", path, c->open_rw ? "read and write" : "reading", strerror(oe));
-    struct stat st;
-    if (fstat(win.fd, &st) != 0) return fail(c, TV_ERR_IO, "fstat %s: %s", path, strerror(errno));
-    if ((uint64_t)st.st_size < file_offset + len)
-        return fail(c, TV_ERR_IO, "%s has %llu bytes, the read needs %llu", path, (unsigned long long)st.st_size,
-                    (unsigned long long)(file_offset + len));
-    if (c->count == 0) return TV_OK;
+    FileWindows win(c);
+    const FileUnit whole{0, file_offset, linear_offset, len, path};
+    int rc = unit_open(c, win, whole);  // the whole segment must be readable (else TV_ERR_IO, recovered by the caller)
+    win.close_file();
+    if (rc || c->count == 0) return rc;
     uint64_t a, b;
     clip_to_shard(c, linear_offset, len, &a, &b);
     if (a >= b) return TV_OK;
     TV_HIP(c, hipSetDevice(c->device));
-    DrainGuard drain(c, lane, /*sync_compute=*/false);
-    for (int k = 0; k < 2; k++) TV_HIP(c, hipEventCreateWithFlags(&drain.ev[k], hipEventDisableTiming));
-    const uint64_t page = (uint64_t)sysconf(_SC_PAGESIZE);
-    const uint64_t chunk = c->file_chunk;
-    int idx = 0;
-    for (uint64_t p = a; p < b; p += chunk, idx++) {
-        const int k = idx & 1;
-        const uint64_t n = std::min(chunk, b - p);
-        const uint64_t fo = file_offset + (p - linear_offset);
-        // the window used two chunks ago must be DMA-complete before it is unmapped
-        if (win.w[k].ptr) {
-            TV_HIP(c, hipEventSynchronize(drain.ev[k]));
-            win.release(k);
-        }
-        const uint64_t map_off = fo / page * page, delta = fo - map_off;
-        // (a file that cannot be mapped, e.g. on a filesystem without mmap, takes the pread path)
-        void* m = c->file_direct ? mmap(nullptr, delta + n, PROT_READ, MAP_SHARED, win.fd, (off_t)map_off) : MAP_FAILED;
-        if (m != MAP_FAILED) {
-            win.w[k].ptr = m;
-            win.w[k].len = delta + n;
-        }
-        // direct only when the file bytes and the resident bytes agree mod 4 (else the DMA is unaligned)
-        if (m != MAP_FAILED && ((fo ^ p) & 3) == 0 && resident_fraction(m, delta + n, page) >= 0.5) {
-            // warm window: register its page-cache pages read-only and DMA them to HBM directly
-            populate_window(m, delta + n);
-            win.w[k].registered = hipHostRegister(m, delta + n, hipHostRegisterReadOnly) == hipSuccess;
-            (void)hipGetLastError();
-        }
-        if (win.w[k].registered) {
-            rc = stage_range(c, p, p + n, (const uint8_t*)m + delta, p, true, lane);
-            if (rc) return rc;
-        } else {
-            // cold window (or direct DMA off / refused): parallel preads into the pinned ring, then DMA
-            win.release(k);
-            for (uint64_t q = 0; q < n; q += kRingSlotBytes - 4) {
-                const uint64_t kq = std::min<uint64_t>(kRingSlotBytes - 4, n - q);
-                SlotLease slot(c, lane);  // lent until every copy out of it is queued
-                rc = slot.take();
-                if (rc) return rc;
-                uint8_t* at = slot.ptr() + ((p + q) & 3);  // at the resident bytes' alignment mod 4
-                const int e = pread_parallel(win.fd, at, fo + q, kq, c->file_threads, numa_cpus(c));
-                if (e) return fail(c, TV_ERR_IO, "read %s at %llu: %s", path, (unsigned long long)(fo + q), strerror(e));
-                rc = stage_range(c, p + q, p + q + kq, at, p + q, true, lane, /*src_in_ring=*/true);
-                if (rc) return rc;
-                rc = slot.release();
-                if (rc) return rc;
-            }
-        }
-        TV_HIP(c, hipEventRecord(drain.ev[k], cs));
-    }
-    TV_HIP(c, hipStreamSynchronize(cs));
-    return TV_OK;
+    int32_t st = TV_OK;
+    rc = stage_units(c, {FileUnit{0, file_offset + (a - linear_offset), a, b - a, path}}, 0, c->file_threads, &st);
+    return rc ? rc : st;
 }
 
 // Read every segment of `segs` into slot memory at its packed offset, on `threads` threads (each
@@ -272,6 +370,7 @@ extern "C" {
 int tv_stage_file(tv_ctx* c, const char* path, uint64_t file_offset, uint64_t linear_offset, uint64_t len) {
     if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
     std::lock_guard<std::mutex> g(c->mu);
+    FileClock call_clock(c, TV_FILE_PHASE_CALL);
     int rc = require_layout(c, false, true);
     if (rc) return rc;
     if (!path) return fail(c, TV_ERR_ARG, "path is NULL");
@@ -326,16 +425,13 @@ namespace {
 int stage_files_core(tv_ctx* c, uint64_t n, const char* const* paths, const uint64_t* file_offsets,
                      const uint64_t* linear_offsets, const uint64_t* lens, int32_t* status_out, bool check_zero) {
     int rc = TV_OK;
-    // Long segments: the windowed page-cache path of tv_stage_file.  Short ones: packed into the pinned
-    // ring's 64 MiB slots, read by the thread pool, DMA'd per run of linear-contiguous segments while the
-    // next slot is read.  With TV_OPT_FILE_CONCURRENT the long segments are split by bytes between a
-    // helper thread on staging lane 1 and this thread (lane 0, before the pool): each lane's copies
-    // queue on its own stream, so the two feed the DMA engines side by side.
+    // Long segments (>= TV_OPT_FILE_DIRECT_MIN bytes) are cut into units of TV_OPT_FILE_CHUNK bytes dealt to two
+    // staging lanes (TV_OPT_FILE_CONCURRENT): this thread on lane 0 and a helper thread on lane 1, each walking its
+    // units in linear order with its own copy stream, ring and half of the reader threads, so one file's bytes feed
+    // the DMA engines from both (a whole segment per lane left a single-file torrent on one lane).  Short segments
+    // are packed into lane 0's 64 MiB ring slots, read by the pool, DMA'd per run of linear-contiguous segments.
     const uint64_t direct_min = c->file_direct_min;
-    struct LongSeg {
-        uint64_t k, fo, a, len;
-    };
-    std::vector<LongSeg> longs;
+    std::vector<FileUnit> longs;
     std::vector<SmallSeg> small;
     uint64_t small_bytes = 0;
     std::string zero_err;
@@ -353,7 +449,9 @@ int stage_files_core(tv_ctx* c, uint64_t n, const char* const* paths, const uint
         if (a >= b) continue;  // nothing of this segment is resident here
         const uint64_t fo = file_offsets[k] + (a - linear_offsets[k]);
         if (b - a >= direct_min) {
-            longs.push_back({k, fo, a, b - a});
+            const uint64_t unit = std::max<uint64_t>(c->file_chunk, 1ull << 20);
+            for (uint64_t o = 0; o < b - a; o += unit)
+                longs.push_back({k, fo + o, a + o, std::min(unit, b - a - o), paths[k]});
         } else {
             const uint64_t part = kRingSlotBytes - 4;  // (pieces of at most one slot, with room to align)
             for (uint64_t o = 0; o < b - a; o += part)
@@ -361,21 +459,20 @@ int stage_files_core(tv_ctx* c, uint64_t n, const char* const* paths, const uint
             small_bytes += b - a;
         }
     }
-    // longest first to the lane with fewer bytes so far (lane 0 also carries the pool's bytes)
-    std::vector<LongSeg> lane_segs[2];
+    // in linear order, each unit to the lane with fewer bytes so far (lane 0 also carries the short segments)
+    std::vector<FileUnit> lane_units[2];
     {
-        std::vector<size_t> order(longs.size());
-        for (size_t q = 0; q < order.size(); q++) order[q] = q;
-        std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return longs[x].len > longs[y].len; });
+        std::stable_sort(longs.begin(), longs.end(), [](const FileUnit& x, const FileUnit& y) { return x.a < y.a; });
         uint64_t load[2] = {small_bytes, 0};
-        for (size_t q : order) {
+        for (const FileUnit& u : longs) {
             const int l = (c->file_concurrent && load[1] < load[0]) ? 1 : 0;
-            lane_segs[l].push_back(longs[q]);
-            load[l] += longs[q].len;
+            lane_units[l].push_back(u);
+            load[l] += u.len;
         }
-        for (auto& v : lane_segs)  // each lane walks its segments in linear order
-            std::sort(v.begin(), v.end(), [](const LongSeg& x, const LongSeg& y) { return x.a < y.a; });
     }
+    // reader threads: the context's TV_OPT_FILE_THREADS shared by the lanes that read
+    const int lanes = lane_units[1].empty() ? 1 : 2;
+    const int threads_per_lane = std::max(1, c->file_threads / lanes);
     int helper_rc = TV_OK;
     std::thread helper;
     struct Joiner {
@@ -384,28 +481,18 @@ int stage_files_core(tv_ctx* c, uint64_t n, const char* const* paths, const uint
             if (t.joinable()) t.join();
         }
     } joiner{helper};  // every exit joins the helper before the ctx lock is released
-    if (!lane_segs[1].empty()) {
+    if (!lane_units[1].empty()) {
         helper = std::thread([&]() {
             pin_thread(numa_cpus(c));  // next to its ring and the GPU (TV_OPT_NUMA_BIND)
             if (hipSetDevice(c->device) != hipSuccess) {
                 helper_rc = fail(c, TV_ERR_HIP, "tv_stage_files: hipSetDevice(%d) failed", c->device);
                 return;
             }
-            for (const LongSeg& sg : lane_segs[1]) {
-                const int r = stage_file_locked(c, paths[sg.k], sg.fo, sg.a, sg.len, 1);
-                if (r == TV_ERR_IO) status_out[sg.k] = TV_ERR_IO;
-                else if (r) {
-                    helper_rc = r;
-                    return;
-                }
-            }
+            helper_rc = stage_units(c, lane_units[1], 1, threads_per_lane, status_out);
         });
     }
-    for (const LongSeg& sg : lane_segs[0]) {
-        rc = stage_file_locked(c, paths[sg.k], sg.fo, sg.a, sg.len, 0);
-        if (rc == TV_ERR_IO) status_out[sg.k] = TV_ERR_IO;
-        else if (rc) return rc;
-    }
+    rc = stage_units(c, lane_units[0], 0, lanes == 2 ? threads_per_lane : c->file_threads, status_out);
+    if (rc) return rc;
     std::string first_err = zero_err;
     std::mutex err_mu;
     DrainGuard drain(c, 0, /*sync_compute=*/false);
@@ -424,8 +511,9 @@ int stage_files_core(tv_ctx* c, uint64_t n, const char* const* paths, const uint
         SlotLease slot(c, 0);  // lent until every copy out of it is queued
         rc = slot.take();
         if (rc) return rc;
-        read_segments(c->pool[0], small, i, j, paths, slot.ptr(), status_out, c->file_threads, c->open_rw, &first_err,
-                      &err_mu);
+        FileClock small_clock(c, TV_FILE_PHASE_SMALL);
+        read_segments(c->pool[0], small, i, j, paths, slot.ptr(), status_out,
+                      lanes == 2 ? threads_per_lane : c->file_threads, c->open_rw, &first_err, &err_mu);
         for (size_t q = i; q < j;) {  // one copy per run of readable, linear-contiguous segments
             if (status_out[small[q].k] != TV_OK) { q++; continue; }
             size_t r = q + 1;
@@ -462,6 +550,7 @@ int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64
                    const uint64_t* linear_offsets, const uint64_t* lens, int32_t* status_out) {
     if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
     std::lock_guard<std::mutex> g(c->mu);
+    FileClock call_clock(c, TV_FILE_PHASE_CALL);
     int rc = require_layout(c, false, true);
     if (rc) return rc;
     if (n == 0) return TV_OK;
