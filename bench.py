@@ -51,6 +51,7 @@ sys.path.insert(0, ROOT)
 
 from torrent_amd import _native  # noqa: E402  (load the HIP library before torch)
 from torrent_amd.verify import shard_ranges  # noqa: E402
+from torrent_amd._cpu import cpu_share  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # SHA-1 VALU roofline from the measured SIMD cost per wave64 instruction (tools/ubench_simd.hip,
@@ -197,35 +198,6 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def cpu_share() -> dict:
-    """The host cores this process may use: the cgroup CPU quota (cpu.max, v2; cfs_quota_us, v1) when one
-    is set, else the box's CPU share as its environment states it (OMP_NUM_THREADS; 16 per GPU on the
-    GPU boxes), else the affinity mask.  Everything it looked at is reported."""
-    aff = len(os.sched_getaffinity(0))
-    quota = None
-    try:
-        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
-        if q != "max":
-            quota = int(q) / int(per)
-    except (OSError, ValueError):
-        try:
-            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
-            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
-            if q > 0:
-                quota = q / per
-        except (OSError, ValueError):
-            pass
-    omp = os.environ.get("OMP_NUM_THREADS")
-    if quota:
-        cores, src = max(1, min(aff, int(quota))), "cgroup CPU quota"
-    elif omp and omp.isdigit() and int(omp) > 0:
-        cores, src = min(aff, int(omp)), "OMP_NUM_THREADS (the box's stated CPU share; no cgroup quota)"
-    else:
-        cores, src = aff, "sched_getaffinity (no cgroup quota, no stated share)"
-    return {"cores": cores, "source": src, "nproc": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota,
-            "omp_num_threads": omp}
-
-
 def _corrupt(dig: bytearray, count: int, salt: int) -> set:
     """Corrupt 1 % of a shard's digests (every 100th piece, plus its last) -> the pieces expected to fail."""
     bad = set(range(salt % 100, count, 100)) | {count - 1}
@@ -285,7 +257,7 @@ def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: b
     ctx = _native.Context(device)
     try:
         ctx.set_option(_native.TV_OPT_KERNEL, kernel_opt)
-        ctx.set_option(_native.TV_OPT_CLOCK_PROBE, 1)   # workgroup 0 samples the shader clock it runs at
+        ctx.set_clock_probe(True)   # workgroup 0 samples the shader clock it runs at
         ctx.set_layout(total, L, P, first, count)
         # a resident step re-hashes the whole shard: the layout must hold it whole (a windowed layout, for a
         # shard above the device budget, would hash once per pass and make repeated verifies compares)
@@ -318,7 +290,7 @@ def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: b
         t1 = time.perf_counter()
         _barrier(dist)
         kernel, _ = ctx.last_kernel()
-        clock_ghz = ctx.counter(_native.TV_COUNTER_LAST_CLOCK_KHZ) / 1e6   # (after the timed region: it syncs)
+        clock_ghz = ctx.last_clock_khz() / 1e6   # (after the timed region: it syncs)
     finally:
         ctx.close()
     t_end = time.perf_counter()

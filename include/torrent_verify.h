@@ -125,13 +125,10 @@ int tv_stage_many(tv_ctx *ctx, uint64_t n, const uint64_t *linear_offsets, const
  * Stage `len` bytes of the file at `path` (a NUL-terminated path), starting at byte `file_offset`,
  * as LINEAR torrent bytes [linear_offset, linear_offset + len).  This is one file segment of
  * Storage.get's mapping (storage.ts:89-137: path, offset in the file, length) read the way
- * fsStorage.get reads it (storage.ts:150-172: open, seek, read).  The file is processed in windows of
- * TV_OPT_FILE_CHUNK bytes.  A window whose pages are mostly in the page cache (mincore) is mapped, its
- * pages registered read-only and DMA'd straight to HBM, with no host copy.  A window mostly on disk is
- * read by parallel preads (4 MiB requests, TV_OPT_FILE_THREADS in flight) into the pinned ring and
- * DMA'd from there.
- * TV_OPT_FILE_DIRECT = 0 forces the second form.  Either way, window k+1 is read while window k
- * copies.  Bytes outside the shard are skipped.  A missing, unopenable or short file (or a read error
+ * fsStorage.get reads it (storage.ts:150-172: open, seek, read).  The bytes are read by parallel preads
+ * (TV_OPT_FILE_THREADS threads, 1-4 MiB requests) into the library's pinned ring, one 64 MiB slot at a time,
+ * and DMA'd from the slot to HBM while the next slot is read (53 GB/s end to end from a warm page cache on
+ * an MI355X host whose PCIe H2D copy runs at 57.6; profiles/r05).  Bytes outside the shard are skipped.  A missing, unopenable or short file (or a read error
  * part-way) returns TV_ERR_IO, and the library marks the pieces Storage.get would return null for
  * (storage.ts:50-65 reads piece by piece): from the piece holding the first byte the file cannot supply
  * to the segment's end.  The whole pieces before that byte are staged and stay readable.  Marked pieces
@@ -149,9 +146,9 @@ int tv_stage_file(tv_ctx *ctx, const char *path, uint64_t file_offset, uint64_t 
  * Stage MANY file segments in one call: a shard's whole Storage.get mapping (storage.ts:89-137), each
  * segment read as fsStorage.get reads it (storage.ts:150-172).  Segment k is `lens[k]` bytes of file
  * `paths[k]` from byte `file_offsets[k]`, staged as LINEAR bytes [linear_offsets[k], +lens[k]).
- *   - Segments of >= TV_OPT_FILE_DIRECT_MIN bytes (default 32 MiB) take the tv_stage_file path. With
- *     TV_OPT_FILE_CONCURRENT (default 1) they are split by bytes between two staging lanes (a helper
- *     thread with its own copy stream and pinned ring, and the calling thread), which DMA side by side.
+ *   - Segments of >= TV_OPT_FILE_DIRECT_MIN bytes (default 32 MiB) take the tv_stage_file path, cut into
+ *     256 MiB units dealt to two staging lanes (a helper thread with its own copy stream and pinned ring,
+ *     and the calling thread; the TV_OPT_FILE_THREADS readers shared between them), which DMA side by side.
  *   - Shorter ones are packed into the pinned ring's 64 MiB slots. TV_OPT_FILE_THREADS threads read
  *     them (open, pread, close; default 16), and each run of linear-contiguous segments is one DMA.
  *     A slot's DMA overlaps the reads of the next slot. This is the many-small-files case: a
@@ -273,41 +270,27 @@ int tv_host_free(void *ptr);
 int tv_host_register(void *ptr, uint64_t bytes);
 int tv_host_unregister(void *ptr);
 
-/* Options (tv_set_option keys). */
-#define TV_OPT_KERNEL 1      /* 0 = auto, 1 = lane, 2 = split (schedule offload), 4 = twin (split with two lanes per
-                                piece); 3 is unused (it was MIX, a work queue measured slower than lane, removed) */
-#define TV_OPT_STRIDE_PAD 2  /* bytes of padding between resident pieces (default 256) */
-#define TV_OPT_STREAM_CHUNK 3 /* tv_verify_host: bytes of each piece per streamed column chunk */
-#define TV_OPT_SPLIT_PAIRS 4  /* split and twin kernels: (rounds, helper) wave pairs per workgroup, 0 = auto, 1, 2 */
-#define TV_OPT_FILE_DIRECT 5  /* tv_stage_file: 1 (default) = warm windows DMA'd from registered page-cache pages, 0 = all via the pinned ring */
-#define TV_OPT_FILE_CHUNK 6   /* tv_stage_file: bytes per mapped file window (default 256 MiB, >= 64 KiB) */
-#define TV_OPT_FILE_DIRECT_MIN 7 /* tv_stage_files: segment length that takes the tv_stage_file path (default 32 MiB) */
-#define TV_OPT_FILE_THREADS 8    /* host threads (default 16): tv_stage_files' readers, and the copies of pageable
-                                    tv_stage sources into the pinned ring (25.8 -> 55.8 GB/s) */
-#define TV_OPT_FILE_CONCURRENT 9 /* tv_stage_files: 1 (default) = long segments on two staging lanes, 0 = one */
+/* Options (tv_set_option keys): what a host integrating the library sets.  (Measurement and test knobs -- kernel
+ * forcing, stride padding, file-staging A/B modes, NUMA binding, probes, fault injection -- are keys of the
+ * library's internal header torrent_amd/csrc/tv_options_internal.h, which only the tests and tools use.) */
+#define TV_OPT_STREAM_CHUNK 3 /* tv_verify_host / tv_stream_*: bytes of each piece per streamed column (0, default:
+                                 automatic, the widest power of two <= L whose column over the shard is <= 512 MiB) */
+#define TV_OPT_FILE_DIRECT_MIN 7 /* tv_stage_files: segment length that takes the long-segment path (default 32 MiB) */
+#define TV_OPT_FILE_THREADS 8    /* host threads of the context (default 16): tv_stage_file(s)' readers (shared by the
+                                    two staging lanes), and the copies of pageable tv_stage sources into the pinned
+                                    ring.  A host running several contexts in one process divides its CPU share
+                                    among them (verify.py / verify.ts do) */
 #define TV_OPT_RESIDENT 10       /* 1 (default): tv_set_layout allocates the resident payload; 0: it does not (a
                                     streamed-only ctx, tv_stream_*; the resident calls then fail with TV_ERR_STATE).
                                     Takes effect at the next tv_set_layout */
-#define TV_OPT_DEBUG_REBOUNCE 11 /* tests: 1 = bounce ring-resident sources through the ring again (the staging
-                                    path that once raced); slot leases must keep it exact.  Default 0 */
-#define TV_OPT_TWIN_PACK 12      /* twin kernel with fewer workgroups than 2 per CU: 1 = launch it on a stream
-                                    CU-masked to ceil(workgroups / 2) CUs, two workgroups on each; 0 = spread
-                                    over every CU.  Default 0 */
-#define TV_OPT_TWIN_FILL 13      /* twin kernel with fewer workgroups than 2 per CU (resident calls): 1 (default) =
-                                    add companion workgroups up to 2 per CU that re-hash main workgroups' pieces
-                                    on the otherwise idle SIMDs and discard the result (a CU running one twin
-                                    workgroup is ~4.5 % slower per block than one running two); 0 = real grid only.
-                                    tv_verify_list adds them only to a list of >= 32 x CUs pieces (one workgroup
-                                    per CU): a shorter flush would fill the GPU with copies of a few pieces;
-                                    2 = add them to every list too (measurement only) */
-#define TV_OPT_TWIN_FILL_READS 14 /* companion workgroups' loads: 0 (default) = every lane of a companion reads its
-                                    main workgroup's first piece (the same instruction stream, 1/32 of the bytes);
-                                    1 = the main workgroup's 32 pieces (round 2; 1.14-1.42 x payload of HBM reads) */
-#define TV_OPT_NUMA_BIND 15 /* 1 (default) = the library's host threads (file readers, ring copies, the staging
-                               helper lane) run on the CPUs of the GPU's NUMA node, and the pinned ring is
-                               allocated on that node (slots allocated after the option is set); 0 = unpinned,
-                               default placement.  An MI355X node has two sockets with four GPUs each: a copy
-                               from the far socket crosses the inter-socket link twice (read, then DMA). */
+#define TV_OPT_TWIN_FILL 13      /* twin kernel with fewer workgroups than 2 per CU (resident calls, cfg4's shards at
+                                    N = 4 / 8): 1 (default) = add light companion workgroups up to 2 per CU that
+                                    run the same instruction stream on one piece of their main workgroup on the
+                                    otherwise idle SIMDs and discard the result (a CU running one twin workgroup
+                                    is ~4.5 % slower per block than one running two; +2.2-3.2 %, 0.2-0.4 % more
+                                    HBM reads); 0 = the real grid only -- the setting for a GPU shared with other
+                                    work, whose CUs the companions would take.  Bitfields are the same either way.
+                                    tv_verify_list adds them only to a list of >= 32 x CUs pieces */
 #define TV_OPT_RESIDENT_BUDGET 16 /* bytes of device memory the resident payload may take (0, default: the GPU's free
                                      memory at tv_set_layout less 4 GiB and 64 B per piece).  A shard larger than it
                                      gets a windowed layout (tv_set_layout).  Takes effect at the next tv_set_layout */
@@ -328,10 +311,6 @@ int tv_host_unregister(void *ptr);
 #define TV_OPT_CLOCK_PROBE 20     /* 1: verify / hash launches (resident, windows, stream units) record the shader clock
                                      they ran at (workgroup 0 reads the shader and 100 MHz real-time counters at its
                                      start and end; TV_COUNTER_LAST_CLOCK_KHZ).  0 (default) = off */
-#define TV_OPT_LANE_PAIRS 21      /* lane kernel loads: 0 (default) = auto: a lane's two 64-B blocks of a 128-B line loaded
-                                     back to back when the launch has >= 256 x CUs pieces (>= 1 wave per SIMD; HBM reads
-                                     1.0004 instead of 1.023 x payload at 262,144 x 64 KiB), else a 3-deep ring of
-                                     single blocks; 1 = pairs always; 2 = never */
 int tv_set_option(tv_ctx *ctx, int key, int64_t value);
 int tv_get_option(tv_ctx *ctx, int key, int64_t *value);
 

@@ -230,16 +230,51 @@ def test_buffer_addresses_are_never_copies():
     assert _native._addr(None) == (None, None) and _native._addr(bytearray())[0] is None
 
 
+def _defines(path):
+    txt = open(os.path.join(ROOT, path)).read()
+    return {m.group(1): int(m.group(2)) for m in
+            re.finditer(r"^#define\s+(TV_(?:OPT|COUNTER|ERR|FILE)_\w+)\s+\(?(-?\d+)\)?", txt, re.M)}
+
+
 def test_option_and_counter_constants_match_header():
-    """Every TV_OPT_* / TV_COUNTER_* / TV_ERR_* value of include/torrent_verify.h is the same in the ctypes
-    binding (torrent_amd/_native.py) and in every constant ts/verify.ts declares."""
+    """Every TV_OPT_* / TV_COUNTER_* / TV_ERR_* value of include/torrent_verify.h and of the library's internal
+    header (tv_options_internal.h: measurement and test knobs) is the same in the ctypes binding
+    (torrent_amd/_native.py), and in every constant ts/verify.ts declares (public ones only)."""
     from torrent_amd import _native
-    txt = open(os.path.join(ROOT, "include", "torrent_verify.h")).read()
-    defs = {m.group(1): int(m.group(2)) for m in
-            re.finditer(r"^#define\s+(TV_(?:OPT|COUNTER|ERR)_\w+)\s+\(?(-?\d+)\)?", txt, re.M)}
-    assert len(defs) >= 30
-    for name, v in defs.items():
+    public = _defines("include/torrent_verify.h")
+    internal = _defines("torrent_amd/csrc/tv_options_internal.h")
+    assert len(public) >= 25 and len(internal) >= 10
+    for name, v in {**public, **internal}.items():
+        if name.startswith("TV_FILE_"):
+            continue
         assert getattr(_native, name) == v, name
+    phases = sorted((v, k) for k, v in internal.items() if k.startswith(("TV_FILE_PHASE_", "TV_FILE_BYTES_")))
+    assert [k.split("_", 3)[3].lower() if k.startswith("TV_FILE_PHASE_") else "bytes_" + k.split("_")[-1].lower()
+            for _, k in phases] == list(_native.TV_FILE_PHASES)
     ts = open(os.path.join(ROOT, "ts", "verify.ts")).read()
     for m in re.finditer(r"const\s+(TV_\w+)\s*=\s*(-?\d+)\s*;", ts):
-        assert defs[m.group(1)] == int(m.group(2)), m.group(1)
+        assert public[m.group(1)] == int(m.group(2)), m.group(1)
+
+
+def test_public_options_are_what_the_hosts_use():
+    """The public header's option set (the reference's whole plugin surface is three methods,
+    storage.ts:16-26) is exactly the set the hosts use: ts/verify.ts, the product modules of torrent_amd, and the
+    public wrappers of _native.Context.  Measurement and test knobs live in tv_options_internal.h, and no key is in
+    both headers."""
+    public = {k for k in _defines("include/torrent_verify.h") if k.startswith("TV_OPT_")}
+    internal = _defines("torrent_amd/csrc/tv_options_internal.h")
+    assert not public & set(internal)
+    pub_vals = {v for k, v in _defines("include/torrent_verify.h").items() if k.startswith("TV_OPT_")}
+    assert not pub_vals & {v for k, v in internal.items() if k.startswith("TV_OPT_")}
+    used = set()
+    ts = open(os.path.join(ROOT, "ts", "verify.ts")).read()
+    used |= set(re.findall(r"\b(TV_OPT_\w+)\b", ts[ts.index("} as const;"):]))
+    pkg = os.path.join(ROOT, "torrent_amd")
+    for f in os.listdir(pkg):
+        if f.endswith(".py") and f != "_native.py":
+            used |= set(re.findall(r"\b(TV_OPT_\w+)\b", open(os.path.join(pkg, f)).read()))
+    nat = open(os.path.join(pkg, "_native.py")).read()
+    api = nat[nat.index("class Context:"):]
+    for m in re.finditer(r"\n    def ([a-z]\w*)\(self[^)]*\)[^:]*:(.*?)(?=\n    def |\Z)", api, re.S):
+        used |= set(re.findall(r"\b(TV_OPT_\w+)\b", m.group(2)))
+    assert used == public, (sorted(used - public), sorted(public - used))

@@ -103,3 +103,38 @@ def test_incremental_verifier_on_cfg4_geometry_holds_k_slots(native, oracle):
         assert sum(bin(b).count("1") for b in v.bitfield) == len(chosen) - len(bad)
     finally:
         v.close()
+
+
+def test_stage_files_on_a_slot_pool_with_two_lanes(native, oracle, tmp_path):
+    """tv_stage_files deals long segments to two staging lanes (a helper thread on lane 1), and on a
+    slot pool both lanes take slots for their pieces (piece_dst) at once: every staged piece must get a slot of its
+    own, none lost or given twice.  Two files of long segments (>= TV_OPT_FILE_DIRECT_MIN) cut into many units;
+    the pool holds every piece; verify_list reads each piece's own bytes."""
+    L = 1 << 16
+    per_file = 96                                    # pieces per file: 6 MiB each
+    P = 2 * per_file
+    total = L * P
+    payload = bytes(oracle.synth_fill(31, 0, total))
+    pieces = bytearray(oracle.hash_pieces(bytearray(payload), total, L, P))
+    pieces[20 * 50] ^= 1
+    paths = []
+    for k in range(2):
+        p = tmp_path / f"f{k}.bin"
+        p.write_bytes(payload[k * per_file * L:(k + 1) * per_file * L])
+        paths.append(str(p))
+    with native.Context(0) as ctx:
+        ctx.set_option(native.TV_OPT_LIST_SLOTS, P)
+        ctx.set_option(native.TV_OPT_FILE_DIRECT_MIN, 1 << 20)
+        ctx.set_option(native.TV_OPT_FILE_CHUNK, 1 << 20)     # 16 units over the two lanes
+        ctx.set_option(native.TV_OPT_FILE_CONCURRENT, 1)
+        ctx.set_layout(total, L, P)
+        ctx.set_digests(bytes(pieces))
+        for rep in range(3):
+            st = ctx.stage_files(paths, [0, 0], [0, per_file * L], [per_file * L, per_file * L])
+            assert list(st) == [native.TV_OK, native.TV_OK]
+            assert ctx.counter(native.TV_COUNTER_SLOTS_USED) == P
+            order = list(range(P))
+            random.Random(rep).shuffle(order)
+            ok = ctx.verify_list(order)
+            assert list(ok) == [int(i != 50) for i in order]
+            assert ctx.counter(native.TV_COUNTER_SLOTS_USED) == 0

@@ -278,3 +278,29 @@ def test_stage_many_equals_stage_calls(native, windowed):
         L_ = ctx._L
         offs, srcs, lens = (ctypes.c_uint64 * 1)(0), (ctypes.c_uint64 * 1)(0), (ctypes.c_uint64 * 1)(16)
         assert L_.tv_stage_many(ctx._h, 1, offs, srcs, lens) == N.TV_ERR_ARG
+
+
+@pytest.mark.gpu
+def test_unstaged_windows_never_verify_against_zero_digests(native, oracle):
+    """the windows a pass never opens get all-zero digest rows; a torrent whose expected digest for
+    such a piece is 20 zero bytes must still read 0 there (the piece was never staged: Storage.get would have
+    given nothing), with or without caller availability bits, while the staged pieces verify."""
+    L, P = 4096, 60
+    total = L * P
+    payload = bytes(oracle.synth_fill(78, 0, total))
+    pieces = bytearray(oracle.hash_pieces(bytearray(payload), total, L, P))
+    for i in (20, 21, 35):                          # crafted: zero digests for pieces of never-staged windows
+        pieces[20 * i:20 * i + 20] = bytes(20)
+    with native.Context(0) as ctx:
+        ctx.set_option(native.TV_OPT_RESIDENT_BUDGET, _budget(L, 7))
+        ctx.set_layout(total, L, P)
+        assert ctx.counter(native.TV_COUNTER_WINDOW_PIECES) == 7
+        ctx.set_digests(bytes(pieces))
+        ctx.stage(0, payload[:14 * L])              # windows 0-1
+        ctx.stage(42 * L, payload[42 * L:])          # windows 6-8 (pieces 14-41 never staged)
+        want = [1 if (i < 14 or i >= 42) else 0 for i in range(P)]
+        assert _bits(ctx.verify(), P) == want
+        assert _bits(ctx.verify(b"\xff" * ((P + 7) // 8)), P) == want
+        ctx.stage(0, payload)                        # a new pass stages everything: the crafted pieces now fail
+        want = [0 if i in (20, 21, 35) else 1 for i in range(P)]
+        assert _bits(ctx.verify(), P) == want

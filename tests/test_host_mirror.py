@@ -151,6 +151,24 @@ def test_storage_fails_if_method_fails():  # storage_test.ts:206-228
     assert Storage(Boom([]), BASE_MULTI, os.getcwd()).get(0, 10) is None
 
 
+def test_storage_get_short_and_long_method_results():
+    """storage.ts:51,57-58: a StorageMethod.get that returns FEWER bytes than asked fills the front of its slice
+    of the zeroed Uint8Array (slice.set(got)) and the get succeeds; MORE bytes make slice.set throw a RangeError,
+    which findAndDo's catch turns into false (:130-133): null.  (no reference fixture pins this, so
+    the expectation is the reference's code read as written.)"""
+    vals = os.urandom(16 * 1024)
+    # inside one file
+    st = Storage(Recorder([vals[:100]]), BASE_MULTI, os.getcwd())
+    assert st.get(0, 1000) == vals[:100] + bytes(900)
+    assert Storage(Recorder([vals[:1001]]), BASE_MULTI, os.getcwd()).get(0, 1000) is None
+    assert Storage(Recorder([b""]), BASE_MULTI, os.getcwd()).get(0, 10) == bytes(10)   # (an empty array is truthy)
+    # across files: each segment's slice is filled from its own front
+    rec = Recorder([vals[:4], vals[10:20]])
+    got = Storage(rec, BASE_MULTI, os.getcwd()).get(16 * 1024, 30)
+    assert got == vals[:4] + bytes(6) + vals[10:20] + bytes(10)
+    assert Storage(Recorder([vals[:11], vals[:5]]), BASE_MULTI, os.getcwd()).get(16 * 1024, 30) is None
+
+
 def test_storage_set_across_files_and_dedupe():  # storage_test.ts:313-335, storage.ts:67-87
     rec = Recorder([])
     st = Storage(rec, BASE_MULTI, os.getcwd())

@@ -24,10 +24,7 @@ from torrent_amd import _native, verify_files  # noqa: E402
 from torrent_amd.verify import _context  # noqa: E402
 
 MiB, GiB = 1 << 20, 1 << 30
-PHASES = ["open", "map", "populate", "register", "read", "wait", "queue", "release", "drain", "small", "call",
-          "bytes_direct", "bytes_read"]
-FILE_DIRECT, FILE_CHUNK, FILE_CONCURRENT = 5, 6, 9        # (tv_options_internal.h / include/torrent_verify.h)
-FILE_CLOCK_RESET, COUNTER_FILE_CLOCK = 100, 100
+FILE_DIRECT, FILE_CHUNK, FILE_CONCURRENT = _native.TV_OPT_FILE_DIRECT, _native.TV_OPT_FILE_CHUNK, _native.TV_OPT_FILE_CONCURRENT
 
 CONFIGS = [  # name, direct, concurrent, threads, chunk
     ("direct, 1 lane", 1, 0, 16, 256 * MiB),
@@ -66,12 +63,12 @@ def main():
             for _ in range(reps):
                 res = fsutil.resident(paths)
                 with _context(0) as ctx:
-                    ctx.set_option(FILE_CLOCK_RESET, 1)
+                    ctx._reset_file_clock()
                 t = time.perf_counter()
                 bf = verify_files(info, root, threads=threads)
                 el = time.perf_counter() - t
                 with _context(0) as ctx:
-                    clock = {ph: ctx.counter(COUNTER_FILE_CLOCK + k) for k, ph in enumerate(PHASES)}
+                    clock = ctx._file_clock()
                     kms, tms = ctx.last_timing()
                 if best is None or el < best[0]:
                     best = (el, bytes(bf) == expect, clock, res, kms)
@@ -88,7 +85,7 @@ def main():
                                           if not ph.startswith("bytes") and ph != "call"},
                   "bytes_direct": clock["bytes_direct"], "bytes_read": clock["bytes_read"]})
         with _context(0) as ctx:   # back to the library defaults
-            ctx.set_option(FILE_DIRECT, 1)
+            ctx.set_option(FILE_DIRECT, 0)
             ctx.set_option(FILE_CONCURRENT, 1)
             ctx.set_option(FILE_CHUNK, 256 * MiB)
         for p in paths:

@@ -40,6 +40,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     host_srcs = [os.path.join(CSRC, s) for s in HOST_SOURCES]
     deps = srcs + host_srcs + [header, os.path.join(CSRC, "tv_internal.h"), os.path.join(CSRC, "tv_host.h"),
                                os.path.join(CSRC, "tv_ctx.h"), os.path.join(CSRC, "tv_options_internal.h"), EXPORTS,
+                               os.path.join(CSRC, "tv_plan.h"),
                                os.path.join(ROOT, "include", "torrent_verify.h")]
     if not (force or _newer(LIB, deps)):
         return LIB

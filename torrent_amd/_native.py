@@ -21,27 +21,34 @@ TV_ERR_STATE = -3
 TV_ERR_NOMEM = -4
 TV_ERR_IO = -5
 
-TV_OPT_KERNEL = 1
-TV_OPT_STRIDE_PAD = 2
+# public options (include/torrent_verify.h)
 TV_OPT_STREAM_CHUNK = 3
-TV_OPT_SPLIT_PAIRS = 4
-TV_OPT_FILE_DIRECT = 5
-TV_OPT_FILE_CHUNK = 6
 TV_OPT_FILE_DIRECT_MIN = 7
 TV_OPT_FILE_THREADS = 8
-TV_OPT_FILE_CONCURRENT = 9
 TV_OPT_RESIDENT = 10
-TV_OPT_DEBUG_REBOUNCE = 11
-TV_OPT_TWIN_PACK = 12
 TV_OPT_TWIN_FILL = 13
-TV_OPT_TWIN_FILL_READS = 14
-TV_OPT_NUMA_BIND = 15
 TV_OPT_RESIDENT_BUDGET = 16
 TV_OPT_LIST_SLOTS = 17
 TV_OPT_OPEN_RW = 18
 TV_OPT_STREAM_ROWS = 19
 TV_OPT_CLOCK_PROBE = 20
+
+# measurement / test knobs (torrent_amd/csrc/tv_options_internal.h; tests and tools only)
+TV_OPT_KERNEL = 1
+TV_OPT_STRIDE_PAD = 2
+TV_OPT_SPLIT_PAIRS = 4
+TV_OPT_FILE_DIRECT = 5
+TV_OPT_FILE_CHUNK = 6
+TV_OPT_FILE_CONCURRENT = 9
+TV_OPT_DEBUG_REBOUNCE = 11
+TV_OPT_TWIN_PACK = 12
+TV_OPT_TWIN_FILL_READS = 14
+TV_OPT_NUMA_BIND = 15
 TV_OPT_LANE_PAIRS = 21
+TV_OPT_FILE_CLOCK_RESET = 100
+TV_COUNTER_FILE_CLOCK = 100
+TV_FILE_PHASES = ("open", "map", "populate", "register", "read", "wait", "queue", "release", "drain", "small", "call",
+                  "bytes_direct", "bytes_read")   # TV_FILE_PHASE_* / TV_FILE_BYTES_* in order
 
 TV_COUNTER_PAYLOAD_ALLOCS = 1
 TV_COUNTER_DEVICE_ALLOCS = 2
@@ -218,6 +225,7 @@ class Context:
         self.device = device
         self.shard_first = 0
         self.shard_count = 0
+        self.thread_budget = 16   # host threads this context's call may use (verify._run_shards sets its share)
 
     # -- plumbing ----------------------------------------------------------------------
     def _err(self) -> str:
@@ -453,3 +461,25 @@ class Context:
 
     def synchronize(self) -> None:
         self._check(self._L.tv_synchronize(self._h))
+
+    def set_companions(self, on: bool) -> None:
+        """TV_OPT_TWIN_FILL: light companion workgroups on the idle SIMDs of twin launches with fewer than 2 workgroups
+        per CU (default on); off for a GPU shared with other work.  The bitfields are the same either way."""
+        self.set_option(TV_OPT_TWIN_FILL, 1 if on else 0)
+
+    def set_clock_probe(self, on: bool) -> None:
+        """TV_OPT_CLOCK_PROBE: verify / hash launches record the shader clock they ran at (last_clock_khz)."""
+        self.set_option(TV_OPT_CLOCK_PROBE, 1 if on else 0)
+
+    def last_clock_khz(self) -> int:
+        """The shader clock of the last probed launch's workgroup 0, kHz (0: no probe); waits for the compute stream."""
+        return self.counter(TV_COUNTER_LAST_CLOCK_KHZ)
+
+    def _reset_file_clock(self) -> None:
+        """Zero the file-staging phase clock (internal: TV_OPT_FILE_CLOCK_RESET)."""
+        self.set_option(TV_OPT_FILE_CLOCK_RESET, 1)
+
+    def _file_clock(self) -> dict:
+        """The file-staging phase clock since the last reset: {phase: ns (or bytes for bytes_*)} (internal counters
+        TV_COUNTER_FILE_CLOCK + TV_FILE_PHASE_*, tv_options_internal.h)."""
+        return {ph: self.counter(TV_COUNTER_FILE_CLOCK + k) for k, ph in enumerate(TV_FILE_PHASES)}

@@ -280,6 +280,8 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
     c->digest_ok.assign((shard_count + 7) / 8 + 8, 0);
     c->file_bad.assign((shard_count + 7) / 8 + 8, 0);
     c->any_file_bad = false;
+    c->unhashed.assign((shard_count + 7) / 8 + 8, 0);
+    c->any_unhashed = false;
     c->win = false;
     c->win_n = 0;
     c->win_bufs = 0;
@@ -322,41 +324,46 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
         }
     }
     // The payload: the whole shard when it fits the budget, else windows (a torrent of any size on a
-    // GPU of any free memory).  A failed allocation is retried at half the budget: only the windows shrink.
-    for (;;) {
-        if (need_payload && !c->slots && need_payload > budget) {
-            uint64_t bufs = 2, W = budget / 2 > kSlack ? (budget / 2 - kSlack) / c->stride : 0;
-            if (W == 0) {
-                bufs = 1;
-                W = budget > kSlack ? (budget - kSlack) / c->stride : 0;
-            }
-            W = std::max<uint64_t>(1, std::min(W, shard_count));  // (one piece larger than the budget: held anyway)
-            if (W >= 256) W = W / 64 * 64;                        // whole 64-piece waves per window
-            c->win = true;
-            c->win_n = W;
-            c->win_bufs = (int)bufs;
-            c->win_buf_bytes = W * c->stride + kSlack;
-            need_payload = bufs * c->win_buf_bytes;
-        }
-        // (an allocation larger than the budget is never kept: the budget bounds what the ctx holds)
-        if (!need_payload || !reuse_fits(need_payload, c->cap_payload) || (budget && c->cap_payload > budget))
-            free_payload(c);
-        if (!need_payload || c->d_payload) break;
-        const hipError_t e = hipMalloc((void**)&c->d_payload, need_payload);
-        if (e == hipSuccess) {
+    // GPU of any free memory).  A failed allocation is retried at half the budget: only the windows shrink
+    // (tv_plan.h allocate_payload; it gives up when the request cannot get smaller).
+    if (need_payload && !c->slots) {
+        PayloadPlan plan;
+        uint64_t failed = 0;
+        hipError_t last = hipSuccess;
+        const int r = allocate_payload(
+            shard_count, c->stride, kSlack, budget,
+            [&](const PayloadPlan& p, uint64_t b) -> int {
+                // (an allocation larger than the budget is never kept: the budget bounds what the ctx holds)
+                if (!reuse_fits(p.bytes, c->cap_payload) || c->cap_payload > b) free_payload(c);
+                if (c->d_payload) return 0;
+                last = hipMalloc((void**)&c->d_payload, p.bytes);
+                if (last == hipSuccess) {
+                    c->cap_payload = p.bytes;
+                    c->n_payload_allocs++;
+                    c->n_device_allocs++;
+                    return 0;
+                }
+                (void)hipGetLastError();
+                c->d_payload = nullptr;
+                return last == hipErrorOutOfMemory ? 1 : 2;
+            },
+            &plan, &budget, &failed);
+        if (r)
+            return fail(c, r == 1 ? TV_ERR_NOMEM : TV_ERR_HIP, "hipMalloc(%llu) of the payload: %s",
+                        (unsigned long long)failed, hipGetErrorString(last));
+        need_payload = plan.bytes;
+        c->win = plan.win;
+        c->win_n = plan.win_n;
+        c->win_bufs = plan.bufs;
+        c->win_buf_bytes = plan.buf_bytes;
+    } else {
+        if (!need_payload || !reuse_fits(need_payload, c->cap_payload)) free_payload(c);
+        if (need_payload && !c->d_payload) {
+            TV_HIP(c, hipMalloc((void**)&c->d_payload, need_payload));
             c->cap_payload = need_payload;
             c->n_payload_allocs++;
             c->n_device_allocs++;
-            break;
         }
-        (void)hipGetLastError();
-        c->d_payload = nullptr;
-        if (e != hipErrorOutOfMemory || c->slots || need_payload <= (64ull << 20))
-            return fail(c, e == hipErrorOutOfMemory ? TV_ERR_NOMEM : TV_ERR_HIP, "hipMalloc(%llu) of the payload: %s",
-                        (unsigned long long)need_payload, hipGetErrorString(e));
-        budget = need_payload / 2;  // windows of half the size
-        need_payload = shard_count * c->stride + kSlack;
-        c->win = false;
     }
     c->budget = budget;
     if (!reuse_fits(shard_count, c->cap_count)) free_per_piece(c);

@@ -288,7 +288,8 @@ int upload_base_avail(tv_ctx* c) {
 // a missing / short file) & not the pieces file staging could not read, queued on the compute stream from
 // the pinned bounce buffer (no host sync).
 int launch_avail(tv_ctx* c, const uint8_t* avail_bits, const uint64_t** out) {
-    if (!avail_bits && !c->any_file_bad) {
+    const bool unhashed = c->win && c->any_unhashed;
+    if (!avail_bits && !c->any_file_bad && !unhashed) {
         *out = c->d_base_avail;
         return TV_OK;
     }
@@ -296,7 +297,7 @@ int launch_avail(tv_ctx* c, const uint8_t* avail_bits, const uint64_t** out) {
     const size_t nbytes = c->bit_words * 8, used = (c->count + 7) / 8;
     for (size_t k = 0; k < nbytes; k++) {
         const uint8_t caller = k < used ? (avail_bits ? avail_bits[k] : 0xFF) : 0;
-        const uint8_t bad = k < used ? c->file_bad[k] : 0;
+        const uint8_t bad = k < used ? (uint8_t)(c->file_bad[k] | (unhashed ? c->unhashed[k] : 0)) : 0;
         c->h_avail[k] = c->base_avail[k] & caller & (uint8_t)~bad;
     }
     TV_HIP(c, hipMemcpyAsync(c->d_avail, c->h_avail, nbytes, hipMemcpyHostToDevice, c->stream));
@@ -485,6 +486,8 @@ TvPieces window_launch(const tv_ctx* c, uint64_t j0, uint64_t n, const uint8_t* 
 
 int zero_hash(tv_ctx* c, uint64_t j0, uint64_t j1) {
     if (j1 <= j0) return TV_OK;
+    for (uint64_t j = j0; j < j1; j++) set_bit(c->unhashed.data(), j);  // (never staged: never verified)
+    c->any_unhashed = true;
     for (int k = 0; k < 5; k++)
         TV_HIP(c, hipMemsetAsync(c->d_hash + (uint64_t)k * c->count + j0, 0, (j1 - j0) * 4, c->stream));
     return TV_OK;
@@ -526,6 +529,8 @@ int win_enter(tv_ctx* c, uint64_t w) {
         c->win_valid = 0;
         c->win_launched = 0;
         c->win_timing = false;
+        std::fill(c->unhashed.begin(), c->unhashed.end(), 0);
+        c->any_unhashed = false;
     }
     if (w == c->win_cur) return TV_OK;
     if ((c->win_cur != UINT64_MAX && w < c->win_cur) || w * c->win_n < c->win_valid)

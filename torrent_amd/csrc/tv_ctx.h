@@ -23,6 +23,7 @@
 #include "tv_host.h"
 #include "tv_internal.h"
 #include "tv_options_internal.h"
+#include "tv_plan.h"
 
 namespace tvi {
 
@@ -164,7 +165,7 @@ struct tv_ctx {
     uint64_t stream_chunk = 0;  // 0 = automatic
     int split_pairs = 0;        // 0 = automatic
     uint64_t file_chunk = 256ull << 20;  // tv_stage_file: bytes per mapped window
-    bool file_direct = true;             // tv_stage_file: DMA from registered page-cache pages
+    bool file_direct = false;            // TV_OPT_FILE_DIRECT: long segments DMA'd from registered page-cache pages
     bool file_concurrent = true;         // tv_stage_files: long segments on two staging lanes
     uint64_t file_direct_min = 32ull << 20;  // tv_stage_files: segments >= this take the tv_stage_file path
     int file_threads = 16;                   // tv_stage_files: reader threads
@@ -205,6 +206,10 @@ struct tv_ctx {
     // reads them (until the next tv_set_layout); tv_verify reports them 0
     std::vector<uint8_t> file_bad;
     bool any_file_bad = false;
+    // windowed layouts: shard-relative MSB-first bits of the pieces in windows this pass never staged (their d_hash
+    // rows are zeroed, never hashed): tv_verify reports them 0 even where an expected digest is 20 zero bytes
+    std::vector<uint8_t> unhashed;
+    bool any_unhashed = false;
 
     // pinned staging ring.  A slot is LENT from take_slot until release_slot records its event after the
     // last copy queued from it; take_slot never hands out a lent slot (it takes the next free one), so a

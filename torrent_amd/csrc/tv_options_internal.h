@@ -3,6 +3,37 @@
 // tools set them through tv_set_option with these values; a host integrating the library never needs them.
 #pragma once
 
+#define TV_OPT_KERNEL 1      /* 0 = auto, 1 = lane, 2 = split (schedule offload), 4 = twin (split with two lanes per
+                                piece); 3 is unused (it was MIX, a work queue measured slower than lane, removed) */
+#define TV_OPT_STRIDE_PAD 2  /* bytes of padding between resident pieces (default 256; set before tv_set_layout) */
+#define TV_OPT_SPLIT_PAIRS 4 /* split and twin kernels: (rounds, helper) wave pairs per workgroup, 0 = auto, 1, 2;
+                                3-5 = SIMD-placement probe shapes (tools/twin_occupancy_probe.py) */
+#define TV_OPT_FILE_DIRECT 5 /* tv_stage_file(s) long segments: 0 (default, round 5) = parallel preads into the pinned
+                                ring; 1 = windows whose pages are mostly cached (mincore) are mapped, registered
+                                (hipHostRegister) and DMA'd from the page cache.  Stamped (tools/f2_stamps.py,
+                                profiles/r05): hipHostUnregister + munmap cost 4.9 ms per 256 MiB window, more than
+                                its 4.7 ms DMA, so 1 runs at 40-43 GB/s where 0 runs at 53 */
+#define TV_OPT_FILE_CHUNK 6  /* long segments: bytes per unit dealt to a lane (and per mapped window with
+                                TV_OPT_FILE_DIRECT = 1); default 256 MiB, >= 64 KiB */
+#define TV_OPT_FILE_CONCURRENT 9 /* tv_stage_files: 1 (default) = long segments on two staging lanes, 0 = one */
+#define TV_OPT_DEBUG_REBOUNCE 11 /* tests: 1 = bounce ring-resident sources through the ring again (the staging
+                                    path that once raced); slot leases must keep it exact.  Default 0 */
+#define TV_OPT_TWIN_PACK 12      /* twin kernel with fewer workgroups than 2 per CU: 1 = launch it on a stream
+                                    CU-masked to ceil(workgroups / 2) CUs, two workgroups on each; 0 (default) =
+                                    spread over every CU */
+/* TV_OPT_TWIN_FILL (public, 13) also takes 2 = companions on every tv_verify_list launch too (measurement only) */
+#define TV_OPT_TWIN_FILL_READS 14 /* companion workgroups' loads: 0 (default) = every lane of a companion reads its
+                                    main workgroup's first piece (the same instruction stream, 1/32 of the bytes);
+                                    1 = the main workgroup's 32 pieces (round 2; 1.14-1.42 x payload of HBM reads) */
+#define TV_OPT_NUMA_BIND 15 /* 1 (default) = the library's host threads (file readers, ring copies, the staging
+                               helper lane) run on the CPUs of the GPU's NUMA node, and the pinned ring is
+                               allocated on that node (slots allocated after the option is set); 0 = unpinned,
+                               default placement (the A/B of profiles/r03/f2_numa_ab.jsonl) */
+#define TV_OPT_LANE_PAIRS 21 /* lane kernel loads: 0 (default) = auto: a lane's two 64-B blocks of a 128-B line loaded
+                                back to back when the launch has >= 256 x CUs pieces (>= 1 wave per SIMD; HBM reads
+                                1.0004 instead of 1.023 x payload at 262,144 x 64 KiB), else a 3-deep ring of
+                                single blocks; 1 = pairs always; 2 = never */
+
 /* ---- file staging phase clock (tv_files.hip), for the stamped breakdown of tools/f2_stamps.py ---------------------
  * tv_get_counter(TV_COUNTER_FILE_CLOCK + phase): nanoseconds tv_stage_file(s) spent in that phase since the last
  * reset, summed over the two staging lanes (each lane's phases are disjoint in time, so a phase's total over both

@@ -1,0 +1,65 @@
+// tv_plan.h -- the resident payload's shape under a device budget (tv_set_layout), as plain host code with no HIP
+// in it, so its retry loop is unit-tested on the CPU (tests/c/plan_test.cpp, tests/test_plan.py).
+#pragma once
+#include <stdint.h>
+
+#include <algorithm>
+
+namespace tvi {
+
+struct PayloadPlan {
+    uint64_t bytes = 0;      // the allocation (0: none)
+    bool win = false;        // windowed: `bufs` buffers of `win_n` pieces, `buf_bytes` each
+    uint64_t win_n = 0;
+    int bufs = 0;
+    uint64_t buf_bytes = 0;
+};
+
+// `count` pieces at `stride` bytes (+ `slack` after the last) under `budget` bytes: the whole shard when it fits,
+// else two window buffers of W pieces (one buffer when the budget holds only one; W >= 1 even when one piece
+// exceeds the budget; a multiple of 64 from 256 up, so each window is whole 64-piece waves).
+inline PayloadPlan plan_payload(uint64_t count, uint64_t stride, uint64_t slack, uint64_t budget) {
+    PayloadPlan p;
+    if (count == 0) return p;
+    p.bytes = count * stride + slack;
+    if (p.bytes <= budget) return p;
+    uint64_t bufs = 2, W = budget / 2 > slack ? (budget / 2 - slack) / stride : 0;
+    if (W == 0) {
+        bufs = 1;
+        W = budget > slack ? (budget - slack) / stride : 0;
+    }
+    W = std::max<uint64_t>(1, std::min(W, count));
+    if (W >= 256) W = W / 64 * 64;
+    p.win = true;
+    p.win_n = W;
+    p.bufs = (int)bufs;
+    p.buf_bytes = W * stride + slack;
+    p.bytes = bufs * p.buf_bytes;
+    return p;
+}
+
+// Plan and allocate: try_alloc(plan, budget) -> 0 (the plan's bytes are held), 1 (out of memory), 2 (another
+// failure).  Out of memory is retried with windows at half the budget while the request still shrinks and is
+// above 64 MiB; a plan that cannot get smaller (a one-piece window of a piece larger than the memory left) is out of
+// memory, not a retry forever.  Returns 0 (*out, *budget_out: what is held), 1 or 2; *failed_bytes:
+// the last request that failed.
+template <class TryAlloc>
+int allocate_payload(uint64_t count, uint64_t stride, uint64_t slack, uint64_t budget, TryAlloc&& try_alloc,
+                     PayloadPlan* out, uint64_t* budget_out, uint64_t* failed_bytes) {
+    uint64_t failed = UINT64_MAX;
+    for (;;) {
+        const PayloadPlan p = plan_payload(count, stride, slack, budget);
+        const int r = try_alloc(p, budget);
+        if (r == 0) {
+            *out = p;
+            *budget_out = budget;
+            return 0;
+        }
+        *failed_bytes = p.bytes;
+        if (r != 1 || p.bytes <= (64ull << 20) || p.bytes >= failed) return r;
+        failed = p.bytes;
+        budget = p.bytes / 2;  // windows of half the size
+    }
+}
+
+}  // namespace tvi

@@ -188,10 +188,12 @@ class Storage:
     # -- reference API -----------------------------------------------------------------
     def get(self, offset: int, length: int):
         """storage.ts:50-65: the bytes [offset, offset + length) read file segment by file segment through
-        the method, or None when a segment fails (or returns another length: the reference's copy into its
-        Uint8Array would throw, :61).  A range inside one file is the method's own bytes (no copy); the
-        segments of a range spanning files are copied into one buffer with the GIL released (memmove), so
-        many readers copy in parallel."""
+        the method, or None when a segment fails.  A segment the method returns SHORTER than asked fills the
+        front of its slice and leaves the rest zero, as the reference's slice.set(got) into its zeroed
+        Uint8Array does (:51,57-58); a LONGER one makes the whole get null (slice.set throws a RangeError,
+        which findAndDo's catch turns into false, :130-133).  A range inside one file is the method's own bytes
+        when they have the full length (no copy); the segments of a range spanning files are copied into one
+        buffer with the GIL released (memmove), so many readers copy in parallel."""
         try:
             segs = self.segments(offset, length)
             if segs is None:
@@ -199,15 +201,21 @@ class Storage:
             if len(segs) == 1:
                 path, foff, n, _ = segs[0]
                 got = self.method.get(path, foff, n)
-                return got if got is not None and len(got) == n else None
+                if got is None or len(got) > n:
+                    return None
+                if len(got) == n:
+                    return got
+                out = bytearray(n)
+                out[:len(got)] = got
+                return out
             out = bytearray(length)
             base = ctypes.addressof((ctypes.c_char * length).from_buffer(out)) if length else 0
             for path, foff, n, start in segs:
                 got = self.method.get(path, foff, n)
-                if got is None or len(got) != n:
+                if got is None or len(got) > n:
                     return None
-                if n:
-                    copy_bytes(base + start, got, n)
+                if len(got):
+                    copy_bytes(base + start, got, len(got))
             return out
         except Exception:
             return None

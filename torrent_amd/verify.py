@@ -36,6 +36,7 @@ from typing import List, Optional, Sequence
 
 from . import _native
 from .metainfo import InfoDict
+from ._cpu import shard_threads
 from .piece import piece_length
 from .storage import copy_bytes
 
@@ -165,14 +166,31 @@ def _chunked_map(pool, fn, n: int, parts: int) -> list:
     return out
 
 
+_node_of: dict = {}            # device -> NUMA node of its GPU (None: unknown), from the library (TV_COUNTER_NUMA_NODE)
+
+
+def _device_node(device: int, slot: int) -> Optional[int]:
+    if device not in _node_of:
+        with _context(device, slot) as ctx:
+            v = ctx.counter(_native.TV_COUNTER_NUMA_NODE)
+        _node_of[device] = None if v >= (1 << 63) else int(v)
+    return _node_of[device]
+
+
 def _run_shards(devs: List[int], n_pieces: int, fn):
-    """fn(ctx, first, count) for each shard, one thread per shard (ctypes releases the GIL)."""
+    """fn(ctx, first, count) for each shard, one thread per shard (ctypes releases the GIL).  The shards share
+    the process's CPUs: each context gets its part (ctx.thread_budget, also set as TV_OPT_FILE_THREADS), so
+    devices=[0..7] does not start 8 x 16 reader threads on a 16-CPU share (_cpu.shard_threads)."""
     ranges = shard_ranges(n_pieces, len(devs))
+    active = [s for s, (_, count) in enumerate(ranges) if count]
+    budget = dict(zip(active, shard_threads([_device_node(devs[s], s) for s in active])))
 
     def run(slot: int, first: int, count: int):
         if count == 0:       # a trailing empty shard (P < 8 x devices): no context, no bits
             return b""
         with _context(devs[slot], slot) as ctx:
+            ctx.thread_budget = budget[slot]
+            ctx.set_option(_native.TV_OPT_FILE_THREADS, budget[slot])
             return fn(ctx, first, count)
 
     if len(devs) == 1:
@@ -218,7 +236,8 @@ def verify_pieces(info: InfoDict, storage, devices=None, threads: int = _STORAGE
             return n
 
         bufs = _batch_buffers(ctx, per_batch * L)
-        with ThreadPoolExecutor(max(1, threads)) as pool, ThreadPoolExecutor(1) as stager:
+        nthr = max(1, min(threads, ctx.thread_budget))   # (the shard's part of the process's CPUs)
+        with ThreadPoolExecutor(nthr) as pool, ThreadPoolExecutor(1) as stager:
             staging = None              # the previous batch's stage (it reads the other buffer)
             j, b = 0, 0
             try:
@@ -226,7 +245,7 @@ def verify_pieces(info: InfoDict, storage, devices=None, threads: int = _STORAGE
                     k = min(per_batch, count - j)
                     buf = bufs[b]       # its last stage (two batches ago) finished before `staging` began
                     hi = 0
-                    got = _chunked_map(pool, lambda q: get(first + j + q, buf.ptr + q * L), k, threads)
+                    got = _chunked_map(pool, lambda q: get(first + j + q, buf.ptr + q * L), k, nthr)
                     for q, n in enumerate(got):
                         if n:           # (an unreadable piece's slot keeps stale bytes: never a readable piece)
                             hi = q * L + n
@@ -319,6 +338,8 @@ def verify_stream(info: InfoDict, read, devices=None, avail: Optional[bytes] = N
     def shard(ctx, first: int, count: int) -> bytes:
         ctx.set_option(_native.TV_OPT_RESIDENT, 0)       # no resident payload for a streamed check
         try:
+            # (a budget an earlier call left on the cached context would cap the row windows: ADVICE r04)
+            ctx.set_option(_native.TV_OPT_RESIDENT_BUDGET, 0)
             ctx.set_option(_native.TV_OPT_STREAM_CHUNK, chunk)
             ctx.set_option(_native.TV_OPT_STREAM_ROWS, 0 if chunk else 1)
             ctx.set_layout(info.length, L, P, first, count)
@@ -326,7 +347,8 @@ def verify_stream(info: InfoDict, read, devices=None, avail: Optional[bytes] = N
         finally:
             ctx.set_option(_native.TV_OPT_RESIDENT, 1)
         ctx.stream_begin(_shard_avail(avail, first, count))
-        pool = ThreadPoolExecutor(threads) if threads > 1 else None
+        nthr = max(1, min(threads, ctx.thread_budget))
+        pool = ThreadPoolExecutor(nthr) if nthr > 1 else None
         try:
             while True:
                 req = ctx.stream_next()
@@ -346,7 +368,7 @@ def verify_stream(info: InfoDict, read, devices=None, avail: Optional[bytes] = N
                     copy_bytes(req.slot + q * req.width, data, n)
                     return None
 
-                for i in _chunked_map(pool, fill, req.rows, threads):
+                for i in _chunked_map(pool, fill, req.rows, nthr):
                     if i is not None:
                         ctx.stream_unreadable(i)
                 ctx.stream_commit(req)
@@ -429,7 +451,7 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
     return avail
 
 
-def verify_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
+def verify_files(info: InfoDict, dir_path: str, devices=None, threads: Optional[int] = None,
                  direct_min: Optional[int] = None, budget: Optional[int] = None) -> bytearray:
     """Resume check from disk: the have-bitfield of the files under dir_path,
     laid out as Storage(fs_storage, info, dir_path) maps them (storage.ts:89-137; single-file
@@ -437,7 +459,8 @@ def verify_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
 
     Same bits as verify_pieces(info, Storage(fs_storage, info, dir_path)), without fsStorage.get's
     side effect of creating missing files, and with every file segment of a shard staged by ONE
-    tv_stage_files call (see _files_shard) instead of one open/seek/read per piece."""
+    tv_stage_files call (see _files_shard) instead of one open/seek/read per piece.  threads: the library's
+    reader threads per shard (default: the shard's part of the process's CPUs, _cpu.shard_threads)."""
     from .storage import Storage, fs_storage
 
     P, L = info.n_pieces, info.piece_length
@@ -448,7 +471,7 @@ def verify_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
         ctx.set_digests(info.pieces_raw)
         if count == 0:
             return b""
-        return ctx.verify(_files_shard(ctx, info, storage, first, count, threads, direct_min))
+        return ctx.verify(_files_shard(ctx, info, storage, first, count, threads or ctx.thread_budget, direct_min))
 
     if P == 0:
         return bytearray()
@@ -456,7 +479,7 @@ def verify_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
     return _concat(slices, ranges, P)
 
 
-def hash_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
+def hash_files(info: InfoDict, dir_path: str, devices=None, threads: Optional[int] = None,
                direct_min: Optional[int] = None, budget: Optional[int] = None) -> bytes:
     """Creation mode from disk: the `pieces` string of the files info describes under dir_path
     (info.pieces is ignored; only the geometry is used).  Raises if a file is missing or short.  Files are
@@ -472,7 +495,8 @@ def hash_files(info: InfoDict, dir_path: str, devices=None, threads: int = 16,
         if count == 0:
             return b""
         status: list = []
-        avail = _files_shard(ctx, info, storage, first, count, threads, direct_min, status, open_rw=False)
+        avail = _files_shard(ctx, info, storage, first, count, threads or ctx.thread_budget, direct_min, status,
+                             open_rw=False)
         full = bytearray(b"\xff" * ((count + 7) // 8))
         if count % 8:
             full[-1] = (0xFF00 >> (count % 8)) & 0xFF

@@ -76,6 +76,25 @@ export interface VerifyOptions {
   /** verifyPiece only: hash on the CPU with the reference's own crypto.subtle.digest("SHA-1", bytes)
    * (tools/make_torrent.ts:28-31) instead of a ~3 ms GPU launch.  Off by default */
   cpuFallback?: boolean;
+  /** host threads the library may use for one call, over all of its shards (default: the machine's,
+   * navigator.hardwareConcurrency): each shard's context gets its part (TV_OPT_FILE_THREADS), so
+   * devices [0..7] do not start 8 x 16 reader threads */
+  threads?: number;
+}
+
+const TV_OPT_FILE_THREADS = 8;
+
+/** Reader / copy threads of each of `active` concurrently running shards: opts.threads (else the machine's CPU
+ * count) divided among them, 1 .. 16 each (16 is the library's default; its page-cache readers already saturate
+ * PCIe there).  Same rule as torrent_amd/_cpu.py shard_threads, without its cgroup / NUMA inputs, which a Deno
+ * process without --allow-read cannot see. */
+export function shardThreads(opts: VerifyOptions, active: number): number {
+  const share = opts.threads || (typeof navigator !== "undefined" && navigator.hardwareConcurrency) || 16;
+  return Math.max(1, Math.min(16, Math.floor(share / Math.max(1, active))));
+}
+
+function activeShards(ranges: [number, number][]): number {
+  return ranges.filter(([, count]) => count > 0).length;
 }
 
 /** SHA-1(bytes) === digest through WebCrypto, the reference's SHA-1 path (make_torrent.ts:28-31). */
@@ -215,10 +234,14 @@ export async function verifyPieces(
   const bitfield = new Uint8Array(Math.ceil(P / 8));
   const batch = Math.max(1, Math.floor((opts.batchBytes || 256 * 2 ** 20) / L));
 
-  await Promise.all(shardRanges(P, devices.length).map(async ([first, count], s) => {
+  const ranges = shardRanges(P, devices.length);
+  const threads = shardThreads(opts, activeShards(ranges));
+  await Promise.all(ranges.map(async ([first, count], s) => {
     if (count === 0) return;
     await withContext(l, devices[s], s, async (ctx) => {
       setLayout(l, ctx, info.length, L, P, first, count, opts.budget);
+      // tv_stage_many copies the batch's buffers into the pinned ring on this many library threads
+      check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_FILE_THREADS, BigInt(threads)));
       check(l, ctx, l.symbols.tv_set_digests(ctx, ptr(raw), BigInt(raw.length)));
       const avail = new Uint8Array(Math.ceil(count / 8));
       const per = Math.min(batch, count);
@@ -296,10 +319,15 @@ export async function verifyStream(info: InfoDict, storage: Storage, opts: Verif
   const devices = opts.devices || [0];
   const raw = piecesRaw(info);
   const bitfield = new Uint8Array(Math.ceil(P / 8));
-  await Promise.all(shardRanges(P, devices.length).map(async ([first, count], s) => {
+  const ranges = shardRanges(P, devices.length);
+  const threads = shardThreads(opts, activeShards(ranges));
+  await Promise.all(ranges.map(async ([first, count], s) => {
     if (count === 0) return;
     await withContext(l, devices[s], s, async (ctx) => {
       check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_RESIDENT, 0n));
+      // (a budget an earlier call left on the cached context would cap the row windows)
+      check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_RESIDENT_BUDGET, 0n));
+      check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_FILE_THREADS, BigInt(threads)));
       check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_STREAM_CHUNK, BigInt(opts.chunk || 0)));
       // default: whole pieces per row (one storage.get, i.e. one fsStorage open, per piece); chunk: columns
       check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_STREAM_ROWS, opts.chunk ? 0n : 1n));
@@ -350,8 +378,9 @@ export async function verifyStream(info: InfoDict, storage: Storage, opts: Verif
  * verifyFiles(info, dir) -> have-bitfield of the files under `dir` (resume from disk, SURVEY 8f
  * row f2), laid out as new Storage(fsStorage, info, dir) maps them (storage.ts:89-137: single-file
  * [dir, name], multi-file [dir, ...path]).  All file segments of a shard go to tv_stage_files in one
- * call: long segments are DMA'd to HBM from the page cache when the file is warm (parallel preads when
- * cold); short ones (many small files) are read by the library's thread pool into pinned slots.
+ * call: long segments are cut into 256 MiB units read by parallel preads into the library's pinned ring on
+ * its two staging lanes and DMA'd from there; short ones (many small files) are read by the library's thread
+ * pool into pinned slots.  The shard's reader threads are its part of opts.threads (shardThreads).
  * The library marks the pieces fsStorage.get would return null for (storage.ts:163-171): a byte in a
  * missing, unopenable or unwritable file or past a short file's end, or a zero-length segment whose open
  * would fail (a directory, a missing parent directory); unlike fsStorage.get, no missing file is created.  Same behaviour as
@@ -368,11 +397,14 @@ export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptio
     : [{ length: info.length, path: [dir, info.name].join("/") }];
   const bitfield = new Uint8Array(Math.ceil(P / 8));
 
-  await Promise.all(shardRanges(P, devices.length).map(async ([first, count], s) => {
+  const ranges = shardRanges(P, devices.length);
+  const threads = shardThreads(opts, activeShards(ranges));
+  await Promise.all(ranges.map(async ([first, count], s) => {
     if (count === 0) return;
     await withContext(l, devices[s], s, async (ctx) => {
       setLayout(l, ctx, info.length, L, P, first, count, opts.budget);
       check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_OPEN_RW, 1n)); // fsStorage.get's read + write open
+      check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_FILE_THREADS, BigInt(threads))); // this shard's readers
       check(l, ctx, l.symbols.tv_set_digests(ctx, ptr(raw), BigInt(raw.length)));
       const avail = new Uint8Array(Math.ceil(count / 8)).fill(0xff);
       if (count % 8) avail[avail.length - 1] = (0xff00 >> (count % 8)) & 0xff;
@@ -463,10 +495,13 @@ export async function hashPieces(payload: Uint8Array, pieceLength: number, opts:
   const l = load(opts.libPath);
   const devices = opts.devices || [0];
   const out = new Uint8Array(20 * P);
-  await Promise.all(shardRanges(P, devices.length).map(async ([first, count], s) => {
+  const ranges = shardRanges(P, devices.length);
+  const threads = shardThreads(opts, activeShards(ranges));
+  await Promise.all(ranges.map(async ([first, count], s) => {
     if (count === 0) return;
     await withContext(l, devices[s], s, async (ctx) => {
       setLayout(l, ctx, payload.length, pieceLength, P, first, count, opts.budget);
+      check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_FILE_THREADS, BigInt(threads)));
       const lo = first * pieceLength, hi = Math.min(payload.length, (first + count) * pieceLength);
       if (hi > lo) check(l, ctx, await l.symbols.tv_stage(ctx, BigInt(lo), ptr(payload.subarray(lo, hi)), BigInt(hi - lo)));
       const digests = new Uint8Array(20 * count);
