@@ -27,6 +27,8 @@ Legs reported beside `value` (never as it):
     host generator into the ring slots inside the timed region; `pinned_pool`: rows are DMA'd straight
     from a 1 GiB page-locked pool of pre-generated pieces (the torrent is that pool repeated), i.e. the
     PCIe path without the producer.
+  * cfg3 (N = 1): BASELINE configs[2], the multi-file torrent (10,000 files, 256 KiB pieces spanning files, short
+    final piece, 1 % corrupted) staged file by file, resident verify at the live clock + one-shot wall clock.
   * piece_saturated (N = 1): 65,536 x 256 KiB pieces (SURVEY 8d suppl.) against the VALU roofline.
   * cfg2_weak (N > 1): cfg2 per GPU, weak scaling.
   * cpu_baseline (rank 0, N = 1): the oracle (C port of the per-piece SHA-1 path, SHA-NI) on the host's
@@ -225,18 +227,25 @@ def ground_truth(seed: int, total: int, L: int, P: int, first: int, count: int, 
     return d, time.perf_counter() - t0
 
 
-def _traffic(workload: str, bytes_per_launch: int):
-    """HBM bytes per launch from profiles/traffic_<workload>.json (PMC passes, corrected as the MI355X guide
-    prescribes), when it was measured on this launch geometry; else None."""
+def _traffic(workload: str, bytes_per_launch: int) -> tuple:
+    """(HBM bytes per launch, note) from profiles/traffic_<workload>.json (PMC passes, corrected as the MI355X guide
+    prescribes), when it was measured on this launch geometry AND on this build of the library (its build_id is
+    the source id compiled into the library the bench loaded); else (None, why not)."""
     tpath = os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
     if not os.path.exists(tpath):
-        return None
+        return None, f"no PMC record ({os.path.relpath(tpath, ROOT)})"
     try:
         rec = json.load(open(tpath))
-    except Exception:
-        return None
-    # a per-launch PMC figure applies only to the launch geometry it was measured on
-    return rec.get("hbm_bytes_per_launch") if rec.get("payload_bytes_per_launch") == bytes_per_launch else None
+    except Exception as exc:
+        return None, f"unreadable PMC record: {exc}"
+    if rec.get("payload_bytes_per_launch") != bytes_per_launch:
+        return None, "the PMC record is of another launch geometry"
+    lib_id = _native.build_id()
+    if rec.get("build_id") != lib_id:
+        return None, (f"the PMC record was measured on build {rec.get('build_id')}, the library timed is build "
+                      f"{lib_id}: re-measure (tools/gpu_r05_pmc.sh)")
+    return rec.get("hbm_bytes_per_launch"), (f"{os.path.relpath(tpath, ROOT)}: PMC passes on build {lib_id}, "
+                                             f"{rec.get('method', '')[:160]}")
 
 
 def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: bool, steps: int, warmup: int,
@@ -483,6 +492,93 @@ def e2e_cfg5(dist, ws: int, rank: int, device: int, steps: int, threads: int, sh
     return out
 
 
+def cfg3_leg(device: int, steps: int, warmup: int, kernel_opt: int, idle_s: float = 0.5) -> dict:
+    """BASELINE configs[2]: the multi-file torrent -- 10,000 files of U[0, 512 KiB] (20 zero-length, 5 under 64 B),
+    256 KiB pieces spanning file boundaries, a short final piece, 1 % corrupted (tests/layouts.py "cfg3", the seeded
+    generator the parity tests use; expected bits committed in tests/golden/layouts.json).  The payload is built in
+    host memory and staged FILE BY FILE (tv_stage_many with one segment per file at its linear offset: the
+    storage.ts:89-137 walk's segments, zero-length files included), so the file -> piece mapping and the short
+    final piece go through the library as a multi-file torrent's would.  Timed: (a) the resident verify, W + K
+    steps with the shader clock probed (the value; frac_of_piece_ceiling is also given at the live clock), and
+    (b) one-shot calls as a host makes them after `idle_s` of GPU idle: stage every file + verify, wall clock,
+    with that call's kernel time and clock."""
+    from tests.layouts import build_layout, by_name
+    t_leg = time.perf_counter()
+    spec = by_name("cfg3")
+    lay = build_layout(spec)
+    info = lay["info"]
+    golden = {r["name"]: r for r in json.load(open(os.path.join(ROOT, "tests", "golden", "layouts.json")))}["cfg3"]
+    want = bytes.fromhex(golden["expected_bitfield"])
+    L, P, total = info.piece_length, info.n_pieces, info.length
+    payload = lay["payload"]
+    mv = memoryview(payload)
+    starts, sizes = lay["starts"], lay["sizes"]
+    segs = [(starts[k], mv[starts[k]:starts[k] + sizes[k]]) for k in range(len(sizes))]
+    t_built = time.perf_counter()
+    ctx = _native.Context(device)
+    try:
+        ctx.set_option(_native.TV_OPT_KERNEL, kernel_opt)
+        ctx.set_clock_probe(True)
+        ctx.set_layout(total, L, P)
+        if ctx.counter(_native.TV_COUNTER_WINDOW_PIECES):
+            raise RuntimeError("cfg3: the shard does not fit the device budget")
+        ctx.set_digests(info.pieces_raw)
+        t0 = time.perf_counter()
+        ctx.stage_many(segs)
+        stage_s = time.perf_counter() - t0
+        _device_sync(ctx, device)
+        for _ in range(warmup):
+            ctx.verify()
+        _device_sync(ctx, device)
+        kernel_ms = []
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            bf = ctx.verify()
+            kernel_ms.append(ctx.last_timing()[0])
+        _device_sync(ctx, device)
+        t1 = time.perf_counter()
+        kernel, _ = ctx.last_kernel()
+        clock_ghz = ctx.last_clock_khz() / 1e6
+        exact = bytes(bf) == want
+        # one-shot calls: a host stages every file and verifies, after the GPU idled
+        shots = []
+        for _ in range(3):
+            time.sleep(idle_s)
+            t2 = time.perf_counter()
+            ctx.stage_many(segs)
+            bf1 = ctx.verify()
+            t3 = time.perf_counter()
+            shots.append({"wall_ms": round((t3 - t2) * 1e3, 2), "gbps": round(total / (t3 - t2) / 1e9, 2),
+                          "kernel_ms": round(ctx.last_timing()[0], 3),
+                          "clock_ghz": round(ctx.last_clock_khz() / 1e6, 3), "exact": bytes(bf1) == want})
+        exact = exact and all(x["exact"] for x in shots)
+    finally:
+        ctx.close()
+    avg = sum(kernel_ms) / len(kernel_ms)
+    achieved = total / (avg / 1e3) / 1e9
+    ceiling = piece_ceiling(kernel, P)
+    ceiling_at_clock = ceiling * clock_ghz / (CLOCK_HZ / 1e9) if clock_ghz else None
+    best = min(shots, key=lambda x: x["wall_ms"])
+    return {"workload": "cfg3: multi-file torrent, 10,000 files of U[0, 512 KiB] (20 zero-length, 5 under 64 B), "
+                        "256 KiB pieces spanning file boundaries + short final piece, 1 % corrupted; staged file by "
+                        "file (one tv_stage_many segment per file), HBM-resident verify",
+            "files": len(sizes), "piece_length": L, "total_pieces": P, "bytes": total,
+            "short_last_piece": total % L, "corrupted": len(lay["corrupted"]),
+            "value": round(total * steps / (t1 - t0) / 1e9, 2), "unit": "GB/s", "steps": steps, "warmup": warmup,
+            "ms_per_step": round((t1 - t0) * 1e3 / steps, 3), "kernel": KERNEL_NAMES.get(kernel, str(kernel)),
+            "kernel_ms_avg": round(avg, 3), "achieved": round(achieved, 1),
+            "piece_parallelism_ceiling": round(ceiling, 1), "frac_of_piece_ceiling": round(achieved / ceiling, 4),
+            "clock_ghz": round(clock_ghz, 3) if clock_ghz else None,
+            "piece_ceiling_at_clock": round(ceiling_at_clock, 1) if ceiling_at_clock else None,
+            "frac_of_piece_ceiling_at_clock": round(achieved / ceiling_at_clock, 4) if ceiling_at_clock else None,
+            "bitfield_exact": exact, "expected": "tests/golden/layouts.json cfg3 expected_bitfield (hashlib digests)",
+            "one_shot": {"what": f"stage all {len(sizes)} files from pageable host memory + verify, wall clock, "
+                                 f"after {idle_s} s of GPU idle (best of {len(shots)})",
+                         "best_wall_ms": best["wall_ms"], "best_gbps": best["gbps"], "calls": shots},
+            "first_stage_s": round(stage_s, 3),
+            "phase_s": {"build_layout": round(t_built - t_leg, 2), "leg": round(time.perf_counter() - t_leg, 2)}}
+
+
 def cpu_baseline(share: dict, target_s: float = 10.0) -> dict:
     """The CPU oracle (C port of the per-piece SHA-1 path; SHA-NI where the host has it: the reference's
     WebCrypto SHA-1 is native code of that class) on the allowed cores, one piece per task:
@@ -537,6 +633,7 @@ def main() -> int:
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-saturating", action="store_true", help="skip the piece_saturated leg (N=1)")
     ap.add_argument("--no-cfg4", action="store_true", help="skip the cfg4 anchor leg (N=1) / cfg2_weak leg (N>1)")
+    ap.add_argument("--no-cfg3", action="store_true", help="skip the cfg3 multi-file leg (N=1)")
     ap.add_argument("--e2e-steps", type=int, default=1, help="timed e2e_cfg5 passes (0 = skip the leg)")
     ap.add_argument("--leg-steps", type=int, default=5, help="timed steps of the cfg4 / cfg2_weak / suppl legs")
     a = ap.parse_args()
@@ -574,6 +671,11 @@ def main() -> int:
         except Exception as exc:  # reported, never fatal to the bench line
             legs["e2e_cfg5"] = {"skipped": f"{type(exc).__name__}: {exc}"}
     cfg4_digests = None
+    if ws == 1 and workload == "cfg2" and not a.no_cfg3:
+        try:
+            legs["cfg3"] = cfg3_leg(device, a.leg_steps, 2, a.kernel)
+        except Exception as exc:
+            legs["cfg3"] = {"skipped": f"{type(exc).__name__}: {exc}"}
     if ws == 1 and workload == "cfg2" and not a.no_saturating:
         try:
             legs["piece_saturated"] = resident_leg(dist, 1, 0, device, "suppl", False, a.leg_steps, 1, a.kernel, threads)
@@ -582,13 +684,12 @@ def main() -> int:
 
     if rank == 0:
         bytes_per_gpu = main_leg["bytes_per_gpu"]
-        traffic = _traffic(workload, bytes_per_gpu)
+        traffic, traffic_note = _traffic(workload, bytes_per_gpu)
         tp = legs.get("piece_saturated")
         if tp and "bytes_per_gpu" in tp:
-            tsat = _traffic("suppl", tp["bytes_per_gpu"])
-            if tsat:
-                tp["traffic_ratio"] = round(tsat / tp["bytes_per_gpu"], 5)
-                tp["traffic_source"] = "profiles/traffic_suppl.json (PMC passes of this geometry, tools/gpu_r04_pmc.sh)"
+            tsat, tnote = _traffic("suppl", tp["bytes_per_gpu"])
+            tp["traffic_ratio"] = round(tsat / tp["bytes_per_gpu"], 5) if tsat else None
+            tp["traffic_source"] = tnote
         achieved = main_leg["achieved"]
         out = {
             "metric": "verified GB/s (SHA-1 pieces, HBM-resident)",
@@ -611,6 +712,8 @@ def main() -> int:
             "expected": main_leg["expected"],
             "roofline": {"bound": "valu", "achieved": achieved, "peak": round(ROOF_PEAK_GBPS, 1), "unit": "GB/s",
                          "frac": round(achieved / ROOF_PEAK_GBPS, 4), "traffic": traffic,
+                         "traffic_ratio": round(traffic / bytes_per_gpu, 6) if traffic else None,
+                         "traffic_source": traffic_note, "build_id": _native.build_id(),
                          "kernel_ms_avg": main_leg["kernel_ms_avg"],
                          "kernel_ms_max_over_ranks": main_leg["kernel_ms_max_over_ranks"],
                          "algorithmic_bytes_per_launch": bytes_per_gpu,

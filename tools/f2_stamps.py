@@ -26,6 +26,12 @@ from torrent_amd.verify import _context  # noqa: E402
 MiB, GiB = 1 << 20, 1 << 30
 FILE_DIRECT, FILE_CHUNK, FILE_CONCURRENT = _native.TV_OPT_FILE_DIRECT, _native.TV_OPT_FILE_CHUNK, _native.TV_OPT_FILE_CONCURRENT
 
+CFG3_CONFIGS = [  # 10,000 files of <= 512 KiB: every segment takes the short-segment path
+    ("short segments, 1 lane, 16 thr", 0, 0, 16, 256 * MiB),
+    ("short segments, 2 lanes, 16 thr", 0, 1, 16, 256 * MiB),
+    ("short segments, 2 lanes, 8 thr", 0, 1, 8, 256 * MiB),
+    ("short segments, 2 lanes, 32 thr", 0, 1, 32, 256 * MiB),
+]
 CONFIGS = [  # name, direct, concurrent, threads, chunk
     ("direct, 1 lane", 1, 0, 16, 256 * MiB),
     ("direct, 2 lanes", 1, 1, 16, 256 * MiB),
@@ -43,18 +49,20 @@ def emit(rec):
 
 def main():
     d = sys.argv[1]
-    names = sys.argv[2:] or ["single16", "files64"]
+    names = sys.argv[2:] or ["single16", "files64", "cfg3"]
     reps = int(os.environ.get("F2_REPS", "3"))
     emit({"host": {"cpus_allowed": len(os.sched_getaffinity(0))}})
     for name in names:
         root = os.path.join(d, name)
         t0 = time.perf_counter()
         info, expect, paths = write_layout(name, root)
+        cwd = os.getcwd()
+        os.chdir(root)       # (Storage paths are relative to the working directory, storage.ts)
         total = info.length
         emit({"layout": name, "files": len(paths), "bytes": total, "pieces": info.n_pieces,
               "write_s": round(time.perf_counter() - t0, 1)})
         verify_files(info, root)            # context creation, allocations, first touch of the ring
-        for cname, direct, conc, threads, chunk in CONFIGS:
+        for cname, direct, conc, threads, chunk in (CFG3_CONFIGS if name == "cfg3" else CONFIGS):
             with _context(0) as ctx:
                 ctx.set_option(FILE_DIRECT, direct)
                 ctx.set_option(FILE_CONCURRENT, conc)
@@ -88,6 +96,7 @@ def main():
             ctx.set_option(FILE_DIRECT, 0)
             ctx.set_option(FILE_CONCURRENT, 1)
             ctx.set_option(FILE_CHUNK, 256 * MiB)
+        os.chdir(cwd)
         for p in paths:
             os.unlink(p)
 

@@ -74,3 +74,47 @@ def drop_cache(paths, max_resident=0.01, tries=3):
             break
         time.sleep(0.5)     # dirty pages still under writeback are not dropped: let it finish
     return r
+
+
+def fs_type(path):
+    """The filesystem type of the mount holding `path` (/proc/mounts, longest matching mount point)."""
+    path = os.path.realpath(path)
+    best, kind = "", "unknown"
+    try:
+        for line in open("/proc/mounts"):
+            parts = line.split()
+            mnt = parts[1].replace("\\040", " ")
+            if (path == mnt or path.startswith(mnt.rstrip("/") + "/")) and len(mnt) > len(best):
+                best, kind = mnt, parts[2]
+    except OSError:
+        pass
+    return kind
+
+
+def evictable(d, mib=64):
+    """Can files under directory `d` be made cold (DONTNEED drops them)?  -> dict(dir, fs, ok, resident_after)."""
+    os.makedirs(d, exist_ok=True)
+    p = os.path.join(d, f".evict_probe_{os.getpid()}")
+    try:
+        with open(p, "wb") as f:
+            f.write(os.urandom(1 << 20) * mib)
+        r = drop_cache([p])
+        return {"dir": d, "fs": fs_type(d), "ok": r <= 0.01, "resident_after_drop": round(r, 4)}
+    except OSError as exc:
+        return {"dir": d, "fs": fs_type(d), "ok": False, "error": str(exc)}
+    finally:
+        try:
+            os.unlink(p)
+        except OSError:
+            pass
+
+
+if __name__ == "__main__":
+    import json
+    import sys
+    if len(sys.argv) > 2 and sys.argv[1] == "pick":
+        # print the first directory whose files can be evicted (else the first one given), details on stderr
+        probes = [evictable(d) for d in sys.argv[2:] if d]
+        print(json.dumps(probes), file=sys.stderr)
+        good = [x["dir"] for x in probes if x["ok"]]
+        print(good[0] if good else sys.argv[2])

@@ -1,0 +1,82 @@
+/* read_ceiling.c -- what the box's storage delivers: every file named on stdin (one path per line) read with
+ * pread in `part`-byte requests by `threads` threads taking (file, offset) tasks from a shared counter, bytes
+ * dropped.  Prints {"bytes": B, "seconds": S, "gbps": G}.  The storage benches (tools/storage_paths_bench.py) run it
+ * after dropping the files from the page cache, so the cold legs have a ceiling measured without Python in the
+ * way (the round-4 Python reader under-measured it for 10,000 small files).
+ * build: gcc -O2 -pthread tools/read_ceiling.c -o read_ceiling;  usage: read_ceiling THREADS PART_BYTES < paths */
+#define _GNU_SOURCE
+#include <fcntl.h>
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+typedef struct { char* path; uint64_t size; int fd; } file_t;
+static file_t* files;
+static uint64_t nfiles, part, ntasks;
+static uint64_t* task_file;   /* task -> file; offset = (task - first task of the file) * part */
+static uint64_t* first_task;
+static atomic_uint_fast64_t next_task, total_bytes;
+
+static void* worker(void* arg) {
+    (void)arg;
+    char* buf = aligned_alloc(4096, part);
+    for (;;) {
+        const uint64_t t = atomic_fetch_add(&next_task, 1);
+        if (t >= ntasks) break;
+        file_t* f = &files[task_file[t]];
+        uint64_t off = (t - first_task[task_file[t]]) * part, n = f->size - off < part ? f->size - off : part;
+        while (n) {
+            const ssize_t got = pread(f->fd, buf, n, (off_t)off);
+            if (got <= 0) break;
+            atomic_fetch_add(&total_bytes, (uint64_t)got);
+            off += (uint64_t)got;
+            n -= (uint64_t)got;
+        }
+    }
+    free(buf);
+    return NULL;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 3) return 2;
+    const int threads = atoi(argv[1]);
+    part = strtoull(argv[2], NULL, 10);
+    uint64_t cap = 1024;
+    files = malloc(cap * sizeof(file_t));
+    char line[8192];
+    while (fgets(line, sizeof line, stdin)) {
+        line[strcspn(line, "\n")] = 0;
+        if (!line[0]) continue;
+        if (nfiles == cap) files = realloc(files, (cap *= 2) * sizeof(file_t));
+        files[nfiles].path = strdup(line);
+        nfiles++;
+    }
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);   /* the opens are part of reading the files */
+    first_task = malloc((nfiles + 1) * sizeof(uint64_t));
+    for (uint64_t k = 0; k < nfiles; k++) {
+        struct stat st;
+        files[k].fd = open(files[k].path, O_RDONLY);
+        files[k].size = (files[k].fd >= 0 && fstat(files[k].fd, &st) == 0) ? (uint64_t)st.st_size : 0;
+        first_task[k] = ntasks;
+        ntasks += (files[k].size + part - 1) / part;
+    }
+    task_file = malloc((ntasks + 1) * sizeof(uint64_t));
+    for (uint64_t k = 0; k < nfiles; k++)
+        for (uint64_t t = first_task[k]; t < first_task[k] + (files[k].size + part - 1) / part; t++) task_file[t] = k;
+    pthread_t* th = malloc(threads * sizeof(pthread_t));
+    for (int i = 0; i < threads; i++) pthread_create(&th[i], NULL, worker, NULL);
+    for (int i = 0; i < threads; i++) pthread_join(th[i], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    const double s = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    const uint64_t b = atomic_load(&total_bytes);
+    printf("{\"bytes\": %llu, \"seconds\": %.4f, \"gbps\": %.3f, \"files\": %llu, \"threads\": %d, \"part\": %llu}\n",
+           (unsigned long long)b, s, (double)b / s / 1e9, (unsigned long long)nfiles, threads, (unsigned long long)part);
+    return 0;
+}

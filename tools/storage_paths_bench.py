@@ -13,7 +13,9 @@ fsStorage, which opens the file once per get call, storage.ts:149-172):
   verify_stream(Storage(fs).get)   the bounded ring, whole-piece rows (TV_OPT_STREAM_ROWS, the default)
   verify_stream(..., chunk=L/4)    the bounded ring, columns: four gets per piece (the round-3 default)
 Warm = the files were just written (page cache); cold = posix_fadvise(DONTNEED) after fsync on every file
-(no root needed), then the same call.  `read_ceiling` = the files read cold by 16 threads of 4 MiB preads into
+(no root needed), re-checked with mincore (tools/fsutil.py): every line carries `resident`, the fraction of the
+files' pages cached when the leg started, and a cold pass whose drop leaves more than 1 % cached is refused
+(freshly written files on some boxes stayed cached and the "cold" legs read memory).  `read_ceiling` = the files read cold by 16 threads of 4 MiB preads into
 host memory, nothing else: what the box's storage delivers.  Each line: GB/s, gets (= opens) per piece.
 
 usage: python tools/storage_paths_bench.py <dir> [layout ...] > out.jsonl
@@ -29,11 +31,14 @@ from concurrent.futures import ThreadPoolExecutor
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import fsutil  # noqa: E402
 from oracle import oracle as O  # noqa: E402  (the checker and the generator)
 from torrent_amd import FileInfo, Storage, make_info, verify_files, verify_pieces, verify_stream  # noqa: E402
 from torrent_amd.storage import FsStorage  # noqa: E402
 
 MiB, GiB = 1 << 20, 1 << 30
+COLD_MAX_RESIDENT = 0.01     # a leg is "cold" only with <= 1 % of its files' pages cached at its start
 
 
 class CountingFs(FsStorage):
@@ -59,17 +64,38 @@ def emit(rec):
 
 
 def drop_cache(paths):
-    for p in paths:
-        fd = os.open(p, os.O_RDONLY)
+    """Evict the files (fsutil.drop_cache: fsync + DONTNEED, re-checked with mincore); the residency left."""
+    return fsutil.drop_cache(paths)
+
+
+_RC_BIN = None
+
+
+def _read_ceiling_bin():
+    """tools/read_ceiling.c built with gcc into TMPDIR (once); None when it cannot be built."""
+    global _RC_BIN
+    if _RC_BIN is None:
+        import subprocess
+        import tempfile
+        exe = os.path.join(tempfile.gettempdir(), f"read_ceiling_{os.getpid()}")
         try:
-            os.fsync(fd)
-            os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
-        finally:
-            os.close(fd)
+            subprocess.check_call(["gcc", "-O2", "-pthread", os.path.join(ROOT, "tools", "read_ceiling.c"), "-o", exe])
+            _RC_BIN = exe
+        except (OSError, subprocess.CalledProcessError):
+            _RC_BIN = ""
+    return _RC_BIN or None
 
 
 def read_ceiling(paths, threads=16, part=4 * MiB):
-    """Bytes/s of reading every file with `threads` parallel preads of `part` bytes (nothing kept)."""
+    """Bytes/s of reading every file with `threads` parallel preads of `part` bytes (nothing kept): the C reader
+    tools/read_ceiling.c (no GIL in the way: the Python form under-measured 10,000 small files), else Python."""
+    exe = _read_ceiling_bin()
+    if exe:
+        import subprocess
+        r = subprocess.run([exe, str(threads), str(part)], input="\n".join(paths), capture_output=True, text=True,
+                           check=True)
+        rec = json.loads(r.stdout)
+        return rec["bytes"] / rec["seconds"]
     jobs = []
     for p in paths:
         n = os.path.getsize(p)
@@ -186,28 +212,32 @@ def main():
                 def gets_only(threads=_STORAGE_THREADS):
                     with ThreadPoolExecutor(threads) as ex:
                         return sum(_chunked_map(ex, lambda i: st4.get(i * L, _plen(i, info)) is not None, P, threads))
-                if cold:
-                    drop_cache(paths)
+                res = drop_cache(paths) if cold else fsutil.resident(paths)
+                if cold and res > COLD_MAX_RESIDENT:
+                    emit({"layout": name, "cache": "cold", "refused": True, "resident_after_drop": round(res, 4),
+                          "why": "the page cache kept the files after fsync + POSIX_FADV_DONTNEED (e.g. a tmpfs or "
+                                 "overlay directory): a 'cold' leg here would measure memory, not the disk"})
+                    break
                 el, n_ok = timed(gets_only, 1 if cold else 2)
                 ngets = fs4.gets
-                emit({"layout": name, "cache": "cold" if cold else "warm",
+                emit({"layout": name, "cache": "cold" if cold else "warm", "resident": round(res, 4),
                       "path": f"Storage(fs).get only, {_STORAGE_THREADS} threads",
                       "best_s": round(el, 3), "gbps": round(total / el / 1e9, 2), "us_per_get":
                       round(el / max(1, ngets / (1 if cold else 2)) * 1e6, 1),
                       "gets_per_piece": round(ngets / (1 if cold else 2) / P, 3)})
                 if cold:
-                    drop_cache(paths)
+                    res = drop_cache(paths)
                     ceil = read_ceiling(paths)
                     emit({"layout": name, "cache": "cold", "read_ceiling_gbps": round(ceil / 1e9, 2),
-                          "how": "16 threads x 4 MiB preads of every file after fadvise DONTNEED"})
+                          "resident": round(res, 4),
+                          "how": "tools/read_ceiling.c: 16 threads x 4 MiB preads of every file after the drop"})
                 for leg, fn, counter in legs:
-                    if cold:
-                        drop_cache(paths)
+                    res = drop_cache(paths) if cold else fsutil.resident(paths)
                     if counter is not None:
                         counter.reset()
                     reps = 1 if cold else (3 if leg == "verify_files" else 2)
                     el, bf = timed(fn, reps)
-                    rec = {"layout": name, "cache": "cold" if cold else "warm", "path": leg,
+                    rec = {"layout": name, "cache": "cold" if cold else "warm", "path": leg, "resident": round(res, 4),
                            "best_s": round(el, 3), "gbps": round(total / el / 1e9, 2),
                            "exact": bytes(bf) == expect}
                     if counter is not None:

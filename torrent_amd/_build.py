@@ -24,6 +24,20 @@ CXX = os.environ.get("CXX", "g++")
 ARCH = os.environ.get("TV_OFFLOAD_ARCH", "gfx950")
 
 
+def source_id() -> str:
+    """16 hex digits of SHA-256 over every source the library is built from (csrc/*.hip / *.h / *.cpp, the export
+    map, include/torrent_verify.h, the asm generator).  Compiled into the library (TV_BUILD_ID=..., read back by
+    _native.build_id()), so a measurement tied to it (profiles/traffic_*.json) applies to that build only."""
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".h", ".cpp", ".map")))
+    for f in [os.path.join(CSRC, f) for f in files] + [os.path.join(ROOT, "include", "torrent_verify.h"),
+                                                         os.path.join(ROOT, "tools", "gen_sha1_asm.py")]:
+        h.update(os.path.relpath(f, ROOT).encode() + b"\0")
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
 def _newer(target: str, deps) -> bool:
     if not os.path.exists(target):
         return True
@@ -46,10 +60,11 @@ def build(force: bool = False, verbose: bool = False) -> str:
         return LIB
     objs = []
     cmds = []
+    sid = source_id()
     for s in srcs:
         o = os.path.join(CSRC, os.path.basename(s) + ".o")
         cmds.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-                     "-I", os.path.join(ROOT, "include"), "-c", s, "-o", o])
+                     f"-DTV_SOURCE_ID=\"{sid}\"", "-I", os.path.join(ROOT, "include"), "-c", s, "-o", o])
         objs.append(o)
     procs = []
     for cmd in cmds:                       # (the translation units compile side by side)

@@ -71,6 +71,18 @@ KERNEL_AUTO, KERNEL_LANE, KERNEL_SPLIT, KERNEL_TWIN = 0, 1, 2, 4   # (3 was MIX,
 _u64, _i64, _int, _p = ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p
 
 
+def build_id(path: Optional[str] = None) -> Optional[str]:
+    """The source id compiled into the library file (torrent_amd/_build.py source_id; the TV_BUILD_ID= marker), or
+    None for a library built without one."""
+    import re
+    try:
+        with open(path or LIB_PATH, "rb") as f:
+            m = re.search(rb"TV_BUILD_ID=([0-9a-f]{16})", f.read())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
+
+
 class StreamReq(ctypes.Structure):
     """tv_stream_req (include/torrent_verify.h): rows [piece, piece+rows) x bytes [offset, offset+width)."""
     _fields_ = [("piece", _u64), ("rows", _u64), ("offset", _u64), ("width", _u64), ("slot", _p), ("seq", _u64)]

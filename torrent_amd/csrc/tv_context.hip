@@ -8,6 +8,13 @@
 
 using namespace tvi;
 
+#ifndef TV_SOURCE_ID
+#define TV_SOURCE_ID "unknown"
+#endif
+// The build's source id (torrent_amd/_build.py source_id), findable in the binary: _native.build_id() reads it, and
+// measurements tied to a build (profiles/traffic_*.json) carry it.
+extern "C" __attribute__((used, visibility("hidden"))) const char tv_build_id_marker[] = "TV_BUILD_ID=" TV_SOURCE_ID;
+
 extern "C" {
 
 

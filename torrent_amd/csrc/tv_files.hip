@@ -315,6 +315,56 @@ void read_segments(Pool& pool, const std::vector<SmallSeg>& segs, size_t lo, siz
     });
 }
 
+// Short segments (one part each, in linear order) packed into lane `lane`'s 64 MiB ring slots at their linear
+// offsets' alignment mod 4, read by the lane's pool (open, pread, close each: read_segments), one DMA per run of
+// readable linear-contiguous segments while the next slot is read.  A failed read sets status[k] = TV_ERR_IO.
+int stage_small(tv_ctx* c, std::vector<SmallSeg>& small, int lane, int threads, const char* const* paths,
+                int32_t* status, std::string* first_err, std::mutex* err_mu) {
+    int rc = TV_OK;
+    DrainGuard drain(c, lane, /*sync_compute=*/false);
+    size_t i = 0;
+    while (i < small.size()) {
+        size_t j = i;
+        uint64_t used = 0;
+        while (j < small.size()) {
+            // each byte sits in the slot at its linear offset's alignment mod 4 (dword-aligned DMA)
+            const uint64_t at = used + ((small[j].linear - used) & 3);
+            if (at + small[j].len > kRingSlotBytes) break;
+            small[j].packed = at;
+            used = at + small[j].len;
+            j++;
+        }
+        SlotLease slot(c, lane);  // lent until every copy out of it is queued
+        {
+            FileClock t(c, TV_FILE_PHASE_WAIT);
+            rc = slot.take();
+            if (rc) return rc;
+        }
+        {
+            FileClock t(c, TV_FILE_PHASE_SMALL);
+            read_segments(c->pool[lane], small, i, j, paths, slot.ptr(), status, threads, c->open_rw, first_err, err_mu);
+        }
+        FileClock t(c, TV_FILE_PHASE_QUEUE);
+        for (size_t q = i; q < j;) {  // one copy per run of readable, linear-contiguous segments
+            if (__atomic_load_n(&status[small[q].k], __ATOMIC_RELAXED) != TV_OK) { q++; continue; }
+            size_t r = q + 1;
+            while (r < j && __atomic_load_n(&status[small[r].k], __ATOMIC_RELAXED) == TV_OK &&
+                   small[r].linear == small[r - 1].linear + small[r - 1].len)
+                r++;
+            const uint64_t lin_a = small[q].linear, lin_b = small[r - 1].linear + small[r - 1].len;
+            rc = stage_range(c, lin_a, lin_b, slot.ptr() + small[q].packed, lin_a, true, lane, /*src_in_ring=*/true);
+            if (rc) return rc;
+            q = r;
+        }
+        rc = slot.release();
+        if (rc) return rc;
+        i = j;
+    }
+    FileClock t(c, TV_FILE_PHASE_DRAIN);
+    TV_HIP(c, hipStreamSynchronize(lane_stream(c, lane)));
+    return TV_OK;
+}
+
 // Mark the shard pieces holding linear bytes [a, b) unreadable (tv_verify reports them 0).
 void mark_bad(tv_ctx* c, uint64_t a, uint64_t b) {
     const uint64_t lo = c->first * c->L;
@@ -459,11 +509,27 @@ int stage_files_core(tv_ctx* c, uint64_t n, const char* const* paths, const uint
             small_bytes += b - a;
         }
     }
-    // in linear order, each unit to the lane with fewer bytes so far (lane 0 also carries the short segments)
+    // Short segments: with two lanes, the first half (by bytes, in linear order) on lane 0 and the second on lane 1
+    // once there are at least two slots of them, so one lane's reads overlap the other's DMA and wait (each lane reads
+    // a slot, queues its DMA, and waits for a free slot in turn)
+    std::vector<SmallSeg> lane_small[2];
+    {
+        std::stable_sort(small.begin(), small.end(), [](const SmallSeg& x, const SmallSeg& y) { return x.linear < y.linear; });
+        const bool split = c->file_concurrent && small_bytes >= 2 * (uint64_t)kRingSlotBytes;
+        uint64_t acc = 0;
+        for (const SmallSeg& sg : small) {
+            lane_small[split && acc >= small_bytes / 2 ? 1 : 0].push_back(sg);
+            acc += sg.len;
+        }
+    }
+    uint64_t small_load[2] = {0, 0};
+    for (int l = 0; l < 2; l++)
+        for (const SmallSeg& sg : lane_small[l]) small_load[l] += sg.len;
+    // in linear order, each unit to the lane with fewer bytes so far
     std::vector<FileUnit> lane_units[2];
     {
         std::stable_sort(longs.begin(), longs.end(), [](const FileUnit& x, const FileUnit& y) { return x.a < y.a; });
-        uint64_t load[2] = {small_bytes, 0};
+        uint64_t load[2] = {small_load[0], small_load[1]};
         for (const FileUnit& u : longs) {
             const int l = (c->file_concurrent && load[1] < load[0]) ? 1 : 0;
             lane_units[l].push_back(u);
@@ -471,7 +537,7 @@ int stage_files_core(tv_ctx* c, uint64_t n, const char* const* paths, const uint
         }
     }
     // reader threads: the context's TV_OPT_FILE_THREADS shared by the lanes that read
-    const int lanes = lane_units[1].empty() ? 1 : 2;
+    const int lanes = (lane_units[1].empty() && lane_small[1].empty()) ? 1 : 2;
     const int threads_per_lane = std::max(1, c->file_threads / lanes);
     int helper_rc = TV_OK;
     std::thread helper;
@@ -481,7 +547,9 @@ int stage_files_core(tv_ctx* c, uint64_t n, const char* const* paths, const uint
             if (t.joinable()) t.join();
         }
     } joiner{helper};  // every exit joins the helper before the ctx lock is released
-    if (!lane_units[1].empty()) {
+    std::string first_err = zero_err;
+    std::mutex err_mu;
+    if (lanes == 2) {
         helper = std::thread([&]() {
             pin_thread(numa_cpus(c));  // next to its ring and the GPU (TV_OPT_NUMA_BIND)
             if (hipSetDevice(c->device) != hipSuccess) {
@@ -489,46 +557,17 @@ int stage_files_core(tv_ctx* c, uint64_t n, const char* const* paths, const uint
                 return;
             }
             helper_rc = stage_units(c, lane_units[1], 1, threads_per_lane, status_out);
+            if (!helper_rc && !lane_small[1].empty())
+                helper_rc = stage_small(c, lane_small[1], 1, threads_per_lane, paths, status_out, &first_err, &err_mu);
         });
     }
     rc = stage_units(c, lane_units[0], 0, lanes == 2 ? threads_per_lane : c->file_threads, status_out);
     if (rc) return rc;
-    std::string first_err = zero_err;
-    std::mutex err_mu;
-    DrainGuard drain(c, 0, /*sync_compute=*/false);
-    size_t i = 0;
-    while (i < small.size()) {
-        size_t j = i;
-        uint64_t used = 0;
-        while (j < small.size()) {
-            // each byte sits in the slot at its linear offset's alignment mod 4 (dword-aligned DMA)
-            const uint64_t at = used + ((small[j].linear - used) & 3);
-            if (at + small[j].len > kRingSlotBytes) break;
-            small[j].packed = at;
-            used = at + small[j].len;
-            j++;
-        }
-        SlotLease slot(c, 0);  // lent until every copy out of it is queued
-        rc = slot.take();
+    if (!lane_small[0].empty()) {
+        rc = stage_small(c, lane_small[0], 0, lanes == 2 ? threads_per_lane : c->file_threads, paths, status_out,
+                         &first_err, &err_mu);
         if (rc) return rc;
-        FileClock small_clock(c, TV_FILE_PHASE_SMALL);
-        read_segments(c->pool[0], small, i, j, paths, slot.ptr(), status_out,
-                      lanes == 2 ? threads_per_lane : c->file_threads, c->open_rw, &first_err, &err_mu);
-        for (size_t q = i; q < j;) {  // one copy per run of readable, linear-contiguous segments
-            if (status_out[small[q].k] != TV_OK) { q++; continue; }
-            size_t r = q + 1;
-            while (r < j && status_out[small[r].k] == TV_OK && small[r].linear == small[r - 1].linear + small[r - 1].len)
-                r++;
-            const uint64_t lin_a = small[q].linear, lin_b = small[r - 1].linear + small[r - 1].len;
-            rc = stage_range(c, lin_a, lin_b, slot.ptr() + small[q].packed, lin_a, true, 0, /*src_in_ring=*/true);
-            if (rc) return rc;
-            q = r;
-        }
-        rc = slot.release();
-        if (rc) return rc;
-        i = j;
     }
-    TV_HIP(c, hipStreamSynchronize(c->copy_stream));
     if (helper.joinable()) helper.join();
     if (helper_rc) return helper_rc;
     // the failed segments: their readable prefixes staged again, the rest of their pieces marked unreadable
