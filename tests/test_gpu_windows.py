@@ -304,3 +304,43 @@ def test_unstaged_windows_never_verify_against_zero_digests(native, oracle):
         ctx.stage(0, payload)                        # a new pass stages everything: the crafted pieces now fail
         want = [0 if i in (20, 21, 35) else 1 for i in range(P)]
         assert _bits(ctx.verify(), P) == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", ["ascending", "shuffled"])
+def test_stage_many_packs_small_buffers(native, oracle, order):
+    """tv_stage_many packs short pageable buffers into ring slots (many per slot, one DMA per run of adjacent
+    bytes): ~150 MiB cut into buffers of 1 B .. 900 KiB at odd addresses, sub-piece and across piece boundaries,
+    with a few 2-3 MiB buffers (staged unpacked) among them, handed over in one call in ascending or shuffled
+    order; every piece verifies (bitfield = hashlib's), and the corrupted ones do not."""
+    from torrent_amd import _native as N
+    L = 1 << 16
+    total = 150 * (1 << 20) + 4321
+    P = -(-total // L)
+    payload = bytes(oracle.synth_fill(91, 0, total))
+    digests = bytearray(oracle.hash_pieces(bytearray(payload), total, L, P))
+    for i in (0, 777, P - 1):
+        digests[20 * i + 3] ^= 0x40
+    rng = random.Random(5)
+    cuts, o = [], 0
+    while o < total:
+        n = rng.choice([rng.randrange(1, 64), rng.randrange(64, 70000), rng.randrange(70000, 900 * 1024),
+                        rng.randrange(2 << 20, 3 << 20) if rng.random() < 0.05 else rng.randrange(1, 5000)])
+        n = min(n, total - o)
+        cuts.append((o, n))
+        o += n
+    if order == "shuffled":
+        rng.shuffle(cuts)
+    keep = []
+    parts = []
+    for off, n in cuts:
+        b = bytearray(b"\x00" * (1 + off % 3) + payload[off:off + n])
+        keep.append(b)
+        parts.append((off, memoryview(b)[1 + off % 3:]))
+    with N.Context(0) as ctx:
+        ctx.set_layout(total, L, P)
+        ctx.set_digests(bytes(digests))
+        ctx.stage_many(parts)
+        bf = ctx.verify()
+    want = [0 if i in (0, 777, P - 1) else 1 for i in range(P)]
+    assert _bits(bf, P) == want

@@ -6,6 +6,70 @@
 
 using namespace tvi;
 
+namespace {
+
+// A caller buffer of tv_stage_many packed into a ring slot: LINEAR [a, b) (inside the shard) from src, at slot
+// offset `packed` (which has a's alignment mod 4: the DMA out of the slot is dword-aligned).
+struct PackedPart {
+    uint64_t a, b;
+    const uint8_t* src;
+    uint64_t packed;
+};
+
+// Buffers shorter than this are packed into ring slots without asking whether they are page-locked (a
+// hipPointerGetAttributes per buffer costs microseconds, more than copying a small buffer); longer ones are
+// checked, and DMA'd directly when they are.
+constexpr uint64_t kPackMax = 1ull << 20;
+
+// Stage LINEAR [a, b) from `src` (in a lane-0 ring slot), window by window on a windowed layout (as stage_locked).
+int stage_ring_run(tv_ctx* c, uint64_t a, uint64_t b, const uint8_t* src) {
+    if (!c->win) return stage_range(c, a, b, src, a, true, 0, /*src_in_ring=*/true);
+    for (uint64_t pos = a; pos < b;) {
+        const uint64_t w = win_of(c, pos / c->L - c->first);
+        int rc = win_enter(c, w);
+        if (rc) return rc;
+        uint64_t wa, wb;
+        clip_to_shard(c, pos, b - pos, &wa, &wb);
+        if (wa < wb) {
+            rc = stage_range(c, wa, wb, src, a, true, 0, /*src_in_ring=*/true);
+            if (rc) return rc;
+        }
+        pos = win_end_linear(c, w);
+    }
+    return TV_OK;
+}
+
+// Copy the packed parts into one lane-0 ring slot on the pool's threads (a task per part, long parts in 4 MiB
+// pieces), then one DMA per run of linear-contiguous parts.
+int flush_packed(tv_ctx* c, std::vector<PackedPart>& parts) {
+    if (parts.empty()) return TV_OK;
+    SlotLease slot(c, 0);  // lent until every copy out of it is queued
+    int rc = slot.take();
+    if (rc) return rc;
+    uint8_t* base = slot.ptr();
+    constexpr uint64_t kPart = 4ull << 20;
+    std::vector<std::pair<uint32_t, uint64_t>> tasks;  // (part, offset inside it)
+    for (uint32_t q = 0; q < parts.size(); q++)
+        for (uint64_t o = 0; o < parts[q].b - parts[q].a; o += kPart) tasks.emplace_back(q, o);
+    c->pool[0].run(c->file_threads, tasks.size(), [&](uint64_t t) {
+        const PackedPart& pp = parts[tasks[t].first];
+        const uint64_t o = tasks[t].second, n = std::min(kPart, pp.b - pp.a - o);
+        tv_copy_host(base + pp.packed + o, pp.src + o, n);
+    });
+    for (size_t q = 0; q < parts.size();) {
+        size_t r = q + 1;
+        while (r < parts.size() && parts[r].a == parts[r - 1].b && parts[r].packed == parts[r - 1].packed + (parts[r - 1].b - parts[r - 1].a))
+            r++;
+        rc = stage_ring_run(c, parts[q].a, parts[r - 1].b, base + parts[q].packed);
+        if (rc) return rc;
+        q = r;
+    }
+    parts.clear();
+    return slot.release();
+}
+
+}  // namespace
+
 extern "C" {
 
 
@@ -42,11 +106,35 @@ int tv_stage_many(tv_ctx* c, uint64_t n, const uint64_t* linear_offsets, const u
     if (c->count == 0) return TV_OK;
     TV_HIP(c, hipSetDevice(c->device));
     DrainGuard drain(c, 0, /*sync_compute=*/false);  // no DMA reads a caller buffer after the call
+    // Short pageable buffers (a torrent's small files, Storage.get results) are packed into ring slots, many per slot
+    // and copied by the pool, one DMA per run of adjacent bytes: one slot round trip per buffer made 10,000 small
+    // buffers a 6 GB/s path.  Long or page-locked ones go as tv_stage sends them.  Caller order is kept.
+    std::vector<PackedPart> parts;
+    uint64_t used = 0;
     for (uint64_t k = 0; k < n; k++) {
         if (!lens[k]) continue;
-        rc = stage_locked(c, linear_offsets[k], srcs[k], lens[k]);
-        if (rc) return rc;
+        uint64_t a, b;
+        clip_to_whole_shard(c, linear_offsets[k], lens[k], &a, &b);
+        if (a >= b) continue;
+        if (b - a >= kPackMax) {   // (stage_locked DMAs a page-locked one directly, bounces a pageable one)
+            rc = flush_packed(c, parts);
+            if (!rc) rc = stage_locked(c, linear_offsets[k], srcs[k], lens[k]);
+            if (rc) return rc;
+            used = 0;
+            continue;
+        }
+        uint64_t at = used + ((a - used) & 3);
+        if (at + (b - a) > kRingSlotBytes) {
+            rc = flush_packed(c, parts);
+            if (rc) return rc;
+            used = 0;
+            at = a & 3;
+        }
+        parts.push_back({a, b, srcs[k] + (a - linear_offsets[k]), at});
+        used = at + (b - a);
     }
+    rc = flush_packed(c, parts);
+    if (rc) return rc;
     TV_HIP(c, hipStreamSynchronize(c->copy_stream));
     for (uint64_t k = 0; k < n; k++)
         if (lens[k]) clear_staged(c, linear_offsets[k], lens[k]);
