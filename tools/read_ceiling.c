@@ -3,7 +3,9 @@
  * dropped.  Prints {"bytes": B, "seconds": S, "gbps": G}.  The storage benches (tools/storage_paths_bench.py) run it
  * after dropping the files from the page cache, so the cold legs have a ceiling measured without Python in the
  * way (the round-4 Python reader under-measured it for 10,000 small files).
- * build: gcc -O2 -pthread tools/read_ceiling.c -o read_ceiling;  usage: read_ceiling THREADS PART_BYTES < paths */
+ * A third argument "direct" opens the files O_DIRECT (reads bypass the page cache; the length of each request is
+ * rounded up to 4 KiB, the file end returns short).
+ * build: gcc -O2 -pthread tools/read_ceiling.c -o read_ceiling;  usage: read_ceiling THREADS PART_BYTES [direct] < paths */
 #define _GNU_SOURCE
 #include <fcntl.h>
 #include <pthread.h>
@@ -22,6 +24,7 @@ static uint64_t nfiles, part, ntasks;
 static uint64_t* task_file;   /* task -> file; offset = (task - first task of the file) * part */
 static uint64_t* first_task;
 static atomic_uint_fast64_t next_task, total_bytes;
+static int direct;
 
 static void* worker(void* arg) {
     (void)arg;
@@ -32,11 +35,14 @@ static void* worker(void* arg) {
         file_t* f = &files[task_file[t]];
         uint64_t off = (t - first_task[task_file[t]]) * part, n = f->size - off < part ? f->size - off : part;
         while (n) {
-            const ssize_t got = pread(f->fd, buf, n, (off_t)off);
+            const uint64_t ask = direct ? (n + 4095) / 4096 * 4096 : n;
+            const ssize_t got = pread(f->fd, buf, ask, (off_t)off);
             if (got <= 0) break;
-            atomic_fetch_add(&total_bytes, (uint64_t)got);
-            off += (uint64_t)got;
-            n -= (uint64_t)got;
+            const uint64_t g = (uint64_t)got < n ? (uint64_t)got : n;
+            atomic_fetch_add(&total_bytes, g);
+            off += g;
+            n -= g;
+            if ((uint64_t)got < ask && n) break;
         }
     }
     free(buf);
@@ -47,6 +53,7 @@ int main(int argc, char** argv) {
     if (argc < 3) return 2;
     const int threads = atoi(argv[1]);
     part = strtoull(argv[2], NULL, 10);
+    direct = argc > 3 && strcmp(argv[3], "direct") == 0;
     uint64_t cap = 1024;
     files = malloc(cap * sizeof(file_t));
     char line[8192];
@@ -62,7 +69,7 @@ int main(int argc, char** argv) {
     first_task = malloc((nfiles + 1) * sizeof(uint64_t));
     for (uint64_t k = 0; k < nfiles; k++) {
         struct stat st;
-        files[k].fd = open(files[k].path, O_RDONLY);
+        files[k].fd = open(files[k].path, O_RDONLY | (direct ? O_DIRECT : 0));
         files[k].size = (files[k].fd >= 0 && fstat(files[k].fd, &st) == 0) ? (uint64_t)st.st_size : 0;
         first_task[k] = ntasks;
         ntasks += (files[k].size + part - 1) / part;
@@ -76,7 +83,8 @@ int main(int argc, char** argv) {
     clock_gettime(CLOCK_MONOTONIC, &t1);
     const double s = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
     const uint64_t b = atomic_load(&total_bytes);
-    printf("{\"bytes\": %llu, \"seconds\": %.4f, \"gbps\": %.3f, \"files\": %llu, \"threads\": %d, \"part\": %llu}\n",
-           (unsigned long long)b, s, (double)b / s / 1e9, (unsigned long long)nfiles, threads, (unsigned long long)part);
+    printf("{\"bytes\": %llu, \"seconds\": %.4f, \"gbps\": %.3f, \"files\": %llu, \"threads\": %d, \"part\": %llu, "
+           "\"direct\": %d}\n", (unsigned long long)b, s, (double)b / s / 1e9, (unsigned long long)nfiles, threads,
+           (unsigned long long)part, direct);
     return 0;
 }

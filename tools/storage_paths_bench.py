@@ -86,16 +86,18 @@ def _read_ceiling_bin():
     return _RC_BIN or None
 
 
-def read_ceiling(paths, threads=16, part=4 * MiB):
+def read_ceiling(paths, threads=16, part=4 * MiB, direct=False):
     """Bytes/s of reading every file with `threads` parallel preads of `part` bytes (nothing kept): the C reader
     tools/read_ceiling.c (no GIL in the way: the Python form under-measured 10,000 small files), else Python."""
     exe = _read_ceiling_bin()
     if exe:
         import subprocess
-        r = subprocess.run([exe, str(threads), str(part)], input="\n".join(paths), capture_output=True, text=True,
-                           check=True)
+        r = subprocess.run([exe, str(threads), str(part)] + (["direct"] if direct else []), input="\n".join(paths),
+                           capture_output=True, text=True, check=True)
         rec = json.loads(r.stdout)
         return rec["bytes"] / rec["seconds"]
+    if direct:
+        return None
     jobs = []
     for p in paths:
         n = os.path.getsize(p)
@@ -231,6 +233,14 @@ def main():
                     emit({"layout": name, "cache": "cold", "read_ceiling_gbps": round(ceil / 1e9, 2),
                           "resident": round(res, 4),
                           "how": "tools/read_ceiling.c: 16 threads x 4 MiB preads of every file after the drop"})
+                    res = drop_cache(paths)
+                    try:
+                        dceil = read_ceiling(paths, direct=True)
+                    except Exception as exc:   # (a filesystem without O_DIRECT)
+                        dceil, why = None, str(exc)[:200]
+                    emit({"layout": name, "cache": "cold", "read_ceiling_direct_gbps": round(dceil / 1e9, 2) if dceil
+                          else None, "resident": round(res, 4),
+                          "how": "tools/read_ceiling.c direct: the same reads with O_DIRECT (no page cache)"})
                 for leg, fn, counter in legs:
                     res = drop_cache(paths) if cold else fsutil.resident(paths)
                     if counter is not None:
@@ -243,6 +253,13 @@ def main():
                     if counter is not None:
                         rec["gets_per_piece"] = round(counter.gets / reps / P, 3)
                     emit(rec)
+                if cold:
+                    # the same ceiling after the legs: a storage layer below the page cache (the virtual disk's own
+                    # cache) that warms with every pass shows here as a higher figure than before the legs
+                    res = drop_cache(paths)
+                    ceil2 = read_ceiling(paths)
+                    emit({"layout": name, "cache": "cold", "read_ceiling_after_legs_gbps": round(ceil2 / 1e9, 2),
+                          "resident": round(res, 4), "how": "tools/read_ceiling.c after the cold legs, after a drop"})
         finally:
             os.chdir(cwd)
         for p in paths:

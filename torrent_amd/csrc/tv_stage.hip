@@ -19,7 +19,7 @@ struct PackedPart {
 // Buffers shorter than this are packed into ring slots without asking whether they are page-locked (a
 // hipPointerGetAttributes per buffer costs microseconds, more than copying a small buffer); longer ones are
 // checked, and DMA'd directly when they are.
-constexpr uint64_t kPackMax = 1ull << 20;
+constexpr uint64_t kPackMax = 16ull << 20;
 
 // Stage LINEAR [a, b) from `src` (in a lane-0 ring slot), window by window on a windowed layout (as stage_locked).
 int stage_ring_run(tv_ctx* c, uint64_t a, uint64_t b, const uint8_t* src) {
