@@ -673,7 +673,9 @@ def main() -> int:
     cfg4_digests = None
     if ws == 1 and workload == "cfg2" and not a.no_cfg3:
         try:
-            legs["cfg3"] = cfg3_leg(device, a.leg_steps, 2, a.kernel)
+            # (3 ms launches: 20 warm-up steps bring the shader clock up from the layout build's idle, and 20 timed
+            # steps average over its last ramp; rocprofv3 showed 5 timed steps still speeding up, profiles/r05/check2)
+            legs["cfg3"] = cfg3_leg(device, max(20, a.leg_steps), 20, a.kernel)
         except Exception as exc:
             legs["cfg3"] = {"skipped": f"{type(exc).__name__}: {exc}"}
     if ws == 1 and workload == "cfg2" and not a.no_saturating:

@@ -1,0 +1,76 @@
+"""Cold-cache staging from files: long segments whose bytes are not in the page cache are read
+with O_DIRECT into the pinned ring (TV_OPT_FILE_ODIRECT; 4 KiB-rounded requests, the bytes at slot + fo % 4096).
+Checked on files evicted from the page cache (tools/fsutil.py: fsync + DONTNEED, re-checked with mincore): sizes
+that are not multiples of 4 KiB, file offsets that do and do not agree with the linear offsets mod 4 (the latter
+read buffered), a short last piece, corrupted pieces, and a file shorter than its segment -- every bitfield equal
+to Storage(fs_storage).get + hashlib's, with O_DIRECT on and off."""
+import hashlib
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(bf, n):
+    return [(bf[i >> 3] >> (7 - (i & 7))) & 1 for i in range(n)]
+
+
+@pytest.mark.parametrize("odirect", [1, 0])
+def test_cold_files_exact(native, oracle, tmp_path, odirect):
+    import fsutil
+    from torrent_amd import FileInfo, Storage, make_info, verify_files
+    from torrent_amd.storage import fs_storage
+    from torrent_amd.verify import _context
+    MiB = 1 << 20
+    L = MiB
+    sizes = [40 * MiB + 4093, 37 * MiB + 2, 50 * MiB + 12345, 33 * MiB]   # (file 1 starts at 40 MiB + 4093: not 0 mod 4)
+    total = sum(sizes)
+    P = -(-total // L)
+    payload = bytearray(oracle.synth_fill(55, 0, total))
+    digests = bytearray(b"".join(hashlib.sha1(bytes(payload[i * L:min(total, (i + 1) * L)])).digest() for i in range(P)))
+    for i in (3, 77, P - 1):
+        digests[20 * i + 1] ^= 0x20
+    files, paths, o = [], [], 0
+    for k, n in enumerate(sizes):
+        p = tmp_path / f"f{k}.bin"
+        data = payload[o:o + n]
+        if k == 2:
+            data = data[:n - 5 * MiB]          # shorter than its segment: its tail pieces read as null
+        p.write_bytes(bytes(data))
+        files.append(FileInfo(n, [f"f{k}.bin"]))
+        paths.append(str(p))
+        o += n
+    info = make_info(L, bytes(digests), "cold", files=files, length=total)
+    want_st = Storage(fs_storage, info, str(tmp_path))
+    want = [0] * P
+    for i in range(P):
+        n = min(L, total - i * L)
+        b = want_st.get(i * L, n)
+        want[i] = int(b is not None and hashlib.sha1(b).digest() == bytes(digests[20 * i:20 * i + 20]))
+    assert fsutil.drop_cache(paths) <= 0.01
+    with _context(0) as ctx:
+        ctx.set_option(native.TV_OPT_FILE_ODIRECT, odirect)
+        ctx._reset_file_clock()
+    try:
+        cwd = os.getcwd()
+        os.chdir(str(tmp_path))
+        try:
+            bf = verify_files(info, str(tmp_path))
+        finally:
+            os.chdir(cwd)
+        with _context(0) as ctx:
+            clock = ctx._file_clock()
+    finally:
+        with _context(0) as ctx:
+            ctx.set_option(native.TV_OPT_FILE_ODIRECT, 1)
+    assert _bits(bf, P) == want
+    if odirect:
+        assert clock["bytes_odirect"] > 0, clock      # (the cold chunks whose offsets agree mod 4 went O_DIRECT)
+        assert clock["bytes_odirect"] < clock["bytes_read"]   # (and the others buffered)
+    else:
+        assert clock["bytes_odirect"] == 0

@@ -121,6 +121,19 @@ def read_ceiling(paths, threads=16, part=4 * MiB, direct=False):
     return total / (time.perf_counter() - t0)
 
 
+def _buffered(fn):
+    """fn() with the cached context's cold reads buffered (TV_OPT_FILE_ODIRECT = 0), then back to the default."""
+    from torrent_amd import _native
+    from torrent_amd.verify import _context
+    with _context(0) as ctx:
+        ctx.set_option(_native.TV_OPT_FILE_ODIRECT, 0)
+    try:
+        return fn()
+    finally:
+        with _context(0) as ctx:
+            ctx.set_option(_native.TV_OPT_FILE_ODIRECT, 1)
+
+
 def write_layout(name, d):
     """-> (info, expected bitfield bytes, file paths)."""
     os.makedirs(d, exist_ok=True)
@@ -194,6 +207,9 @@ def main():
         try:
             for cold in (False, True):
                 legs = [("verify_files", lambda: verify_files(info, root), None)]
+                if cold:   # the A/B of the cold reads: O_DIRECT (the default) against the page cache's reads
+                    legs.append(("verify_files, buffered reads (TV_OPT_FILE_ODIRECT=0)", lambda: _buffered(
+                        lambda: verify_files(info, root)), None))
                 fs = CountingFs()
                 st_ = Storage(fs, info, root)
                 legs.append(("verify_pieces(Storage(fs))", lambda: verify_pieces(info, st_), fs))

@@ -45,10 +45,11 @@ TV_OPT_TWIN_PACK = 12
 TV_OPT_TWIN_FILL_READS = 14
 TV_OPT_NUMA_BIND = 15
 TV_OPT_LANE_PAIRS = 21
+TV_OPT_FILE_ODIRECT = 22
 TV_OPT_FILE_CLOCK_RESET = 100
 TV_COUNTER_FILE_CLOCK = 100
 TV_FILE_PHASES = ("open", "map", "populate", "register", "read", "wait", "queue", "release", "drain", "small", "call",
-                  "bytes_direct", "bytes_read")   # TV_FILE_PHASE_* / TV_FILE_BYTES_* in order
+                  "bytes_direct", "bytes_read", "bytes_odirect")   # TV_FILE_PHASE_* / TV_FILE_BYTES_* in order
 
 TV_COUNTER_PAYLOAD_ALLOCS = 1
 TV_COUNTER_DEVICE_ALLOCS = 2

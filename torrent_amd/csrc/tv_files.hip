@@ -4,6 +4,7 @@
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <cerrno>
@@ -40,9 +41,11 @@ double resident_fraction(void* m, uint64_t n, uint64_t page) {
 }
 
 // Read file bytes [fo, fo + n) into dst with parallel preads on the lane's persistent workers (`threads` of
-// them; parts of 1-4 MiB, at least two per thread so the slowest part ends the slot early).  Returns 0 or an errno
-// value (EIO for a short read).  The round-1..4 form spawned `threads` std::threads per 64 MiB slot.
-int pread_pool(Pool& pool, int threads, int fd, uint8_t* dst, uint64_t fo, uint64_t n) {
+// them; parts of 1-4 MiB, at least two per thread so the slowest part ends the slot early).  The first `need`
+// bytes must all be read (n - need: an O_DIRECT read's rounding past the end of the file, which may come back
+// short).  Returns 0 or an errno value (EIO for a short read).  The round-1..4 form spawned `threads` std::threads
+// per 64 MiB slot.
+int pread_pool(Pool& pool, int threads, int fd, uint8_t* dst, uint64_t fo, uint64_t n, uint64_t need) {
     threads = std::max(1, threads);
     uint64_t part = n / (2 * (uint64_t)threads);
     part = std::min<uint64_t>(4ull << 20, std::max<uint64_t>(1ull << 20, (part + 65535) / 65536 * 65536));
@@ -55,6 +58,7 @@ int pread_pool(Pool& pool, int threads, int fd, uint8_t* dst, uint64_t fo, uint6
             const ssize_t got = pread(fd, dst + o, e - o, (off_t)(fo + o));
             if (got < 0 && errno == EINTR) continue;
             if (got <= 0) {
+                if (got == 0 && o >= need) return;  // the end of the file, past the bytes asked for
                 int expect = 0;
                 err.compare_exchange_strong(expect, got < 0 ? errno : EIO);
                 return;
@@ -63,6 +67,25 @@ int pread_pool(Pool& pool, int threads, int fd, uint8_t* dst, uint64_t fo, uint6
         }
     });
     return err.load();
+}
+
+#ifndef SYS_cachestat
+#define SYS_cachestat 451  // Linux >= 6.5 (x86-64); older kernels: ENOSYS, and the mincore path below
+#endif
+
+// Fraction of file bytes [fo, fo + n) in the page cache: cachestat(2) where the kernel has it, else a mapping's
+// mincore; -1 when neither can tell.
+double cached_fraction(int fd, uint64_t fo, uint64_t n) {
+    if (n == 0) return 1.0;
+    const uint64_t page = (uint64_t)sysconf(_SC_PAGESIZE);
+    struct { uint64_t off, len; } range{fo / page * page, (fo % page + n + page - 1) / page * page};
+    struct { uint64_t nr_cache, nr_dirty, nr_writeback, nr_evicted, nr_recently_evicted; } cs{};
+    if (syscall(SYS_cachestat, fd, &range, &cs, 0) == 0) return (double)cs.nr_cache * page / (double)range.len;
+    void* m = mmap(nullptr, range.len, PROT_READ, MAP_SHARED, fd, (off_t)range.off);
+    if (m == MAP_FAILED) return -1.0;
+    const double f = resident_fraction(m, range.len, page);
+    munmap(m, range.len);
+    return f;
 }
 
 // The phase clock of file staging (internal counters TV_COUNTER_FILE_NS_*, tv_options_internal.h): nanoseconds a
@@ -89,6 +112,7 @@ struct FileWindows {
     tv_ctx* c;
     W w[2];
     int fd = -1;
+    int fd_direct = -1;           // the same file opened O_DIRECT for cold units (-2: the filesystem refused it)
     const char* path = nullptr;   // the open file (units of one segment on one lane share the open)
     uint64_t size = 0;
     explicit FileWindows(tv_ctx* ctx) : c(ctx) {}
@@ -103,8 +127,18 @@ struct FileWindows {
     }
     void close_file() {
         if (fd >= 0) close(fd);
-        fd = -1;
+        if (fd_direct >= 0) close(fd_direct);
+        fd = fd_direct = -1;
         path = nullptr;
+    }
+    // The O_DIRECT descriptor of the open file, opened as the first one was (read + write or read-only); -1 when the
+    // filesystem does not take O_DIRECT (the buffered descriptor is used then).
+    int direct_fd(bool rw) {
+        if (fd_direct == -1) {
+            fd_direct = open(path, (rw ? O_RDWR : O_RDONLY) | O_DIRECT | O_CLOEXEC);
+            if (fd_direct < 0) fd_direct = -2;
+        }
+        return fd_direct >= 0 ? fd_direct : -1;
     }
     ~FileWindows() {
         release(0);
@@ -167,7 +201,14 @@ int stage_units(tv_ctx* c, const std::vector<FileUnit>& units, int lane, int thr
             __atomic_store_n(&status[u.k], TV_ERR_IO, __ATOMIC_RELAXED);
             continue;
         }
-        const uint64_t chunk = c->file_direct ? c->file_chunk : (uint64_t)kRingSlotBytes - 4;
+        // (the pread path's chunks are one ring slot, less room for an O_DIRECT read's 4 KiB rounding)
+        const uint64_t chunk = c->file_direct ? c->file_chunk : (uint64_t)kRingSlotBytes - 8192;
+        bool unit_cold = false;   // the unit's bytes are mostly not in the page cache: O_DIRECT reads
+        if (!c->file_direct && c->file_odirect) {
+            FileClock t(c, TV_FILE_PHASE_MAP);
+            const double f = cached_fraction(win.fd, u.fo, u.len);
+            unit_cold = f >= 0 && f < 0.5;
+        }
         bool unit_ok = true;
         for (uint64_t p = u.a; p < u.a + u.len && unit_ok; p += chunk, idx++) {
             const int k = idx & 1;
@@ -216,21 +257,37 @@ int stage_units(tv_ctx* c, const std::vector<FileUnit>& units, int lane, int thr
                 if (rc) return rc;
                 c->file_ns[TV_FILE_BYTES_DIRECT].fetch_add(n, std::memory_order_relaxed);
             } else {
-                // cold window (or direct DMA off / refused): parallel preads into the pinned ring, then DMA
+                // parallel preads into the pinned ring, then DMA.  A chunk whose bytes are mostly not in the page
+                // cache is read with O_DIRECT (TV_OPT_FILE_ODIRECT): cold reads ran 35 % faster that way on the
+                // gpurun boxes (tools/read_ceiling.c: 14.5-18.6 against 10.3-14.0 GB/s buffered, profiles/r05), and
+                // the page cache keeps nothing the verify will not read again.  Its requests are whole 4 KiB blocks
+                // into the slot's page-aligned start, so the chunk's bytes sit at slot + (fo % 4096): aligned for the
+                // DMA when the file offset and the linear offset agree mod 4 (else the buffered read, placed at the
+                // linear offset's alignment, is used).
                 win.release(k);
-                for (uint64_t q = 0; q < n; q += kRingSlotBytes - 4) {
-                    const uint64_t kq = std::min<uint64_t>(kRingSlotBytes - 4, n - q);
+                const int dfd = (unit_cold && ((fo ^ p) & 3) == 0) ? win.direct_fd(c->open_rw) : -1;
+                const uint64_t step = dfd >= 0 ? (uint64_t)kRingSlotBytes - 8192 : (uint64_t)kRingSlotBytes - 4;
+                for (uint64_t q = 0; q < n; q += step) {
+                    const uint64_t kq = std::min<uint64_t>(step, n - q);
                     SlotLease slot(c, lane);  // lent until every copy out of it is queued
                     {
                         FileClock t(c, TV_FILE_PHASE_WAIT);
                         rc = slot.take();
                         if (rc) return rc;
                     }
-                    uint8_t* at = slot.ptr() + ((p + q) & 3);  // at the resident bytes' alignment mod 4
+                    uint8_t* at;
                     int e;
-                    {
+                    if (dfd >= 0) {
+                        const uint64_t al = (fo + q) / 4096 * 4096, lead = fo + q - al;
+                        at = slot.ptr() + lead;
                         FileClock t(c, TV_FILE_PHASE_READ);
-                        e = pread_pool(c->pool[lane], threads, win.fd, at, fo + q, kq);
+                        e = pread_pool(c->pool[lane], threads, dfd, slot.ptr(), al, (lead + kq + 4095) / 4096 * 4096,
+                                       lead + kq);
+                        if (!e) c->file_ns[TV_FILE_BYTES_ODIRECT].fetch_add(kq, std::memory_order_relaxed);
+                    } else {
+                        at = slot.ptr() + ((p + q) & 3);  // at the resident bytes' alignment mod 4
+                        FileClock t(c, TV_FILE_PHASE_READ);
+                        e = pread_pool(c->pool[lane], threads, win.fd, at, fo + q, kq, kq);
                     }
                     if (e) {
                         fail(c, TV_ERR_IO, "read %s at %llu: %s", u.path, (unsigned long long)(fo + q), strerror(e));

@@ -16,6 +16,8 @@
 #define TV_OPT_FILE_CHUNK 6  /* long segments: bytes per unit dealt to a lane (and per mapped window with
                                 TV_OPT_FILE_DIRECT = 1); default 256 MiB, >= 64 KiB */
 #define TV_OPT_FILE_CONCURRENT 9 /* tv_stage_files: 1 (default) = long segments on two staging lanes, 0 = one */
+#define TV_OPT_FILE_ODIRECT 22   /* pread path: 1 (default) = chunks mostly not in the page cache are read O_DIRECT;
+                                    0 = every read buffered */
 #define TV_OPT_DEBUG_REBOUNCE 11 /* tests: 1 = bounce ring-resident sources through the ring again (the staging
                                     path that once raced); slot leases must keep it exact.  Default 0 */
 #define TV_OPT_TWIN_PACK 12      /* twin kernel with fewer workgroups than 2 per CU: 1 = launch it on a stream
@@ -41,7 +43,8 @@
 #define TV_OPT_FILE_CLOCK_RESET 100
 #define TV_COUNTER_FILE_CLOCK 100
 #define TV_FILE_PHASE_OPEN 0      /* open + fstat of a unit's file (once per file and lane) */
-#define TV_FILE_PHASE_MAP 1       /* direct path: mmap of a window + the mincore residency check */
+#define TV_FILE_PHASE_MAP 1       /* mmap of a window + the mincore residency check (direct path); the page-cache
+                                     residency check of a chunk (pread path, cachestat) */
 #define TV_FILE_PHASE_POPULATE 2  /* direct path: MADV_POPULATE_READ of a warm window */
 #define TV_FILE_PHASE_REGISTER 3  /* direct path: hipHostRegister of the window's page-cache pages */
 #define TV_FILE_PHASE_READ 4      /* pread path: the parallel preads of one ring slot (wall time of the slot) */
@@ -53,4 +56,5 @@
 #define TV_FILE_PHASE_CALL 10     /* wall time of tv_stage_files / tv_stage_file calls */
 #define TV_FILE_BYTES_DIRECT 11   /* bytes DMA'd from registered page-cache pages */
 #define TV_FILE_BYTES_READ 12     /* bytes read by preads into the ring (long segments) */
+#define TV_FILE_BYTES_ODIRECT 13  /* of which read with O_DIRECT (cold chunks, TV_OPT_FILE_ODIRECT) */
 #define TV_FILE_CLOCK_N 16
