@@ -257,6 +257,14 @@ def main():
                     emit({"layout": name, "cache": "cold", "read_ceiling_direct_gbps": round(dceil / 1e9, 2) if dceil
                           else None, "resident": round(res, 4),
                           "how": "tools/read_ceiling.c direct: the same reads with O_DIRECT (no page cache)"})
+                    res = drop_cache(paths)
+                    try:
+                        dceil32 = read_ceiling(paths, threads=32, part=8 * MiB, direct=True)
+                    except Exception:
+                        dceil32 = None
+                    emit({"layout": name, "cache": "cold", "read_ceiling_direct_32x8_gbps": round(dceil32 / 1e9, 2)
+                          if dceil32 else None, "resident": round(res, 4),
+                          "how": "tools/read_ceiling.c direct, 32 threads x 8 MiB requests (more in flight)"})
                 for leg, fn, counter in legs:
                     res = drop_cache(paths) if cold else fsutil.resident(paths)
                     if counter is not None:

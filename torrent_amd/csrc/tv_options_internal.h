@@ -44,7 +44,7 @@
 #define TV_COUNTER_FILE_CLOCK 100
 #define TV_FILE_PHASE_OPEN 0      /* open + fstat of a unit's file (once per file and lane) */
 #define TV_FILE_PHASE_MAP 1       /* mmap of a window + the mincore residency check (direct path); the page-cache
-                                     residency check of a chunk (pread path, cachestat) */
+                                     residency check of a unit (pread path: 64 sampled pages) */
 #define TV_FILE_PHASE_POPULATE 2  /* direct path: MADV_POPULATE_READ of a warm window */
 #define TV_FILE_PHASE_REGISTER 3  /* direct path: hipHostRegister of the window's page-cache pages */
 #define TV_FILE_PHASE_READ 4      /* pread path: the parallel preads of one ring slot (wall time of the slot) */
