@@ -32,6 +32,10 @@ CFG3_CONFIGS = [  # 10,000 files of <= 512 KiB: every segment takes the short-se
     ("short segments, 2 lanes, 8 thr", 0, 1, 8, 256 * MiB),
     ("short segments, 2 lanes, 32 thr", 0, 1, 32, 256 * MiB),
 ]
+COLD_CONFIGS = [  # after fsutil.drop_cache (residency re-checked): (name, odirect)
+    ("cold, pread 2 lanes 16 thr, O_DIRECT", 1),
+    ("cold, pread 2 lanes 16 thr, buffered", 0),
+]
 CONFIGS = [  # name, direct, concurrent, threads, chunk
     ("direct, 1 lane", 1, 0, 16, 256 * MiB),
     ("direct, 2 lanes", 1, 1, 16, 256 * MiB),
@@ -91,7 +95,28 @@ def main():
                   "phase_ms": {ph: round(v / 1e6, 1) for ph, v in clock.items() if not ph.startswith("bytes")},
                   "phase_ms_per_256MiB": {ph: round(v / 1e6 / per, 3) for ph, v in clock.items()
                                           if not ph.startswith("bytes") and ph != "call"},
-                  "bytes_direct": clock["bytes_direct"], "bytes_read": clock["bytes_read"]})
+                  "bytes_direct": clock["bytes_direct"], "bytes_read": clock["bytes_read"],
+                  "bytes_odirect": clock["bytes_odirect"]})
+        if os.environ.get("F2_COLD", "1") == "1" and name != "cfg3":
+            for cname, odirect in COLD_CONFIGS:
+                with _context(0) as ctx:
+                    ctx.set_option(FILE_DIRECT, 0)
+                    ctx.set_option(FILE_CONCURRENT, 1)
+                    ctx.set_option(FILE_CHUNK, 256 * MiB)
+                    ctx.set_option(_native.TV_OPT_FILE_ODIRECT, odirect)
+                    ctx._reset_file_clock()
+                res = fsutil.drop_cache(paths)
+                t = time.perf_counter()
+                bf = verify_files(info, root)
+                el = time.perf_counter() - t
+                with _context(0) as ctx:
+                    clock = ctx._file_clock()
+                    ctx.set_option(_native.TV_OPT_FILE_ODIRECT, 1)
+                emit({"layout": name, "config": cname, "resident": round(res, 4), "best_s": round(el, 4),
+                      "gbps": round(total / el / 1e9, 2), "exact": bytes(bf) == expect,
+                      "stage_files_ms": round(clock["call"] / 1e6, 1),
+                      "phase_ms": {ph: round(v / 1e6, 1) for ph, v in clock.items() if not ph.startswith("bytes")},
+                      "bytes_read": clock["bytes_read"], "bytes_odirect": clock["bytes_odirect"]})
         with _context(0) as ctx:   # back to the library defaults
             ctx.set_option(FILE_DIRECT, 0)
             ctx.set_option(FILE_CONCURRENT, 1)
