@@ -86,3 +86,35 @@ def test_cold_files_exact(native, oracle, tmp_path, odirect):
         assert clock["bytes_odirect"] < clock["bytes_read"]   # (and the others buffered)
     else:
         assert clock["bytes_odirect"] == 0
+
+
+@pytest.mark.parametrize("seed", list(range(24)))
+def test_random_layouts_cold_long_path(native, tmp_path, monkeypatch, seed):
+    """The seeded random layouts of tests/test_gpu_fuzz.py (zero-length, tiny, boundary-aligned, missing and
+    truncated files, odd piece lengths, ragged digests) with every non-empty segment forced onto the long-segment
+    path (direct_min = 1 byte: units dealt to both staging lanes) on a page cache dropped first, so the units go
+    O_DIRECT wherever the file and linear offsets agree mod 4: bits equal fsStorage.get + hashlib's."""
+    import shutil
+    import fsutil
+    from tests.test_gpu_fuzz import _disk, _draw, _expected
+    from torrent_amd import Storage, verify_files
+    from torrent_amd.storage import fs_storage
+    info, payload, sizes, missing, short, single = _draw(seed)
+    P = info.n_pieces
+    monkeypatch.chdir(tmp_path)
+    disk = _disk(info, payload, sizes, missing, short, single)
+    paths = []
+    for root in ("dl", "ref"):
+        for k, data in disk.items():
+            p = tmp_path.joinpath(root, *k)
+            p.parent.mkdir(parents=True, exist_ok=True)
+            p.write_bytes(data)
+            if root == "dl":
+                paths.append(str(p))
+    want_fs = _expected(info, Storage(fs_storage, info, str(tmp_path / "ref")))
+    shutil.rmtree(tmp_path / "ref", ignore_errors=True)
+    for devices in ([0], [0, 0, 0]):
+        if paths:
+            assert fsutil.drop_cache(paths) <= 0.01
+        bf = verify_files(info, str(tmp_path / "dl"), devices=devices, threads=4, direct_min=1)
+        assert _bits(bf, P) == want_fs, (seed, devices)
