@@ -308,11 +308,13 @@ def test_unstaged_windows_never_verify_against_zero_digests(native, oracle):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("order", ["ascending", "shuffled"])
-def test_stage_many_packs_small_buffers(native, oracle, order):
+@pytest.mark.parametrize("big", [False, True])
+def test_stage_many_packs_small_buffers(native, oracle, order, big):
     """tv_stage_many packs short pageable buffers into ring slots (many per slot, one DMA per run of adjacent
     bytes): ~150 MiB cut into buffers of 1 B .. 900 KiB at odd addresses, sub-piece and across piece boundaries,
-    with a few 16-20 MiB buffers (staged unpacked) among them, handed over in one call in ascending or shuffled
-    order; every piece verifies (bitfield = hashlib's), and the corrupted ones do not."""
+    with (big) or without a few 16-20 MiB buffers (staged unpacked) among them -- without, the buffers are dealt to
+    both staging lanes -- handed over in one call in ascending or shuffled order; every piece verifies (bitfield =
+    hashlib's), and the corrupted ones do not."""
     from torrent_amd import _native as N
     L = 1 << 16
     total = 200 * (1 << 20) + 4321
@@ -325,7 +327,7 @@ def test_stage_many_packs_small_buffers(native, oracle, order):
     cuts, o = [], 0
     while o < total:
         n = rng.choice([rng.randrange(1, 64), rng.randrange(64, 70000), rng.randrange(70000, 900 * 1024),
-                        rng.randrange(16 << 20, 20 << 20) if rng.random() < 0.01 else rng.randrange(1, 5000)])
+                        rng.randrange(16 << 20, 20 << 20) if (big and rng.random() < 0.05) else rng.randrange(1, 5000)])
         n = min(n, total - o)
         cuts.append((o, n))
         o += n

@@ -1,6 +1,7 @@
 // tv_stage.hip -- staging from host memory (tv_stage, tv_stage_many), reading back (tv_read) and the synthetic
 // device fill (tv_fill_synthetic).
 #include <cstring>
+#include <thread>
 
 #include "tv_ctx.h"
 
@@ -21,9 +22,10 @@ struct PackedPart {
 // checked, and DMA'd directly when they are.
 constexpr uint64_t kPackMax = 16ull << 20;
 
-// Stage LINEAR [a, b) from `src` (in a lane-0 ring slot), window by window on a windowed layout (as stage_locked).
-int stage_ring_run(tv_ctx* c, uint64_t a, uint64_t b, const uint8_t* src) {
-    if (!c->win) return stage_range(c, a, b, src, a, true, 0, /*src_in_ring=*/true);
+// Stage LINEAR [a, b) from `src` (in a ring slot of `lane`), window by window on a windowed layout (as
+// stage_locked; windowed layouts stage on lane 0 only).
+int stage_ring_run(tv_ctx* c, uint64_t a, uint64_t b, const uint8_t* src, int lane) {
+    if (!c->win) return stage_range(c, a, b, src, a, true, lane, /*src_in_ring=*/true);
     for (uint64_t pos = a; pos < b;) {
         const uint64_t w = win_of(c, pos / c->L - c->first);
         int rc = win_enter(c, w);
@@ -31,7 +33,7 @@ int stage_ring_run(tv_ctx* c, uint64_t a, uint64_t b, const uint8_t* src) {
         uint64_t wa, wb;
         clip_to_shard(c, pos, b - pos, &wa, &wb);
         if (wa < wb) {
-            rc = stage_range(c, wa, wb, src, a, true, 0, /*src_in_ring=*/true);
+            rc = stage_range(c, wa, wb, src, a, true, lane, /*src_in_ring=*/true);
             if (rc) return rc;
         }
         pos = win_end_linear(c, w);
@@ -39,34 +41,55 @@ int stage_ring_run(tv_ctx* c, uint64_t a, uint64_t b, const uint8_t* src) {
     return TV_OK;
 }
 
-// Copy the packed parts into one lane-0 ring slot on the pool's threads (a task per part, long parts in 4 MiB
-// pieces), then one DMA per run of linear-contiguous parts.
-int flush_packed(tv_ctx* c, std::vector<PackedPart>& parts) {
-    if (parts.empty()) return TV_OK;
-    SlotLease slot(c, 0);  // lent until every copy out of it is queued
-    int rc = slot.take();
-    if (rc) return rc;
-    uint8_t* base = slot.ptr();
-    constexpr uint64_t kPart = 4ull << 20;
-    std::vector<std::pair<uint32_t, uint64_t>> tasks;  // (part, offset inside it)
-    for (uint32_t q = 0; q < parts.size(); q++)
-        for (uint64_t o = 0; o < parts[q].b - parts[q].a; o += kPart) tasks.emplace_back(q, o);
-    c->pool[0].run(c->file_threads, tasks.size(), [&](uint64_t t) {
-        const PackedPart& pp = parts[tasks[t].first];
-        const uint64_t o = tasks[t].second, n = std::min(kPart, pp.b - pp.a - o);
-        tv_copy_host(base + pp.packed + o, pp.src + o, n);
-    });
-    for (size_t q = 0; q < parts.size();) {
-        size_t r = q + 1;
-        while (r < parts.size() && parts[r].a == parts[r - 1].b && parts[r].packed == parts[r - 1].packed + (parts[r - 1].b - parts[r - 1].a))
-            r++;
-        rc = stage_ring_run(c, parts[q].a, parts[r - 1].b, base + parts[q].packed);
-        if (rc) return rc;
-        q = r;
+// Short buffers packed into the ring slots of one staging lane: add() places a buffer at the next offset with its
+// linear offset's alignment mod 4 (a full slot is flushed first); flush() copies the slot's buffers in on the lane's
+// pool (a task per buffer, long ones in 4 MiB pieces) and queues one DMA per run of linear-contiguous buffers.
+struct Packer {
+    tv_ctx* c;
+    int lane, threads;
+    std::vector<PackedPart> parts;
+    uint64_t used = 0;
+
+    int add(uint64_t a, uint64_t b, const uint8_t* src) {
+        uint64_t at = used + ((a - used) & 3);
+        if (at + (b - a) > kRingSlotBytes) {
+            const int rc = flush();
+            if (rc) return rc;
+            at = a & 3;
+        }
+        parts.push_back({a, b, src, at});
+        used = at + (b - a);
+        return TV_OK;
     }
-    parts.clear();
-    return slot.release();
-}
+    int flush() {
+        used = 0;
+        if (parts.empty()) return TV_OK;
+        SlotLease slot(c, lane);  // lent until every copy out of it is queued
+        int rc = slot.take();
+        if (rc) return rc;
+        uint8_t* base = slot.ptr();
+        constexpr uint64_t kPart = 4ull << 20;
+        std::vector<std::pair<uint32_t, uint64_t>> tasks;  // (part, offset inside it)
+        for (uint32_t q = 0; q < parts.size(); q++)
+            for (uint64_t o = 0; o < parts[q].b - parts[q].a; o += kPart) tasks.emplace_back(q, o);
+        c->pool[lane].run(threads, tasks.size(), [&](uint64_t t) {
+            const PackedPart& pp = parts[tasks[t].first];
+            const uint64_t o = tasks[t].second, n = std::min(kPart, pp.b - pp.a - o);
+            tv_copy_host(base + pp.packed + o, pp.src + o, n);
+        });
+        for (size_t q = 0; q < parts.size();) {
+            size_t r = q + 1;
+            while (r < parts.size() && parts[r].a == parts[r - 1].b &&
+                   parts[r].packed == parts[r - 1].packed + (parts[r - 1].b - parts[r - 1].a))
+                r++;
+            rc = stage_ring_run(c, parts[q].a, parts[r - 1].b, base + parts[q].packed, lane);
+            if (rc) return rc;
+            q = r;
+        }
+        parts.clear();
+        return slot.release();
+    }
+};
 
 }  // namespace
 
@@ -108,33 +131,74 @@ int tv_stage_many(tv_ctx* c, uint64_t n, const uint64_t* linear_offsets, const u
     DrainGuard drain(c, 0, /*sync_compute=*/false);  // no DMA reads a caller buffer after the call
     // Short pageable buffers (a torrent's small files, Storage.get results) are packed into ring slots, many per slot
     // and copied by the pool, one DMA per run of adjacent bytes: one slot round trip per buffer made 10,000 small
-    // buffers a 6 GB/s path.  Long or page-locked ones go as tv_stage sends them.  Caller order is kept.
-    std::vector<PackedPart> parts;
-    uint64_t used = 0;
+    // buffers a 6 GB/s path.  Long or page-locked ones go as tv_stage sends them.  Caller order is kept within a lane.
+    // When every buffer is short and they fill at least two slots (and the payload is the whole shard: windows must
+    // ascend), the second half (by bytes, in caller order) goes to staging lane 1 on a helper thread, as
+    // tv_stage_files deals its segments, each lane with half of the context's threads.
+    uint64_t small_bytes = 0;
+    bool all_small = true;
     for (uint64_t k = 0; k < n; k++) {
-        if (!lens[k]) continue;
         uint64_t a, b;
         clip_to_whole_shard(c, linear_offsets[k], lens[k], &a, &b);
         if (a >= b) continue;
-        if (b - a >= kPackMax) {   // (stage_locked DMAs a page-locked one directly, bounces a pageable one)
-            rc = flush_packed(c, parts);
-            if (!rc) rc = stage_locked(c, linear_offsets[k], srcs[k], lens[k]);
-            if (rc) return rc;
-            used = 0;
-            continue;
-        }
-        uint64_t at = used + ((a - used) & 3);
-        if (at + (b - a) > kRingSlotBytes) {
-            rc = flush_packed(c, parts);
-            if (rc) return rc;
-            used = 0;
-            at = a & 3;
-        }
-        parts.push_back({a, b, srcs[k] + (a - linear_offsets[k]), at});
-        used = at + (b - a);
+        if (b - a >= kPackMax) all_small = false;
+        small_bytes += b - a;
     }
-    rc = flush_packed(c, parts);
+    const bool two = all_small && c->file_concurrent && !c->win && !c->slots && small_bytes >= 2 * (uint64_t)kRingSlotBytes;
+    uint64_t mid = n;
+    if (two) {
+        uint64_t acc = 0;
+        for (mid = 0; mid < n && acc < small_bytes / 2; mid++) {
+            uint64_t a, b;
+            clip_to_whole_shard(c, linear_offsets[mid], lens[mid], &a, &b);
+            if (a < b) acc += b - a;
+        }
+    }
+    const int threads = two ? std::max(1, c->file_threads / 2) : c->file_threads;
+    // the buffers [k0, k1) on `lane`
+    auto run = [&](uint64_t k0, uint64_t k1, int lane) -> int {
+        Packer pk{c, lane, threads};
+        for (uint64_t k = k0; k < k1; k++) {
+            if (!lens[k]) continue;
+            uint64_t a, b;
+            clip_to_whole_shard(c, linear_offsets[k], lens[k], &a, &b);
+            if (a >= b) continue;
+            int rc2;
+            if (b - a >= kPackMax) {   // (stage_locked DMAs a page-locked one directly, bounces a pageable one)
+                rc2 = pk.flush();
+                if (!rc2) rc2 = stage_locked(c, linear_offsets[k], srcs[k], lens[k]);
+            } else {
+                rc2 = pk.add(a, b, srcs[k] + (a - linear_offsets[k]));
+            }
+            if (rc2) return rc2;
+        }
+        return pk.flush();
+    };
+    int helper_rc = TV_OK;
+    std::thread helper;
+    struct Joiner {
+        std::thread& t;
+        ~Joiner() {
+            if (t.joinable()) t.join();
+        }
+    } joiner{helper};  // every exit joins the helper before the ctx lock is released
+    if (two && mid < n) {
+        helper = std::thread([&]() {
+            pin_thread(numa_cpus(c));  // next to its ring and the GPU
+            if (hipSetDevice(c->device) != hipSuccess) {
+                helper_rc = fail(c, TV_ERR_HIP, "tv_stage_many: hipSetDevice(%d) failed", c->device);
+                return;
+            }
+            DrainGuard drain1(c, 1, /*sync_compute=*/false);
+            helper_rc = run(mid, n, 1);
+            if (!helper_rc && hipStreamSynchronize(c->copy_stream2) != hipSuccess)
+                helper_rc = fail(c, TV_ERR_HIP, "tv_stage_many: a copy on staging lane 1 failed");
+        });
+    }
+    rc = run(0, mid, 0);
+    if (helper.joinable()) helper.join();
     if (rc) return rc;
+    if (helper_rc) return helper_rc;
     TV_HIP(c, hipStreamSynchronize(c->copy_stream));
     for (uint64_t k = 0; k < n; k++)
         if (lens[k]) clear_staged(c, linear_offsets[k], lens[k]);
