@@ -496,7 +496,7 @@ def cfg3_leg(device: int, steps: int, warmup: int, kernel_opt: int, idle_s: floa
     """BASELINE configs[2]: the multi-file torrent -- 10,000 files of U[0, 512 KiB] (20 zero-length, 5 under 64 B),
     256 KiB pieces spanning file boundaries, a short final piece, 1 % corrupted (tests/layouts.py "cfg3", the seeded
     generator the parity tests use; expected bits committed in tests/golden/layouts.json).  The payload is built in
-    host memory and staged FILE BY FILE (tv_stage_many with one segment per file at its linear offset: the
+    host memory and staged FILE BY FILE (tv_stage_many with one range per file at its linear offset: the
     storage.ts:89-137 walk's segments, zero-length files included), so the file -> piece mapping and the short
     final piece go through the library as a multi-file torrent's would.  Timed: (a) the resident verify, W + K
     steps with the shader clock probed (the value; frac_of_piece_ceiling is also given at the live clock), and
@@ -511,9 +511,14 @@ def cfg3_leg(device: int, steps: int, warmup: int, kernel_opt: int, idle_s: floa
     want = bytes.fromhex(golden["expected_bitfield"])
     L, P, total = info.piece_length, info.n_pieces, info.length
     payload = lay["payload"]
-    mv = memoryview(payload)
     starts, sizes = lay["starts"], lay["sizes"]
-    segs = [(starts[k], mv[starts[k]:starts[k] + sizes[k]]) for k in range(len(sizes))]
+    import numpy as np
+    # one range of the payload per file, at its linear offset (the file table; zero-length files included)
+    seg_lin = np.asarray(starts[:len(sizes)], dtype=np.uint64)
+    seg_len = np.asarray(sizes, dtype=np.uint64)
+
+    def stage_files_from_memory():
+        ctx.stage_ranges(payload, seg_lin, seg_lin, seg_len)
     t_built = time.perf_counter()
     ctx = _native.Context(device)
     try:
@@ -524,7 +529,7 @@ def cfg3_leg(device: int, steps: int, warmup: int, kernel_opt: int, idle_s: floa
             raise RuntimeError("cfg3: the shard does not fit the device budget")
         ctx.set_digests(info.pieces_raw)
         t0 = time.perf_counter()
-        ctx.stage_many(segs)
+        stage_files_from_memory()
         stage_s = time.perf_counter() - t0
         _device_sync(ctx, device)
         for _ in range(warmup):
@@ -545,7 +550,7 @@ def cfg3_leg(device: int, steps: int, warmup: int, kernel_opt: int, idle_s: floa
         for _ in range(3):
             time.sleep(idle_s)
             t2 = time.perf_counter()
-            ctx.stage_many(segs)
+            stage_files_from_memory()
             bf1 = ctx.verify()
             t3 = time.perf_counter()
             shots.append({"wall_ms": round((t3 - t2) * 1e3, 2), "gbps": round(total / (t3 - t2) / 1e9, 2),

@@ -346,3 +346,29 @@ def test_stage_many_packs_small_buffers(native, oracle, order, big):
         bf = ctx.verify()
     want = [0 if i in (0, 777, P - 1) else 1 for i in range(P)]
     assert _bits(bf, P) == want
+
+
+@pytest.mark.gpu
+def test_stage_ranges_of_one_buffer(native, oracle):
+    """_native.Context.stage_ranges (tv_stage_many over ranges of one host buffer, addresses computed with numpy):
+    a payload staged as its file table's ranges -- zero-length and tiny files, ranges across piece boundaries --
+    verifies as the whole payload does."""
+    import numpy as np
+    from torrent_amd import _native as N
+    L = 1 << 15
+    rng = random.Random(9)
+    sizes = [rng.choice([0, rng.randrange(1, 64), rng.randrange(64, 3 * L)]) for _ in range(3000)]
+    total = sum(sizes)
+    P = -(-total // L)
+    payload = bytes(oracle.synth_fill(33, 0, total))
+    digests = bytearray(oracle.hash_pieces(bytearray(payload), total, L, P))
+    digests[20 * 5] ^= 1
+    starts = np.cumsum([0] + sizes[:-1]).astype(np.uint64)
+    with N.Context(0) as ctx:
+        ctx.set_layout(total, L, P)
+        ctx.set_digests(bytes(digests))
+        ctx.stage_ranges(payload, starts, starts, np.asarray(sizes, dtype=np.uint64))
+        bf = ctx.verify()
+        with pytest.raises(ValueError):
+            ctx.stage_ranges(payload, [0], [total - 3], [4])
+    assert _bits(bf, P) == [0 if i == 5 else 1 for i in range(P)]

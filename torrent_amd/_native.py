@@ -313,6 +313,27 @@ class Context:
         self._check(self._L.tv_stage_many(self._h, n, offs, ptrs, lens))
         del keeps
 
+    def stage_ranges(self, buf, linear_offsets, buf_offsets, lens) -> None:
+        """tv_stage_many over ranges of ONE host buffer: range k is buf[buf_offsets[k] : + lens[k]] staged at LINEAR
+        linear_offsets[k] (e.g. a payload in memory and its file table: one range per file).  The addresses are
+        computed with numpy (stage_many's per-buffer address lookup costs ~5 us in Python: 50 ms for 10,000 files)."""
+        import numpy as np
+        lo = np.ascontiguousarray(linear_offsets, dtype=np.uint64)
+        bo = np.ascontiguousarray(buf_offsets, dtype=np.uint64)
+        ln = np.ascontiguousarray(lens, dtype=np.uint64)
+        n = len(lo)
+        if n == 0:
+            return
+        if len(bo) != n or len(ln) != n:
+            raise ValueError("stage_ranges: linear_offsets, buf_offsets and lens differ in length")
+        base, keep = _addr(buf)
+        size = memoryview(buf).nbytes
+        if n and int((bo + ln).max()) > size:
+            raise ValueError("stage_ranges: a range reaches past the buffer")
+        ptrs = bo + np.uint64(base or 0)
+        self._check(self._L.tv_stage_many(self._h, n, lo.ctypes.data, ptrs.ctypes.data, ln.ctypes.data))
+        del keep
+
     def stage_file(self, path, file_offset: int, linear_offset: int, length: int) -> bool:
         """tv_stage_file: stage `length` bytes of file `path` from `file_offset` as linear bytes
         [linear_offset, +length).  False when the file is missing, unopenable or short (TV_ERR_IO): the
