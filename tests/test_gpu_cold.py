@@ -3,7 +3,8 @@ with O_DIRECT into the pinned ring (TV_OPT_FILE_ODIRECT; 4 KiB-rounded requests,
 Checked on files evicted from the page cache (tools/fsutil.py: fsync + DONTNEED, re-checked with mincore): sizes
 that are not multiples of 4 KiB, file offsets that do and do not agree with the linear offsets mod 4 (the latter
 read buffered), a short last piece, corrupted pieces, and a file shorter than its segment -- every bitfield equal
-to Storage(fs_storage).get + hashlib's, with O_DIRECT on and off."""
+to Storage(fs_storage).get + hashlib's, with O_DIRECT on, off, and refused by the filesystem (fault injection:
+the file falls back to buffered reads, never to unreadable pieces)."""
 import hashlib
 import os
 import sys
@@ -20,7 +21,7 @@ def _bits(bf, n):
     return [(bf[i >> 3] >> (7 - (i & 7))) & 1 for i in range(n)]
 
 
-@pytest.mark.parametrize("odirect", [1, 0])
+@pytest.mark.parametrize("odirect", [1, 0, 2])
 def test_cold_files_exact(native, oracle, tmp_path, odirect):
     import fsutil
     from torrent_amd import FileInfo, Storage, make_info, verify_files
@@ -81,10 +82,10 @@ def test_cold_files_exact(native, oracle, tmp_path, odirect):
         with _context(0) as ctx:
             ctx.set_option(native.TV_OPT_FILE_ODIRECT, 1)
     assert _bits(bf, P) == want
-    if odirect:
+    if odirect == 1:
         assert clock["bytes_odirect"] > 0, clock      # (the cold chunks whose offsets agree mod 4 went O_DIRECT)
         assert clock["bytes_odirect"] < clock["bytes_read"]   # (and the others buffered)
-    else:
+    else:   # off, or (2) every O_DIRECT read refused: the same bits through the buffered fallback
         assert clock["bytes_odirect"] == 0
 
 

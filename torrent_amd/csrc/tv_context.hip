@@ -159,8 +159,8 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
             c->file_concurrent = value != 0;
             return TV_OK;
         case TV_OPT_FILE_ODIRECT:
-            if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_FILE_ODIRECT must be 0 or 1");
-            c->file_odirect = value != 0;
+            if (value < 0 || value > 2) return fail(c, TV_ERR_ARG, "TV_OPT_FILE_ODIRECT must be 0, 1 or 2");
+            c->file_odirect = (int)value;
             return TV_OK;
         case TV_OPT_RESIDENT:
             if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_RESIDENT must be 0 or 1");
@@ -237,7 +237,7 @@ int tv_get_option(tv_ctx* c, int key, int64_t* value) {
         case TV_OPT_FILE_DIRECT_MIN: *value = (int64_t)c->file_direct_min; return TV_OK;
         case TV_OPT_FILE_THREADS: *value = c->file_threads; return TV_OK;
         case TV_OPT_FILE_CONCURRENT: *value = c->file_concurrent ? 1 : 0; return TV_OK;
-        case TV_OPT_FILE_ODIRECT: *value = c->file_odirect ? 1 : 0; return TV_OK;
+        case TV_OPT_FILE_ODIRECT: *value = c->file_odirect; return TV_OK;
         case TV_OPT_RESIDENT: *value = c->resident ? 1 : 0; return TV_OK;
         case TV_OPT_DEBUG_REBOUNCE: *value = c->debug_rebounce ? 1 : 0; return TV_OK;
         case TV_OPT_TWIN_PACK: *value = c->twin_pack ? 1 : 0; return TV_OK;

@@ -167,7 +167,7 @@ struct tv_ctx {
     uint64_t file_chunk = 256ull << 20;  // tv_stage_file: bytes per mapped window
     bool file_direct = false;            // TV_OPT_FILE_DIRECT: long segments DMA'd from registered page-cache pages
     bool file_concurrent = true;         // tv_stage_files: long segments on two staging lanes
-    bool file_odirect = true;            // TV_OPT_FILE_ODIRECT: cold chunks read with O_DIRECT
+    int file_odirect = 1;                // TV_OPT_FILE_ODIRECT: cold chunks read with O_DIRECT (2: its reads fail, tests)
     uint64_t file_direct_min = 32ull << 20;  // tv_stage_files: segments >= this take the tv_stage_file path
     int file_threads = 16;                   // tv_stage_files: reader threads
     bool resident = true;                    // TV_OPT_RESIDENT

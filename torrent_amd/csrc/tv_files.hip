@@ -135,6 +135,10 @@ struct FileWindows {
     }
     // The O_DIRECT descriptor of the open file, opened as the first one was (read + write or read-only); -1 when the
     // filesystem does not take O_DIRECT (the buffered descriptor is used then).
+    void no_direct() {
+        if (fd_direct >= 0) close(fd_direct);
+        fd_direct = -2;
+    }
     int direct_fd(bool rw) {
         if (fd_direct == -1) {
             fd_direct = open(path, (rw ? O_RDWR : O_RDONLY) | O_DIRECT | O_CLOEXEC);
@@ -267,7 +271,7 @@ int stage_units(tv_ctx* c, const std::vector<FileUnit>& units, int lane, int thr
                 // DMA when the file offset and the linear offset agree mod 4 (else the buffered read, placed at the
                 // linear offset's alignment, is used).
                 win.release(k);
-                const int dfd = (unit_cold && ((fo ^ p) & 3) == 0) ? win.direct_fd(c->open_rw) : -1;
+                int dfd = (unit_cold && ((fo ^ p) & 3) == 0) ? win.direct_fd(c->open_rw) : -1;
                 const uint64_t step = dfd >= 0 ? (uint64_t)kRingSlotBytes - 8192 : (uint64_t)kRingSlotBytes - 4;
                 for (uint64_t q = 0; q < n; q += step) {
                     const uint64_t kq = std::min<uint64_t>(step, n - q);
@@ -283,9 +287,19 @@ int stage_units(tv_ctx* c, const std::vector<FileUnit>& units, int lane, int thr
                         const uint64_t al = (fo + q) / 4096 * 4096, lead = fo + q - al;
                         at = slot.ptr() + lead;
                         FileClock t(c, TV_FILE_PHASE_READ);
-                        e = pread_pool(c->pool[lane], threads, dfd, slot.ptr(), al, (lead + kq + 4095) / 4096 * 4096,
-                                       lead + kq);
+                        e = c->file_odirect == 2 ? EINVAL  // (fault injection: the filesystem refusing O_DIRECT reads)
+                                                 : pread_pool(c->pool[lane], threads, dfd, slot.ptr(), al,
+                                                              (lead + kq + 4095) / 4096 * 4096, lead + kq);
                         if (!e) c->file_ns[TV_FILE_BYTES_ODIRECT].fetch_add(kq, std::memory_order_relaxed);
+                        if (e) {
+                            // an O_DIRECT read the filesystem refuses (EINVAL: alignment it does not take, a tmpfs)
+                            // is not the file's failure: this file reads buffered from here on, this chunk included,
+                            // and only a buffered failure counts (it is what fsStorage.get's read would see)
+                            win.no_direct();
+                            dfd = -1;
+                            at = slot.ptr() + ((p + q) & 3);
+                            e = pread_pool(c->pool[lane], threads, win.fd, at, fo + q, kq, kq);
+                        }
                     } else {
                         at = slot.ptr() + ((p + q) & 3);  // at the resident bytes' alignment mod 4
                         FileClock t(c, TV_FILE_PHASE_READ);

@@ -17,7 +17,8 @@
                                 TV_OPT_FILE_DIRECT = 1); default 256 MiB, >= 64 KiB */
 #define TV_OPT_FILE_CONCURRENT 9 /* tv_stage_files: 1 (default) = long segments on two staging lanes, 0 = one */
 #define TV_OPT_FILE_ODIRECT 22   /* pread path: 1 (default) = chunks mostly not in the page cache are read O_DIRECT;
-                                    0 = every read buffered */
+                                    0 = every read buffered; 2 = tests: every O_DIRECT read fails as a filesystem that
+                                    refuses it would (EINVAL), so the file must fall back to buffered reads */
 #define TV_OPT_DEBUG_REBOUNCE 11 /* tests: 1 = bounce ring-resident sources through the ring again (the staging
                                     path that once raced); slot leases must keep it exact.  Default 0 */
 #define TV_OPT_TWIN_PACK 12      /* twin kernel with fewer workgroups than 2 per CU: 1 = launch it on a stream
