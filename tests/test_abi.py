@@ -278,3 +278,14 @@ def test_public_options_are_what_the_hosts_use():
     for m in re.finditer(r"\n    def ([a-z]\w*)\(self[^)]*\)[^:]*:(.*?)(?=\n    def |\Z)", api, re.S):
         used |= set(re.findall(r"\b(TV_OPT_\w+)\b", m.group(2)))
     assert used == public, (sorted(used - public), sorted(public - used))
+
+
+def test_source_id_ignores_comments_only():
+    """The library's build id (torrent_amd/_build.py source_id, compiled in as TV_BUILD_ID) hashes code, not
+    comments: a measurement tied to a build (profiles/traffic_*.json) survives a documentation edit, not a code one."""
+    from torrent_amd._build import _code_only
+    a = 'int f(int x) { // add one\n  return x + 1; /* plain */ }\nconst char* s = "// not a comment";\n'
+    b = '/* new header text */\nint f(int x) {\n  return x + 1;   }\n\nconst char* s = "// not a comment";\n'
+    assert _code_only(a).split() == _code_only(b).split()
+    assert '"// not a comment"' in _code_only(a)
+    assert _code_only(a) != _code_only(a.replace("x + 1", "x + 2"))

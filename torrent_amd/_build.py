@@ -24,17 +24,47 @@ CXX = os.environ.get("CXX", "g++")
 ARCH = os.environ.get("TV_OFFLOAD_ARCH", "gfx950")
 
 
+def _code_only(text: str) -> str:
+    """C / C++ source without its comments and blank-line / trailing-space differences (string and character
+    literals kept as they are), so that a comment or documentation edit does not change the source id."""
+    out, i, n = [], 0, len(text)
+    while i < n:
+        c = text[i]
+        if c in "\"'":                                   # a literal: copied up to its closing quote
+            j = i + 1
+            while j < n and text[j] != c:
+                j += 2 if text[j] == "\\" else 1
+            out.append(text[i:j + 1])
+            i = j + 1
+        elif text.startswith("//", i):
+            j = text.find("\n", i)
+            i = n if j < 0 else j
+        elif text.startswith("/*", i):
+            j = text.find("*/", i + 2)
+            i = n if j < 0 else j + 2
+            out.append(" ")
+        else:
+            out.append(c)
+            i += 1
+    lines = [ln.rstrip() for ln in "".join(out).split("\n")]
+    return "\n".join(ln for ln in lines if ln)
+
+
 def source_id() -> str:
-    """16 hex digits of SHA-256 over every source the library is built from (csrc/*.hip / *.h / *.cpp, the export
-    map, include/torrent_verify.h, the asm generator).  Compiled into the library (TV_BUILD_ID=..., read back by
-    _native.build_id()), so a measurement tied to it (profiles/traffic_*.json) applies to that build only."""
+    """16 hex digits of SHA-256 over the code the library is built from (csrc/*.hip / *.h / *.cpp and the export map,
+    include/torrent_verify.h -- comments stripped -- and the asm generator).  Compiled into the library
+    (TV_BUILD_ID=..., read back by _native.build_id()), so a measurement tied to it (profiles/traffic_*.json) applies
+    to that build only; a comment edit keeps the id."""
     import hashlib
     h = hashlib.sha256()
     files = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".h", ".cpp", ".map")))
     for f in [os.path.join(CSRC, f) for f in files] + [os.path.join(ROOT, "include", "torrent_verify.h"),
                                                          os.path.join(ROOT, "tools", "gen_sha1_asm.py")]:
+        text = open(f, encoding="utf-8", errors="surrogateescape").read()
+        if not f.endswith(".py"):
+            text = _code_only(text)
         h.update(os.path.relpath(f, ROOT).encode() + b"\0")
-        h.update(open(f, "rb").read())
+        h.update(text.encode("utf-8", "surrogateescape"))
     return h.hexdigest()[:16]
 
 

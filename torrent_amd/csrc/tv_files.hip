@@ -585,10 +585,12 @@ int stage_files_core(tv_ctx* c, uint64_t n, const char* const* paths, const uint
     // Short segments: with two lanes, the first half (by bytes, in linear order) on lane 0 and the second on lane 1
     // once there are at least two slots of them, so one lane's reads overlap the other's DMA and wait (each lane reads
     // a slot, queues its DMA, and waits for a free slot in turn)
+    // (a context with one host thread stages on one lane: a second lane would be a second thread)
+    const bool concurrent = c->file_concurrent && c->file_threads >= 2;
     std::vector<SmallSeg> lane_small[2];
     {
         std::stable_sort(small.begin(), small.end(), [](const SmallSeg& x, const SmallSeg& y) { return x.linear < y.linear; });
-        const bool split = c->file_concurrent && small_bytes >= 2 * (uint64_t)kRingSlotBytes;
+        const bool split = concurrent && small_bytes >= 2 * (uint64_t)kRingSlotBytes;
         uint64_t acc = 0;
         for (const SmallSeg& sg : small) {
             lane_small[split && acc >= small_bytes / 2 ? 1 : 0].push_back(sg);
@@ -604,7 +606,7 @@ int stage_files_core(tv_ctx* c, uint64_t n, const char* const* paths, const uint
         std::stable_sort(longs.begin(), longs.end(), [](const FileUnit& x, const FileUnit& y) { return x.a < y.a; });
         uint64_t load[2] = {small_load[0], small_load[1]};
         for (const FileUnit& u : longs) {
-            const int l = (c->file_concurrent && load[1] < load[0]) ? 1 : 0;
+            const int l = (concurrent && load[1] < load[0]) ? 1 : 0;
             lane_units[l].push_back(u);
             load[l] += u.len;
         }

@@ -144,7 +144,8 @@ int tv_stage_many(tv_ctx* c, uint64_t n, const uint64_t* linear_offsets, const u
         if (b - a >= kPackMax) all_small = false;
         small_bytes += b - a;
     }
-    const bool two = all_small && c->file_concurrent && !c->win && !c->slots && small_bytes >= 2 * (uint64_t)kRingSlotBytes;
+    const bool two = all_small && c->file_concurrent && c->file_threads >= 2 && !c->win && !c->slots &&
+                     small_bytes >= 2 * (uint64_t)kRingSlotBytes;
     uint64_t mid = n;
     if (two) {
         uint64_t acc = 0;
