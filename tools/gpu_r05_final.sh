@@ -16,7 +16,7 @@ mkdir -p /tmp/tsb && UV_THREADPOOL_SIZE=16 timeout -k 10 300 python3 -u tools/ts
 CHECK_OUT=${CHECK_OUT:-r05_final}/pmc bash tools/gpu_r05_pmc.sh > $out/pmc.log 2>&1 && echo PMC_OK &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/prof -o run -- python3 bench.py --steps 10 --warmup 3 \
     > $out/bench_prof.json 2> $out/bench_prof.err && echo PROF_OK &&
-bash tools/rehearse_ranks.sh $out/rehearse 2 && echo REHEARSE_OK
+bash tools/rehearse_ranks.sh $out/rehearse ${REHEARSE_N:-2} && echo REHEARSE_OK
 rc=$?
 rm -rf /tmp/tsb
 tail -3 $out/pytest_gpu.log; head -c 400 $out/bench_n1.json; echo; tail -3 $out/pmc.log
