@@ -288,13 +288,15 @@ int tv_host_unregister(void *ptr);
                                     streamed-only ctx, tv_stream_*; the resident calls then fail with TV_ERR_STATE).
                                     Takes effect at the next tv_set_layout */
 #define TV_OPT_TWIN_FILL 13      /* twin kernel with fewer workgroups than 2 per CU (resident calls, cfg4's shards at
-                                    N = 4 / 8): 1 (default) = add light companion workgroups up to 2 per CU that
-                                    run the same instruction stream on one piece of their main workgroup on the
-                                    otherwise idle SIMDs and discard the result (a CU running one twin workgroup
-                                    is ~4.5 % slower per block than one running two; +2.2-3.2 %, 0.2-0.4 % more
-                                    HBM reads); 0 = the real grid only -- the setting for a GPU shared with other
-                                    work, whose CUs the companions would take.  Bitfields are the same either way.
-                                    tv_verify_list adds them only to a list of >= 32 x CUs pieces */
+                                    N = 4 / 8): 1 (default, auto) = add light companion workgroups up to 2 per CU
+                                    that run the same instruction stream on one piece of their main workgroup on
+                                    the otherwise idle SIMDs and discard the result (a CU running one twin
+                                    workgroup is ~4.5 % slower per block than one running two; +2.2-3.2 %, 0.2-0.4 %
+                                    more HBM reads) -- unless other processes hold >= 1 GiB of this GPU's memory
+                                    (the kernel driver's per-process accounting): on a GPU shared with other work
+                                    the companions would take CUs it may be using; 0 = the real grid only, always.
+                                    Bitfields are the same either way.  tv_verify_list adds them only to a list of
+                                    >= 32 x CUs pieces */
 #define TV_OPT_RESIDENT_BUDGET 16 /* bytes of device memory the resident payload may take (0, default: the GPU's free
                                      memory at tv_set_layout less 4 GiB and 64 B per piece).  A shard larger than it
                                      gets a windowed layout (tv_set_layout).  Takes effect at the next tv_set_layout */

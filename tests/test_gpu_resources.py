@@ -331,3 +331,56 @@ def test_contexts_release_threads_and_memory(native, tmp_path):
     assert threads1 <= threads0, (threads0, threads1)
     assert free1 >= free0 - (64 << 20), (free0, free1)               # no device memory left behind
     assert rss1 <= rss0 + (256 << 20), (rss0, rss1)                  # nor pinned rings (384 MiB a ctx)
+
+
+@pytest.mark.gpu
+def test_companions_stand_down_on_a_shared_gpu(native, oracle):
+    """TV_OPT_TWIN_FILL = 1 (auto): while another process holds >= 1 GiB of the GPU's memory (the kernel driver's
+    per-process accounting, /sys/class/kfd/kfd/proc/<pid>/vram_<gpu_id>), a twin launch with fewer than 2 x CUs
+    workgroups runs its real grid only -- the companions would take CUs the other process may be using; once it has
+    gone they are back.  3 keeps them regardless.  The bits are the same every time."""
+    import subprocess
+    import sys
+    import time
+    L, P = 1 << 16, 64 * 32            # 64 twin workgroups: fewer than 2 per CU
+    payload = bytes(oracle.synth_fill(61, 0, L * P))
+    pieces = bytearray(oracle.hash_pieces(bytearray(payload), L * P, L, P))
+    pieces[20 * 9] ^= 1
+    cus = _cus()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with native.Context(0) as ctx:
+        if ctx.counter(native.TV_COUNTER_KFD_GPU_ID) == 0:
+            pytest.skip("the kernel driver's process accounting is not readable here")
+        ctx.set_option(native.TV_OPT_KERNEL, native.KERNEL_TWIN)
+        ctx.set_layout(L * P, L, P)
+        ctx.set_digests(bytes(pieces))
+        ctx.stage(0, payload)
+        want = ctx.verify()
+        assert ctx.counter(native.TV_COUNTER_COTENANT_VRAM) < (1 << 30)
+        assert ctx.counter(native.TV_COUNTER_LAST_WORKGROUPS) == 2 * cus          # alone: companions
+        child = subprocess.Popen(
+            [sys.executable, "-c",
+             "import sys; sys.path.insert(0, %r)\n"
+             "from torrent_amd import _native\n"
+             "c = _native.Context(0)\n"
+             "c.set_layout(2 << 30, 1 << 20, 2048)\n"         # ~2 GiB of resident payload
+             "c.fill_synthetic(1)\n"
+             "print('ready', flush=True)\n"
+             "sys.stdin.read()\n" % root],
+            stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+        try:
+            assert child.stdout.readline().strip() == "ready"
+            time.sleep(1.1)                                  # (the library re-reads the accounting once a second)
+            assert ctx.counter(native.TV_COUNTER_COTENANT_VRAM) >= (1 << 30)
+            assert ctx.verify() == want
+            assert ctx.counter(native.TV_COUNTER_LAST_WORKGROUPS) == P // 32    # the real grid only
+            ctx.set_option(native.TV_OPT_TWIN_FILL, 3)
+            assert ctx.verify() == want
+            assert ctx.counter(native.TV_COUNTER_LAST_WORKGROUPS) == 2 * cus    # forced on
+            ctx.set_option(native.TV_OPT_TWIN_FILL, 1)
+        finally:
+            child.stdin.close()
+            child.wait(timeout=60)
+        time.sleep(1.1)
+        assert ctx.verify() == want
+        assert ctx.counter(native.TV_COUNTER_LAST_WORKGROUPS) == 2 * cus          # alone again

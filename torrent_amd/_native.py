@@ -48,6 +48,8 @@ TV_OPT_LANE_PAIRS = 21
 TV_OPT_FILE_ODIRECT = 22
 TV_OPT_FILE_CLOCK_RESET = 100
 TV_COUNTER_FILE_CLOCK = 100
+TV_COUNTER_COTENANT_VRAM = 120
+TV_COUNTER_KFD_GPU_ID = 121
 TV_FILE_PHASES = ("open", "map", "populate", "register", "read", "wait", "queue", "release", "drain", "small", "call",
                   "bytes_direct", "bytes_read", "bytes_odirect")   # TV_FILE_PHASE_* / TV_FILE_BYTES_* in order
 
@@ -498,7 +500,8 @@ class Context:
 
     def set_companions(self, on: bool) -> None:
         """TV_OPT_TWIN_FILL: light companion workgroups on the idle SIMDs of twin launches with fewer than 2 workgroups
-        per CU (default on); off for a GPU shared with other work.  The bitfields are the same either way."""
+        per CU (default: on, unless other processes hold >= 1 GiB of the GPU's memory); False keeps them off
+        whatever the GPU's other users.  The bitfields are the same either way."""
         self.set_option(TV_OPT_TWIN_FILL, 1 if on else 0)
 
     def set_clock_probe(self, on: bool) -> None:

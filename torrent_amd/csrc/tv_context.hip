@@ -67,6 +67,7 @@ int tv_create(tv_ctx** out, int device) {
     // workers go back to when the binding is turned off
     c->proc_cpus_ok = sched_getaffinity(0, sizeof c->proc_cpus, &c->proc_cpus) == 0;
     c->numa_node = gpu_numa_node(device);
+    c->kfd_gpu_id = kfd_gpu_id(device);
     c->numa_cpus_ok = node_cpus(c->numa_node, &c->numa_cpus);
     apply_numa(c);
     *out = c;
@@ -175,7 +176,7 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
             c->twin_pack = value != 0;
             return TV_OK;
         case TV_OPT_TWIN_FILL:
-            if (value < 0 || value > 2) return fail(c, TV_ERR_ARG, "TV_OPT_TWIN_FILL must be 0, 1 or 2");
+            if (value < 0 || value > 3) return fail(c, TV_ERR_ARG, "TV_OPT_TWIN_FILL must be 0, 1, 2 or 3");
             c->twin_fill = (int)value;
             return TV_OK;
         case TV_OPT_TWIN_FILL_READS:
@@ -510,6 +511,8 @@ int tv_get_counter(tv_ctx* c, int key, uint64_t* value) {
         case TV_COUNTER_FILE_CLOCK + TV_FILE_PHASE_OPEN ... TV_COUNTER_FILE_CLOCK + TV_FILE_CLOCK_N - 1:
             *value = c->file_ns[key - TV_COUNTER_FILE_CLOCK].load();
             return TV_OK;
+        case TV_COUNTER_COTENANT_VRAM: *value = cotenant_vram(c); return TV_OK;
+        case TV_COUNTER_KFD_GPU_ID: *value = c->kfd_gpu_id; return TV_OK;
         case TV_COUNTER_LAST_CLOCK_KHZ: {
             *value = 0;
             if (!c->d_clock) return TV_OK;

@@ -7,7 +7,10 @@
 #include <sys/syscall.h>
 #include <unistd.h>
 
+#include <dirent.h>
+
 #include <cctype>
+#include <chrono>
 #include <cerrno>
 #include <cstdarg>
 #include <cstdio>
@@ -102,6 +105,140 @@ int page_node(const void* p) {
     return node;
 }
 
+
+// The KFD gpu_id of HIP device `device` (the topology node whose PCI location matches; 0: not found or not
+// readable).  /sys/class/kfd/kfd/topology/nodes/N/properties carries `domain` and `location_id` = bus << 8 |
+// device << 3 | function.
+static uint32_t kfd_topology_gpu_id(int device) {
+    char bdf[64] = {0};
+    if (hipDeviceGetPCIBusId(bdf, (int)sizeof bdf, device) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    unsigned dom = 0, bus = 0, dev = 0, fn = 0;
+    if (sscanf(bdf, "%x:%x:%x.%x", &dom, &bus, &dev, &fn) != 4) return 0;
+    const unsigned loc = (bus << 8) | (dev << 3) | fn;
+    for (int node = 0; node < 256; node++) {
+        char path[128];
+        snprintf(path, sizeof path, "/sys/class/kfd/kfd/topology/nodes/%d/properties", node);
+        FILE* f = fopen(path, "r");
+        if (!f) {
+            if (errno == ENOENT) break;   // past the last node (EPERM: a node this process may not see)
+            continue;
+        }
+        char key[64];
+        unsigned long long v = 0, l = ~0ull, d = ~0ull;
+        while (fscanf(f, "%63s %llu", key, &v) == 2) {
+            if (!strcmp(key, "location_id")) l = v;
+            else if (!strcmp(key, "domain")) d = v;
+        }
+        fclose(f);
+        if (l != loc || d != dom) continue;
+        snprintf(path, sizeof path, "/sys/class/kfd/kfd/topology/nodes/%d/gpu_id", node);
+        f = fopen(path, "r");
+        unsigned id = 0;
+        if (f) {
+            if (fscanf(f, "%u", &id) != 1) id = 0;
+            fclose(f);
+        }
+        return id;
+    }
+    return 0;
+}
+
+// vram_<gpu_id> of every process in KFD's accounting (pid as the kernel driver numbers it), sorted by pid.
+static std::vector<std::pair<long, uint64_t>> kfd_vram(uint32_t gpu_id) {
+    std::vector<std::pair<long, uint64_t>> out;
+    if (DIR* d = opendir("/sys/class/kfd/kfd/proc")) {
+        while (dirent* e = readdir(d)) {
+            char* end = nullptr;
+            const long pid = strtol(e->d_name, &end, 10);
+            if (end == e->d_name || *end) continue;
+            char path[128];
+            snprintf(path, sizeof path, "/sys/class/kfd/kfd/proc/%ld/vram_%u", pid, gpu_id);
+            if (FILE* f = fopen(path, "r")) {
+                unsigned long long v = 0;
+                if (fscanf(f, "%llu", &v) == 1) out.emplace_back(pid, (uint64_t)v);
+                fclose(f);
+            }
+        }
+        closedir(d);
+    }
+    std::sort(out.begin(), out.end());
+    return out;
+}
+
+// This process's pid in KFD's accounting.  The directory names are pids of the host's pid namespace, which a
+// process in a container does not know (getpid() differs), so it is found by a probe: the one process whose
+// vram_<gpu_id> grows by exactly a 64 MiB device allocation made in between two reads.  Resolved once per
+// process (a forked child probes again); 0 = not found (then no co-tenant check: companions stay on).
+static long kfd_self_pid(int device, uint32_t gpu_id) {
+    static std::mutex mu;
+    static long self = 0, for_pid = -1;
+    std::lock_guard<std::mutex> g(mu);
+    if (for_pid == (long)getpid()) return self;
+    for_pid = (long)getpid();
+    self = 0;
+    constexpr uint64_t kProbe = 64ull << 20;
+    int prev = 0;
+    if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    for (int attempt = 0; attempt < 3 && !self; attempt++) {
+        const auto before = kfd_vram(gpu_id);
+        void* p = nullptr;
+        if (hipMalloc(&p, kProbe) != hipSuccess) {
+            (void)hipGetLastError();
+            break;
+        }
+        const auto after = kfd_vram(gpu_id);
+        (void)hipFree(p);
+        long found = 0;
+        int matches = 0;
+        for (const auto& [pid, v] : after) {
+            auto it = std::lower_bound(before.begin(), before.end(), std::make_pair(pid, (uint64_t)0));
+            const uint64_t was = (it != before.end() && it->first == pid) ? it->second : 0;
+            if (v == was + kProbe) {
+                found = pid;
+                matches++;
+            }
+        }
+        if (matches == 1) self = found;   // another process allocating exactly 64 MiB at the same time: again
+    }
+    (void)hipSetDevice(prev);
+    return self;
+}
+
+// The KFD gpu_id of HIP device `device` for the co-tenant check: the topology node whose PCI location matches,
+// provided this process's own entry in the accounting can be told apart (kfd_self_pid); 0 = no check.
+uint32_t kfd_gpu_id(int device) {
+    const uint32_t id = kfd_topology_gpu_id(device);
+    if (!id || !kfd_self_pid(device, id)) return 0;
+    return id;
+}
+
+// Bytes of this GPU's memory other processes hold (KFD's per-process accounting,
+// /sys/class/kfd/kfd/proc/<pid>/vram_<gpu_id>), or 0 when it cannot be read.  Cached for a second.
+uint64_t cotenant_vram(tv_ctx* c) {
+    if (!c->kfd_gpu_id) return 0;
+    const auto now = std::chrono::steady_clock::now();
+    if (c->cotenant_checked && now - c->cotenant_at < std::chrono::seconds(1)) return c->cotenant_bytes;
+    const long self = kfd_self_pid(c->device, c->kfd_gpu_id);
+    uint64_t sum = 0;
+    for (const auto& [pid, v] : kfd_vram(c->kfd_gpu_id))
+        if (pid != self) sum += v;
+    c->cotenant_bytes = sum;
+    c->cotenant_at = now;
+    c->cotenant_checked = true;
+    return sum;
+}
+
+bool companions_on(tv_ctx* c) {
+    if (c->twin_fill == 0) return false;
+    if (c->twin_fill >= 2) return true;
+    return cotenant_vram(c) < kCotenantBytes;   // auto: not on a GPU another process is using
+}
 
 int fail(tv_ctx* c, int code, const char* fmt, ...) {
     char buf[512];
@@ -347,7 +484,7 @@ int launch_resident(tv_ctx* c, const TvPieces& p_in, int kernel, bool hash) {
     // (PMC GRBM_GUI_ACTIVE: 1,806 vs 1,727; sleeping fillers do not help, working ones do: DESIGN.md section 5).
     // With fewer real workgroups than 2 per CU, companions fill the grid to 2 x CUs: they re-hash main
     // workgroups' pieces on otherwise idle SIMDs and discard the result (TV_OPT_TWIN_FILL, default on).
-    if (kernel == TV_KERNEL_TWIN && c->twin_fill && !c->twin_pack && (c->split_pairs < 2 || c->split_pairs > 5)) {
+    if (kernel == TV_KERNEL_TWIN && !c->twin_pack && (c->split_pairs < 2 || c->split_pairs > 5) && companions_on(c)) {
         p.fill_to = 2u * (uint32_t)c->cus;
         p.fill_all = c->fill_all ? 1u : 0u;
     }

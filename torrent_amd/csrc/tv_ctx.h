@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <functional>
@@ -173,7 +174,11 @@ struct tv_ctx {
     bool resident = true;                    // TV_OPT_RESIDENT
     bool debug_rebounce = false;             // TV_OPT_DEBUG_REBOUNCE
     bool twin_pack = false;                  // TV_OPT_TWIN_PACK
-    int twin_fill = 1;                       // TV_OPT_TWIN_FILL: 0 off, 1 auto, 2 also on short lists
+    int twin_fill = 1;                       // TV_OPT_TWIN_FILL: 0 off, 1 auto, 2 also on short lists, 3 on always
+    uint32_t kfd_gpu_id = 0;                 // the GPU's KFD id (co-tenant check of the companions; 0 = unknown)
+    bool cotenant_checked = false;           // cotenant_bytes is fresh (read at cotenant_at)
+    uint64_t cotenant_bytes = 0;             // this GPU's memory other processes hold (KFD accounting)
+    std::chrono::steady_clock::time_point cotenant_at;
     bool fill_all = false;                   // TV_OPT_TWIN_FILL_READS
     hipStream_t pack_stream = nullptr;       // twin launches CU-masked to pack_cus CUs (TV_OPT_TWIN_PACK)
     int pack_cus = 0;
@@ -338,6 +343,15 @@ void free_chunks(tv_ctx* c);
 void free_list(tv_ctx* c);
 void free_device(tv_ctx* c);
 bool reuse_fits(uint64_t need, uint64_t cap);
+
+// ---- companion workgroups on a shared GPU (TV_OPT_TWIN_FILL) ----------------------------------------------------
+
+// Another process holding this much of the GPU's memory makes it a co-tenant: TV_OPT_TWIN_FILL = 1 (auto) then
+// launches no companion workgroups (they would take CUs the other process may be using).
+constexpr uint64_t kCotenantBytes = 1ull << 30;
+uint32_t kfd_gpu_id(int device);
+uint64_t cotenant_vram(tv_ctx* c);
+bool companions_on(tv_ctx* c);
 int ensure_hbits(tv_ctx* c, size_t bytes);
 
 // ---- staging lanes: a copy stream and a ring of pinned slots each ---------------------------------------------------

@@ -24,7 +24,11 @@
 #define TV_OPT_TWIN_PACK 12      /* twin kernel with fewer workgroups than 2 per CU: 1 = launch it on a stream
                                     CU-masked to ceil(workgroups / 2) CUs, two workgroups on each; 0 (default) =
                                     spread over every CU */
-/* TV_OPT_TWIN_FILL (public, 13) also takes 2 = companions on every tv_verify_list launch too (measurement only) */
+/* TV_OPT_TWIN_FILL (public, 13) also takes 2 = companions on every tv_verify_list launch too (measurement only), and
+   3 = companions whatever other processes hold on the GPU (the co-tenant check of 1 skipped) */
+#define TV_COUNTER_COTENANT_VRAM 120 /* bytes of this GPU's memory other processes hold (KFD: /sys/class/kfd/kfd/proc/
+                                        <pid>/vram_<gpu_id>; 0 when unreadable): >= 1 GiB turns auto companions off */
+#define TV_COUNTER_KFD_GPU_ID 121    /* the GPU's KFD gpu_id (0: not found) */
 #define TV_OPT_TWIN_FILL_READS 14 /* companion workgroups' loads: 0 (default) = every lane of a companion reads its
                                     main workgroup's first piece (the same instruction stream, 1/32 of the bytes);
                                     1 = the main workgroup's 32 pieces (round 2; 1.14-1.42 x payload of HBM reads) */

@@ -136,7 +136,8 @@ int tv_verify_list(tv_ctx* c, const uint64_t* pieces, uint64_t n, uint8_t* ok_ou
         // fill 2 x CUs workgroups with copies re-hashing the same few pieces (a 1-piece flush: 512 copies) for a
         // ~4 % shorter flush (r03 latency: tools/latency_probe.py)
         const uint64_t list_wgs = (m + 31) / 32;
-        if (kernel == TV_KERNEL_TWIN && (c->twin_fill == 2 || (c->twin_fill == 1 && list_wgs >= (uint64_t)c->cus))) {
+        if (kernel == TV_KERNEL_TWIN && (c->twin_fill == 2 || ((c->twin_fill == 1 || c->twin_fill == 3) &&
+                                                                list_wgs >= (uint64_t)c->cus && companions_on(c)))) {
             p.fill_to = 2u * (uint32_t)c->cus;
             p.fill_all = c->fill_all ? 1u : 0u;
         }
