@@ -122,3 +122,37 @@ def test_random_layouts_cold_long_path(native, tmp_path, monkeypatch, seed):
             assert fsutil.drop_cache(paths) <= 0.01
         bf = verify_files(info, str(tmp_path / "dl"), devices=devices, threads=4, direct_min=1, budget=budget)
         assert _bits(bf, P) == want_fs, (seed, devices, budget)
+
+
+def test_cold_file_end_stays_o_direct(native, oracle, tmp_path):
+    """A cold file whose size is not a multiple of 4 KiB: the O_DIRECT request for its last chunk runs past the end
+    of the file and comes back short.  That read is complete (the bytes asked for are in) and must not be continued
+    (a next request would start off a 4 KiB boundary and be refused, sending the chunk through the buffered fallback
+    a second time): every byte is counted as read O_DIRECT, and the bits are exact."""
+    import fsutil
+    from torrent_amd import FileInfo, make_info, verify_files
+    from torrent_amd.verify import _context
+    MiB = 1 << 20
+    L = MiB
+    total = 150 * MiB + 4097                      # three 64 MiB-ish ring chunks, the last one ragged
+    P = -(-total // L)
+    payload = bytes(oracle.synth_fill(57, 0, total))
+    digests = bytearray(b"".join(hashlib.sha1(payload[i * L:min(total, (i + 1) * L)]).digest() for i in range(P)))
+    digests[20 * (P - 1)] ^= 1
+    f = tmp_path / "one.bin"
+    f.write_bytes(payload)
+    info = make_info(L, bytes(digests), "one", files=[FileInfo(total, ["one.bin"])], length=total)
+    assert fsutil.drop_cache([str(f)]) <= 0.01
+    with _context(0) as ctx:
+        ctx.set_option(native.TV_OPT_FILE_ODIRECT, 1)
+        ctx._reset_file_clock()
+    cwd = os.getcwd()
+    os.chdir(str(tmp_path))
+    try:
+        bf = verify_files(info, str(tmp_path))
+    finally:
+        os.chdir(cwd)
+    with _context(0) as ctx:
+        clock = ctx._file_clock()
+    assert _bits(bf, P) == [1] * (P - 1) + [0]
+    assert clock["bytes_odirect"] == clock["bytes_read"] == total, clock

@@ -53,11 +53,12 @@ int pread_pool(Pool& pool, int threads, int fd, uint8_t* dst, uint64_t fo, uint6
     pool.run(threads, nparts, [&](uint64_t q) {
         uint64_t o = q * part;
         const uint64_t e = std::min(n, o + part);
-        while (o < e && !err.load(std::memory_order_relaxed)) {
+        // (o >= need: the bytes asked for are in -- an O_DIRECT read that came back short at the end of the file
+        // must not be continued, as its next request would start off a 4 KiB boundary and be refused)
+        while (o < e && o < need && !err.load(std::memory_order_relaxed)) {
             const ssize_t got = pread(fd, dst + o, e - o, (off_t)(fo + o));
             if (got < 0 && errno == EINTR) continue;
             if (got <= 0) {
-                if (got == 0 && o >= need) return;  // the end of the file, past the bytes asked for
                 int expect = 0;
                 err.compare_exchange_strong(expect, got < 0 ? errno : EIO);
                 return;
@@ -381,7 +382,7 @@ void read_segments(Pool& pool, const std::vector<SmallSeg>& segs, size_t lo, siz
             close(fd);
         }
         if (e) {
-            status[sg.k] = TV_ERR_IO;
+            __atomic_store_n(&status[sg.k], TV_ERR_IO, __ATOMIC_RELAXED);
             std::lock_guard<std::mutex> g(*err_mu);
             if (first_err->empty()) *first_err = std::string(path) + ": " + strerror(e);
         }
@@ -614,6 +615,9 @@ int stage_files_core(tv_ctx* c, uint64_t n, const char* const* paths, const uint
     // reader threads: the context's TV_OPT_FILE_THREADS shared by the lanes that read
     const int lanes = (lane_units[1].empty() && lane_small[1].empty()) ? 1 : 2;
     const int threads_per_lane = std::max(1, c->file_threads / lanes);
+    // (everything the helper touches is declared before the joiner, so an early return joins it first)
+    std::string first_err = zero_err;
+    std::mutex err_mu;
     int helper_rc = TV_OK;
     std::thread helper;
     struct Joiner {
@@ -622,8 +626,6 @@ int stage_files_core(tv_ctx* c, uint64_t n, const char* const* paths, const uint
             if (t.joinable()) t.join();
         }
     } joiner{helper};  // every exit joins the helper before the ctx lock is released
-    std::string first_err = zero_err;
-    std::mutex err_mu;
     if (lanes == 2) {
         helper = std::thread([&]() {
             pin_thread(numa_cpus(c));  // next to its ring and the GPU (TV_OPT_NUMA_BIND)
