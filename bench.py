@@ -300,6 +300,8 @@ def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: b
         _barrier(dist)
         kernel, _ = ctx.last_kernel()
         clock_ghz = ctx.last_clock_khz() / 1e6   # (after the timed region: it syncs)
+        grid = ctx.counter(_native.TV_COUNTER_LAST_WORKGROUPS)
+        cotenant = ctx.counter(_native.TV_COUNTER_COTENANT_VRAM)
     finally:
         ctx.close()
     t_end = time.perf_counter()
@@ -324,6 +326,9 @@ def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: b
            "clock_note": "shader clock of the last timed launch (its workgroup 0's shader-counter ticks over 100 MHz "
                          "real-time ticks, TV_OPT_CLOCK_PROBE); R_valu is quoted at 2.4 GHz, "
                          "frac_of_valu_peak_at_clock rescales it to this clock",
+           "workgroups": grid, "cotenant_vram_max_over_ranks": int(_max(dist, float(cotenant))),
+           "grid_note": "workgroups of the last launch (twin with fewer than 2 per CU: companions fill it to 2 x CUs "
+                        "unless other processes hold >= 1 GiB of the GPU, cotenant_vram: KFD accounting)",
            "bitfield_exact": exact, "expected": "oracle digests of every piece, 1 % corrupted",
            "ground_truth_s": round(gt_s, 2), "ground_truth_threads": threads,
            "phase_s": {"ground_truth": round(gt_s, 2), "setup": round(t_warm - t_setup, 2),
