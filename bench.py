@@ -5,12 +5,10 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-`value` (the timed workload):
-  * N = 1: BASELINE configs[1] = cfg2, a 16 GiB synthetic single-file torrent in 16,384 pieces of 1 MiB,
-    HBM-resident on one MI355X.
-  * N > 1: BASELINE configs[3] = cfg4, ONE 200 GiB torrent in 51,200 pieces of 4 MiB, strong-scaled: rank
-    r verifies the contiguous 8-aligned shard shard_ranges(51200, N)[r] (no data-path collective; the
-    bitfield slices are whole bytes and concatenate).  `--weak` runs cfg2 per GPU instead.
+`value` (the timed workload): BASELINE configs[1] = cfg2, a 16 GiB synthetic single-file torrent in 16,384 pieces
+of 1 MiB, HBM-resident on one MI355X; at N > 1 weak-scaled (the pieces are independent units, sharded with no
+data-path collective): an N x 16 GiB torrent of N x 16,384 pieces, rank r verifying its contiguous 16 GiB shard,
+so the driver's 1 -> 8 curve is one configuration.  `--workload cfg4 --strong` times BASELINE configs[3] instead.
   One step = one tv_verify of the rank's whole resident shard (availability bits up, the verify kernel,
   the bitfield slice down).  W untimed steps, then exactly K steps between a barrier + device synchronize
   on both sides; time = max over ranks; value = bytes of all ranks' shards x K / time.
@@ -20,7 +18,9 @@ digests): the rank's whole shard is hashed on the host's cores before the timed 
 digests are corrupted, so `bitfield_exact` means "equal, on every piece, to the oracle's bitfield".
 
 Legs reported beside `value` (never as it):
-  * cfg4 (N = 1): the whole 200 GiB torrent on one GPU -- the same-config anchor of the 1 -> 8 GPU curve.
+  * cfg4: BASELINE configs[3], ONE 200 GiB torrent in 51,200 pieces of 4 MiB, strong-scaled: rank r verifies
+    the contiguous 8-aligned shard shard_ranges(51200, N)[r] (the bitfield slices are whole bytes and
+    concatenate); at N = 1 the whole torrent on one GPU.  Piece-bound past one GPU.
   * e2e_cfg5: BASELINE configs[4], the end-to-end resume check: the cfg4 torrent streamed from host memory
     over PCIe through the library's BOUNDED pinned ring (tv_stream_*; 3 x 64 MiB per GPU, no resident
     payload, no whole-shard host buffer), each rank its shard.  `generated`: the bytes are produced by the
@@ -30,7 +30,6 @@ Legs reported beside `value` (never as it):
   * cfg3 (N = 1): BASELINE configs[2], the multi-file torrent (10,000 files, 256 KiB pieces spanning files, short
     final piece, 1 % corrupted) staged file by file, resident verify at the live clock + one-shot wall clock.
   * piece_saturated (N = 1): 65,536 x 256 KiB pieces (SURVEY 8d suppl.) against the VALU roofline.
-  * cfg2_weak (N > 1): cfg2 per GPU, weak scaling.
   * cpu_baseline (rank 0, N = 1): the oracle (C port of the per-piece SHA-1 path, SHA-NI) on the host's
     allowed cores: a bounded sample of the cfg2 workload, BASELINE configs[0] (cfg1) as its own entry, the
     1-core figure, and the full-shard ground-truth pass.
@@ -312,7 +311,13 @@ def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: b
     bytes_all = _sum(dist, float(bytes_rank))
     achieved = bytes_rank / (avg / 1e3) / 1e9
     ceiling = piece_ceiling(kernel, count)
-    out = {"workload": desc if not strong else desc.split(" (")[0] + f" ({P} pieces in all, {ws} shard(s), strong scaling)",
+    if strong:
+        what = desc.split(" (")[0] + f" ({P} pieces in all, {ws} shard(s), strong scaling)"
+    elif ws > 1:
+        what = desc + f"; per GPU: one {ws}-shard torrent of {P} pieces, each rank its {n}-piece shard (weak scaling)"
+    else:
+        what = desc
+    out = {"workload": what,
            "piece_length": L, "total_pieces": P, "pieces_per_gpu": count, "bytes_per_gpu": bytes_rank,
            "value": round(bytes_all * steps / elapsed / 1e9, 2), "unit": "GB/s", "steps": steps, "warmup": warmup,
            "ms_per_step": round(elapsed * 1e3 / steps, 3), "scaling": "strong" if strong else "weak",
@@ -634,7 +639,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
-                    help="timed workload (default: cfg2 at N=1, cfg4 strong at N>1)")
+                    help="timed workload (default: cfg2, weak-scaled at N>1)")
     sc = ap.add_mutually_exclusive_group()
     sc.add_argument("--strong", action="store_true", help="the workload's pieces are the WHOLE torrent, sharded")
     sc.add_argument("--weak", action="store_true", help="the workload's pieces are per GPU")
@@ -642,10 +647,10 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-saturating", action="store_true", help="skip the piece_saturated leg (N=1)")
-    ap.add_argument("--no-cfg4", action="store_true", help="skip the cfg4 anchor leg (N=1) / cfg2_weak leg (N>1)")
+    ap.add_argument("--no-cfg4", action="store_true", help="skip the cfg4 leg (the 200 GiB torrent, strong-scaled)")
     ap.add_argument("--no-cfg3", action="store_true", help="skip the cfg3 multi-file leg (N=1)")
     ap.add_argument("--e2e-steps", type=int, default=1, help="timed e2e_cfg5 passes (0 = skip the leg)")
-    ap.add_argument("--leg-steps", type=int, default=5, help="timed steps of the cfg4 / cfg2_weak / suppl legs")
+    ap.add_argument("--leg-steps", type=int, default=5, help="timed steps of the cfg4 / suppl legs")
     a = ap.parse_args()
 
     dist, rank, ws, local = _dist()
@@ -657,8 +662,12 @@ def main() -> int:
     share["cores_per_rank"] = threads
     placement = rank_placement(dist, ws, rank, local, device, ndev)
     physical = len({p["pci_bus_id"] for p in placement}) if placement else 1
-    workload = a.workload or ("cfg2" if ws == 1 else "cfg4")
-    strong = a.strong or (not a.weak and a.workload is None and ws > 1)
+    # `value`: cfg2 at every N, weak-scaled (the units -- pieces -- are independent and sharded with no data-path
+    # collective: each rank verifies its own 16 GiB / 16,384-piece shard of an N x 16 GiB torrent), so the 1 -> 8
+    # curve is one configuration; cfg4 (BASELINE configs[3], one 200 GiB torrent strong-scaled over the N GPUs) is
+    # the `cfg4` leg at every N
+    workload = a.workload or "cfg2"
+    strong = a.strong
 
     main_leg = resident_leg(dist, ws, rank, device, workload, strong, a.steps, a.warmup, a.kernel, threads,
                             want_digests=(workload == "cfg4" and strong))
@@ -667,13 +676,11 @@ def main() -> int:
     if workload == "cfg4" and strong:
         cfg4_digests = main_leg.pop("_digests")
         main_leg.pop("_first")
-    elif ws == 1 and not a.no_cfg4:
-        legs["cfg4"] = resident_leg(dist, 1, 0, device, "cfg4", True, a.leg_steps, 1, a.kernel, threads,
+    elif not a.no_cfg4:
+        legs["cfg4"] = resident_leg(dist, ws, rank, device, "cfg4", True, a.leg_steps, 1, a.kernel, threads,
                                     want_digests=True)
         cfg4_digests = legs["cfg4"].pop("_digests")
         legs["cfg4"].pop("_first")
-    if ws > 1 and not a.no_cfg4 and not (workload == "cfg2" and not strong):
-        legs["cfg2_weak"] = resident_leg(dist, ws, rank, device, "cfg2", False, a.leg_steps, 1, a.kernel, threads)
     if a.e2e_steps > 0:
         try:
             legs["e2e_cfg5"] = e2e_cfg5(dist, ws, rank, device, a.e2e_steps, threads, cfg4_digests, share,

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Rehearse the driver's N > 1 bench path on ONE GPU: torchrun with N ranks, every rank on the same card
 # (bench.py places rank r on device LOCAL_RANK % visible devices).  Default workload as the driver runs it:
-# cfg4 strong (N shards of the 200 GiB torrent resident at once), cfg2_weak and e2e_cfg5 legs.
+# cfg2 weak-scaled (one 16 GiB shard per rank), the cfg4 leg (N shards of the 200 GiB torrent resident at once)
+# and e2e_cfg5.
 # Usage: tools/rehearse_ranks.sh OUTDIR N [N ...]      (each N under its own 600 s limit, the driver's)
 set -o pipefail
 out=${1:?outdir}; shift
