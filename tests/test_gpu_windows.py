@@ -371,4 +371,6 @@ def test_stage_ranges_of_one_buffer(native, oracle):
         bf = ctx.verify()
         with pytest.raises(ValueError):
             ctx.stage_ranges(payload, [0], [total - 3], [4])
+        with pytest.raises(ValueError):       # an offset that wraps when added (-1 as uint64) is refused too
+            ctx.stage_ranges(payload, [0], np.array([-1], dtype=np.int64), [2])
     assert _bits(bf, P) == [0 if i == 5 else 1 for i in range(P)]

@@ -330,7 +330,9 @@ class Context:
             raise ValueError("stage_ranges: linear_offsets, buf_offsets and lens differ in length")
         base, keep = _addr(buf)
         size = memoryview(buf).nbytes
-        if n and int((bo + ln).max()) > size:
+        # (checked without adding, so a huge offset -- e.g. a negative one cast to uint64 -- cannot wrap past it)
+        sz = np.uint64(size)
+        if bool((bo > sz).any()) or bool((ln > sz - np.minimum(bo, sz)).any()):
             raise ValueError("stage_ranges: a range reaches past the buffer")
         ptrs = bo + np.uint64(base or 0)
         self._check(self._L.tv_stage_many(self._h, n, lo.ctypes.data, ptrs.ctypes.data, ln.ctypes.data))
