@@ -1,0 +1,78 @@
+"""Cold verify_files against the box's O_DIRECT read ceiling, interleaved (is the cold path at the storage bound?).
+
+For each layout (tools/storage_paths_bench.write_layout: single16, files64), `rounds` rounds of, each after a
+residency-checked drop (tools/fsutil.drop_cache; a leg above 1 % resident is recorded and skipped):
+  * the C reader's O_DIRECT ceiling at 16 threads x 4 MiB and at 64 threads x 4 MiB (tools/read_ceiling.c);
+  * verify_files with O_DIRECT at 16, 32 and 64 reader threads (two staging lanes share them),
+so a queue-depth effect shows beside the box's own storage variance.
+
+usage: python tools/cold_sweep.py <dir> [layout ...] > out.jsonl
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import fsutil  # noqa: E402
+from storage_paths_bench import read_ceiling, write_layout  # noqa: E402
+from torrent_amd import _native, verify_files  # noqa: E402
+from torrent_amd.verify import _context  # noqa: E402
+
+MiB = 1 << 20
+
+
+def emit(rec):
+    print(json.dumps(rec), flush=True)
+
+
+def main():
+    d = sys.argv[1]
+    names = sys.argv[2:] or ["single16", "files64"]
+    rounds = int(os.environ.get("COLD_ROUNDS", "2"))
+    for name in names:
+        root = os.path.join(d, name)
+        info, expect, paths = write_layout(name, root)
+        total = info.length
+        cwd = os.getcwd()
+        os.chdir(root)
+        verify_files(info, root)          # context, allocations, ring (warm; not measured)
+        with _context(0) as ctx:
+            ctx.set_option(_native.TV_OPT_FILE_ODIRECT, 1)
+        legs = [("ceiling direct 16x4MiB", 16), ("ceiling direct 64x4MiB", 64),
+                ("verify_files O_DIRECT", 16), ("verify_files O_DIRECT", 32), ("verify_files O_DIRECT", 64)]
+        for rnd in range(rounds):
+            for what, thr in legs:
+                res = fsutil.drop_cache(paths)
+                rec = {"layout": name, "round": rnd, "leg": what, "threads": thr, "resident": round(res, 4)}
+                if res > 0.01:
+                    rec["skipped"] = "still cached after the drop"
+                    emit(rec)
+                    continue
+                if what.startswith("ceiling"):
+                    t = time.perf_counter()
+                    got = read_ceiling(paths, threads=thr, part=4 * MiB, direct=True)
+                    rec["gbps"] = round(got / 1e9, 2) if got else None
+                    rec["s"] = round(time.perf_counter() - t, 3)
+                else:
+                    with _context(0) as ctx:
+                        ctx._reset_file_clock()
+                    t = time.perf_counter()
+                    bf = verify_files(info, root, threads=thr)
+                    el = time.perf_counter() - t
+                    with _context(0) as ctx:
+                        clock = ctx._file_clock()
+                    rec.update({"gbps": round(total / el / 1e9, 2), "s": round(el, 3), "exact": bytes(bf) == expect,
+                                "read_ms_sum_lanes": round(clock["read"] / 1e6, 1),
+                                "wait_ms": round(clock["wait"] / 1e6, 1),
+                                "bytes_odirect": clock["bytes_odirect"], "bytes_read": clock["bytes_read"]})
+                emit(rec)
+        os.chdir(cwd)
+        for p in paths:
+            os.unlink(p)
+
+
+if __name__ == "__main__":
+    main()
