@@ -418,6 +418,46 @@ import("{mod}").then(async (m) => {{
             assert g[n]["shards"] == ws, (seed, n)
 
 
+def test_verify_files_paths_in_one_buffer(tmp_path):
+    """verifyFiles hands the library every path from ONE NUL-separated buffer (interior pointers): non-ASCII names
+    (2-, 3- and 4-byte UTF-8, a surrogate pair among them) arrive intact and in order, and a name holding a NUL --
+    which Deno.open refuses, so fsStorage.get's piece is null -- arrives as "", which the library cannot open
+    either.  CPU, with the JS model of the library recording the plan."""
+    mod = erased_module(tmp_path)
+    L = 4096
+    names = [["a", "caf\u00e9.bin"], ["\u65e5\u672c", "x.bin"], ["e\U0001f600.bin"], ["bad\u0000name"], ["z.bin"]]
+    sizes = [3000, 5000, 0, 700, 4000]
+    total = sum(sizes)
+    P = -(-total // L)
+    spec = _info_json(L, total, bytes(20 * P), list(zip(sizes, names)), "t")
+    (tmp_path / "spec.json").write_text(json.dumps(spec))
+    out = run_node(tmp_path, f"""
+import {{ createRequire }} from "module";
+const require = createRequire("{HARNESS}/");
+const Deno = require("./fake_deno.js");
+Deno.fakeAvailOnly = true;
+const fs = require("fs");
+import("{mod}").then(async (m) => {{
+  const d = JSON.parse(fs.readFileSync("{tmp_path}/spec.json", "utf8"));
+  const info = {{ pieceLength: d.pieceLength, length: d.length, pieces: [], name: d.name, private: 0, files: d.files }};
+  const raw = Buffer.from(d.pieces, "base64");
+  for (let i = 0; i < raw.length; i += 20) info.pieces.push(new Uint8Array(raw.subarray(i, i + 20)));
+  await m.verifyFiles(info, "/r");
+  const segs = [];
+  for (const c of Deno.fakeContexts.values()) if (c.segments) segs.push(...c.segments);
+  console.log(JSON.stringify(segs));
+}}).catch((e) => {{ console.error(e); process.exit(1); }});
+""")
+    segs = json.loads(out)
+    want = [("/r/" + "/".join(p) if "\0" not in "".join(p) else "") for p in names]
+    got_paths = [sg[0] for sg in segs]
+    assert set(got_paths) <= set(want), got_paths
+    for k, (n, p) in enumerate(zip(sizes, names)):
+        if n:
+            assert any(sg[0] == want[k] and sg[3] > 0 for sg in segs), (k, got_paths)
+    assert "" in got_paths                                          # the NUL name: unopenable, as in Deno
+
+
 def test_verify_stream_host_logic_on_cpu(tmp_path):
     """verifyStream's host side (ts/verify.ts: request loop, row lengths, unreadable rows, the worker pool of
     reads, shard concatenation) on CPU against the JS model of the tv_stream_* protocol (several requests per

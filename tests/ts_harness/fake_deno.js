@@ -21,9 +21,20 @@ const memory = new Map();
 let nextAddress = 0x1000n;
 
 function bytesOf(p) {
-  const ta = typeof p === "bigint" ? memory.get(p) : p;
+  let ta = typeof p === "bigint" ? memory.get(p) : p;
+  let off = 0;
+  if (!ta && typeof p === "bigint") {   // an interior pointer: a registered array's address + an offset into it
+    for (const [a, t] of memory) {
+      if (p > a && p < a + BigInt(t.byteLength)) {
+        ta = t;
+        off = Number(p - a);
+        break;
+      }
+    }
+  }
   if (!ta) throw new Error("fake_deno: unknown pointer " + p);
-  return ta instanceof Uint8Array ? ta : new Uint8Array(ta.buffer, ta.byteOffset, ta.byteLength);
+  const b = ta instanceof Uint8Array ? ta : new Uint8Array(ta.buffer, ta.byteOffset, ta.byteLength);
+  return off ? b.subarray(off) : b;
 }
 
 function u64s(p, n) {
@@ -251,7 +262,8 @@ const Deno = {
   UnsafePointer: {
     of(ta) {
       const a = nextAddress;
-      nextAddress += 0x1000n;
+      // (addresses at least one page apart and past the array's end, so an interior pointer names one array)
+      nextAddress += (BigInt(ta.byteLength) + 0x1fffn) / 0x1000n * 0x1000n;
       memory.set(a, ta);
       return a;
     },
