@@ -386,6 +386,22 @@ export async function verifyStream(info: InfoDict, storage: Storage, opts: Verif
  * would fail (a directory, a missing parent directory); unlike fsStorage.get, no missing file is created.  Same behaviour as
  * torrent_amd.verify_files.
  */
+/** Numbers (< 2^52) as the little-endian u64 words of a C array (Deno runs on little-endian hosts only), written
+ * as 32-bit halves -- a BigInt per element cost ~3-4 ms on a 10,000-file verifyFiles -- with `base` (a pointer)
+ * added to each. */
+function u64Words(vals: number[], base: bigint): Uint32Array {
+  const out = new Uint32Array(2 * vals.length);
+  const bLo = Number(base & 0xffffffffn);
+  const bHi = Number(base >> 32n);
+  for (let k = 0; k < vals.length; k++) {
+    const v = vals[k] + bLo;                 // exact in a double
+    const hi = Math.floor(v / 4294967296);
+    out[2 * k] = v - hi * 4294967296;
+    out[2 * k + 1] = bHi + hi;
+  }
+  return out;
+}
+
 export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptions = {}): Promise<Uint8Array> {
   const l = load(opts.libPath);
   const P = info.pieces.length;
@@ -465,14 +481,8 @@ export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptio
       if (segFile.length) {
         const n = segFile.length;
         const base = BigInt(Deno.UnsafePointer.value(Deno.UnsafePointer.of(pathBuf)));
-        const paths = new BigUint64Array(n);
-        const fo = new BigUint64Array(n), lin = new BigUint64Array(n), len = new BigUint64Array(n);
-        for (let k = 0; k < n; k++) {
-          paths[k] = base + BigInt(pathAt[segFile[k]]);
-          fo[k] = BigInt(segFo[k]);
-          lin[k] = BigInt(segLin[k]);
-          len[k] = BigInt(segLen[k]);
-        }
+        const paths = u64Words(segFile.map((f) => pathAt[f]), base);
+        const fo = u64Words(segFo, 0n), lin = u64Words(segLin, 0n), len = u64Words(segLen, 0n);
         const status = new Int32Array(n);
         const u8 = (a: ArrayBufferView) => new Uint8Array(a.buffer, a.byteOffset, a.byteLength);
         // a failed segment's pieces are marked inside the library (tv_verify reports them 0), from the piece
