@@ -89,22 +89,28 @@ def test_device_placement_rule():
 
 
 @pytest.mark.gpu
-def test_bench_two_ranks_on_the_hip_path():
+@pytest.mark.parametrize("scaling", ["strong", "weak"])
+def test_bench_two_ranks_on_the_hip_path(scaling):
     """The N>1 path itself, on one GPU: `torch.distributed.run --nproc-per-node 2 bench.py` (gloo barriers,
-    max-over-ranks time), each rank verifying its strong-scaled shard of one torrent through the HIP
-    library against the oracle's digests; rank 0 prints one valid JSON line with an exact bitfield."""
+    max-over-ranks time), each rank verifying its shard of one torrent through the HIP library against the
+    oracle's digests -- strong-scaled (the torrent's pieces split over the ranks) and weak-scaled (each rank its
+    own whole-size shard of an N-times larger torrent, the default `value`); rank 0 prints one valid JSON line
+    with an exact bitfield."""
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
-           "--workload", "tiny", "--strong", "--steps", "3", "--warmup", "1", "--no-cfg4", "--e2e-steps", "0",
+           "--workload", "tiny", "--" + scaling, "--steps", "3", "--warmup", "1", "--no-cfg4", "--e2e-steps", "0",
            "--no-cpu-baseline"]
     r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout
     rec = json.loads(lines[0])
-    assert rec["n_gpus"] == 2 and rec["scaling"] == "strong" and rec["bitfield_exact"] is True
-    assert rec["config"]["total_pieces"] == 1000 and rec["config"]["pieces_per_gpu"] == 504
+    assert rec["n_gpus"] == 2 and rec["scaling"] == scaling and rec["bitfield_exact"] is True
+    if scaling == "strong":
+        assert rec["config"]["total_pieces"] == 1000 and rec["config"]["pieces_per_gpu"] == 504
+    else:
+        assert rec["config"]["total_pieces"] == 2000 and rec["config"]["pieces_per_gpu"] == 1000
