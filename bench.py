@@ -454,8 +454,9 @@ def e2e_cfg5(dist, ws: int, rank: int, device: int, steps: int, threads: int, sh
         # pinned_pool: the torrent is a 1 GiB page-locked pool of 256 pieces repeated; rows DMA'd from it
         t_p0 = time.perf_counter()
         pool = _native.PinnedBuffer(POOL_PIECES * L)
-        pool.mv[:] = O.synth_fill(seed + 100, 0, POOL_PIECES * L)
-        pool_dig = O.hash_pieces(pool.mv, POOL_PIECES * L, L, POOL_PIECES, threads=threads)
+        from tests import synth   # (inputs and their hashlib digests; the oracle runs only as the ground truth)
+        synth.fill_into(pool.mv, seed + 100, 0, threads=threads)
+        pool_dig = synth.hash_pieces(pool.mv, L, POOL_PIECES, threads=threads)
         dp = bytearray(20 * P)
         for j in range(count):
             k = j % POOL_PIECES
@@ -512,10 +513,11 @@ def cfg3_leg(device: int, steps: int, warmup: int, kernel_opt: int, idle_s: floa
     steps with the shader clock probed (the value; frac_of_piece_ceiling is also given at the live clock), and
     (b) one-shot calls as a host makes them after `idle_s` of GPU idle: stage every file + verify, wall clock,
     with that call's kernel time and clock."""
+    from tests import synth
     from tests.layouts import build_layout, by_name
     t_leg = time.perf_counter()
     spec = by_name("cfg3")
-    lay = build_layout(spec)
+    lay = build_layout(spec, fill=synth.fill)   # (hashlib digests of tests/synth.py's bytes; bits: the golden file)
     info = lay["info"]
     golden = {r["name"]: r for r in json.load(open(os.path.join(ROOT, "tests", "golden", "layouts.json")))}["cfg3"]
     want = bytes.fromhex(golden["expected_bitfield"])

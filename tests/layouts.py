@@ -58,15 +58,19 @@ def _sizes(spec: dict, rng: random.Random):
     return sizes
 
 
-def build_layout(spec: dict) -> dict:
-    from oracle import oracle as O  # the byte generator only (pinned in test_oracle.py)
+def build_layout(spec: dict, fill=None) -> dict:
+    """fill(seed, off, n): the byte generator -- the oracle's by default (tests); tools and bench.py pass
+    tests/synth.py's numpy restatement of it (pinned equal in test_oracle.py), so they call nothing under oracle/."""
+    if fill is None:
+        from oracle import oracle as O  # the byte generator only (pinned in test_oracle.py)
+        fill = O.synth_fill
 
     rng = random.Random(spec["seed"])
     sizes = _sizes(spec, rng)
     L = spec["piece_length"]
     total = sum(sizes)
     files = [FileInfo(length=s, path=[f"d{k % 7}", f"f{k:05d}.bin"]) for k, s in enumerate(sizes)]
-    clean = O.synth_fill(spec["seed"], 0, total)
+    clean = fill(spec["seed"], 0, total)
     P = -(-total // L)
     pieces_raw = b"".join(hashlib.sha1(bytes(clean[i * L:min(total, (i + 1) * L)])).digest()
                           for i in range(P))

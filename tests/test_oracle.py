@@ -126,3 +126,20 @@ def test_synthetic_generator_definition(oracle):
     d = oracle.synth_piece_digests(42, 10000, 4096, 3, threads=2)
     full = oracle.synth_fill(42, 0, 10000)
     assert d == b"".join(hashlib.sha1(bytes(full[i:i + 4096])).digest() for i in range(0, 10000, 4096))
+
+
+def test_numpy_generator_equals_the_oracles(oracle):
+    """tests/synth.py (the numpy generator and hashlib digests the tools and bench.py generate inputs with, so they
+    call nothing under oracle/) gives the oracle's bytes at aligned and unaligned offsets, across its 16 MiB
+    chunks and threads, and the oracle's piece digests."""
+    import random
+    from tests import synth
+    rng = random.Random(5)
+    for seed in (0, 3, 2**64 - 1, 12345678901234567):
+        for off, n in [(0, 0), (0, 1), (7, 9), (13, 50), (8, 64), (rng.randrange(1 << 40), rng.randrange(1, 5000))]:
+            assert bytes(synth.fill(seed, off, n)) == bytes(oracle.synth_fill(seed, off, n)), (seed, off, n)
+    big = (16 << 20) * 2 + 12345
+    assert bytes(synth.fill(9, 5, big, threads=4)) == bytes(oracle.synth_fill(9, 5, big))
+    assert synth.piece_digests(42, 10000, 4096, 3, threads=2) == oracle.synth_piece_digests(42, 10000, 4096, 3)
+    buf = oracle.synth_fill(7, 0, 70000)
+    assert synth.hash_pieces(buf, 16384, 5) == oracle.hash_pieces(buf, 70000, 16384, 5)

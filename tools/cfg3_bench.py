@@ -15,13 +15,14 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from tests.layouts import build_layout, by_name  # noqa: E402
+from tests import synth  # noqa: E402
 from torrent_amd import verify_files, verify_payload  # noqa: E402
 from torrent_amd.verify import _context  # noqa: E402
 
 d = sys.argv[1]
 rec = {r["name"]: r for r in json.load(open(os.path.join(ROOT, "tests", "golden", "layouts.json")))}["cfg3"]
 t0 = time.perf_counter()
-lay = build_layout(by_name("cfg3"))
+lay = build_layout(by_name("cfg3"), fill=synth.fill)
 info = lay["info"]
 print(f"cfg3: {len(lay['sizes'])} files, {info.length:,} B, {info.n_pieces} pieces of {info.piece_length} B, "
       f"{len(lay['corrupted'])} corrupted (layout built in {time.perf_counter() - t0:.1f} s)", flush=True)

@@ -18,10 +18,11 @@ if os.environ.get("CPUS"):                      # before anything touches the GP
     os.sched_setaffinity(0, {c for a, b in lo_hi for c in range(a, b + 1)})
 sys.path.insert(0, os.environ["TV_ROOT"])
 from tests.layouts import build_layout, by_name
+from tests import synth  # noqa: E402
 from torrent_amd import verify_files
 d = sys.argv[1]
 rec = {r["name"]: r for r in json.load(open(os.path.join(os.environ["TV_ROOT"], "tests", "golden", "layouts.json")))}["cfg3"]
-info = build_layout(by_name("cfg3"))["info"]
+info = build_layout(by_name("cfg3"), fill=synth.fill)["info"]
 os.chdir(d)
 best = None
 for _ in range(5):
@@ -86,7 +87,7 @@ def numa_info():
 def main():
     d, names = sys.argv[1], sys.argv[2:]
     from tests.layouts import build_layout, by_name
-    lay = build_layout(by_name("cfg3"))
+    lay = build_layout(by_name("cfg3"), fill=synth.fill)
     for path, data in lay["disk_files"]().items():
         p = os.path.join(d, *path)
         os.makedirs(os.path.dirname(p), exist_ok=True)

@@ -13,11 +13,12 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from tests.layouts import build_layout, by_name  # noqa: E402
+from tests import synth  # noqa: E402
 from torrent_amd import _native, verify_files  # noqa: E402
 
 d = sys.argv[1]
 rec = {r["name"]: r for r in json.load(open(os.path.join(ROOT, "tests", "golden", "layouts.json")))}["cfg3"]
-lay = build_layout(by_name("cfg3"))
+lay = build_layout(by_name("cfg3"), fill=synth.fill)
 info = lay["info"]
 for path, data in lay["disk_files"]().items():
     p = os.path.join(d, *path)

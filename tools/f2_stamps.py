@@ -1,6 +1,6 @@
 """Stamped breakdown of verify_files on warm 16 GiB layouts.
 
-For each layout (single16: one 16 GiB file; files64: 16 GiB in 64 files; 1 MiB pieces, 1 % corrupted, the oracle's
+For each layout (single16: one 16 GiB file; files64: 16 GiB in 64 files; 1 MiB pieces, 1 % corrupted, hashlib's
 bits; written by tools/storage_paths_bench.write_layout) and each file-staging configuration of the library
 (TV_OPT_FILE_DIRECT: registered page-cache DMA vs preads into the pinned ring; TV_OPT_FILE_CONCURRENT: one or two
 staging lanes; reader threads), verify_files runs `reps` times on a warm page cache (residency measured by mincore

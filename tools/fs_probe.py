@@ -2,8 +2,9 @@ import os, sys, time
 from concurrent.futures import ThreadPoolExecutor
 sys.path.insert(0, os.getcwd())
 from tests.layouts import build_layout, by_name
+from tests import synth  # noqa: E402
 d = "/tmp/tvfsp"
-lay = build_layout(by_name("cfg3"))
+lay = build_layout(by_name("cfg3"), fill=synth.fill)
 paths = []
 for path, data in lay["disk_files"]().items():
     p = os.path.join(d, *path); os.makedirs(os.path.dirname(p), exist_ok=True)

@@ -9,11 +9,12 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from tests.layouts import build_layout, by_name  # noqa: E402
+from tests import synth  # noqa: E402
 from torrent_amd import _native  # noqa: E402
 from torrent_amd.storage import Storage, fs_storage  # noqa: E402
 
 d = sys.argv[1]
-lay = build_layout(by_name("cfg3"))
+lay = build_layout(by_name("cfg3"), fill=synth.fill)
 info = lay["info"]
 for path, data in lay["disk_files"]().items():
     p = os.path.join(d, *path)

@@ -1,7 +1,7 @@
 """The reference-shaped Storage paths against verify_files, warm and cold.
 
-Layouts written under <dir> (payload: the oracle's splitmix64 generator; digests: the CPU oracle, 1 % of them
-corrupted, so every result is checked against the oracle's bitfield):
+Layouts written under <dir> (payload: the splitmix64 generator, tests/synth.py's numpy form; digests: hashlib, 1 % of
+them corrupted, so every result is checked against hashlib's bitfield):
   cfg3      BASELINE config 3: 10,000 files of U[0, 512 KiB], 256 KiB pieces (tests/layouts.py; committed bits)
   single16  one 16 GiB file, 1 MiB pieces (cfg2's geometry)
   files64   16 GiB in 64 files, 1 MiB pieces (the round-1 resume-from-disk layout)
@@ -33,7 +33,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import fsutil  # noqa: E402
-from oracle import oracle as O  # noqa: E402  (the checker and the generator)
+from tests import synth  # noqa: E402  (the generator and hashlib digests: nothing under oracle/ runs here)
 from torrent_amd import FileInfo, Storage, make_info, verify_files, verify_pieces, verify_stream  # noqa: E402
 from torrent_amd.storage import FsStorage  # noqa: E402
 
@@ -139,7 +139,7 @@ def write_layout(name, d):
     os.makedirs(d, exist_ok=True)
     if name == "cfg3":
         from tests.layouts import build_layout, by_name
-        lay = build_layout(by_name("cfg3"))
+        lay = build_layout(by_name("cfg3"), fill=synth.fill)
         rec = {r["name"]: r for r in json.load(open(os.path.join(ROOT, "tests", "golden", "layouts.json")))}["cfg3"]
         paths = []
         for path, data in lay["disk_files"]().items():
@@ -153,10 +153,10 @@ def write_layout(name, d):
     P = total // L
     nf = 1 if name == "single16" else 64
     seed = 16 if nf == 1 else 64
-    digests = bytearray(O.synth_piece_digests(seed, total, L, P, threads=16))
+    digests = bytearray(synth.piece_digests(seed, total, L, P, threads=16))
     for i in range(5, P, 100):
         digests[20 * i + 3] ^= 0x08
-    bits = bytearray(b"\xff" * (P // 8))     # the oracle's digests of the written payload, 1 % corrupted
+    bits = bytearray(b"\xff" * (P // 8))     # hashlib digests of the written payload, 1 % corrupted
     for i in range(5, P, 100):
         bits[i >> 3] &= ~(0x80 >> (i & 7)) & 0xFF
     expect = bytes(bits)
@@ -174,7 +174,7 @@ def write_layout(name, d):
         with open(p, "wb") as f:
             for o in range(0, s, chunk):
                 n = min(chunk, s - o)
-                f.write(O.synth_fill(seed, off + o, n))
+                f.write(synth.fill(seed, off + o, n))
         off += s
     info = make_info(L, bytes(digests), "single16.bin" if nf == 1 else "files64", files=files, length=total)
     return info, expect, paths

@@ -1,6 +1,6 @@
 """verify_pieces / verify_stream over Storage(fs_storage) by reader threads (1 .. 16), page cache warm: how many
 threads the reference-shaped Storage paths should use per layout.  Every bitfield is checked against the committed /
-oracle bits.
+hashlib bits (tools/storage_paths_bench.write_layout).
 
     THREADS=1,2,4,8,16 REPS=2 python tools/threads_sweep.py DIR [cfg3|single16|files64 ...]"""
 import json

@@ -2,7 +2,7 @@
 tests/ts_harness, on the GPU) runs verifyPieces / verifyStream over a JS restatement of the reference's `Storage` +
 `fsStorage` (storage.ts:50-65,89-137,149-172: every get opens the file read + write, reads, closes -- here through
 Node's fs, whose work runs on libuv's thread pool as Deno's ops run on its blocking pool) and verifyFiles over the
-same directory.  Every bitfield is compared with the oracle's / the committed bits.
+same directory.  Every bitfield is compared with hashlib's / the committed bits.
 
     python tools/ts_storage_bench.py DIR [single16|files64|cfg3 ...]      (env UV_THREADPOOL_SIZE: libuv's pool;
                                                                            TS_SRC: another verify.ts, for A/Bs)

@@ -1,7 +1,7 @@
 """What a windowed layout costs: verify_payload over a payload in page-locked host memory with the whole shard
 resident (one window) and under smaller device budgets (TV_OPT_RESIDENT_BUDGET: windows of pieces staged while the
 previous window hashes), beside the streamed path (verify_stream over the same memory).  Every bitfield is checked
-against the oracle's digests of the payload (1 % of them corrupted).
+against hashlib's digests of the payload (1 % of them corrupted; tests/synth.py generates it).
 
     python tools/window_bench.py [--gib 16] [--piece-mib 1] [--budgets 0,8,2,0.5] [--reps 3]
 
@@ -17,7 +17,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from oracle import oracle as O  # noqa: E402  (the generator and the checker)
+from tests import synth  # noqa: E402  (the generator and hashlib digests: nothing under oracle/ runs here)
 from torrent_amd import _native as N  # noqa: E402
 from torrent_amd.metainfo import make_info  # noqa: E402
 from torrent_amd.verify import context_counters, verify_payload, verify_stream  # noqa: E402
@@ -40,8 +40,8 @@ def main():
     chunk = 256 * MiB
     for o in range(0, total, chunk):
         n = min(chunk, total - o)
-        ctypes.memmove(buf.ptr + o, bytes(O.synth_fill(seed, o, n)), n)
-    digests = bytearray(O.synth_piece_digests(seed, total, L, P, threads=16))
+        ctypes.memmove(buf.ptr + o, bytes(synth.fill(seed, o, n)), n)
+    digests = bytearray(synth.piece_digests(seed, total, L, P, threads=16))
     for i in range(5, P, 100):
         digests[20 * i + 3] ^= 0x08
     expect = bytearray(b"\xff" * ((P + 7) // 8))
