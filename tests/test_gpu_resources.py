@@ -389,3 +389,20 @@ def test_companions_stand_down_on_a_shared_gpu(native, oracle):
         time.sleep(1.1)
         assert ctx.verify() == want
         assert ctx.counter(native.TV_COUNTER_LAST_WORKGROUPS) == 2 * cus          # alone again
+
+
+def test_verify_files_name_with_a_nul_reads_as_null(native, tmp_path, monkeypatch):
+    """A file name holding a NUL cannot be opened (Deno.open throws inside fsStorage.get's try, so the reference's
+    piece is null, storage.ts:157-170): verify_files reports its pieces 0 -- no exception -- and the pieces of the
+    other files as their bytes say."""
+    from torrent_amd import make_info, verify_files
+    from torrent_amd.metainfo import FileInfo
+    L = 4096
+    data = [bytes((k * 7 + j) & 0xFF for j in range(L)) for k in range(3)]
+    names = [["a.bin"], ["bad\0name"], ["c.bin"]]
+    digests = b"".join(hashlib.sha1(d).digest() for d in data)
+    info = make_info(L, digests, "t", files=[FileInfo(L, n) for n in names])
+    (tmp_path / "a.bin").write_bytes(data[0])
+    (tmp_path / "c.bin").write_bytes(data[2])
+    monkeypatch.chdir(tmp_path)
+    assert _bits(verify_files(info, str(tmp_path)), 3) == [1, 0, 1]

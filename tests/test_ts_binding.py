@@ -456,6 +456,21 @@ import("{mod}").then(async (m) => {{
         if n:
             assert any(sg[0] == want[k] and sg[3] > 0 for sg in segs), (k, got_paths)
     assert "" in got_paths                                          # the NUL name: unopenable, as in Deno
+    # the Python host hands the library the same paths ("" for the NUL name; no exception)
+    from torrent_amd import make_info, verify
+    from torrent_amd.metainfo import FileInfo
+    from torrent_amd.storage import Storage, fs_storage
+
+    class Raw(_PlanCtx):
+        def stage_files(self, paths, fo, lin, lens):
+            # (Storage keeps the directory relative to the working directory, storage.ts: compare absolute paths)
+            self.segments += [os.path.abspath(p) if p else "" for p, n in zip(paths, lens) if n]
+            return [0] * len(paths)
+
+    info = make_info(L, bytes(20 * P), "t", files=[FileInfo(n, p) for n, p in zip(sizes, names)])
+    ctx = Raw()
+    verify._files_shard(ctx, info, Storage(fs_storage, info, "/r"), 0, P, threads=1)
+    assert sorted(set(ctx.segments)) == sorted({sg[0] for sg in segs if sg[3] > 0})
 
 
 def test_verify_stream_host_logic_on_cpu(tmp_path):

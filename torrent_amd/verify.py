@@ -439,7 +439,9 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
         nbytes = np.concatenate([nbytes, np.zeros(len(zk), np.int64)])
     if len(k) == 0:
         return avail
-    paths = storage.file_paths()
+    # a path holding a NUL cannot be opened (Deno.open throws, so fsStorage.get's piece is null, storage.ts:157-170):
+    # it goes as "", which the library cannot open either (ts/verify.ts does the same)
+    paths = [p if "\0" not in p else "" for p in storage.file_paths()]
     ctx.set_option(_native.TV_OPT_FILE_THREADS, max(1, threads))
     ctx.set_option(_native.TV_OPT_OPEN_RW, 1 if open_rw else 0)
     ctx.set_option(_native.TV_OPT_FILE_DIRECT_MIN, _DIRECT_MIN_BYTES if direct_min is None else direct_min)
