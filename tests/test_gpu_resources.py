@@ -398,11 +398,13 @@ def test_verify_files_name_with_a_nul_reads_as_null(native, tmp_path, monkeypatc
     from torrent_amd import make_info, verify_files
     from torrent_amd.metainfo import FileInfo
     L = 4096
-    data = [bytes((k * 7 + j) & 0xFF for j in range(L)) for k in range(3)]
-    names = [["a.bin"], ["bad\0name"], ["c.bin"]]
-    digests = b"".join(hashlib.sha1(d).digest() for d in data)
-    info = make_info(L, digests, "t", files=[FileInfo(L, n) for n in names])
-    (tmp_path / "a.bin").write_bytes(data[0])
-    (tmp_path / "c.bin").write_bytes(data[2])
+    payload = bytes((j * 7 + 3) & 0xFF for j in range(3 * L))
+    # a: piece 0; the NUL name: 100 bytes of piece 1; c: the rest of piece 1 and piece 2 (the NUL name does not end
+    # on piece 2's start, where Storage.get's walk would open it again with 0 bytes and null piece 2 as well)
+    sizes, names = [L, 100, 2 * L - 100], [["a.bin"], ["bad\0name"], ["c.bin"]]
+    digests = b"".join(hashlib.sha1(payload[i * L:(i + 1) * L]).digest() for i in range(3))
+    info = make_info(L, digests, "t", files=[FileInfo(n, p) for n, p in zip(sizes, names)])
+    (tmp_path / "a.bin").write_bytes(payload[:L])
+    (tmp_path / "c.bin").write_bytes(payload[L + 100:])
     monkeypatch.chdir(tmp_path)
     assert _bits(verify_files(info, str(tmp_path)), 3) == [1, 0, 1]
