@@ -322,6 +322,8 @@ def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: b
            "value": round(bytes_all * steps / elapsed / 1e9, 2), "unit": "GB/s", "steps": steps, "warmup": warmup,
            "ms_per_step": round(elapsed * 1e3 / steps, 3), "scaling": "strong" if strong else "weak",
            "kernel": KERNEL_NAMES.get(kernel, str(kernel)), "kernel_ms_avg": round(avg, 3),
+           "kernel_ms_median": round(sorted(kernel_ms)[len(kernel_ms) // 2], 3),
+           "kernel_ms_min_max": [round(min(kernel_ms), 3), round(max(kernel_ms), 3)],
            "kernel_ms_max_over_ranks": round(_max(dist, avg), 3), "achieved": round(achieved, 1),
            "piece_parallelism_ceiling": round(ceiling, 1), "frac_of_piece_ceiling": round(achieved / ceiling, 4),
            "frac_of_valu_peak": round(achieved / VALU_PEAK_GBPS, 4),
@@ -583,7 +585,8 @@ def cfg3_leg(device: int, steps: int, warmup: int, kernel_opt: int, idle_s: floa
             "short_last_piece": total % L, "corrupted": len(lay["corrupted"]),
             "value": round(total * steps / (t1 - t0) / 1e9, 2), "unit": "GB/s", "steps": steps, "warmup": warmup,
             "ms_per_step": round((t1 - t0) * 1e3 / steps, 3), "kernel": KERNEL_NAMES.get(kernel, str(kernel)),
-            "kernel_ms_avg": round(avg, 3), "achieved": round(achieved, 1),
+            "kernel_ms_avg": round(avg, 3), "kernel_ms_median": round(sorted(kernel_ms)[len(kernel_ms) // 2], 3),
+            "kernel_ms_min_max": [round(min(kernel_ms), 3), round(max(kernel_ms), 3)], "achieved": round(achieved, 1),
             "piece_parallelism_ceiling": round(ceiling, 1), "frac_of_piece_ceiling": round(achieved / ceiling, 4),
             "clock_ghz": round(clock_ghz, 3) if clock_ghz else None,
             "piece_ceiling_at_clock": round(ceiling_at_clock, 1) if ceiling_at_clock else None,
@@ -735,7 +738,8 @@ def main() -> int:
                          "frac": round(achieved / ROOF_PEAK_GBPS, 4), "traffic": traffic,
                          "traffic_ratio": round(traffic / bytes_per_gpu, 6) if traffic else None,
                          "traffic_source": traffic_note, "build_id": _native.build_id(),
-                         "kernel_ms_avg": main_leg["kernel_ms_avg"],
+                         "kernel_ms_avg": main_leg["kernel_ms_avg"], "kernel_ms_median": main_leg["kernel_ms_median"],
+                         "kernel_ms_min_max": main_leg["kernel_ms_min_max"],
                          "kernel_ms_max_over_ranks": main_leg["kernel_ms_max_over_ranks"],
                          "algorithmic_bytes_per_launch": bytes_per_gpu,
                          "peak_is": "min(HBM 8000 GB/s, R_valu)", "valu_peak": round(VALU_PEAK_GBPS, 1),
