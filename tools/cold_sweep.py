@@ -43,6 +43,14 @@ def main():
             ctx.set_option(_native.TV_OPT_FILE_ODIRECT, 1)
         legs = [("ceiling direct 16x4MiB", 16), ("ceiling direct 64x4MiB", 64),
                 ("verify_files O_DIRECT", 16), ("verify_files O_DIRECT", 32), ("verify_files O_DIRECT", 64)]
+        if os.environ.get("COLD_DEPTH"):      # reads in flight: fewer threads, one or two lanes, C reader alike
+            legs = [("ceiling direct 8x4MiB", 8), ("verify_files O_DIRECT", 8), ("verify_files O_DIRECT", 4),
+                    ("verify_files O_DIRECT 1 lane", 8), ("ceiling direct 4x4MiB", 4), ("verify_files O_DIRECT", 12),
+                    ("ceiling direct 12x4MiB", 12), ("verify_files O_DIRECT", 16)]
+        if os.environ.get("COLD_LANES"):      # also one staging lane (TV_OPT_FILE_CONCURRENT = 0)
+            legs = [("ceiling direct 16x4MiB", 16), ("verify_files O_DIRECT", 16),
+                    ("verify_files O_DIRECT 1 lane", 16), ("verify_files O_DIRECT 1 lane", 32),
+                    ("ceiling direct 8x4MiB", 8), ("ceiling direct 32x4MiB", 32)]
         for rnd in range(rounds):
             for what, thr in legs:
                 res = fsutil.drop_cache(paths)
@@ -59,6 +67,7 @@ def main():
                 else:
                     with _context(0) as ctx:
                         ctx._reset_file_clock()
+                        ctx.set_option(_native.TV_OPT_FILE_CONCURRENT, 0 if "1 lane" in what else 1)
                     t = time.perf_counter()
                     bf = verify_files(info, root, threads=thr)
                     el = time.perf_counter() - t
