@@ -47,6 +47,26 @@ def main():
             legs = [("ceiling direct 8x4MiB", 8), ("verify_files O_DIRECT", 8), ("verify_files O_DIRECT", 4),
                     ("verify_files O_DIRECT 1 lane", 8), ("ceiling direct 4x4MiB", 4), ("verify_files O_DIRECT", 12),
                     ("ceiling direct 12x4MiB", 12), ("verify_files O_DIRECT", 16)]
+        if os.environ.get("COLD_PROBE"):      # what the library's reader differs in from the C reader
+            legs = [("ceiling direct 4x4MiB", 4), ("ceiling direct 4x4MiB pinned", 4),
+                    ("ceiling direct 4x4MiB node", 4), ("ceiling direct 4x4MiB pinned node", 4),
+                    ("verify_files O_DIRECT 1 lane", 4), ("verify_files O_DIRECT 1 lane nobind", 4)]
+        if os.environ.get("COLD_SPREAD"):     # destination footprint: a 4 MiB buffer per reader vs a 192 MiB ring
+            legs = [("ceiling direct 4x4MiB", 4), ("ceiling direct 4x4MiB spread", 4),
+                    ("ceiling direct 4x4MiB pinned spread", 4), ("verify_files O_DIRECT 1 lane", 4),
+                    ("ceiling direct 16x4MiB spread", 16), ("ceiling direct 16x4MiB", 16)]
+        if os.environ.get("COLD_SUB"):        # the sub-buffered cold path (TV_OPT_FILE_COLD_SUB / _COLD_THREADS)
+            legs = [("ceiling direct 4x4MiB", 4), ("verify_files O_DIRECT", 16), ("verify_files O_DIRECT sub16", 16),
+                    ("verify_files O_DIRECT sub16 1 lane", 16), ("verify_files O_DIRECT sub8", 16),
+                    ("verify_files O_DIRECT sub16 t2", 16), ("verify_files O_DIRECT sub32 t8", 16),
+                    ("ceiling direct 4x4MiB spread32", 4)]
+        if os.environ.get("COLD_FOOT"):       # the destination footprint at which the reads slow down
+            legs = [("ceiling direct 4x4MiB", 4), ("ceiling direct 4x4MiB spread16", 4),
+                    ("ceiling direct 4x4MiB spread32", 4), ("ceiling direct 4x4MiB spread64", 4),
+                    ("ceiling direct 8x4MiB spread32", 8), ("ceiling direct 6x4MiB spread48", 6)]
+        if os.environ.get("COLD_FEW"):        # few reads in flight, the library on one lane against the C reader
+            legs = [("ceiling direct 4x4MiB", 4), ("verify_files O_DIRECT 1 lane", 4), ("verify_files O_DIRECT", 4),
+                    ("ceiling direct 2x4MiB", 2), ("verify_files O_DIRECT 1 lane", 2), ("verify_files O_DIRECT", 16)]
         if os.environ.get("COLD_LANES"):      # also one staging lane (TV_OPT_FILE_CONCURRENT = 0)
             legs = [("ceiling direct 16x4MiB", 16), ("verify_files O_DIRECT", 16),
                     ("verify_files O_DIRECT 1 lane", 16), ("verify_files O_DIRECT 1 lane", 32),
@@ -60,14 +80,32 @@ def main():
                     emit(rec)
                     continue
                 if what.startswith("ceiling"):
+                    env = {}
+                    if "pinned" in what:
+                        env["RC_HOST_ALLOC_LIB"] = os.path.join(ROOT, "torrent_amd", "libtorrent_verify.so")
+                    if "spread" in what:
+                        mib = what.split("spread", 1)[1].split()[0] if what.split("spread", 1)[1][:1].isdigit() else "192"
+                        env["RC_SPREAD"] = str(int(mib) * MiB)
+                    if "node" in what:
+                        with _context(0) as ctx:
+                            nd = ctx.counter(_native.TV_COUNTER_NUMA_NODE)
+                        env["RC_CPU_NODE"] = str(nd if nd < (1 << 63) else 0)
+                        rec["node"] = env["RC_CPU_NODE"]
                     t = time.perf_counter()
-                    got = read_ceiling(paths, threads=thr, part=4 * MiB, direct=True)
+                    got = read_ceiling(paths, threads=thr, part=4 * MiB, direct=True, env=env)
                     rec["gbps"] = round(got / 1e9, 2) if got else None
                     rec["s"] = round(time.perf_counter() - t, 3)
                 else:
                     with _context(0) as ctx:
                         ctx._reset_file_clock()
                         ctx.set_option(_native.TV_OPT_FILE_CONCURRENT, 0 if "1 lane" in what else 1)
+                        ctx.set_option(_native.TV_OPT_NUMA_BIND, 0 if "nobind" in what else 1)
+                        import re
+                        m = re.search(r"sub(\d+)", what)
+                        if m or os.environ.get("COLD_SUB"):
+                            ctx.set_option(_native.TV_OPT_FILE_COLD_SUB, int(m.group(1)) * MiB if m else 0)
+                        m = re.search(r" t(\d+)", what)
+                        ctx.set_option(_native.TV_OPT_FILE_COLD_THREADS, int(m.group(1)) if m else 4)
                     t = time.perf_counter()
                     bf = verify_files(info, root, threads=thr)
                     el = time.perf_counter() - t

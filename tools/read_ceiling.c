@@ -5,9 +5,15 @@
  * way (the round-4 Python reader under-measured it for 10,000 small files).
  * A third argument "direct" opens the files O_DIRECT (reads bypass the page cache; the length of each request is
  * rounded up to 4 KiB, the file end returns short).
- * build: gcc -O2 -pthread tools/read_ceiling.c -o read_ceiling;  usage: read_ceiling THREADS PART_BYTES [direct] < paths */
+ * Environment (probes of what the library's reader differs in): RC_HOST_ALLOC_LIB=<libtorrent_verify.so> reads into
+ * buffers from its tv_host_alloc (page-locked, as the library's staging ring); RC_CPU_NODE=<n> pins the readers to the
+ * CPUs of NUMA node n (as the library pins its readers next to the GPU); RC_SPREAD=<bytes> reads request t into a
+ * shared buffer of that size at (t mod (bytes / part)) * part, as the library's readers fill its ring slots.
+ * build: gcc -O2 -pthread tools/read_ceiling.c -o read_ceiling -ldl;  usage: read_ceiling THREADS PART_BYTES [direct] < paths */
 #define _GNU_SOURCE
+#include <dlfcn.h>
 #include <fcntl.h>
+#include <sched.h>
 #include <pthread.h>
 #include <stdatomic.h>
 #include <stdint.h>
@@ -26,9 +32,22 @@ static uint64_t* first_task;
 static atomic_uint_fast64_t next_task, total_bytes;
 static int direct;
 
+static int (*host_alloc)(uint64_t, void**);
+static char* spread_buf;
+static uint64_t spread_parts;
+static cpu_set_t node_cpus;
+static int pin_node;
+
 static void* worker(void* arg) {
     (void)arg;
-    char* buf = aligned_alloc(4096, part);
+    if (pin_node) sched_setaffinity(0, sizeof node_cpus, &node_cpus);
+    char* buf = NULL;
+    if (host_alloc) {
+        void* p = NULL;
+        if (host_alloc(part, &p) == 0) buf = p;
+    }
+    const int own = buf == NULL;
+    if (own) buf = aligned_alloc(4096, part);
     for (;;) {
         const uint64_t t = atomic_fetch_add(&next_task, 1);
         if (t >= ntasks) break;
@@ -36,7 +55,8 @@ static void* worker(void* arg) {
         uint64_t off = (t - first_task[task_file[t]]) * part, n = f->size - off < part ? f->size - off : part;
         while (n) {
             const uint64_t ask = direct ? (n + 4095) / 4096 * 4096 : n;
-            const ssize_t got = pread(f->fd, buf, ask, (off_t)off);
+            char* dst = spread_buf ? spread_buf + (t % spread_parts) * part : buf;
+            const ssize_t got = pread(f->fd, dst, ask, (off_t)off);
             if (got <= 0) break;
             const uint64_t g = (uint64_t)got < n ? (uint64_t)got : n;
             atomic_fetch_add(&total_bytes, g);
@@ -45,7 +65,7 @@ static void* worker(void* arg) {
             if ((uint64_t)got < ask && n) break;
         }
     }
-    free(buf);
+    if (own) free(buf);   /* (a tv_host_alloc buffer lives until the process ends) */
     return NULL;
 }
 
@@ -54,6 +74,41 @@ int main(int argc, char** argv) {
     const int threads = atoi(argv[1]);
     part = strtoull(argv[2], NULL, 10);
     direct = argc > 3 && strcmp(argv[3], "direct") == 0;
+    const char* lib = getenv("RC_HOST_ALLOC_LIB");
+    if (lib && lib[0]) {
+        void* h = dlopen(lib, RTLD_NOW);
+        if (h) host_alloc = (int (*)(uint64_t, void**))dlsym(h, "tv_host_alloc");
+        if (!host_alloc) { fprintf(stderr, "RC_HOST_ALLOC_LIB: %s\n", dlerror()); return 3; }
+    }
+    const char* spread = getenv("RC_SPREAD");
+    if (spread && spread[0]) {
+        const uint64_t sb = strtoull(spread, NULL, 10) / part * part;
+        spread_parts = sb / part;
+        if (spread_parts) {
+            void* p = NULL;
+            if (host_alloc && host_alloc(sb, &p) == 0) spread_buf = p;
+            else spread_buf = aligned_alloc(4096, sb);
+            memset(spread_buf, 0, sb);
+        }
+    }
+    const char* node = getenv("RC_CPU_NODE");
+    if (node && node[0]) {
+        char path[128], list[4096];
+        snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", atoi(node));
+        FILE* f = fopen(path, "r");
+        if (f && fgets(list, sizeof list, f)) {
+            CPU_ZERO(&node_cpus);
+            for (char* tok = strtok(list, ",\n"); tok; tok = strtok(NULL, ",\n")) {
+                int a = 0, b = 0;
+                if (sscanf(tok, "%d-%d", &a, &b) == 2) { for (int c = a; c <= b; c++) CPU_SET(c, &node_cpus); }
+                else if (sscanf(tok, "%d", &a) == 1) CPU_SET(a, &node_cpus);
+            }
+            cpu_set_t mine;
+            if (sched_getaffinity(0, sizeof mine, &mine) == 0) CPU_AND(&node_cpus, &node_cpus, &mine);
+            pin_node = CPU_COUNT(&node_cpus) > 0;
+        }
+        if (f) fclose(f);
+    }
     uint64_t cap = 1024;
     files = malloc(cap * sizeof(file_t));
     char line[8192];

@@ -79,21 +79,22 @@ def _read_ceiling_bin():
         import tempfile
         exe = os.path.join(tempfile.gettempdir(), f"read_ceiling_{os.getpid()}")
         try:
-            subprocess.check_call(["gcc", "-O2", "-pthread", os.path.join(ROOT, "tools", "read_ceiling.c"), "-o", exe])
+            subprocess.check_call(["gcc", "-O2", "-pthread", os.path.join(ROOT, "tools", "read_ceiling.c"), "-o", exe,
+                                   "-ldl"])
             _RC_BIN = exe
         except (OSError, subprocess.CalledProcessError):
             _RC_BIN = ""
     return _RC_BIN or None
 
 
-def read_ceiling(paths, threads=16, part=4 * MiB, direct=False):
+def read_ceiling(paths, threads=16, part=4 * MiB, direct=False, env=None):
     """Bytes/s of reading every file with `threads` parallel preads of `part` bytes (nothing kept): the C reader
     tools/read_ceiling.c (no GIL in the way: the Python form under-measured 10,000 small files), else Python."""
     exe = _read_ceiling_bin()
     if exe:
         import subprocess
         r = subprocess.run([exe, str(threads), str(part)] + (["direct"] if direct else []), input="\n".join(paths),
-                           capture_output=True, text=True, check=True)
+                           capture_output=True, text=True, check=True, env={**os.environ, **(env or {})})
         rec = json.loads(r.stdout)
         return rec["bytes"] / rec["seconds"]
     if direct:
