@@ -15,24 +15,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 pytestmark = pytest.mark.gpu
-SUB_DEFAULT = None   # the library's default TV_OPT_FILE_COLD_SUB, read once (tests restore it)
-
-
-@pytest.fixture(autouse=True)
-def _cold_sub_default(native):
-    global SUB_DEFAULT
-    if SUB_DEFAULT is None:
-        with native.Context(0) as ctx:
-            SUB_DEFAULT = ctx.get_option(native.TV_OPT_FILE_COLD_SUB)
 
 
 def _bits(bf, n):
     return [(bf[i >> 3] >> (7 - (i & 7))) & 1 for i in range(n)]
 
 
-@pytest.mark.parametrize("sub", [0, 16 << 20, 1 << 20])
 @pytest.mark.parametrize("odirect", [1, 0, 2])
-def test_cold_files_exact(native, oracle, tmp_path, odirect, sub):
+def test_cold_files_exact(native, oracle, tmp_path, odirect):
     import fsutil
     from torrent_amd import FileInfo, Storage, make_info, verify_files
     from torrent_amd.storage import fs_storage
@@ -65,7 +55,6 @@ def test_cold_files_exact(native, oracle, tmp_path, odirect, sub):
         want[i] = int(b is not None and hashlib.sha1(b).digest() == bytes(digests[20 * i:20 * i + 20]))
     with _context(0) as ctx:
         ctx.set_option(native.TV_OPT_FILE_ODIRECT, odirect)
-        ctx.set_option(native.TV_OPT_FILE_COLD_SUB, sub)   # (0: whole ring slots; else the sub-buffered cold path)
         ctx._reset_file_clock()
     # warm (just written): read through the page cache, never O_DIRECT (an overlay /tmp once made warm files look
     # cold to cachestat and sent them to the disk at a third of the speed)
@@ -92,7 +81,6 @@ def test_cold_files_exact(native, oracle, tmp_path, odirect, sub):
     finally:
         with _context(0) as ctx:
             ctx.set_option(native.TV_OPT_FILE_ODIRECT, 1)
-            ctx.set_option(native.TV_OPT_FILE_COLD_SUB, SUB_DEFAULT)
     assert _bits(bf, P) == want
     if odirect == 1:
         assert clock["bytes_odirect"] > 0, clock      # (the cold chunks whose offsets agree mod 4 went O_DIRECT)
@@ -129,25 +117,14 @@ def test_random_layouts_cold_long_path(native, tmp_path, monkeypatch, seed):
     stride = -(-info.piece_length // 64) * 64 + 256
     # whole shards on one and three devices, then a windowed layout (a budget of ~3 pieces per window: the lanes
     # stage window by window, each window hashed while the next stages)
-    from torrent_amd.verify import _context
-    for devices, budget, sub in (([0], None, 0), ([0, 0, 0], None, 0), ([0], 2 * (3 * stride + 256), 0),
-                                 ([0], None, 1 << 20), ([0, 0], 2 * (3 * stride + 256), 1 << 20)):
-        for slot in range(len(devices)):
-            with _context(0, slot) as ctx:
-                ctx.set_option(native.TV_OPT_FILE_COLD_SUB, sub)
+    for devices, budget in (([0], None), ([0, 0, 0], None), ([0], 2 * (3 * stride + 256))):
         if paths:
             assert fsutil.drop_cache(paths) <= 0.01
-        try:
-            bf = verify_files(info, str(tmp_path / "dl"), devices=devices, threads=4, direct_min=1, budget=budget)
-        finally:
-            for slot in range(len(devices)):
-                with _context(0, slot) as ctx:
-                    ctx.set_option(native.TV_OPT_FILE_COLD_SUB, SUB_DEFAULT)
-        assert _bits(bf, P) == want_fs, (seed, devices, budget, sub)
+        bf = verify_files(info, str(tmp_path / "dl"), devices=devices, threads=4, direct_min=1, budget=budget)
+        assert _bits(bf, P) == want_fs, (seed, devices, budget)
 
 
-@pytest.mark.parametrize("sub", [0, 16 << 20])
-def test_cold_file_end_stays_o_direct(native, oracle, tmp_path, sub):
+def test_cold_file_end_stays_o_direct(native, oracle, tmp_path):
     """A cold file whose size is not a multiple of 4 KiB: the O_DIRECT request for its last chunk runs past the end
     of the file and comes back short.  That read is complete (the bytes asked for are in) and must not be continued
     (a next request would start off a 4 KiB boundary and be refused, sending the chunk through the buffered fallback
@@ -168,7 +145,6 @@ def test_cold_file_end_stays_o_direct(native, oracle, tmp_path, sub):
     assert fsutil.drop_cache([str(f)]) <= 0.01
     with _context(0) as ctx:
         ctx.set_option(native.TV_OPT_FILE_ODIRECT, 1)
-        ctx.set_option(native.TV_OPT_FILE_COLD_SUB, sub)
         ctx._reset_file_clock()
     cwd = os.getcwd()
     os.chdir(str(tmp_path))
@@ -178,6 +154,5 @@ def test_cold_file_end_stays_o_direct(native, oracle, tmp_path, sub):
         os.chdir(cwd)
     with _context(0) as ctx:
         clock = ctx._file_clock()
-        ctx.set_option(native.TV_OPT_FILE_COLD_SUB, SUB_DEFAULT)
     assert _bits(bf, P) == [1] * (P - 1) + [0]
     assert clock["bytes_odirect"] == clock["bytes_read"] == total, clock

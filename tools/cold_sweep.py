@@ -55,11 +55,6 @@ def main():
             legs = [("ceiling direct 4x4MiB", 4), ("ceiling direct 4x4MiB spread", 4),
                     ("ceiling direct 4x4MiB pinned spread", 4), ("verify_files O_DIRECT 1 lane", 4),
                     ("ceiling direct 16x4MiB spread", 16), ("ceiling direct 16x4MiB", 16)]
-        if os.environ.get("COLD_SUB"):        # the sub-buffered cold path (TV_OPT_FILE_COLD_SUB / _COLD_THREADS)
-            legs = [("ceiling direct 4x4MiB", 4), ("verify_files O_DIRECT", 16), ("verify_files O_DIRECT sub16", 16),
-                    ("verify_files O_DIRECT sub16 1 lane", 16), ("verify_files O_DIRECT sub8", 16),
-                    ("verify_files O_DIRECT sub16 t2", 16), ("verify_files O_DIRECT sub32 t8", 16),
-                    ("ceiling direct 4x4MiB spread32", 4)]
         if os.environ.get("COLD_FOOT"):       # the destination footprint at which the reads slow down
             legs = [("ceiling direct 4x4MiB", 4), ("ceiling direct 4x4MiB spread16", 4),
                     ("ceiling direct 4x4MiB spread32", 4), ("ceiling direct 4x4MiB spread64", 4),
@@ -100,12 +95,6 @@ def main():
                         ctx._reset_file_clock()
                         ctx.set_option(_native.TV_OPT_FILE_CONCURRENT, 0 if "1 lane" in what else 1)
                         ctx.set_option(_native.TV_OPT_NUMA_BIND, 0 if "nobind" in what else 1)
-                        import re
-                        m = re.search(r"sub(\d+)", what)
-                        if m or os.environ.get("COLD_SUB"):
-                            ctx.set_option(_native.TV_OPT_FILE_COLD_SUB, int(m.group(1)) * MiB if m else 0)
-                        m = re.search(r" t(\d+)", what)
-                        ctx.set_option(_native.TV_OPT_FILE_COLD_THREADS, int(m.group(1)) if m else 4)
                     t = time.perf_counter()
                     bf = verify_files(info, root, threads=thr)
                     el = time.perf_counter() - t

@@ -46,8 +46,6 @@ TV_OPT_TWIN_FILL_READS = 14
 TV_OPT_NUMA_BIND = 15
 TV_OPT_LANE_PAIRS = 21
 TV_OPT_FILE_ODIRECT = 22
-TV_OPT_FILE_COLD_SUB = 23
-TV_OPT_FILE_COLD_THREADS = 24
 TV_OPT_FILE_CLOCK_RESET = 100
 TV_COUNTER_FILE_CLOCK = 100
 TV_COUNTER_COTENANT_VRAM = 120

@@ -163,15 +163,6 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
             if (value < 0 || value > 2) return fail(c, TV_ERR_ARG, "TV_OPT_FILE_ODIRECT must be 0, 1 or 2");
             c->file_odirect = (int)value;
             return TV_OK;
-        case TV_OPT_FILE_COLD_SUB:
-            if (value != 0 && (value < (1 << 20) || (uint64_t)value > kRingSlotBytes / 2 || value % 65536))
-                return fail(c, TV_ERR_ARG, "TV_OPT_FILE_COLD_SUB must be 0 or a multiple of 64 KiB in 1 MiB .. 32 MiB");
-            c->file_cold_sub = (uint64_t)value;
-            return TV_OK;
-        case TV_OPT_FILE_COLD_THREADS:
-            if (value < 1 || value > 64) return fail(c, TV_ERR_ARG, "TV_OPT_FILE_COLD_THREADS must be 1 .. 64");
-            c->file_cold_threads = (int)value;
-            return TV_OK;
         case TV_OPT_RESIDENT:
             if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_RESIDENT must be 0 or 1");
             c->resident = value != 0;  // takes effect at the next tv_set_layout
@@ -248,8 +239,6 @@ int tv_get_option(tv_ctx* c, int key, int64_t* value) {
         case TV_OPT_FILE_THREADS: *value = c->file_threads; return TV_OK;
         case TV_OPT_FILE_CONCURRENT: *value = c->file_concurrent ? 1 : 0; return TV_OK;
         case TV_OPT_FILE_ODIRECT: *value = c->file_odirect; return TV_OK;
-        case TV_OPT_FILE_COLD_SUB: *value = (int64_t)c->file_cold_sub; return TV_OK;
-        case TV_OPT_FILE_COLD_THREADS: *value = c->file_cold_threads; return TV_OK;
         case TV_OPT_RESIDENT: *value = c->resident ? 1 : 0; return TV_OK;
         case TV_OPT_DEBUG_REBOUNCE: *value = c->debug_rebounce ? 1 : 0; return TV_OK;
         case TV_OPT_TWIN_PACK: *value = c->twin_pack ? 1 : 0; return TV_OK;

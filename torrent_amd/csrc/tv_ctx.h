@@ -169,8 +169,6 @@ struct tv_ctx {
     bool file_direct = false;            // TV_OPT_FILE_DIRECT: long segments DMA'd from registered page-cache pages
     bool file_concurrent = true;         // tv_stage_files: long segments on two staging lanes
     int file_odirect = 1;                // TV_OPT_FILE_ODIRECT: cold chunks read with O_DIRECT (2: its reads fail, tests)
-    uint64_t file_cold_sub = 0;          // TV_OPT_FILE_COLD_SUB: sub-buffer bytes of the cold path (0: whole slots)
-    int file_cold_threads = 4;           // TV_OPT_FILE_COLD_THREADS: readers per lane on that path
     uint64_t file_direct_min = 32ull << 20;  // tv_stage_files: segments >= this take the tv_stage_file path
     int file_threads = 16;                   // tv_stage_files: reader threads
     bool resident = true;                    // TV_OPT_RESIDENT

@@ -187,56 +187,6 @@ int unit_open(tv_ctx* c, FileWindows& win, const FileUnit& u) {
     return TV_OK;
 }
 
-// The sub-buffered cold path (TV_OPT_FILE_COLD_SUB): chunk bytes [fo, fo + n) of the O_DIRECT descriptor `dfd` ->
-// LINEAR [p, p + n), through two sub-buffers at the start of one ring slot of `lane`: sub-chunk i + 1 is read (by
-// `threads` readers) while sub-chunk i is DMA'd, and a sub-buffer is read into again only once the DMA that read it
-// two sub-chunks before has finished (ev[0..1]).  The reads land in 2 x sub bytes of re-used memory instead of
-// across the lane's ring.  *done = the bytes staged.  Returns TV_OK, a HIP / state error, or TV_ERR_IO with *err =
-// the errno of the O_DIRECT read that failed (the caller reads the rest of the chunk buffered).
-int cold_sub_chunk(tv_ctx* c, int lane, int threads, int dfd, uint64_t fo, uint64_t p, uint64_t n, hipEvent_t* ev,
-                   uint64_t* done, int* err) {
-    const uint64_t sub = c->file_cold_sub, step = sub - 8192;  // (room for an O_DIRECT read's 4 KiB rounding)
-    hipStream_t cs = lane_stream(c, lane);
-    *done = 0;
-    *err = 0;
-    SlotLease slot(c, lane);  // lent until every copy out of it is queued
-    {
-        FileClock t(c, TV_FILE_PHASE_WAIT);
-        const int rc = slot.take();
-        if (rc) return rc;
-    }
-    for (uint64_t q = 0, i = 0; q < n; q += step, i++) {
-        const uint64_t kq = std::min(step, n - q);
-        uint8_t* sb = slot.ptr() + (i & 1) * sub;
-        if (i >= 2) {
-            FileClock t(c, TV_FILE_PHASE_WAIT);
-            TV_HIP(c, hipEventSynchronize(ev[i & 1]));
-        }
-        const uint64_t al = (fo + q) / 4096 * 4096, lead = fo + q - al;
-        int e;
-        {
-            FileClock t(c, TV_FILE_PHASE_READ);
-            e = c->file_odirect == 2 ? EINVAL  // (fault injection: the filesystem refusing O_DIRECT reads)
-                                     : pread_pool(c->pool[lane], threads, dfd, sb, al, (lead + kq + 4095) / 4096 * 4096,
-                                                  lead + kq);
-        }
-        if (e) {
-            *err = e;
-            return TV_ERR_IO;
-        }
-        {
-            FileClock t(c, TV_FILE_PHASE_QUEUE);
-            const int rc = stage_range(c, p + q, p + q + kq, sb + lead, p + q, true, lane, /*src_in_ring=*/true);
-            if (rc) return rc;
-        }
-        TV_HIP(c, hipEventRecord(ev[i & 1], cs));
-        c->file_ns[TV_FILE_BYTES_ODIRECT].fetch_add(kq, std::memory_order_relaxed);
-        c->file_ns[TV_FILE_BYTES_READ].fetch_add(kq, std::memory_order_relaxed);
-        *done = q + kq;
-    }
-    return slot.release();
-}
-
 // Stage the units (each lane's in ascending linear order) on staging lane `lane` with `threads` reader threads.
 // Per chunk of the unit: with TV_OPT_FILE_DIRECT a window of TV_OPT_FILE_CHUNK bytes whose pages are mostly in the
 // page cache is mapped, registered read-only and DMA'd to HBM from the page cache; otherwise (and for cold windows)
@@ -249,7 +199,7 @@ int stage_units(tv_ctx* c, const std::vector<FileUnit>& units, int lane, int thr
     hipStream_t cs = lane_stream(c, lane);
     FileWindows win(c);  // before `drain`: unmapped after the stream is drained
     DrainGuard drain(c, lane, /*sync_compute=*/false);
-    for (int k = 0; k < 4; k++) TV_HIP(c, hipEventCreateWithFlags(&drain.ev[k], hipEventDisableTiming));
+    for (int k = 0; k < 2; k++) TV_HIP(c, hipEventCreateWithFlags(&drain.ev[k], hipEventDisableTiming));
     const uint64_t page = (uint64_t)sysconf(_SC_PAGESIZE);
     int idx = 0;
     int rc = TV_OK;
@@ -323,22 +273,8 @@ int stage_units(tv_ctx* c, const std::vector<FileUnit>& units, int lane, int thr
                 // linear offset's alignment, is used).
                 win.release(k);
                 int dfd = (unit_cold && ((fo ^ p) & 3) == 0) ? win.direct_fd(c->open_rw) : -1;
-                uint64_t q0 = 0;  // (the bytes of the chunk the sub-buffered cold path staged)
-                if (dfd >= 0 && c->file_cold_sub) {
-                    int err = 0;
-                    rc = cold_sub_chunk(c, lane, std::min(threads, c->file_cold_threads), dfd, fo, p, n, &drain.ev[2],
-                                        &q0, &err);
-                    if (rc == TV_ERR_IO) {
-                        // a read the filesystem refused (see below): this file reads buffered from here on
-                        win.no_direct();
-                        dfd = -1;
-                    } else if (rc) {
-                        return rc;
-                    }
-                    rc = TV_OK;
-                }
                 const uint64_t step = dfd >= 0 ? (uint64_t)kRingSlotBytes - 8192 : (uint64_t)kRingSlotBytes - 4;
-                for (uint64_t q = q0; q < n; q += step) {
+                for (uint64_t q = 0; q < n; q += step) {
                     const uint64_t kq = std::min<uint64_t>(step, n - q);
                     SlotLease slot(c, lane);  // lent until every copy out of it is queued
                     {

@@ -19,13 +19,6 @@
 #define TV_OPT_FILE_ODIRECT 22   /* pread path: 1 (default) = chunks mostly not in the page cache are read O_DIRECT;
                                     0 = every read buffered; 2 = tests: every O_DIRECT read fails as a filesystem that
                                     refuses it would (EINVAL), so the file must fall back to buffered reads */
-#define TV_OPT_FILE_COLD_SUB 23     /* cold (O_DIRECT) chunks read through two sub-buffers of this many bytes at the
-                                       start of one ring slot -- sub-chunk i + 1 read while sub-chunk i is DMA'd -- so
-                                       the reads land in a small, re-used destination (the boxes' O_DIRECT reads ran
-                                       markedly faster into 16-32 MiB of re-used memory than across a 192 MiB ring:
-                                       profiles/r05/cold_sweep_foot.jsonl); 0 = the whole-slot path.  1 MiB .. half a
-                                       slot */
-#define TV_OPT_FILE_COLD_THREADS 24 /* reader threads per staging lane on the sub-buffered cold path (1 .. 64) */
 #define TV_OPT_DEBUG_REBOUNCE 11 /* tests: 1 = bounce ring-resident sources through the ring again (the staging
                                     path that once raced); slot leases must keep it exact.  Default 0 */
 #define TV_OPT_TWIN_PACK 12      /* twin kernel with fewer workgroups than 2 per CU: 1 = launch it on a stream
