@@ -24,6 +24,37 @@ from torrent_amd.verify import _context  # noqa: E402
 MiB = 1 << 20
 
 
+class _DmaLoad:
+    """H2D DMA from a 1 GiB page-locked buffer into a resident layout, in a loop on a background thread (ctypes
+    releases the GIL), as the library's staging keeps the GPU's copy engines busy beside its file reads."""
+
+    def __init__(self):
+        import threading
+        self.buf = _native.PinnedBuffer(1 << 30)
+        self.ctx = _native.Context(0)
+        self.ctx.set_layout(4 << 30, 4 * MiB, 1024)
+        self.bytes = 0
+        self.halt = threading.Event()
+        self.t0 = time.perf_counter()
+        self.th = threading.Thread(target=self._run)
+        self.th.start()
+
+    def _run(self):
+        off = 0
+        while not self.halt.is_set():
+            self.ctx.stage(off, self.buf.mv)
+            self.bytes += 1 << 30
+            off = (off + (1 << 30)) % (4 << 30)
+
+    def stop(self):
+        self.halt.set()
+        self.th.join()
+        g = self.bytes / (time.perf_counter() - self.t0) / 1e9
+        self.ctx.close()
+        self.buf.close()
+        return round(g, 2)
+
+
 def emit(rec):
     print(json.dumps(rec), flush=True)
 
@@ -55,6 +86,19 @@ def main():
             legs = [("ceiling direct 4x4MiB", 4), ("ceiling direct 4x4MiB spread", 4),
                     ("ceiling direct 4x4MiB pinned spread", 4), ("verify_files O_DIRECT 1 lane", 4),
                     ("ceiling direct 16x4MiB spread", 16), ("ceiling direct 16x4MiB", 16)]
+        if os.environ.get("COLD_SUB"):        # the sub-buffered cold path (TV_OPT_FILE_COLD_SUB / _COLD_THREADS)
+            legs = [("ceiling direct 4x4MiB", 4), ("verify_files O_DIRECT", 16), ("verify_files O_DIRECT sub16", 16),
+                    ("verify_files O_DIRECT sub8", 16), ("verify_files O_DIRECT sub8 1 lane", 16),
+                    ("verify_files O_DIRECT sub16 1 lane", 16), ("verify_files O_DIRECT sub8 t2", 16),
+                    ("verify_files O_DIRECT sub4 t2", 16)]
+        if os.environ.get("COLD_SUB2"):       # the candidates again, three rounds
+            legs = [("verify_files O_DIRECT", 16), ("verify_files O_DIRECT sub8 1 lane", 16),
+                    ("verify_files O_DIRECT sub4 1 lane", 16), ("verify_files O_DIRECT sub8 1 lane t8", 16),
+                    ("ceiling direct 4x4MiB spread16", 4)]
+        if os.environ.get("COLD_DMA"):        # the C reader with and without the GPU's H2D DMA running beside it
+            legs = [("ceiling direct 4x4MiB", 4), ("ceiling direct 4x4MiB dma", 4),
+                    ("ceiling direct 16x4MiB", 16), ("ceiling direct 16x4MiB dma", 16),
+                    ("ceiling direct 4x4MiB spread192", 4), ("ceiling direct 4x4MiB spread192 dma", 4)]
         if os.environ.get("COLD_FOOT"):       # the destination footprint at which the reads slow down
             legs = [("ceiling direct 4x4MiB", 4), ("ceiling direct 4x4MiB spread16", 4),
                     ("ceiling direct 4x4MiB spread32", 4), ("ceiling direct 4x4MiB spread64", 4),
@@ -86,8 +130,15 @@ def main():
                             nd = ctx.counter(_native.TV_COUNTER_NUMA_NODE)
                         env["RC_CPU_NODE"] = str(nd if nd < (1 << 63) else 0)
                         rec["node"] = env["RC_CPU_NODE"]
+                    dma = None
+                    if "dma" in what:
+                        dma = _DmaLoad()
                     t = time.perf_counter()
-                    got = read_ceiling(paths, threads=thr, part=4 * MiB, direct=True, env=env)
+                    try:
+                        got = read_ceiling(paths, threads=thr, part=4 * MiB, direct=True, env=env)
+                    finally:
+                        if dma:
+                            rec["dma_gbps"] = dma.stop()
                     rec["gbps"] = round(got / 1e9, 2) if got else None
                     rec["s"] = round(time.perf_counter() - t, 3)
                 else:
@@ -95,6 +146,12 @@ def main():
                         ctx._reset_file_clock()
                         ctx.set_option(_native.TV_OPT_FILE_CONCURRENT, 0 if "1 lane" in what else 1)
                         ctx.set_option(_native.TV_OPT_NUMA_BIND, 0 if "nobind" in what else 1)
+                        if hasattr(_native, "TV_OPT_FILE_COLD_SUB"):
+                            import re
+                            m = re.search(r"sub(\d+)", what)
+                            ctx.set_option(_native.TV_OPT_FILE_COLD_SUB, int(m.group(1)) * MiB if m else 0)
+                            m = re.search(r" t(\d+)", what)
+                            ctx.set_option(_native.TV_OPT_FILE_COLD_THREADS, int(m.group(1)) if m else 4)
                     t = time.perf_counter()
                     bf = verify_files(info, root, threads=thr)
                     el = time.perf_counter() - t
