@@ -4,7 +4,16 @@ For each layout (tools/storage_paths_bench.write_layout: single16, files64), `ro
 residency-checked drop (tools/fsutil.drop_cache; a leg above 1 % resident is recorded and skipped):
   * the C reader's O_DIRECT ceiling at 16 threads x 4 MiB and at 64 threads x 4 MiB (tools/read_ceiling.c);
   * verify_files with O_DIRECT at 16, 32 and 64 reader threads (two staging lanes share them),
-so a queue-depth effect shows beside the box's own storage variance.
+so a queue-depth effect shows beside the box's own storage variance.  Other leg sets (environment variables), each a
+question the round-5 records under profiles/r05/cold_sweep_*.jsonl answer:
+  COLD_LANES   one staging lane (TV_OPT_FILE_CONCURRENT = 0) against two
+  COLD_DEPTH   fewer reads in flight, the library and the C reader alike
+  COLD_FEW     2 and 4 reads in flight, the library on one lane
+  COLD_PROBE   the C reader into page-locked buffers (RC_HOST_ALLOC_LIB) / on the GPU's NUMA node (RC_CPU_NODE);
+               the library with its NUMA binding off
+  COLD_SPREAD  the C reader's destination spread over 192 MiB (RC_SPREAD), as the library fills its ring
+  COLD_FOOT    that destination at 16 / 32 / 48 / 64 MiB
+  COLD_DMA     the C reader with a page-locked H2D DMA stream running beside it
 
 usage: python tools/cold_sweep.py <dir> [layout ...] > out.jsonl
 """
@@ -86,15 +95,6 @@ def main():
             legs = [("ceiling direct 4x4MiB", 4), ("ceiling direct 4x4MiB spread", 4),
                     ("ceiling direct 4x4MiB pinned spread", 4), ("verify_files O_DIRECT 1 lane", 4),
                     ("ceiling direct 16x4MiB spread", 16), ("ceiling direct 16x4MiB", 16)]
-        if os.environ.get("COLD_SUB"):        # the sub-buffered cold path (TV_OPT_FILE_COLD_SUB / _COLD_THREADS)
-            legs = [("ceiling direct 4x4MiB", 4), ("verify_files O_DIRECT", 16), ("verify_files O_DIRECT sub16", 16),
-                    ("verify_files O_DIRECT sub8", 16), ("verify_files O_DIRECT sub8 1 lane", 16),
-                    ("verify_files O_DIRECT sub16 1 lane", 16), ("verify_files O_DIRECT sub8 t2", 16),
-                    ("verify_files O_DIRECT sub4 t2", 16)]
-        if os.environ.get("COLD_SUB2"):       # the candidates again, three rounds
-            legs = [("verify_files O_DIRECT", 16), ("verify_files O_DIRECT sub8 1 lane", 16),
-                    ("verify_files O_DIRECT sub4 1 lane", 16), ("verify_files O_DIRECT sub8 1 lane t8", 16),
-                    ("ceiling direct 4x4MiB spread16", 4)]
         if os.environ.get("COLD_DMA"):        # the C reader with and without the GPU's H2D DMA running beside it
             legs = [("ceiling direct 4x4MiB", 4), ("ceiling direct 4x4MiB dma", 4),
                     ("ceiling direct 16x4MiB", 16), ("ceiling direct 16x4MiB dma", 16),
@@ -146,12 +146,6 @@ def main():
                         ctx._reset_file_clock()
                         ctx.set_option(_native.TV_OPT_FILE_CONCURRENT, 0 if "1 lane" in what else 1)
                         ctx.set_option(_native.TV_OPT_NUMA_BIND, 0 if "nobind" in what else 1)
-                        if hasattr(_native, "TV_OPT_FILE_COLD_SUB"):
-                            import re
-                            m = re.search(r"sub(\d+)", what)
-                            ctx.set_option(_native.TV_OPT_FILE_COLD_SUB, int(m.group(1)) * MiB if m else 0)
-                            m = re.search(r" t(\d+)", what)
-                            ctx.set_option(_native.TV_OPT_FILE_COLD_THREADS, int(m.group(1)) if m else 4)
                     t = time.perf_counter()
                     bf = verify_files(info, root, threads=thr)
                     el = time.perf_counter() - t
