@@ -50,6 +50,12 @@ int tv_abi_version(void);
 /* Number of visible HIP devices. */
 int tv_device_count(int *count);
 
+/* Host CPUs this process may use, as the library sees them (no HIP call, no context): the cgroup CPU quota
+ * (cpu.max, v2; cpu.cfs_quota_us / cfs_period_us, v1) when one is set, else OMP_NUM_THREADS when set (a stated
+ * share), else the affinity mask; never more than the affinity mask, at least 1.  Hosts divide it among the shards
+ * of a call (TV_OPT_FILE_THREADS per context), as torrent_amd/_cpu.py cpu_share does. */
+int tv_cpu_share(uint32_t *cores);
+
 /* Create a context bound to HIP device `device`. */
 int tv_create(tv_ctx **out, int device);
 
@@ -172,6 +178,21 @@ int tv_stage_file(tv_ctx *ctx, const char *path, uint64_t file_offset, uint64_t 
  */
 int tv_stage_files(tv_ctx *ctx, uint64_t n, const char *const *paths, const uint64_t *file_offsets,
                    const uint64_t *linear_offsets, const uint64_t *lens, int32_t *status_out);
+
+/*
+ * Stage the shard's bytes from the torrent's FILE TABLE in one call: the library makes Storage.get's walk
+ * (storage.ts:89-137) itself.  File k holds `lengths[k]` bytes and is found at the k-th of the n NUL-terminated
+ * paths packed back to back in `paths` (`paths_bytes` bytes in all): [dir, ...info.files[k].path] joined, or
+ * [dir, info.name] for a single-file torrent (n = 1).  Files are in info.files order, so file k starts at the sum
+ * of the lengths before it.  Every segment of the walk that meets the shard is staged as tv_stage_files stages
+ * it, the zero-length segments fsStorage.get still opens included (storage.ts:109-110,158).  status_out[k] (n
+ * entries, one per FILE) = TV_ERR_IO when a segment of file k failed, else TV_OK; as for tv_stage_files the
+ * library marks the unreadable pieces itself and the status is informational.  A host thus passes its file table
+ * (which it may keep across calls) and does no per-file work per call.  TV_ERR_ARG when `paths` holds fewer than
+ * n NUL-terminated paths or the lengths overflow 64-bit offsets.
+ */
+int tv_stage_file_table(tv_ctx *ctx, uint64_t n, const uint64_t *lengths, const char *paths, uint64_t paths_bytes,
+                        int32_t *status_out);
 
 /* The inverse of tv_stage: copy `len` resident bytes at LINEAR offset `linear_offset` to host
  * `dst` (HBM as the piece store serving block requests, torrent.ts:164-167 Storage.get).  Bytes

@@ -67,6 +67,14 @@ static int run_cpu(void) {
     CHECK(tv_set_layout(NULL, 7, 3, 3, 0, 3) == TV_ERR_ARG, "NULL ctx");
     CHECK(tv_verify(NULL, NULL, NULL) == TV_ERR_ARG, "NULL ctx verify");
     CHECK(tv_host_alloc(16, NULL) == TV_ERR_ARG, "NULL out");
+    uint32_t cores = 0;
+    CHECK(tv_cpu_share(&cores) == TV_OK && cores >= 1, "cpu share %u", cores);
+    CHECK(tv_cpu_share(NULL) == TV_ERR_ARG, "NULL cores must be TV_ERR_ARG");
+    {
+        const uint64_t lens[1] = {7};
+        int32_t st[1];
+        CHECK(tv_stage_file_table(NULL, 1, lens, "a", 2, st) == TV_ERR_ARG, "NULL ctx file table");
+    }
     if (n == 0) {  /* no GPU: creating a context is an error with a message, never a crash */
         tv_ctx *c = NULL;
         int rc = tv_create(&c, 0);

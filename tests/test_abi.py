@@ -37,6 +37,13 @@ def test_abi_version_and_no_device_errors(native):
         assert ei.value.code == native.TV_ERR_ARG and "out of range" in str(ei.value)
 
 
+def test_cpu_share_equals_the_python_host(native):
+    """tv_cpu_share (the TS host's default thread share) reads the CPU share by the rule of
+    torrent_amd/_cpu.py cpu_share (cgroup quota, else OMP_NUM_THREADS, else the affinity mask) -- no GPU needed."""
+    from torrent_amd import _cpu
+    assert native.cpu_share() == _cpu.cpu_share()["cores"]
+
+
 def test_null_ctx_is_an_error_not_a_crash(native):
     lib = native.lib()
     assert lib.tv_set_layout(None, 1, 1, 1, 0, 1) == native.TV_ERR_ARG
@@ -248,9 +255,11 @@ def test_option_and_counter_constants_match_header():
         if name.startswith("TV_FILE_"):
             continue
         assert getattr(_native, name) == v, name
-    phases = sorted((v, k) for k, v in internal.items() if k.startswith(("TV_FILE_PHASE_", "TV_FILE_BYTES_")))
-    assert [k.split("_", 3)[3].lower() if k.startswith("TV_FILE_PHASE_") else "bytes_" + k.split("_")[-1].lower()
-            for _, k in phases] == list(_native.TV_FILE_PHASES)
+    phases = sorted((v, k) for k, v in internal.items()
+                    if k.startswith(("TV_FILE_PHASE_", "TV_FILE_BYTES_", "TV_FILE_ODIRECT_")))
+    assert [k.split("_", 3)[3].lower() if k.startswith("TV_FILE_PHASE_") else
+            "bytes_" + k.split("_")[-1].lower() if k.startswith("TV_FILE_BYTES_") else
+            "odirect_" + k.split("_")[-1].lower() for _, k in phases] == list(_native.TV_FILE_PHASES)
     ts = open(os.path.join(ROOT, "ts", "verify.ts")).read()
     for m in re.finditer(r"const\s+(TV_\w+)\s*=\s*(-?\d+)\s*;", ts):
         assert public[m.group(1)] == int(m.group(2)), m.group(1)

@@ -5,6 +5,7 @@ that are not multiples of 4 KiB, file offsets that do and do not agree with the 
 read buffered), a short last piece, corrupted pieces, and a file shorter than its segment -- every bitfield equal
 to Storage(fs_storage).get + hashlib's, with O_DIRECT on, off, and refused by the filesystem (fault injection:
 the file falls back to buffered reads, never to unreadable pieces)."""
+import errno
 import hashlib
 import os
 import sys
@@ -85,8 +86,13 @@ def test_cold_files_exact(native, oracle, tmp_path, odirect):
     if odirect == 1:
         assert clock["bytes_odirect"] > 0, clock      # (the cold chunks whose offsets agree mod 4 went O_DIRECT)
         assert clock["bytes_odirect"] < clock["bytes_read"]   # (and the others buffered)
+        assert clock["odirect_fallbacks"] == 0 and clock["odirect_errno"] == 0, clock   # (no read was refused)
     else:   # off, or (2) every O_DIRECT read refused: the same bits through the buffered fallback
         assert clock["bytes_odirect"] == 0
+        if odirect == 2:   # (the refusal is counted, with its errno: EINVAL, as a filesystem without O_DIRECT)
+            assert clock["odirect_fallbacks"] > 0 and clock["odirect_errno"] == errno.EINVAL, clock
+        else:
+            assert clock["odirect_fallbacks"] == 0, clock
 
 
 @pytest.mark.parametrize("seed", list(range(24)))
@@ -156,3 +162,4 @@ def test_cold_file_end_stays_o_direct(native, oracle, tmp_path):
         clock = ctx._file_clock()
     assert _bits(bf, P) == [1] * (P - 1) + [0]
     assert clock["bytes_odirect"] == clock["bytes_read"] == total, clock
+    assert clock["odirect_fallbacks"] == 0, clock

@@ -113,3 +113,16 @@ import("{mod}").then(async (m) => {{
     assert res["8 devices"] == [2] * 8
     assert res["1 device"] == [16]
     assert res["8 devices, threads 4"] == [1] * 8
+
+
+def test_storage_paths_honour_an_explicit_thread_count():
+    """verify_pieces / verify_stream: the default (threads=None) is _STORAGE_THREADS capped at the
+    shard's CPU part; an explicit count -- e.g. 32 readers for a Storage whose gets mostly wait -- is used as given."""
+    ctx = _FakeCtx(0)
+    ctx.thread_budget = 2
+    assert verify._storage_threads(ctx, None) == 2
+    ctx.thread_budget = 16
+    assert verify._storage_threads(ctx, None) == verify._STORAGE_THREADS
+    assert verify._storage_threads(ctx, 32) == 32
+    assert verify._storage_threads(ctx, 1) == 1
+    assert verify._storage_threads(ctx, 0) == 1

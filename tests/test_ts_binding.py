@@ -40,6 +40,19 @@ def build_addon() -> str:
     return ADDON
 
 
+WALK = os.path.join(HARNESS, "walk_main")
+
+
+def build_walk() -> str:
+    """The library's file-table walk (tv_plan.h walk_file_table) as a CPU program (tests/c/walk_main.cpp): the JS
+    model of the library runs it for tv_stage_file_table, so the CPU tests see the library's own walk."""
+    src = os.path.join(ROOT, "tests", "c", "walk_main.cpp")
+    hdr = os.path.join(ROOT, "torrent_amd", "csrc", "tv_plan.h")
+    if not os.path.exists(WALK) or os.path.getmtime(WALK) < max(os.path.getmtime(src), os.path.getmtime(hdr)):
+        subprocess.check_call(["g++", "-std=c++17", "-O1", "-Wall", src, "-o", WALK])
+    return WALK
+
+
 def erased_module(tmp_path) -> str:
     import sys
     sys.path.insert(0, HARNESS)
@@ -54,7 +67,8 @@ def run_node(tmp_path, script: str) -> str:
     path = os.path.join(str(tmp_path), "probe.mjs")
     with open(path, "w") as f:
         f.write(script)
-    r = subprocess.run([NODE, path], capture_output=True, text=True, timeout=120, cwd=HARNESS)
+    env = dict(os.environ, TV_WALK_EXE=build_walk())
+    r = subprocess.run([NODE, path], capture_output=True, text=True, timeout=120, cwd=HARNESS, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     return r.stdout
 

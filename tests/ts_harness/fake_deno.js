@@ -2,7 +2,8 @@
 // infrastructure only; tests/test_ts_binding.py).  Deno.dlopen returns JavaScript implementations of the
 // calls PieceVerifier makes (tv_create / tv_set_layout / tv_set_digests / tv_stage(_many) / tv_verify_list /
 // tv_destroy / tv_last_error / tv_abi_version) and hashPieces makes (tv_hash), with SHA-1 from node's crypto as the checker, and the
-// calls verifyFiles makes (tv_set_option, tv_stage_files recording the host's segment plan, tv_verify
+// calls verifyFiles makes (tv_set_option, tv_stage_file_table recording the segment plan the library's own walk makes of
+// the host's file table, tv_cpu_share, tv_verify
 // returning the host's availability bits) and verifyStream makes (the tv_stream_* protocol, modelled with
 // several requests per column); every other symbol throws if called.  Pointers are BigInt
 // addresses of registered typed arrays.  `nonblocking` symbols resolve on a
@@ -192,6 +193,38 @@ const impl = {
     c.segments = c.segments || [];
     for (let q = 0; q < k; q++) c.segments.push([cString(paths[q]), Number(fo[q]), Number(lin[q]), Number(len[q])]);
     new Int32Array(bytesOf(statusp).buffer, bytesOf(statusp).byteOffset, k).fill(0);
+    return 0;
+  },
+  // tv_stage_file_table: the library's own walk of the file table (tv_plan.h walk_file_table, built for the CPU as
+  // tests/c/walk_main.cpp; $TV_WALK_EXE) gives the shard's segments, recorded as tv_stage_files records them
+  tv_stage_file_table(ctx, n, lensp, pathsp, pathsBytes, statusp) {
+    const k = Number(n);
+    const c = contexts.get(ctx);
+    const lens = u64s(lensp, k);
+    const buf = bytesOf(pathsp).subarray(0, Number(pathsBytes));
+    const paths = [];
+    for (let q = 0, o = 0; q < k; q++) {
+      const e = buf.indexOf(0, o);
+      if (e < 0) return -2;   // TV_ERR_ARG: fewer than n paths
+      paths.push(Buffer.from(buf.subarray(o, e)).toString("utf8"));
+      o = e + 1;
+    }
+    const last = c.first + c.count - 1;
+    const plen = last === c.P - 1 && c.total % c.L ? c.total % c.L : c.L;
+    const lo = c.first * c.L, hi = Math.min(c.total, last * c.L + plen);
+    if (!process.env.TV_WALK_EXE) throw new Error("fake_deno: tv_stage_file_table needs $TV_WALK_EXE");
+    const out = require("child_process").execFileSync(process.env.TV_WALK_EXE,
+      { input: `${k} ${lo} ${hi} ${c.L}\n${lens.join(" ")}\n` }).toString();
+    for (const ln of out.split("\n")) {
+      if (!ln || ln.startsWith("reached")) continue;
+      const [f, fo, lin, len] = ln.split(" ").map(Number);
+      (c.segments = c.segments || []).push([paths[f], fo, lin, len]);
+    }
+    new Int32Array(bytesOf(statusp).buffer, bytesOf(statusp).byteOffset, k).fill(0);
+    return 0;
+  },
+  tv_cpu_share(outp) {
+    new Uint32Array(bytesOf(outp).buffer, bytesOf(outp).byteOffset, 1)[0] = Deno.fakeCpuShare || 16;
     return 0;
   },
   // tv_verify: the host's availability bits (shard-relative) and, unless Deno.fakeAvailOnly (the files plan

@@ -14,6 +14,8 @@ question the round-5 records under profiles/r05/cold_sweep_*.jsonl answer:
   COLD_SPREAD  the C reader's destination spread over 192 MiB (RC_SPREAD), as the library fills its ring
   COLD_FOOT    that destination at 16 / 32 / 48 / 64 MiB
   COLD_DMA     the C reader with a page-locked H2D DMA stream running beside it
+  COLD_BOUNCE  the C reader into its own reused buffer, then memcpy'd to the 192 MiB spread (bounce) or DMA'd to the GPU
+               from two reused page-locked buffers per reader (bouncedma), against the library (round 6)
 
 usage: python tools/cold_sweep.py <dir> [layout ...] > out.jsonl
 """
@@ -106,6 +108,13 @@ def main():
         if os.environ.get("COLD_FEW"):        # few reads in flight, the library on one lane against the C reader
             legs = [("ceiling direct 4x4MiB", 4), ("verify_files O_DIRECT 1 lane", 4), ("verify_files O_DIRECT", 4),
                     ("ceiling direct 2x4MiB", 2), ("verify_files O_DIRECT 1 lane", 2), ("verify_files O_DIRECT", 16)]
+        if os.environ.get("COLD_BOUNCE"):     # a compact reused read destination, then a copy or a DMA from it
+            legs = [("ceiling direct 4x4MiB", 4), ("ceiling direct 4x4MiB spread", 4),
+                    ("ceiling direct 4x4MiB bouncedma", 4), ("ceiling direct 4x4MiB bouncedma1", 4),
+                    ("ceiling direct 8x4MiB bouncedma1", 8), ("ceiling direct 6x4MiB bouncedma1", 6),
+                    ("verify_files O_DIRECT", 16)]
+            if os.environ.get("COLD_BOUNCE") == "copy":   # (round 6's first sweep: the host-copy form too)
+                legs += [("ceiling direct 4x4MiB bounce spread", 4), ("ceiling direct 8x4MiB bounce spread", 8)]
         if os.environ.get("COLD_LANES"):      # also one staging lane (TV_OPT_FILE_CONCURRENT = 0)
             legs = [("ceiling direct 16x4MiB", 16), ("verify_files O_DIRECT", 16),
                     ("verify_files O_DIRECT 1 lane", 16), ("verify_files O_DIRECT 1 lane", 32),
@@ -125,13 +134,17 @@ def main():
                     if "spread" in what:
                         mib = what.split("spread", 1)[1].split()[0] if what.split("spread", 1)[1][:1].isdigit() else "192"
                         env["RC_SPREAD"] = str(int(mib) * MiB)
+                    if "bouncedma" in what:
+                        env["RC_BOUNCE"] = "dma1" if "bouncedma1" in what else "dma"
+                    elif "bounce" in what:
+                        env["RC_BOUNCE"] = "copy"
                     if "node" in what:
                         with _context(0) as ctx:
                             nd = ctx.counter(_native.TV_COUNTER_NUMA_NODE)
                         env["RC_CPU_NODE"] = str(nd if nd < (1 << 63) else 0)
                         rec["node"] = env["RC_CPU_NODE"]
                     dma = None
-                    if "dma" in what:
+                    if what.endswith(" dma"):   # (not the bouncedma legs: their DMA is the reader's own)
                         dma = _DmaLoad()
                     t = time.perf_counter()
                     try:

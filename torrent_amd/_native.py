@@ -51,7 +51,7 @@ TV_COUNTER_FILE_CLOCK = 100
 TV_COUNTER_COTENANT_VRAM = 120
 TV_COUNTER_KFD_GPU_ID = 121
 TV_FILE_PHASES = ("open", "map", "populate", "register", "read", "wait", "queue", "release", "drain", "small", "call",
-                  "bytes_direct", "bytes_read", "bytes_odirect")   # TV_FILE_PHASE_* / TV_FILE_BYTES_* in order
+                  "bytes_direct", "bytes_read", "bytes_odirect", "odirect_fallbacks", "odirect_errno")   # TV_FILE_PHASE_* / TV_FILE_BYTES_* in order
 
 TV_COUNTER_PAYLOAD_ALLOCS = 1
 TV_COUNTER_DEVICE_ALLOCS = 2
@@ -97,6 +97,7 @@ _REQ = ctypes.POINTER(StreamReq)
 SYMBOLS = [
     ("tv_abi_version", _int, []),
     ("tv_device_count", _int, [ctypes.POINTER(_int)]),
+    ("tv_cpu_share", _int, [ctypes.POINTER(ctypes.c_uint32)]),
     ("tv_create", _int, [ctypes.POINTER(_p), _int]),
     ("tv_destroy", None, [_p]),
     ("tv_last_error", _int, [_p, ctypes.c_char_p, ctypes.c_size_t]),
@@ -106,6 +107,7 @@ SYMBOLS = [
     ("tv_stage_many", _int, [_p, _u64, _p, _p, _p]),
     ("tv_stage_file", _int, [_p, ctypes.c_char_p, _u64, _u64, _u64]),
     ("tv_stage_files", _int, [_p, _u64, _p, _p, _p, _p, _p]),
+    ("tv_stage_file_table", _int, [_p, _u64, _p, _p, _u64, _p]),
     ("tv_read", _int, [_p, _u64, _p, _u64]),
     ("tv_fill_synthetic", _int, [_p, _u64]),
     ("tv_verify", _int, [_p, _p, _p]),
@@ -184,6 +186,15 @@ def _addr(buf, writable: bool = False) -> tuple:
 def device_count() -> int:
     n = _int(0)
     rc = lib().tv_device_count(ctypes.byref(n))
+    if rc:
+        raise NativeError(rc, _thread_error())
+    return n.value
+
+
+def cpu_share() -> int:
+    """tv_cpu_share: the host CPUs this process may use as the library sees them (no GPU call)."""
+    n = ctypes.c_uint32(0)
+    rc = lib().tv_cpu_share(ctypes.byref(n))
     if rc:
         raise NativeError(rc, _thread_error())
     return n.value
@@ -348,6 +359,27 @@ class Context:
             return False
         self._check(rc)
         return True
+
+    def stage_file_table(self, lengths, paths) -> list:
+        """tv_stage_file_table: the shard's bytes from the torrent's file table (file k: lengths[k] bytes at
+        paths[k], in info.files order); the library makes Storage.get's walk itself.  One status per FILE."""
+        import numpy as np
+
+        n = len(paths)
+        if len(lengths) != n:
+            raise ValueError("stage_file_table: lengths and paths differ in length")
+        if n == 0:
+            return []
+        if all(type(x) is str for x in paths):
+            blob = ("\0".join(paths) + "\0").encode(sys.getfilesystemencoding(), "surrogateescape")
+        else:
+            blob = b"\0".join(os.fsencode(x) for x in paths) + b"\0"
+        if blob.count(b"\0") != n:
+            raise ValueError("stage_file_table: a path contains a NUL byte")
+        ln = np.ascontiguousarray(lengths, dtype=np.uint64)
+        st = np.zeros(n, dtype=np.int32)
+        self._check(self._L.tv_stage_file_table(self._h, n, ln.ctypes.data, blob, len(blob), st.ctypes.data))
+        return st.tolist()
 
     def stage_files(self, paths, file_offsets, linear_offsets, lens) -> list:
         """tv_stage_files: stage many file segments in one call.  Returns one status per segment:

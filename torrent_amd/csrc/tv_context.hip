@@ -1,7 +1,10 @@
 // tv_context.hip -- the context's lifecycle and settings: tv_create / tv_destroy, options, tv_set_layout (the
 // payload: the whole shard, windows, or a slot pool), tv_set_digests, pinned-host helpers, timing and counters.
 #include <sched.h>
+#include <unistd.h>
 
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "tv_ctx.h"
@@ -27,6 +30,34 @@ int tv_device_count(int* count) {
     if (e == hipErrorNoDevice) n = 0;
     else if (e != hipSuccess) return fail(nullptr, TV_ERR_HIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
     *count = n;
+    return TV_OK;
+}
+
+int tv_cpu_share(uint32_t* cores) {
+    if (!cores) return fail(nullptr, TV_ERR_ARG, "cores is NULL");
+    cpu_set_t set;
+    const int aff = sched_getaffinity(0, sizeof set, &set) == 0 ? std::max(1, CPU_COUNT(&set)) : 1;
+    double quota = 0;
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        unsigned long long per = 0;
+        if (fscanf(f, "%31s %llu", q, &per) == 2 && strcmp(q, "max") != 0 && per) quota = atof(q) / (double)per;
+        fclose(f);
+    } else if (FILE* f1 = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+        long long q = 0, per = 0;
+        if (fscanf(f1, "%lld", &q) == 1 && q > 0) {
+            if (FILE* f2 = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+                if (fscanf(f2, "%lld", &per) == 1 && per > 0) quota = (double)q / (double)per;
+                fclose(f2);
+            }
+        }
+        fclose(f1);
+    }
+    int n = aff;
+    const char* omp = getenv("OMP_NUM_THREADS");
+    if (quota > 0) n = std::max(1, std::min(aff, (int)quota));
+    else if (omp && *omp && strspn(omp, "0123456789") == strlen(omp) && atoi(omp) > 0) n = std::min(aff, atoi(omp));
+    *cores = (uint32_t)n;
     return TV_OK;
 }
 
@@ -67,7 +98,8 @@ int tv_create(tv_ctx** out, int device) {
     // workers go back to when the binding is turned off
     c->proc_cpus_ok = sched_getaffinity(0, sizeof c->proc_cpus, &c->proc_cpus) == 0;
     c->numa_node = gpu_numa_node(device);
-    c->kfd_gpu_id = kfd_gpu_id(device);
+    c->kfd_gpu_id = kfd_gpu_id(device);   // (this process's own KFD entry is probed lazily: kfd_check_id)
+    c->create_pid = (long)getpid();
     c->numa_cpus_ok = node_cpus(c->numa_node, &c->numa_cpus);
     apply_numa(c);
     *out = c;
@@ -512,7 +544,7 @@ int tv_get_counter(tv_ctx* c, int key, uint64_t* value) {
             *value = c->file_ns[key - TV_COUNTER_FILE_CLOCK].load();
             return TV_OK;
         case TV_COUNTER_COTENANT_VRAM: *value = cotenant_vram(c); return TV_OK;
-        case TV_COUNTER_KFD_GPU_ID: *value = c->kfd_gpu_id; return TV_OK;
+        case TV_COUNTER_KFD_GPU_ID: *value = kfd_check_id(c); return TV_OK;
         case TV_COUNTER_LAST_CLOCK_KHZ: {
             *value = 0;
             if (!c->d_clock) return TV_OK;

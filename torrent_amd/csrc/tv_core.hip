@@ -170,29 +170,40 @@ static std::vector<std::pair<long, uint64_t>> kfd_vram(uint32_t gpu_id) {
 
 // This process's pid in KFD's accounting.  The directory names are pids of the host's pid namespace, which a
 // process in a container does not know (getpid() differs), so it is found by a probe: the one process whose
-// vram_<gpu_id> grows by exactly a 64 MiB device allocation made in between two reads.  Resolved once per
-// process (a forked child probes again); 0 = not found (then no co-tenant check: companions stay on).
-static long kfd_self_pid(int device, uint32_t gpu_id) {
+// vram_<gpu_id> grows by exactly a 64 MiB device allocation made in between two reads.  Probed lazily, by the
+// first co-tenant check (a twin launch that could add companions, or the counter), never at tv_create; a probe that
+// finds no single match (another allocation in this process or another one at the same moment) is retried on a later
+// check, at most once a second.  Only the process that created the ctx probes: in a forked child (getpid() differs
+// from c->create_pid) no HIP call is made and there is no check.  0 = not known (no check: companions stay on).
+static long kfd_self_pid(tv_ctx* c) {
     static std::mutex mu;
     static long self = 0, for_pid = -1;
+    static std::chrono::steady_clock::time_point failed_at;
+    static bool failed = false;
+    const long me = (long)getpid();
+    if (me != c->create_pid) return 0;
     std::lock_guard<std::mutex> g(mu);
-    if (for_pid == (long)getpid()) return self;
-    for_pid = (long)getpid();
+    if (for_pid == me && self) return self;
+    const auto now = std::chrono::steady_clock::now();
+    if (for_pid == me && failed && now - failed_at < std::chrono::seconds(1)) return 0;
+    for_pid = me;
     self = 0;
     constexpr uint64_t kProbe = 64ull << 20;
     int prev = 0;
-    if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) {
+    if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(c->device) != hipSuccess) {
         (void)hipGetLastError();
+        failed = true;
+        failed_at = now;
         return 0;
     }
     for (int attempt = 0; attempt < 3 && !self; attempt++) {
-        const auto before = kfd_vram(gpu_id);
+        const auto before = kfd_vram(c->kfd_gpu_id);
         void* p = nullptr;
         if (hipMalloc(&p, kProbe) != hipSuccess) {
             (void)hipGetLastError();
             break;
         }
-        const auto after = kfd_vram(gpu_id);
+        const auto after = kfd_vram(c->kfd_gpu_id);
         (void)hipFree(p);
         long found = 0;
         int matches = 0;
@@ -207,16 +218,18 @@ static long kfd_self_pid(int device, uint32_t gpu_id) {
         if (matches == 1) self = found;   // another process allocating exactly 64 MiB at the same time: again
     }
     (void)hipSetDevice(prev);
+    failed = self == 0;
+    failed_at = now;
     return self;
 }
 
-// The KFD gpu_id of HIP device `device` for the co-tenant check: the topology node whose PCI location matches,
-// provided this process's own entry in the accounting can be told apart (kfd_self_pid); 0 = no check.
-uint32_t kfd_gpu_id(int device) {
-    const uint32_t id = kfd_topology_gpu_id(device);
-    if (!id || !kfd_self_pid(device, id)) return 0;
-    return id;
-}
+// The KFD gpu_id of HIP device `device` for the co-tenant check: the topology node whose PCI location matches
+// (0 = none; no HIP allocation is made here: the process's own entry is found later, kfd_self_pid).
+uint32_t kfd_gpu_id(int device) { return kfd_topology_gpu_id(device); }
+
+// The gpu_id when the co-tenant check can run (the GPU is in the topology and this process's entry in the
+// accounting is known, probing for it now if need be), else 0.
+uint32_t kfd_check_id(tv_ctx* c) { return (c->kfd_gpu_id && kfd_self_pid(c)) ? c->kfd_gpu_id : 0; }
 
 // Bytes of this GPU's memory other processes hold (KFD's per-process accounting,
 // /sys/class/kfd/kfd/proc/<pid>/vram_<gpu_id>), or 0 when it cannot be read.  Cached for a second.
@@ -224,13 +237,14 @@ uint64_t cotenant_vram(tv_ctx* c) {
     if (!c->kfd_gpu_id) return 0;
     const auto now = std::chrono::steady_clock::now();
     if (c->cotenant_checked && now - c->cotenant_at < std::chrono::seconds(1)) return c->cotenant_bytes;
-    const long self = kfd_self_pid(c->device, c->kfd_gpu_id);
+    const long self = kfd_self_pid(c);
     uint64_t sum = 0;
-    for (const auto& [pid, v] : kfd_vram(c->kfd_gpu_id))
-        if (pid != self) sum += v;
+    if (self)
+        for (const auto& [pid, v] : kfd_vram(c->kfd_gpu_id))
+            if (pid != self) sum += v;
     c->cotenant_bytes = sum;
     c->cotenant_at = now;
-    c->cotenant_checked = true;
+    c->cotenant_checked = self != 0;   // (an unresolved probe is retried by the next check, not cached)
     return sum;
 }
 
@@ -586,9 +600,12 @@ int piece_dst(tv_ctx* c, uint64_t i, uint8_t** out) {
 
 // The same for reading (tv_read): a slot pool's piece must hold a slot.
 int piece_src(tv_ctx* c, uint64_t i, const uint8_t** out) {
-    if (c->slots && !c->slot_of.count(i - c->first))
-        return fail(c, TV_ERR_STATE, "piece %llu holds no slot (it was never staged, or was listed since)",
-                    (unsigned long long)i);
+    if (c->slots) {
+        std::lock_guard<std::mutex> g(c->slot_mu);  // (as piece_dst: a lane-1 helper may take a slot meanwhile)
+        if (!c->slot_of.count(i - c->first))
+            return fail(c, TV_ERR_STATE, "piece %llu holds no slot (it was never staged, or was listed since)",
+                        (unsigned long long)i);
+    }
     uint8_t* p = nullptr;
     const int rc = piece_dst(c, i, &p);
     *out = p;

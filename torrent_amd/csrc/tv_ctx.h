@@ -176,6 +176,7 @@ struct tv_ctx {
     bool twin_pack = false;                  // TV_OPT_TWIN_PACK
     int twin_fill = 1;                       // TV_OPT_TWIN_FILL: 0 off, 1 auto, 2 also on short lists, 3 on always
     uint32_t kfd_gpu_id = 0;                 // the GPU's KFD id (co-tenant check of the companions; 0 = unknown)
+    long create_pid = 0;                     // getpid() at tv_create (a forked child makes no co-tenant probe)
     bool cotenant_checked = false;           // cotenant_bytes is fresh (read at cotenant_at)
     uint64_t cotenant_bytes = 0;             // this GPU's memory other processes hold (KFD accounting)
     std::chrono::steady_clock::time_point cotenant_at;
@@ -350,6 +351,7 @@ bool reuse_fits(uint64_t need, uint64_t cap);
 // launches no companion workgroups (they would take CUs the other process may be using).
 constexpr uint64_t kCotenantBytes = 1ull << 30;
 uint32_t kfd_gpu_id(int device);
+uint32_t kfd_check_id(tv_ctx* c);
 uint64_t cotenant_vram(tv_ctx* c);
 bool companions_on(tv_ctx* c);
 int ensure_hbits(tv_ctx* c, size_t bytes);

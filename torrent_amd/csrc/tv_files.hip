@@ -295,7 +295,12 @@ int stage_units(tv_ctx* c, const std::vector<FileUnit>& units, int lane, int thr
                         if (e) {
                             // an O_DIRECT read the filesystem refuses (EINVAL: alignment it does not take, a tmpfs)
                             // is not the file's failure: this file reads buffered from here on, this chunk included,
-                            // and only a buffered failure counts (it is what fsStorage.get's read would see)
+                            // and only a buffered failure counts (it is what fsStorage.get's read would see).  The
+                            // fallback is counted and its first errno kept, so a systematic one (a ring slot the
+                            // kernel cannot pin for direct I/O) shows (TV_FILE_ODIRECT_FALLBACKS / _ERRNO)
+                            c->file_ns[TV_FILE_ODIRECT_FALLBACKS].fetch_add(1, std::memory_order_relaxed);
+                            uint64_t none = 0;
+                            c->file_ns[TV_FILE_ODIRECT_ERRNO].compare_exchange_strong(none, (uint64_t)e);
                             win.no_direct();
                             dfd = -1;
                             at = slot.ptr() + ((p + q) & 3);
@@ -658,6 +663,9 @@ int stage_files_core(tv_ctx* c, uint64_t n, const char* const* paths, const uint
     return TV_OK;
 }
 
+int stage_files_locked(tv_ctx* c, uint64_t n, const char* const* paths, const uint64_t* file_offsets,
+                       const uint64_t* linear_offsets, const uint64_t* lens, int32_t* status_out);
+
 }  // namespace
 
 extern "C" {
@@ -678,6 +686,63 @@ int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64
             return fail(c, TV_ERR_ARG, "segment %llu: offset + len overflows", (unsigned long long)k);
         status_out[k] = TV_OK;
     }
+    return stage_files_locked(c, n, paths, file_offsets, linear_offsets, lens, status_out);
+}
+
+int tv_stage_file_table(tv_ctx* c, uint64_t n, const uint64_t* lengths, const char* paths, uint64_t paths_bytes,
+                        int32_t* status_out) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    FileClock call_clock(c, TV_FILE_PHASE_CALL);
+    int rc = require_layout(c, false, true);
+    if (rc) return rc;
+    if (n == 0) return TV_OK;
+    if (!lengths || !paths || !status_out) return fail(c, TV_ERR_ARG, "NULL argument");
+    // file k's path: the k-th NUL-terminated string of the buffer
+    std::vector<const char*> path(n);
+    uint64_t o = 0;
+    for (uint64_t k = 0; k < n; k++) {
+        const void* z = o < paths_bytes ? memchr(paths + o, 0, paths_bytes - o) : nullptr;
+        if (!z)
+            return fail(c, TV_ERR_ARG, "paths holds %llu NUL-terminated paths in %llu bytes, the table %llu files",
+                        (unsigned long long)k, (unsigned long long)paths_bytes, (unsigned long long)n);
+        path[k] = paths + o;
+        o = (uint64_t)((const char*)z - paths) + 1;
+        status_out[k] = TV_OK;
+    }
+    if (c->count == 0) return TV_OK;
+    // findAndDo's walk over the files in order (storage.ts:98-137), restricted to the shard's bytes (tv_plan.h)
+    const uint64_t last = c->first + c->count - 1;
+    const uint64_t lo = c->first * c->L, hi = std::min(c->total, last * c->L + piece_len(c, last));
+    std::vector<TableSeg> segs;
+    uint64_t bad = 0, reached = 0;
+    if (!walk_file_table(n, lengths, lo, hi, c->L, &segs, &bad, &reached))
+        return fail(c, TV_ERR_ARG, "file %llu: the lengths overflow 64-bit offsets", (unsigned long long)bad);
+    std::vector<const char*> sp;
+    std::vector<uint64_t> sfo, slin, slen;
+    for (const TableSeg& g : segs) {
+        sp.push_back(path[g.file]);
+        sfo.push_back(g.file_offset);
+        slin.push_back(g.linear);
+        slen.push_back(g.len);
+    }
+    std::vector<int32_t> st(sp.size(), TV_OK);
+    if (!sp.empty()) rc = stage_files_locked(c, sp.size(), sp.data(), sfo.data(), slin.data(), slen.data(), st.data());
+    for (size_t q = 0; q < sp.size(); q++)
+        if (st[q] != TV_OK) status_out[segs[q].file] = st[q];
+    // the files end before the shard does: Storage.get's walk for a piece past their end never completes (null)
+    if (!rc && reached < hi) mark_bad(c, reached, hi);
+    return rc;
+}
+
+}  // extern "C"
+
+namespace {
+
+// tv_stage_files' work with the lock held and the segments checked (status_out preset to TV_OK).
+int stage_files_locked(tv_ctx* c, uint64_t n, const char* const* paths, const uint64_t* file_offsets,
+                       const uint64_t* linear_offsets, const uint64_t* lens, int32_t* status_out) {
+    int rc = TV_OK;
     if (c->count == 0) return TV_OK;
     TV_HIP(c, hipSetDevice(c->device));
     // the pieces whose every byte this call stages lose an earlier call's unreadable mark (the union of the
@@ -718,4 +783,4 @@ int tv_stage_files(tv_ctx* c, uint64_t n, const char* const* paths, const uint64
     return check_zero ? stage_files_core(c, n, paths, file_offsets, linear_offsets, lens, status_out, true) : TV_OK;
 }
 
-}  // extern "C"
+}  // namespace

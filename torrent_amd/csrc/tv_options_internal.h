@@ -28,7 +28,8 @@
    3 = companions whatever other processes hold on the GPU (the co-tenant check of 1 skipped) */
 #define TV_COUNTER_COTENANT_VRAM 120 /* bytes of this GPU's memory other processes hold (KFD: /sys/class/kfd/kfd/proc/
                                         <pid>/vram_<gpu_id>; 0 when unreadable): >= 1 GiB turns auto companions off */
-#define TV_COUNTER_KFD_GPU_ID 121    /* the GPU's KFD gpu_id (0: not found) */
+#define TV_COUNTER_KFD_GPU_ID 121    /* the GPU's KFD gpu_id when the co-tenant check can run (reading it probes for this
+                                        process's own accounting entry if not yet known); 0: it cannot */
 #define TV_OPT_TWIN_FILL_READS 14 /* companion workgroups' loads: 0 (default) = every lane of a companion reads its
                                     main workgroup's first piece (the same instruction stream, 1/32 of the bytes);
                                     1 = the main workgroup's 32 pieces (round 2; 1.14-1.42 x payload of HBM reads) */
@@ -62,4 +63,7 @@
 #define TV_FILE_BYTES_DIRECT 11   /* bytes DMA'd from registered page-cache pages */
 #define TV_FILE_BYTES_READ 12     /* bytes read by preads into the ring (long segments) */
 #define TV_FILE_BYTES_ODIRECT 13  /* of which read with O_DIRECT (cold chunks, TV_OPT_FILE_ODIRECT) */
+#define TV_FILE_ODIRECT_FALLBACKS 14  /* O_DIRECT reads that failed and were read again buffered (that file then reads
+                                         buffered on that lane) */
+#define TV_FILE_ODIRECT_ERRNO 15  /* the errno of the first of them since the reset (0: none) */
 #define TV_FILE_CLOCK_N 16

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <vector>
 
 namespace tvi {
 
@@ -60,6 +61,38 @@ int allocate_payload(uint64_t count, uint64_t stride, uint64_t slack, uint64_t b
         failed = p.bytes;
         budget = p.bytes / 2;  // windows of half the size
     }
+}
+
+// One segment of Storage.get's walk over a torrent's file table: `len` bytes of file `file` from byte `file_offset`
+// are LINEAR bytes [linear, linear + len); len == 0 for the walk's zero-length segments.
+struct TableSeg {
+    uint64_t file, file_offset, linear, len;
+};
+
+// findAndDo's walk (storage.ts:98-137) over the files in order -- file k holds lengths[k] bytes and starts where the
+// files before it end -- restricted to the LINEAR bytes [lo, hi) of a shard (lo a multiple of L): every segment with
+// bytes there, and the zero-length segments fsStorage.get still opens (storage.ts:109-110,158): a file ending inside
+// [lo, hi) that is empty or ends exactly where a piece starts.  The hosts' walks make the same list
+// (torrent_amd/verify.py _files_shard over storage.py segment_arrays / zero_length_segments).  *reached: where the
+// walk stopped (< hi: the files end before the shard does, and Storage.get returns null for a piece past their end).
+// false (*bad = the file) when the lengths overflow 64-bit offsets.  tv_stage_file_table uses it;
+// tests/c/walk_main.cpp runs it on the CPU.
+inline bool walk_file_table(uint64_t n, const uint64_t* lengths, uint64_t lo, uint64_t hi, uint64_t L,
+                            std::vector<TableSeg>* out, uint64_t* bad, uint64_t* reached) {
+    uint64_t start = 0;
+    for (uint64_t k = 0; k < n && start < hi; k++) {
+        if (lengths[k] > UINT64_MAX - start) {
+            *bad = k;
+            return false;
+        }
+        const uint64_t end = start + lengths[k];
+        const uint64_t a = std::max(lo, start), b = std::min(hi, end);
+        if (b > a) out->push_back({k, a - start, a, b - a});
+        if (end >= lo && end < hi && (lengths[k] == 0 || end % L == 0)) out->push_back({k, lengths[k], end, 0});
+        start = end;
+    }
+    *reached = start;
+    return true;
 }
 
 }  // namespace tvi

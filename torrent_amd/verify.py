@@ -207,12 +207,22 @@ def _run_shards(devs: List[int], n_pieces: int, fn):
 _STORAGE_THREADS = 4
 
 
-def verify_pieces(info: InfoDict, storage, devices=None, threads: int = _STORAGE_THREADS,
+def _storage_threads(ctx, threads: Optional[int]) -> int:
+    """Reader threads of a Storage path: the caller's count as given, or by default _STORAGE_THREADS capped at the
+    shard's part of the process's CPUs (ctx.thread_budget; ADVICE r05: an explicit count is never cut silently)."""
+    if threads is None:
+        return max(1, min(_STORAGE_THREADS, ctx.thread_budget))
+    return max(1, int(threads))
+
+
+def verify_pieces(info: InfoDict, storage, devices=None, threads: Optional[int] = None,
                   budget: Optional[int] = None) -> bytearray:
     """verifyPieces(info, storage): have-bitfield of every piece read through `storage`
     (a torrent_amd.storage.Storage, i.e. the reference's Storage over any StorageMethod).  The gets
     of a batch are in flight together on `threads` threads, as ts/verify.ts keeps them outstanding
-    with Promise.all (make_torrent.ts:96,111 does the same); threads=1 reads them one by one.
+    with Promise.all (make_torrent.ts:96,111 does the same); threads=1 reads them one by one.  threads=None (the
+    default): _STORAGE_THREADS, capped at the shard's part of the process's CPUs (ctx.thread_budget); an explicit
+    count is used as given (e.g. more threads for a Storage whose gets mostly wait).
     Reads and staging overlap: batch k + 1 is read (into the other of two page-locked buffers) while batch
     k is DMA'd to HBM (and, on a windowed layout, while the windows before it hash); each reader thread
     copies its piece into the batch buffer itself, without the GIL."""
@@ -236,7 +246,7 @@ def verify_pieces(info: InfoDict, storage, devices=None, threads: int = _STORAGE
             return n
 
         bufs = _batch_buffers(ctx, per_batch * L)
-        nthr = max(1, min(threads, ctx.thread_budget))   # (the shard's part of the process's CPUs)
+        nthr = _storage_threads(ctx, threads)
         with ThreadPoolExecutor(nthr) as pool, ThreadPoolExecutor(1) as stager:
             staging = None              # the previous batch's stage (it reads the other buffer)
             j, b = 0, 0
@@ -321,7 +331,7 @@ def _shard_avail(avail: Optional[bytes], first: int, count: int) -> Optional[byt
 
 
 def verify_stream(info: InfoDict, read, devices=None, avail: Optional[bytes] = None, chunk: int = 0,
-                  threads: int = _STORAGE_THREADS) -> bytearray:
+                  threads: Optional[int] = None) -> bytearray:
     """End-to-end resume check through the library's BOUNDED pinned ring (tv_stream_*; SURVEY 8d config 5:
     the resume flow Client.add -> verify -> Torrent.bitfield -> sendBitfield, client.ts:53-67,
     torrent.ts:56-60,101).  No resident payload and no whole-shard host buffer.  By default (chunk=0) each
@@ -332,7 +342,8 @@ def verify_stream(info: InfoDict, read, devices=None, avail: Optional[bytes] = N
     [c*C, c*C + C) of every piece; all of the shard's pieces in each launch).  None makes that piece
     unreadable (bit 0); a piece is readable iff every slice of it reads.  Host memory in flight: 3 x 64 MiB
     per device, whatever the size.  The reads of a request are in flight together on `threads` threads (as
-    verify_pieces; threads=1 reads them one by one), each writing its own row of the slot."""
+    verify_pieces; threads=1 reads them one by one; None: the default and CPU cap of verify_pieces), each writing its
+    own row of the slot."""
     P, L = info.n_pieces, info.piece_length
 
     def shard(ctx, first: int, count: int) -> bytes:
@@ -347,7 +358,7 @@ def verify_stream(info: InfoDict, read, devices=None, avail: Optional[bytes] = N
         finally:
             ctx.set_option(_native.TV_OPT_RESIDENT, 1)
         ctx.stream_begin(_shard_avail(avail, first, count))
-        nthr = max(1, min(threads, ctx.thread_budget))
+        nthr = _storage_threads(ctx, threads)
         pool = ThreadPoolExecutor(nthr) if nthr > 1 else None
         try:
             while True:

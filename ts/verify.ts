@@ -20,6 +20,7 @@ import type { Storage } from "../storage.ts";
 const SYMBOLS = {
   tv_abi_version: { parameters: [], result: "i32" },
   tv_device_count: { parameters: ["pointer"], result: "i32" },
+  tv_cpu_share: { parameters: ["pointer"], result: "i32" },
   tv_create: { parameters: ["pointer", "i32"], result: "i32" },
   tv_destroy: { parameters: ["pointer"], result: "void" },
   tv_last_error: { parameters: ["pointer", "pointer", "usize"], result: "i32" },
@@ -30,6 +31,11 @@ const SYMBOLS = {
   tv_stage_file: { parameters: ["pointer", "pointer", "u64", "u64", "u64"], result: "i32", nonblocking: true },
   tv_stage_files: {
     parameters: ["pointer", "u64", "pointer", "pointer", "pointer", "pointer", "pointer"],
+    result: "i32",
+    nonblocking: true,
+  },
+  tv_stage_file_table: {
+    parameters: ["pointer", "u64", "pointer", "pointer", "u64", "pointer"],
     result: "i32",
     nonblocking: true,
   },
@@ -76,20 +82,31 @@ export interface VerifyOptions {
   /** verifyPiece only: hash on the CPU with the reference's own crypto.subtle.digest("SHA-1", bytes)
    * (tools/make_torrent.ts:28-31) instead of a ~3 ms GPU launch.  Off by default */
   cpuFallback?: boolean;
-  /** host threads the library may use for one call, over all of its shards (default: the machine's,
-   * navigator.hardwareConcurrency): each shard's context gets its part (TV_OPT_FILE_THREADS), so
-   * devices [0..7] do not start 8 x 16 reader threads */
+  /** host threads the library may use for one call, over all of its shards (default: the process's CPU share as
+   * the library reads it, tv_cpu_share: the cgroup quota, else OMP_NUM_THREADS, else the affinity mask): each
+   * shard's context gets its part (TV_OPT_FILE_THREADS), so devices [0..7] do not start 8 x 16 reader threads */
   threads?: number;
 }
 
 const TV_OPT_FILE_THREADS = 8;
 
-/** Reader / copy threads of each of `active` concurrently running shards: opts.threads (else the machine's CPU
- * count) divided among them, 1 .. 16 each (16 is the library's default; its page-cache readers already saturate
- * PCIe there).  Same rule as torrent_amd/_cpu.py shard_threads, without its cgroup / NUMA inputs, which a Deno
- * process without --allow-read cannot see. */
-export function shardThreads(opts: VerifyOptions, active: number): number {
-  const share = opts.threads || (typeof navigator !== "undefined" && navigator.hardwareConcurrency) || 16;
+/** The process's CPU share as the library reads it (tv_cpu_share; cached).  The library reads the cgroup files
+ * itself, so a Deno process without --allow-read still gets the container's quota, not the machine's cores. */
+let cpuShareCache = 0;
+function libCpuShare(l: Lib | null): number {
+  if (!cpuShareCache && l) {
+    const out = new Uint32Array(1);
+    if (l.symbols.tv_cpu_share(ptr(new Uint8Array(out.buffer))) === 0) cpuShareCache = out[0];
+  }
+  return cpuShareCache;
+}
+
+/** Reader / copy threads of each of `active` concurrently running shards: opts.threads (else the process's CPU
+ * share, tv_cpu_share) divided among them, 1 .. 16 each (16 is the library's default; its page-cache readers
+ * already saturate PCIe there).  Same rule as torrent_amd/_cpu.py shard_threads, without its per-NUMA-node cap. */
+export function shardThreads(opts: VerifyOptions, active: number, l: Lib | null = lib): number {
+  const share = opts.threads || libCpuShare(l) ||
+    (typeof navigator !== "undefined" && navigator.hardwareConcurrency) || 16;
   return Math.max(1, Math.min(16, Math.floor(share / Math.max(1, active))));
 }
 
@@ -377,29 +394,76 @@ export async function verifyStream(info: InfoDict, storage: Storage, opts: Verif
 /**
  * verifyFiles(info, dir) -> have-bitfield of the files under `dir` (resume from disk, SURVEY 8f
  * row f2), laid out as new Storage(fsStorage, info, dir) maps them (storage.ts:89-137: single-file
- * [dir, name], multi-file [dir, ...path]).  All file segments of a shard go to tv_stage_files in one
- * call: long segments are cut into 256 MiB units read by parallel preads into the library's pinned ring on
- * its two staging lanes and DMA'd from there; short ones (many small files) are read by the library's thread
- * pool into pinned slots.  The shard's reader threads are its part of opts.threads (shardThreads).
+ * [dir, name], multi-file [dir, ...path]).  Each shard hands the library the torrent's FILE TABLE in one
+ * tv_stage_file_table call and the library makes Storage.get's walk itself (the segments of the shard, the
+ * zero-length ones fsStorage.get still opens included): long segments are cut into 256 MiB units read by
+ * parallel preads into the library's pinned ring on its two staging lanes and DMA'd from there; short ones
+ * (many small files) are read by the library's thread pool into pinned slots.  The table (lengths and one
+ * NUL-separated path buffer) is built once per (info, dir) and kept, so a repeat call does no per-file encoding.
+ * The shard's reader threads are its part of opts.threads (shardThreads).
  * The library marks the pieces fsStorage.get would return null for (storage.ts:163-171): a byte in a
  * missing, unopenable or unwritable file or past a short file's end, or a zero-length segment whose open
- * would fail (a directory, a missing parent directory); unlike fsStorage.get, no missing file is created.  Same behaviour as
- * torrent_amd.verify_files.
+ * would fail (a directory, a missing parent directory); unlike fsStorage.get, no missing file is created.  Same
+ * behaviour as torrent_amd.verify_files.
  */
 /** Numbers (< 2^52) as the little-endian u64 words of a C array (Deno runs on little-endian hosts only), written
- * as 32-bit halves -- a BigInt per element cost ~3-4 ms on a 10,000-file verifyFiles -- with `base` (a pointer)
- * added to each. */
-function u64Words(vals: number[], base: bigint): Uint32Array {
+ * as 32-bit halves -- a BigInt per element cost ~3-4 ms on a 10,000-file verifyFiles. */
+function u64Words(vals: number[]): Uint32Array {
   const out = new Uint32Array(2 * vals.length);
-  const bLo = Number(base & 0xffffffffn);
-  const bHi = Number(base >> 32n);
   for (let k = 0; k < vals.length; k++) {
-    const v = vals[k] + bLo;                 // exact in a double
-    const hi = Math.floor(v / 4294967296);
-    out[2 * k] = v - hi * 4294967296;
-    out[2 * k + 1] = bHi + hi;
+    const hi = Math.floor(vals[k] / 4294967296);
+    out[2 * k] = vals[k] - hi * 4294967296;
+    out[2 * k + 1] = hi;
   }
   return out;
+}
+
+/** A torrent's file table as tv_stage_file_table takes it: file k's length (u64 words) and its path, the k-th
+ * NUL-terminated string of one buffer.  A path holding a NUL cannot be opened (Deno.open refuses it, so
+ * fsStorage.get's piece is null): it goes as "", which the library cannot open either. */
+interface FileTable {
+  dir: string;
+  n: number;
+  lengths: Uint32Array;
+  paths: Uint8Array;
+  // what it was built from: each file's length and path (array) object, compared on reuse without allocating
+  lens: number[];
+  refs: (string[] | string)[];
+}
+const fileTables = new WeakMap<InfoDict, FileTable>();
+
+function fileTable(info: InfoDict, dir: string): FileTable {
+  const files = "files" in info ? info.files : null;
+  const n = files ? files.length : 1;
+  const lenOf = (k: number) => files ? files[k].length : info.length;
+  const refOf = (k: number): string[] | string => files ? files[k].path : info.name;
+  const hit = fileTables.get(info);
+  if (hit && hit.dir === dir && hit.n === n) {
+    let same = true;
+    for (let k = 0; k < n && same; k++) same = hit.lens[k] === lenOf(k) && hit.refs[k] === refOf(k);
+    if (same) return hit;
+  }
+  const enc = new TextEncoder();
+  const lens: number[] = [];
+  const refs: (string[] | string)[] = [];
+  const joined: string[] = [];
+  for (let k = 0; k < n; k++) {
+    const r = refOf(k);
+    lens.push(lenOf(k));
+    refs.push(r);
+    joined.push(typeof r === "string" ? [dir, r].join("/") : [dir, ...r].join("/"));
+  }
+  let cap = n;
+  for (const p of joined) cap += 3 * p.length;   // (UTF-8: at most 3 bytes per UTF-16 code unit)
+  const buf = new Uint8Array(cap);
+  let o = 0;
+  for (const p of joined) {
+    if (!p.includes("\0")) o += enc.encodeInto(p, buf.subarray(o)).written;
+    buf[o++] = 0;
+  }
+  const t = { dir, n, lengths: u64Words(lens), paths: buf.subarray(0, o), lens, refs };
+  fileTables.set(info, t);
+  return t;
 }
 
 export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptions = {}): Promise<Uint8Array> {
@@ -408,28 +472,12 @@ export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptio
   const L = info.pieceLength;
   const devices = opts.devices || [0];
   const raw = piecesRaw(info);
-  const files = "files" in info
-    ? info.files.map((f) => ({ length: f.length, path: [dir, ...f.path].join("/") }))
-    : [{ length: info.length, path: [dir, info.name].join("/") }];
+  const table = fileTable(info, dir);
   const bitfield = new Uint8Array(Math.ceil(P / 8));
-  // every file's path, NUL-terminated, in ONE buffer and one pointer, and where each path starts in it (a
-  // TextEncoder and an UnsafePointer per segment cost 20-30 ms on 10,000 files); it stays referenced by this
-  // call until every shard's nonblocking tv_stage_files has settled.  A path holding a NUL cannot be opened
-  // (Deno.open refuses it, so fsStorage.get's piece is null): it goes as "", which the library cannot open either.
-  const enc = new TextEncoder();
-  let cap = files.length;
-  for (const f of files) cap += 3 * f.path.length;   // (UTF-8: at most 3 bytes per UTF-16 code unit)
-  const pathBuf = new Uint8Array(cap);
-  const pathAt = new Float64Array(files.length);
-  for (let k = 0, o = 0; k < files.length; k++) {
-    pathAt[k] = o;
-    const p = files[k].path;
-    if (!p.includes("\0")) o += enc.encodeInto(p, pathBuf.subarray(o)).written;
-    pathBuf[o++] = 0;
-  }
+  const u8 = (a: ArrayBufferView) => new Uint8Array(a.buffer, a.byteOffset, a.byteLength);
 
   const ranges = shardRanges(P, devices.length);
-  const threads = shardThreads(opts, activeShards(ranges));
+  const threads = shardThreads(opts, activeShards(ranges), l);
   await Promise.all(ranges.map(async ([first, count], s) => {
     if (count === 0) return;
     await withContext(l, devices[s], s, async (ctx) => {
@@ -439,57 +487,16 @@ export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptio
       check(l, ctx, l.symbols.tv_set_digests(ctx, ptr(raw), BigInt(raw.length)));
       const avail = new Uint8Array(Math.ceil(count / 8)).fill(0xff);
       if (count % 8) avail[avail.length - 1] = (0xff00 >> (count % 8)) & 0xff;
-      const clear = (lo: number, hi: number) => {
-        for (let j = Math.max(0, lo); j <= Math.min(count - 1, hi); j++) avail[j >> 3] &= ~(128 >> (j % 8));
-      };
       // pieces whose bytes extend past the last file (more digests than data) are unreadable
-      for (let j = count - 1; j >= 0 && (first + j) * L + pieceLength(first + j, info) > info.length; j--) clear(j, j);
-      const lo = first * L;
-      const hi = Math.min(info.length, (first + count - 1) * L + pieceLength(first + count - 1, info));
-      // findAndDo's walk over the files in order (storage.ts:105-128), restricted to [lo, hi): every
-      // segment of the shard goes to the library in ONE tv_stage_files call
-      // The walk's zero-length segments go too (storage.ts:109-110: a file ending exactly where a piece starts,
-      // a zero-length file inside a piece): fsStorage.get still opens them (storage.ts:158), and the library
-      // marks the segment's piece (linear / L) where that open would fail.
-      // segment k: file segFile[k] bytes [segFo[k], + segLen[k]) -> linear segLin[k]
-      const segFile: number[] = [];
-      const segFo: number[] = [];
-      const segLin: number[] = [];
-      const segLen: number[] = [];
-      let fileStart = 0;
-      for (let k = 0; k < files.length; k++) {
-        const f = files[k];
-        const fileEnd = fileStart + f.length;
-        const a = Math.max(lo, fileStart);
-        const b = Math.min(hi, fileEnd);
-        if (b > a) {
-          segFile.push(k);
-          segFo.push(a - fileStart);
-          segLin.push(a);
-          segLen.push(b - a);
-        }
-        // (a file with bytes in the range also gives one when it ends on a later piece's start)
-        if (fileEnd >= lo && fileEnd < hi && (f.length === 0 || fileEnd % L === 0)) {
-          segFile.push(k);
-          segFo.push(f.length);
-          segLin.push(fileEnd);
-          segLen.push(0);
-        }
-        fileStart = fileEnd;
-        if (fileStart >= hi) break;
+      for (let j = count - 1; j >= 0 && (first + j) * L + pieceLength(first + j, info) > info.length; j--) {
+        avail[j >> 3] &= ~(128 >> (j % 8));
       }
-      if (segFile.length) {
-        const n = segFile.length;
-        const base = BigInt(Deno.UnsafePointer.value(Deno.UnsafePointer.of(pathBuf)));
-        const paths = u64Words(segFile.map((f) => pathAt[f]), base);
-        const fo = u64Words(segFo, 0n), lin = u64Words(segLin, 0n), len = u64Words(segLen, 0n);
-        const status = new Int32Array(n);
-        const u8 = (a: ArrayBufferView) => new Uint8Array(a.buffer, a.byteOffset, a.byteLength);
-        // a failed segment's pieces are marked inside the library (tv_verify reports them 0), from the piece
-        // holding its first unreadable byte on, as Storage.get reads piece by piece: `status` is informational
-        check(l, ctx, await l.symbols.tv_stage_files(ctx, BigInt(n), ptr(u8(paths)), ptr(u8(fo)), ptr(u8(lin)),
-                                                     ptr(u8(len)), ptr(u8(status))));
-      }
+      // the shard's segments of findAndDo's walk (storage.ts:105-128), made by the library from the table; a failed
+      // segment's pieces are marked inside the library (tv_verify reports them 0), from the piece holding its first
+      // unreadable byte on, as Storage.get reads piece by piece: the per-file `status` is informational
+      const status = new Int32Array(table.n);
+      check(l, ctx, await l.symbols.tv_stage_file_table(ctx, BigInt(table.n), ptr(u8(table.lengths)), ptr(table.paths),
+                                                        BigInt(table.paths.length), ptr(u8(status))));
       const out = new Uint8Array(Math.ceil(count / 8));
       check(l, ctx, await l.symbols.tv_verify(ctx, ptr(avail), ptr(out)));
       bitfield.set(out, first / 8);
