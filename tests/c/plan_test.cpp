@@ -4,6 +4,8 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include <algorithm>
+
 #include "../../torrent_amd/csrc/tv_plan.h"
 
 using tvi::PayloadPlan;
@@ -19,7 +21,7 @@ static int failures = 0;
 
 // allocate under a device that holds `capacity` bytes; returns the status, the plan, the tries
 static int run(uint64_t count, uint64_t stride, uint64_t budget, uint64_t capacity, PayloadPlan* plan, int* tries,
-               uint64_t* held_budget) {
+               uint64_t* held_budget, int bufs = tvi::kWinBufsDefault) {
     const uint64_t slack = 256;
     *tries = 0;
     uint64_t failed = 0;
@@ -33,7 +35,7 @@ static int run(uint64_t count, uint64_t stride, uint64_t budget, uint64_t capaci
             }
             return p.bytes <= capacity ? 0 : 1;
         },
-        plan, held_budget, &failed);
+        plan, held_budget, &failed, bufs);
 }
 
 int main() {
@@ -44,9 +46,20 @@ int main() {
     // cfg2 on an idle MI355X: the whole shard
     CHECK(run(16384, MiB + 256, 280 * GiB, 288 * GiB, &p, &tries, &b) == 0 && !p.win && tries == 1);
     CHECK(p.bytes == 16384 * (MiB + 256) + 256);
-    // a budget below the shard: two windows within the budget, a multiple of 64 pieces
-    CHECK(run(16384, MiB + 256, 2 * GiB, 288 * GiB, &p, &tries, &b) == 0 && p.win && p.bufs == 2);
+    // a budget below the shard: the default window buffers within the budget, a multiple of 64 pieces
+    CHECK(run(16384, MiB + 256, 2 * GiB, 288 * GiB, &p, &tries, &b) == 0 && p.win && p.bufs == tvi::kWinBufsDefault);
     CHECK(p.bytes <= 2 * GiB && p.win_n % 64 == 0 && p.win_n >= 256);
+    // two buffers asked for: two windows of twice the pieces
+    CHECK(run(16384, MiB + 256, 2 * GiB, 288 * GiB, &p, &tries, &b, 2) == 0 && p.win && p.bufs == 2);
+    CHECK(p.bytes <= 2 * GiB && p.win_n == 1024 - 64);
+    // a budget of three one-piece windows asks for four buffers: three (one piece each)
+    CHECK(run(100, MiB + 256, 3 * (MiB + 512), 288 * GiB, &p, &tries, &b) == 0 && p.bufs == 3 && p.win_n == 1);
+    // more buffers than windows are never allocated
+    CHECK(run(3, MiB + 256, 3 * MiB, 288 * GiB, &p, &tries, &b, 8) == 0 && p.win && p.win_n * p.bufs <= 3 + 2);
+    for (int B = 1; B <= tvi::kWinBufsMax + 2; B++) {
+        CHECK(run(16384, MiB + 256, GiB / 2, 288 * GiB, &p, &tries, &b, B) == 0 && p.win && p.bytes <= GiB / 2);
+        CHECK(p.bufs == std::min(B, tvi::kWinBufsMax));
+    }
     // the budget says yes, the device says no: retried with smaller windows until one fits
     CHECK(run(51200, 4 * MiB + 256, 200 * GiB, 3 * GiB, &p, &tries, &b) == 0 && p.win && p.bytes <= 3 * GiB);
     CHECK(tries > 1 && b < 200 * GiB);

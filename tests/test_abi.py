@@ -260,6 +260,8 @@ def test_option_and_counter_constants_match_header():
     assert [k.split("_", 3)[3].lower() if k.startswith("TV_FILE_PHASE_") else
             "bytes_" + k.split("_")[-1].lower() if k.startswith("TV_FILE_BYTES_") else
             "odirect_" + k.split("_")[-1].lower() for _, k in phases] == list(_native.TV_FILE_PHASES)
+    plan = open(os.path.join(ROOT, "torrent_amd", "csrc", "tv_plan.h")).read()
+    assert int(re.search(r"kWinBufsDefault = (\d+);", plan).group(1)) == _native.WIN_BUFS_DEFAULT
     ts = open(os.path.join(ROOT, "ts", "verify.ts")).read()
     for m in re.finditer(r"const\s+(TV_\w+)\s*=\s*(-?\d+)\s*;", ts):
         assert public[m.group(1)] == int(m.group(2)), m.group(1)

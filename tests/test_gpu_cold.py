@@ -123,7 +123,7 @@ def test_random_layouts_cold_long_path(native, tmp_path, monkeypatch, seed):
     stride = -(-info.piece_length // 64) * 64 + 256
     # whole shards on one and three devices, then a windowed layout (a budget of ~3 pieces per window: the lanes
     # stage window by window, each window hashed while the next stages)
-    for devices, budget in (([0], None), ([0, 0, 0], None), ([0], 2 * (3 * stride + 256))):
+    for devices, budget in (([0], None), ([0, 0, 0], None), ([0], native.WIN_BUFS_DEFAULT * (3 * stride + 256))):
         if paths:
             assert fsutil.drop_cache(paths) <= 0.01
         bf = verify_files(info, str(tmp_path / "dl"), devices=devices, threads=4, direct_min=1, budget=budget)

@@ -88,7 +88,7 @@ def test_restaged_file_clears_the_unreadable_mark(native, oracle, tmp_path, wind
     a.write_bytes(payload[:cut])
     with native.Context(0) as ctx:
         if windowed:                         # windows of 4 pieces: every stage is a new pass
-            ctx.set_option(native.TV_OPT_RESIDENT_BUDGET, 2 * (4 * (L + 256) + 256))
+            ctx.set_option(native.TV_OPT_RESIDENT_BUDGET, native.WIN_BUFS_DEFAULT * (4 * (L + 256) + 256))
         ctx.set_layout(total, L, P)
         ctx.set_digests(pieces)
         assert ctx.stage_file(str(a), 0, 0, cut)

@@ -22,9 +22,11 @@ def _stride(L):
     return -(-L // 64) * 64 + 256
 
 
-def _budget(L, pieces_per_window):
-    """A budget whose windows hold `pieces_per_window` pieces (two buffers of them)."""
-    return 2 * (pieces_per_window * _stride(L) + 256)
+def _budget(L, pieces_per_window, bufs=None):
+    """A budget whose windows hold `pieces_per_window` pieces (the default count of window buffers of them,
+    tv_plan.h kWinBufsDefault, or `bufs`)."""
+    from torrent_amd import _native
+    return (bufs or _native.WIN_BUFS_DEFAULT) * (pieces_per_window * _stride(L) + 256)
 
 
 def _check_windowed(budget, expect_windowed=True):
@@ -192,10 +194,12 @@ def test_windowed_rules(native, oracle):
         ctx.set_option(native.TV_OPT_RESIDENT_BUDGET, P * stride + 256)      # fits exactly: not windowed
         ctx.set_layout(total, L, P)
         assert ctx.counter(native.TV_COUNTER_WINDOW_PIECES) == 0
-        ctx.set_option(native.TV_OPT_RESIDENT_BUDGET, 2 * (7 * stride + 256))
+        ctx.set_option(native.TV_OPT_RESIDENT_BUDGET, _budget(L, 7))
         ctx.set_layout(total, L, P)
         assert ctx.counter(native.TV_COUNTER_WINDOW_PIECES) == 7
-        assert ctx.counter(native.TV_COUNTER_PAYLOAD_BYTES) == 2 * (7 * stride + 256)
+        assert ctx.counter(native.TV_COUNTER_PAYLOAD_BYTES) == _budget(L, 7)
+        assert ctx.counter(native.TV_COUNTER_WINDOW_BUFS) == native.WIN_BUFS_DEFAULT
+        assert ctx.counter(native.TV_COUNTER_WINDOW_STREAMS) == native.WIN_BUFS_DEFAULT - 1
         ctx.set_digests(pieces)
         ctx.stage(0, payload[:30 * L])                  # windows 0-4 (pieces 0-29)
         out = bytearray(L)
@@ -374,3 +378,44 @@ def test_stage_ranges_of_one_buffer(native, oracle):
         with pytest.raises(ValueError):       # an offset that wraps when added (-1 as uint64) is refused too
             ctx.stage_ranges(payload, [0], np.array([-1], dtype=np.int64), [2])
     assert _bits(bf, P) == [0 if i == 5 else 1 for i in range(P)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bufs,streams", [(1, 0), (2, 0), (2, 1), (3, 0), (4, 0), (4, 1), (4, 2), (8, 0), (8, 4)])
+def test_window_buffers_and_hash_streams(native, oracle, bufs, streams):
+    """Windows hashed side by side (TV_OPT_WIN_BUFS buffers, TV_OPT_WIN_STREAMS hash streams)
+    give the bits and digests of one buffer at a time: a ragged 203-piece shard with a short last piece and
+    corrupted digests, staged in one call and in uneven calls (some pieces twice, a gap), filled by the device
+    generator, verified and hashed -- every combination equal to the oracle, and the payload within the budget."""
+    L, P = 8192, 203
+    total = L * (P - 1) + 777
+    payload = bytes(oracle.synth_fill(91, 0, total))
+    pieces = bytearray(oracle.hash_pieces(bytearray(payload), total, L, P))
+    clean = bytes(pieces)
+    for i in (0, 17, 64, 150, P - 1):
+        pieces[20 * i + 5] ^= 0x40
+    want = [0 if i in (0, 17, 64, 150, P - 1) else 1 for i in range(P)]
+    budget = _budget(L, 9, bufs)
+    with native.Context(0) as ctx:
+        ctx.set_option(native.TV_OPT_WIN_BUFS, bufs)
+        ctx.set_option(native.TV_OPT_WIN_STREAMS, streams)
+        ctx.set_option(native.TV_OPT_RESIDENT_BUDGET, budget)
+        ctx.set_layout(total, L, P)
+        assert ctx.counter(native.TV_COUNTER_WINDOW_PIECES) == 9
+        assert ctx.counter(native.TV_COUNTER_WINDOW_BUFS) == bufs
+        assert ctx.counter(native.TV_COUNTER_WINDOW_STREAMS) == (streams or max(1, min(4, bufs - 1)))
+        assert ctx.counter(native.TV_COUNTER_PAYLOAD_BYTES) <= budget
+        ctx.set_digests(bytes(pieces))
+        ctx.stage(0, payload)
+        assert _bits(ctx.verify(), P) == want
+        assert ctx.counter(native.TV_COUNTER_WINDOWS) == -(-P // 9)
+        ctx.stage(0, payload)                        # a new pass: the hash of every piece
+        assert ctx.hash() == clean
+        # uneven calls: pieces 0-40 in ragged parts, 41-59 never staged, the rest in one call
+        for a, b in ((0, 5 * L + 3), (5 * L + 3, 5 * L + 4), (5 * L + 4, 41 * L)):
+            ctx.stage(a, payload[a:b])
+        ctx.stage(60 * L, payload[60 * L:])
+        assert _bits(ctx.verify(), P) == [0 if 41 <= i < 60 else w for i, w in enumerate(want)]
+        ctx.fill_synthetic(5)                        # the device generator fills every window
+        synth = bytes(oracle.synth_fill(5, 0, total))
+        assert ctx.hash() == bytes(oracle.hash_pieces(bytearray(synth), total, L, P))

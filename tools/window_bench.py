@@ -3,7 +3,10 @@ resident (one window) and under smaller device budgets (TV_OPT_RESIDENT_BUDGET: 
 previous window hashes), beside the streamed path (verify_stream over the same memory).  Every bitfield is checked
 against hashlib's digests of the payload (1 % of them corrupted; tests/synth.py generates it).
 
-    python tools/window_bench.py [--gib 16] [--piece-mib 1] [--budgets 0,8,2,0.5] [--reps 3]
+    python tools/window_bench.py [--gib 16] [--piece-mib 1] [--budgets 0,8,2,0.5] [--reps 3] [--variants 4:0,2:1]
+
+--variants: window buffers : hash streams (TV_OPT_WIN_BUFS / TV_OPT_WIN_STREAMS; 0 = the library's default) tried
+on every windowed budget (round 6: windows hashed side by side on hash streams of their own).
 
 Prints one JSON line per leg: path, budget (GiB; 0 = automatic), windows and window pieces (the library's
 counters), best and median wall seconds of the call, GB/s (payload bytes / best wall, H2D included)."""
@@ -20,7 +23,7 @@ sys.path.insert(0, ROOT)
 from tests import synth  # noqa: E402  (the generator and hashlib digests: nothing under oracle/ runs here)
 from torrent_amd import _native as N  # noqa: E402
 from torrent_amd.metainfo import make_info  # noqa: E402
-from torrent_amd.verify import context_counters, verify_payload, verify_stream  # noqa: E402
+from torrent_amd.verify import _context, context_counters, verify_payload, verify_stream  # noqa: E402
 
 GiB, MiB = 1 << 30, 1 << 20
 
@@ -31,6 +34,7 @@ def main():
     ap.add_argument("--piece-mib", type=float, default=1)
     ap.add_argument("--budgets", default="0,8,2,0.5")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--variants", default="0:0")
     a = ap.parse_args()
     L = int(a.piece_mib * MiB)
     total = int(a.gib * GiB) // L * L
@@ -51,7 +55,7 @@ def main():
         expect[-1] &= (0xFF << (8 - P % 8)) & 0xFF
     info = make_info(L, bytes(digests), "w", length=total)
 
-    def leg(name, fn, budget_gib):
+    def leg(name, fn, budget_gib, variant=None):
         walls, ok = [], True
         for _ in range(a.reps):
             t0 = time.perf_counter()
@@ -59,7 +63,10 @@ def main():
             walls.append(time.perf_counter() - t0)
             ok &= bytes(bf) == bytes(expect)
         cnt = next(iter(context_counters().values()), {})
+        with _context(0) as ctx:
+            wb, ws = ctx.counter(N.TV_COUNTER_WINDOW_BUFS), ctx.counter(N.TV_COUNTER_WINDOW_STREAMS)
         print(json.dumps({"path": name, "bytes": total, "piece_length": L, "pieces": P, "budget_gib": budget_gib,
+                          "variant": variant, "window_bufs": wb, "hash_streams": ws,
                           "windows": cnt.get("windows"), "window_pieces": cnt.get("window_pieces"),
                           "payload_bytes": cnt.get("payload_bytes"), "best_s": round(min(walls), 4),
                           "median_s": round(statistics.median(walls), 4),
@@ -67,7 +74,15 @@ def main():
 
     for b in [float(x) for x in a.budgets.split(",")]:
         budget = int(b * GiB) if b else None
-        leg("verify_payload resident", lambda: verify_payload(info, buf.mv, budget=budget), b)
+        for v in (a.variants.split(",") if b else ["0:0"]):
+            nb, ns = (int(x) for x in v.split(":"))
+            with _context(0) as ctx:
+                ctx.set_option(N.TV_OPT_WIN_BUFS, nb)
+                ctx.set_option(N.TV_OPT_WIN_STREAMS, ns)
+            leg("verify_payload resident", lambda: verify_payload(info, buf.mv, budget=budget), b, v)
+    with _context(0) as ctx:
+        ctx.set_option(N.TV_OPT_WIN_BUFS, 0)
+        ctx.set_option(N.TV_OPT_WIN_STREAMS, 0)
     leg("verify_stream rows", lambda: verify_stream(info, lambda off, n: buf.mv[off:off + n]), None)
     buf.close()
 

@@ -85,9 +85,13 @@ int tv_create(tv_ctx** out, int device) {
     for (int k = 0; k < 2; k++) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->col_ev[k], hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done_ev[k], hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->win_ev[k], hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->win_cp[k], hipEventDisableTiming);
     }
+    for (int k = 0; k < tvi::kWinBufsMax; k++)
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->win_ev[k], hipEventDisableTiming);
+    for (int k = 0; k < tvi::kWinHashStreams; k++)
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->win_hs_ev[k], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->win_fill_ev, hipEventDisableTiming);
     if (e != hipSuccess) {
         fail(nullptr, TV_ERR_HIP, "tv_create: %s", hipGetErrorString(e));
         tv_destroy(c);
@@ -113,6 +117,7 @@ void tv_destroy(tv_ctx* c) {
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     if (c->copy_stream2) (void)hipStreamSynchronize(c->copy_stream2);
     if (c->pack_stream) (void)hipStreamSynchronize(c->pack_stream);
+    (void)win_sync_streams(c);
     free_device(c);
     for (int s = 0; s < kRingSlots; s++) {
         if (c->ring[s]) (void)hipHostFree(c->ring[s]);
@@ -123,9 +128,15 @@ void tv_destroy(tv_ctx* c) {
     if (c->h_bits) (void)hipHostFree(c->h_bits);
     if (c->d_clock) (void)hipFree(c->d_clock);
     for (hipEvent_t ev : {c->ev_call0, c->ev_k0, c->ev_k1, c->ev_call1, c->ev_avail, c->col_ev[0], c->col_ev[1],
-                          c->done_ev[0], c->done_ev[1], c->ev_fork, c->ev_join, c->win_ev[0], c->win_ev[1],
-                          c->win_cp[0], c->win_cp[1]})
+                          c->done_ev[0], c->done_ev[1], c->ev_fork, c->ev_join, c->win_cp[0], c->win_cp[1],
+                          c->win_fill_ev})
         if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : c->win_ev)
+        if (ev) (void)hipEventDestroy(ev);
+    for (int k = 0; k < tvi::kWinHashStreams; k++) {
+        if (c->win_hs_ev[k]) (void)hipEventDestroy(c->win_hs_ev[k]);
+        if (c->win_hs[k]) (void)hipStreamDestroy(c->win_hs[k]);
+    }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->copy_stream2) (void)hipStreamDestroy(c->copy_stream2);
@@ -248,6 +259,16 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
         case TV_OPT_FILE_CLOCK_RESET:
             for (auto& v : c->file_ns) v.store(0);
             return TV_OK;
+        case TV_OPT_WIN_BUFS:
+            if (value < 0 || value > kWinBufsMax)
+                return fail(c, TV_ERR_ARG, "TV_OPT_WIN_BUFS must be 0 (default) .. %d", kWinBufsMax);
+            c->win_bufs_opt = (int)value;   // takes effect at the next tv_set_layout
+            return TV_OK;
+        case TV_OPT_WIN_STREAMS:
+            if (value < 0 || value > kWinHashStreams)
+                return fail(c, TV_ERR_ARG, "TV_OPT_WIN_STREAMS must be 0 (default) .. %d", kWinHashStreams);
+            c->win_streams_opt = (int)value;   // takes effect at the next tv_set_layout
+            return TV_OK;
         case TV_OPT_STREAM_ROWS:
             if (value != 0 && value != 1) return fail(c, TV_ERR_ARG, "TV_OPT_STREAM_ROWS must be 0 or 1");
             if (c->st.active) return fail(c, TV_ERR_STATE, "TV_OPT_STREAM_ROWS cannot change during a stream");
@@ -283,6 +304,8 @@ int tv_get_option(tv_ctx* c, int key, int64_t* value) {
         case TV_OPT_STREAM_ROWS: *value = c->stream_rows ? 1 : 0; return TV_OK;
         case TV_OPT_CLOCK_PROBE: *value = c->clock_probe ? 1 : 0; return TV_OK;
         case TV_OPT_LANE_PAIRS: *value = c->lane_pairs; return TV_OK;
+        case TV_OPT_WIN_BUFS: *value = c->win_bufs_opt; return TV_OK;
+        case TV_OPT_WIN_STREAMS: *value = c->win_streams_opt; return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
 }
@@ -313,6 +336,10 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
     TV_HIP(c, hipStreamSynchronize(c->stream));
     TV_HIP(c, hipStreamSynchronize(c->copy_stream));
     TV_HIP(c, hipStreamSynchronize(c->copy_stream2));
+    {
+        const int rc = win_sync_streams(c);   // (a window hash of the last layout may still read the payload)
+        if (rc) return rc;
+    }
     c->has_layout = false;
     c->digests_set = false;
     c->total = total_length;
@@ -330,6 +357,7 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
     c->win = false;
     c->win_n = 0;
     c->win_bufs = 0;
+    c->win_nhs = 1;
     c->win_buf_bytes = 0;
     c->win_cur = UINT64_MAX;
     c->win_buf = 1;
@@ -392,7 +420,7 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
                 c->d_payload = nullptr;
                 return last == hipErrorOutOfMemory ? 1 : 2;
             },
-            &plan, &budget, &failed);
+            &plan, &budget, &failed, c->win_bufs_opt > 0 ? c->win_bufs_opt : kWinBufsDefault);
         if (r)
             return fail(c, r == 1 ? TV_ERR_NOMEM : TV_ERR_HIP, "hipMalloc(%llu) of the payload: %s",
                         (unsigned long long)failed, hipGetErrorString(last));
@@ -401,6 +429,12 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
         c->win_n = plan.win_n;
         c->win_bufs = plan.bufs;
         c->win_buf_bytes = plan.buf_bytes;
+        // hash streams: one per window that may hash while the next one stages (TV_OPT_WIN_STREAMS overrides)
+        c->win_nhs = c->win ? std::max(1, std::min(kWinHashStreams, c->win_streams_opt > 0 ? c->win_streams_opt
+                                                                                          : plan.bufs - 1))
+                            : 1;
+        for (int k = 0; c->win_nhs > 1 && k < c->win_nhs; k++)
+            if (!c->win_hs[k]) TV_HIP(c, hipStreamCreateWithFlags(&c->win_hs[k], hipStreamNonBlocking));
     } else {
         if (!need_payload || !reuse_fits(need_payload, c->cap_payload)) free_payload(c);
         if (need_payload && !c->d_payload) {
@@ -538,6 +572,8 @@ int tv_get_counter(tv_ctx* c, int key, uint64_t* value) {
         }
         case TV_COUNTER_WINDOW_PIECES: *value = c->win ? c->win_n : 0; return TV_OK;
         case TV_COUNTER_WINDOWS: *value = c->win_launched; return TV_OK;
+        case TV_COUNTER_WINDOW_BUFS: *value = c->win ? (uint64_t)c->win_bufs : 0; return TV_OK;
+        case TV_COUNTER_WINDOW_STREAMS: *value = c->win ? (uint64_t)c->win_nhs : 0; return TV_OK;
         case TV_COUNTER_BUDGET: *value = c->budget; return TV_OK;
         case TV_COUNTER_SLOTS_USED: *value = c->slot_of.size(); return TV_OK;
         case TV_COUNTER_FILE_CLOCK + TV_FILE_PHASE_OPEN ... TV_COUNTER_FILE_CLOCK + TV_FILE_CLOCK_N - 1:

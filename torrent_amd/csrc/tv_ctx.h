@@ -31,6 +31,7 @@ namespace tvi {
 constexpr uint64_t kSlack = 256;                          // bytes past the last resident piece (tail over-read)
 constexpr int kRingSlots = TV_STREAM_RING_SLOTS;          // pinned staging buffers per lane
 constexpr size_t kRingSlotBytes = TV_STREAM_SLOT_BYTES;
+constexpr int kWinHashStreams = 4;                        // hash streams of a windowed layout, at most
 
 // Pin the calling thread to `cpus` (nullptr: leave it).  Used for the library's own threads only.
 void pin_thread(const cpu_set_t* cpus);
@@ -262,7 +263,7 @@ struct tv_ctx {
     uint64_t budget = 0;               // the budget the last tv_set_layout applied (0: no resident payload)
     bool win = false;                  // the layout is windowed
     uint64_t win_n = 0;                // pieces per window
-    int win_bufs = 0;                  // buffers in d_payload (2: window k + 1 stages while k hashes; 1)
+    int win_bufs = 0;                  // buffers in d_payload (window k + 1 stages while those before it hash)
     uint64_t win_buf_bytes = 0;        // bytes per buffer (win_n * stride + kSlack)
     uint64_t win_cur = UINT64_MAX;     // window open for staging (UINT64_MAX: none)
     int win_buf = 1;                   // its buffer
@@ -271,8 +272,16 @@ struct tv_ctx {
     bool win_timing = false;           // ev_call0 / ev_k0 recorded for this pass
     uint64_t win_launched = 0;         // windows hashed this pass
     uint64_t win_passes = 0;           // passes finalized since tv_set_layout
-    hipEvent_t win_ev[2] = {nullptr, nullptr};  // the last kernel reading buffer k
+    hipEvent_t win_ev[tvi::kWinBufsMax] = {};   // the last kernel reading buffer k
     hipEvent_t win_cp[2] = {nullptr, nullptr};  // copies into the window queued on lane k (kernel waits on them)
+    // Hash streams: with more than one, window w hashes on win_hs[w mod win_nhs] (companions off), so windows hash
+    // side by side while the next ones stage; with one, on the compute stream (the round-1..5 form).
+    int win_bufs_opt = 0;              // TV_OPT_WIN_BUFS (0: tv_plan.h kWinBufsDefault)
+    int win_streams_opt = 0;           // TV_OPT_WIN_STREAMS (0: win_bufs - 1, at most kWinHashStreams)
+    int win_nhs = 1;                   // hash streams of the current windowed layout
+    hipStream_t win_hs[tvi::kWinHashStreams] = {};
+    hipEvent_t win_hs_ev[tvi::kWinHashStreams] = {};  // joins a hash stream into the compute stream
+    hipEvent_t win_fill_ev = nullptr;  // compute-stream work (window fills) a window's hash waits for
 
     // Slot pool (TV_OPT_LIST_SLOTS = K): the payload holds K piece slots instead of the shard; a staged piece
     // takes a slot until tv_verify_list lists it (incremental verify).
@@ -437,7 +446,8 @@ int launch_avail(tv_ctx* c, const uint8_t* avail_bits, const uint64_t** out);
 int choose_kernel_n(const tv_ctx* c, uint64_t n, bool short_last);
 int choose_kernel(const tv_ctx* c);
 uint32_t lane_pairs_for(const tv_ctx* c, uint64_t n);
-int launch_resident(tv_ctx* c, const TvPieces& p_in, int kernel, bool hash);
+int launch_resident(tv_ctx* c, const TvPieces& p_in, int kernel, bool hash, hipStream_t on = nullptr);
+int win_sync_streams(tv_ctx* c);
 TvPieces resident_launch(const tv_ctx* c);
 TvPieces window_launch(const tv_ctx* c, uint64_t j0, uint64_t n, const uint8_t* data);
 int read_bits(tv_ctx* c, uint8_t* out);

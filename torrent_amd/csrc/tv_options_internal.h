@@ -28,6 +28,12 @@
    3 = companions whatever other processes hold on the GPU (the co-tenant check of 1 skipped) */
 #define TV_COUNTER_COTENANT_VRAM 120 /* bytes of this GPU's memory other processes hold (KFD: /sys/class/kfd/kfd/proc/
                                         <pid>/vram_<gpu_id>; 0 when unreadable): >= 1 GiB turns auto companions off */
+#define TV_OPT_WIN_BUFS 23    /* windowed layouts: window buffers, 0 (default) = tv_plan.h kWinBufsDefault (4), else 1..8
+                                 (set before tv_set_layout) */
+#define TV_OPT_WIN_STREAMS 24 /* windowed layouts: hash streams, 0 (default) = buffers - 1 (at most 4), else 1..4; 1 =
+                                 every window hashed on the compute stream, one after the other (rounds 1-5) */
+#define TV_COUNTER_WINDOW_BUFS 122    /* window buffers of the current windowed layout (0: not windowed) */
+#define TV_COUNTER_WINDOW_STREAMS 123 /* its hash streams (1: the compute stream) */
 #define TV_COUNTER_KFD_GPU_ID 121    /* the GPU's KFD gpu_id when the co-tenant check can run (reading it probes for this
                                         process's own accounting entry if not yet known); 0: it cannot */
 #define TV_OPT_TWIN_FILL_READS 14 /* companion workgroups' loads: 0 (default) = every lane of a companion reads its

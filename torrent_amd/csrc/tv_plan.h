@@ -16,26 +16,36 @@ struct PayloadPlan {
     uint64_t buf_bytes = 0;
 };
 
+// Window buffers of a windowed layout by default (TV_OPT_WIN_BUFS = 0): window w + 1 stages while up to three
+// windows before it hash, each on a hash stream of its own (a window's hash takes one piece's serial SHA-1 whatever
+// its piece count, so under a small budget the windows must hash side by side to keep staging busy).
+constexpr int kWinBufsDefault = 4;
+constexpr int kWinBufsMax = 8;
+
 // `count` pieces at `stride` bytes (+ `slack` after the last) under `budget` bytes: the whole shard when it fits,
-// else two window buffers of W pieces (one buffer when the budget holds only one; W >= 1 even when one piece
-// exceeds the budget; a multiple of 64 from 256 up, so each window is whole 64-piece waves).
-inline PayloadPlan plan_payload(uint64_t count, uint64_t stride, uint64_t slack, uint64_t budget) {
+// else `bufs` window buffers of W pieces (fewer buffers when the budget cannot hold one piece in each; never more
+// than there are windows; W >= 1 even when one piece exceeds the budget; a multiple of 64 from 256 up, so each
+// window is whole 64-piece waves).
+inline PayloadPlan plan_payload(uint64_t count, uint64_t stride, uint64_t slack, uint64_t budget,
+                                int bufs = kWinBufsDefault) {
     PayloadPlan p;
     if (count == 0) return p;
     p.bytes = count * stride + slack;
     if (p.bytes <= budget) return p;
-    uint64_t bufs = 2, W = budget / 2 > slack ? (budget / 2 - slack) / stride : 0;
-    if (W == 0) {
-        bufs = 1;
-        W = budget > slack ? (budget - slack) / stride : 0;
+    uint64_t B = (uint64_t)std::max(1, std::min(bufs, kWinBufsMax)), W = 0;
+    for (; B > 1; B--) {
+        W = budget / B > slack ? (budget / B - slack) / stride : 0;
+        if (W) break;
     }
+    if (B == 1) W = budget > slack ? (budget - slack) / stride : 0;
     W = std::max<uint64_t>(1, std::min(W, count));
     if (W >= 256) W = W / 64 * 64;
+    B = std::max<uint64_t>(1, std::min(B, (count + W - 1) / W));
     p.win = true;
     p.win_n = W;
-    p.bufs = (int)bufs;
+    p.bufs = (int)B;
     p.buf_bytes = W * stride + slack;
-    p.bytes = bufs * p.buf_bytes;
+    p.bytes = B * p.buf_bytes;
     return p;
 }
 
@@ -46,10 +56,10 @@ inline PayloadPlan plan_payload(uint64_t count, uint64_t stride, uint64_t slack,
 // the last request that failed.
 template <class TryAlloc>
 int allocate_payload(uint64_t count, uint64_t stride, uint64_t slack, uint64_t budget, TryAlloc&& try_alloc,
-                     PayloadPlan* out, uint64_t* budget_out, uint64_t* failed_bytes) {
+                     PayloadPlan* out, uint64_t* budget_out, uint64_t* failed_bytes, int bufs = kWinBufsDefault) {
     uint64_t failed = UINT64_MAX;
     for (;;) {
-        const PayloadPlan p = plan_payload(count, stride, slack, budget);
+        const PayloadPlan p = plan_payload(count, stride, slack, budget, bufs);
         const int r = try_alloc(p, budget);
         if (r == 0) {
             *out = p;
