@@ -84,6 +84,21 @@ def piece_ceiling(kernel: int, count: int) -> float:
     rate = 64 * CLOCK_HZ / (SERIAL_INSTR.get(kernel, SERIAL_INSTR[1]) * LONE_WAVE_CYC)   # B/s per piece
     return min(VALU_PEAK_GBPS, count * rate / 1e9)
 
+def kernel_for(count: int, cus: int = 256) -> int:
+    """The library's automatic kernel for a resident launch of `count` full pieces (tv_core.hip choose_kernel_n):
+    twin while its 32-piece workgroups number <= 2 per CU, split up to 32,768 pieces, the lane kernel beyond."""
+    if (count + 31) // 32 <= 2 * cus:
+        return 4
+    return 2 if count <= 32768 else 1
+
+
+def aggregate_piece_ceiling(workload: str, n_gpus: int, cus: int = 256) -> float:
+    """What a STRONG-scaled resident workload (one torrent, shard_ranges over n_gpus) can reach at most in all:
+    the sum over ranks of each shard's piece-parallelism ceiling under the kernel the library picks for it."""
+    _, P, _, _ = WORKLOADS[workload]
+    return sum(piece_ceiling(kernel_for(c, cus), c) for _, c in shard_ranges(P, n_gpus) if c)
+
+
 # one page-locked 1 GiB host -> HBM copy on a gpurun box (tools/pcie_probe.py, profiles/r02/pcie_ceiling.json)
 PCIE_H2D_GBPS = 57.6
 
@@ -311,6 +326,7 @@ def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: b
     bytes_all = _sum(dist, float(bytes_rank))
     achieved = bytes_rank / (avg / 1e3) / 1e9
     ceiling = piece_ceiling(kernel, count)
+    ceiling_all = _sum(dist, ceiling)   # every rank's shard at its own kernel's piece ceiling
     if strong:
         what = desc.split(" (")[0] + f" ({P} pieces in all, {ws} shard(s), strong scaling)"
     elif ws > 1:
@@ -327,6 +343,11 @@ def resident_leg(dist, ws: int, rank: int, device: int, workload: str, strong: b
            "kernel_ms_max_over_ranks": round(_max(dist, avg), 3), "achieved": round(achieved, 1),
            "piece_parallelism_ceiling": round(ceiling, 1), "frac_of_piece_ceiling": round(achieved / ceiling, 4),
            "frac_of_valu_peak": round(achieved / VALU_PEAK_GBPS, 4),
+           "aggregate_piece_ceiling": round(ceiling_all, 1),
+           "frac_of_aggregate_piece_ceiling": round(bytes_all * steps / elapsed / 1e9 / ceiling_all, 4),
+           "aggregate_note": "the sum over ranks of each rank's shard piece ceiling (its kernel's serial SHA-1 rate "
+                             "x its pieces): the most this configuration can verify per second on these GPUs; "
+                             "frac_of_aggregate_piece_ceiling = value / it",
            "clock_ghz": round(clock_ghz, 3) if clock_ghz else None,
            "frac_of_valu_peak_at_clock": round(achieved / (VALU_PEAK_GBPS * clock_ghz / (CLOCK_HZ / 1e9)), 4)
            if clock_ghz else None,
@@ -696,7 +717,7 @@ def main() -> int:
     if ws == 1 and workload == "cfg2" and not a.no_cfg3:
         try:
             # (3 ms launches: 20 warm-up steps bring the shader clock up from the layout build's idle, and 20 timed
-            # steps average over its last ramp; rocprofv3 showed 5 timed steps still speeding up, profiles/r05/check2)
+            # steps average over its last ramp; rocprofv3 showed 5 timed steps still speeding up in round 5)
             legs["cfg3"] = cfg3_leg(device, max(20, a.leg_steps), 20, a.kernel)
         except Exception as exc:
             legs["cfg3"] = {"skipped": f"{type(exc).__name__}: {exc}"}
@@ -746,6 +767,8 @@ def main() -> int:
                          "hbm_peak": HBM_PEAK_GBPS, "frac_hbm": round(achieved / HBM_PEAK_GBPS, 4),
                          "piece_parallelism_ceiling": main_leg["piece_parallelism_ceiling"],
                          "frac_of_piece_ceiling": main_leg["frac_of_piece_ceiling"],
+                         "aggregate_piece_ceiling": main_leg["aggregate_piece_ceiling"],
+                         "frac_of_aggregate_piece_ceiling": main_leg["frac_of_aggregate_piece_ceiling"],
                          "clock_ghz": main_leg["clock_ghz"], "frac_at_clock": main_leg["frac_of_valu_peak_at_clock"],
                          "valu_peak_derivation": VALU_DERIVATION,
                          "note": "SHA-1 is serial per piece, so P pieces per GPU cap the rate at P x 64 B / "
@@ -754,6 +777,21 @@ def main() -> int:
                                  "pieces per GPU (piece_saturated)"},
             "ground_truth_s": main_leg["ground_truth_s"],
         }
+        out["scaling_note"] = (
+            f"value is {workload} {'strong' if strong else 'weak'}-scaled "
+            + ("(each GPU verifies its own 16 GiB / 16,384-piece shard of an N x 16 GiB torrent, no collective), "
+               if workload == "cfg2" and not strong else "")
+            + "so the driver's per-N curve of value is one configuration; BASELINE configs[3] -- ONE 200 GiB torrent "
+              "of 51,200 x 4 MiB pieces sharded over the N GPUs -- is the cfg4 leg at every N: read the sharded "
+              "curve from cfg4.value against cfg4.aggregate_piece_ceiling (piece-bound past one GPU, "
+              f"predicted {round(aggregate_piece_ceiling('cfg4', ws), 1)} GB/s at N = {ws})")
+        if "cfg4" in legs and "value" in legs["cfg4"]:
+            out["scaling_figure"] = {"workload": "cfg4 (BASELINE configs[3], strong)", "value": legs["cfg4"]["value"],
+                                     "aggregate_piece_ceiling": legs["cfg4"]["aggregate_piece_ceiling"],
+                                     "frac_of_aggregate_piece_ceiling":
+                                         legs["cfg4"]["frac_of_aggregate_piece_ceiling"],
+                                     "predicted_aggregate_piece_ceiling":
+                                         round(aggregate_piece_ceiling("cfg4", ws), 1)}
         out.update(legs)
         if ws == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(share, a.cpu_seconds)

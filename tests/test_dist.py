@@ -110,7 +110,29 @@ def test_bench_two_ranks_on_the_hip_path(scaling):
     assert len(lines) == 1, r.stdout
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["scaling"] == scaling and rec["bitfield_exact"] is True
+    assert "cfg4" in rec["scaling_note"] and rec["roofline"]["aggregate_piece_ceiling"] > 0
     if scaling == "strong":
         assert rec["config"]["total_pieces"] == 1000 and rec["config"]["pieces_per_gpu"] == 504
     else:
         assert rec["config"]["total_pieces"] == 2000 and rec["config"]["pieces_per_gpu"] == 1000
+
+
+def test_aggregate_piece_ceiling_follows_the_shards():
+    """bench.aggregate_piece_ceiling (what BASELINE configs[3], the 200 GiB cfg4 torrent sharded
+    over N GPUs, can reach at most): the sum over verify.shard_ranges(51200, N) of each shard's piece ceiling under
+    the kernel the library picks for it -- the lane kernel on one GPU (51,200 pieces saturate R_valu's cap), the
+    twin kernel on 6,400-piece shards at N = 8 -- for N = 1, 2, 4, 8."""
+    import bench
+    from torrent_amd.verify import shard_ranges
+    for n in (1, 2, 4, 8):
+        shards = [c for _, c in shard_ranges(51200, n) if c]
+        assert sum(shards) == 51200 and len(shards) == n
+        want = sum(bench.piece_ceiling(bench.kernel_for(c), c) for c in shards)
+        assert bench.aggregate_piece_ceiling("cfg4", n) == pytest.approx(want)
+    assert [bench.kernel_for(c) for c in (6400, 12800, 16384, 16385, 25600, 32768, 32769, 51200)] == \
+        [4, 4, 4, 2, 2, 2, 1, 1]
+    one = bench.aggregate_piece_ceiling("cfg4", 1)
+    assert one == pytest.approx(min(bench.VALU_PEAK_GBPS, bench.piece_ceiling(1, 51200)))
+    eight = bench.aggregate_piece_ceiling("cfg4", 8)
+    assert eight == pytest.approx(8 * bench.piece_ceiling(4, 6400))
+    assert 4000 < eight < 5000     # piece-bound past one GPU (DESIGN.md: flat at ~4.2-4.5 TB/s measured)

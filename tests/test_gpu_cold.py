@@ -22,8 +22,9 @@ def _bits(bf, n):
     return [(bf[i >> 3] >> (7 - (i & 7))) & 1 for i in range(n)]
 
 
+@pytest.mark.parametrize("bounce", [0, 4])      # the ring path / the bounce path (the default)
 @pytest.mark.parametrize("odirect", [1, 0, 2])
-def test_cold_files_exact(native, oracle, tmp_path, odirect):
+def test_cold_files_exact(native, oracle, tmp_path, odirect, bounce):
     import fsutil
     from torrent_amd import FileInfo, Storage, make_info, verify_files
     from torrent_amd.storage import fs_storage
@@ -56,6 +57,7 @@ def test_cold_files_exact(native, oracle, tmp_path, odirect):
         want[i] = int(b is not None and hashlib.sha1(b).digest() == bytes(digests[20 * i:20 * i + 20]))
     with _context(0) as ctx:
         ctx.set_option(native.TV_OPT_FILE_ODIRECT, odirect)
+        ctx.set_option(native.TV_OPT_FILE_BOUNCE, bounce)   # (4 readers per lane into 4 MiB bounce buffers)
         ctx._reset_file_clock()
     # warm (just written): read through the page cache, never O_DIRECT (an overlay /tmp once made warm files look
     # cold to cachestat and sent them to the disk at a third of the speed)
@@ -82,6 +84,7 @@ def test_cold_files_exact(native, oracle, tmp_path, odirect):
     finally:
         with _context(0) as ctx:
             ctx.set_option(native.TV_OPT_FILE_ODIRECT, 1)
+            ctx.set_option(native.TV_OPT_FILE_BOUNCE, native.FILE_BOUNCE_DEFAULT)
     assert _bits(bf, P) == want
     if odirect == 1:
         assert clock["bytes_odirect"] > 0, clock      # (the cold chunks whose offsets agree mod 4 went O_DIRECT)
@@ -123,14 +126,23 @@ def test_random_layouts_cold_long_path(native, tmp_path, monkeypatch, seed):
     stride = -(-info.piece_length // 64) * 64 + 256
     # whole shards on one and three devices, then a windowed layout (a budget of ~3 pieces per window: the lanes
     # stage window by window, each window hashed while the next stages)
-    for devices, budget in (([0], None), ([0, 0, 0], None), ([0], native.WIN_BUFS_DEFAULT * (3 * stride + 256))):
+    from torrent_amd.verify import _context
+    for devices, budget, bounce in (([0], None, 4), ([0, 0, 0], None, 4), ([0], None, 0), ([0], None, 2),
+                                    ([0], native.WIN_BUFS_DEFAULT * (3 * stride + 256), 0)):
         if paths:
             assert fsutil.drop_cache(paths) <= 0.01
-        bf = verify_files(info, str(tmp_path / "dl"), devices=devices, threads=4, direct_min=1, budget=budget)
-        assert _bits(bf, P) == want_fs, (seed, devices, budget)
+        with _context(0) as ctx:
+            ctx.set_option(native.TV_OPT_FILE_BOUNCE, bounce)
+        try:
+            bf = verify_files(info, str(tmp_path / "dl"), devices=devices, threads=4, direct_min=1, budget=budget)
+        finally:
+            with _context(0) as ctx:
+                ctx.set_option(native.TV_OPT_FILE_BOUNCE, native.FILE_BOUNCE_DEFAULT)
+        assert _bits(bf, P) == want_fs, (seed, devices, budget, bounce)
 
 
-def test_cold_file_end_stays_o_direct(native, oracle, tmp_path):
+@pytest.mark.parametrize("bounce", [0, 3])
+def test_cold_file_end_stays_o_direct(native, oracle, tmp_path, bounce):
     """A cold file whose size is not a multiple of 4 KiB: the O_DIRECT request for its last chunk runs past the end
     of the file and comes back short.  That read is complete (the bytes asked for are in) and must not be continued
     (a next request would start off a 4 KiB boundary and be refused, sending the chunk through the buffered fallback
@@ -151,6 +163,7 @@ def test_cold_file_end_stays_o_direct(native, oracle, tmp_path):
     assert fsutil.drop_cache([str(f)]) <= 0.01
     with _context(0) as ctx:
         ctx.set_option(native.TV_OPT_FILE_ODIRECT, 1)
+        ctx.set_option(native.TV_OPT_FILE_BOUNCE, bounce)
         ctx._reset_file_clock()
     cwd = os.getcwd()
     os.chdir(str(tmp_path))
@@ -158,6 +171,8 @@ def test_cold_file_end_stays_o_direct(native, oracle, tmp_path):
         bf = verify_files(info, str(tmp_path))
     finally:
         os.chdir(cwd)
+        with _context(0) as ctx:
+            ctx.set_option(native.TV_OPT_FILE_BOUNCE, native.FILE_BOUNCE_DEFAULT)
     with _context(0) as ctx:
         clock = ctx._file_clock()
     assert _bits(bf, P) == [1] * (P - 1) + [0]

@@ -90,7 +90,7 @@ def test_golden_layouts_windowed(native, layout, tmp_path, monkeypatch):
         budget = _budget(L, rng.choice(sizes))
         assert bytes(verify_payload(info, lay["payload"], avail=lay["avail"], devices=devices,
                                     budget=budget)).hex() == rec["expected_bitfield"], (devices, budget)
-        _check_windowed(budget, expect_windowed=devices == [0] and info.n_pieces > 16)
+        _check_windowed(budget, expect_windowed=devices == [0] and info.n_pieces * _stride(L) + 256 > budget)
     monkeypatch.chdir(tmp_path)
     for path, data in lay["disk_files"]().items():
         p = tmp_path.joinpath("dl", *path)
@@ -100,7 +100,7 @@ def test_golden_layouts_windowed(native, layout, tmp_path, monkeypatch):
         budget = _budget(L, rng.choice([2, 5, 16] if info.n_pieces < 1000 else [16, 64]))
         assert bytes(verify_files(info, str(tmp_path / "dl"), devices=devices, threads=4,
                                   budget=budget)).hex() == rec["expected_bitfield"], (devices, budget)
-        _check_windowed(budget, expect_windowed=devices == [0] and info.n_pieces > 16)
+        _check_windowed(budget, expect_windowed=devices == [0] and info.n_pieces * _stride(L) + 256 > budget)
     clean = hashlib.sha1(lay["pieces_raw"]).hexdigest()
     assert clean == rec["pieces_sha1"]
     if not lay["corrupted"]:

@@ -14,6 +14,9 @@ question the round-5 records under profiles/r05/cold_sweep_*.jsonl answer:
   COLD_SPREAD  the C reader's destination spread over 192 MiB (RC_SPREAD), as the library fills its ring
   COLD_FOOT    that destination at 16 / 32 / 48 / 64 MiB
   COLD_DMA     the C reader with a page-locked H2D DMA stream running beside it
+  COLD_LIBBOUNCE  the library's own bounce path (TV_OPT_FILE_BOUNCE = R readers per lane) against the ring path
+               (a "verify_files" leg runs the library's default, since round 6 the bounce path with 4 readers per lane;
+               "ring" names the rounds 4-5 ring path)
   COLD_BOUNCE  the C reader into its own reused buffer, then memcpy'd to the 192 MiB spread (bounce) or DMA'd to the GPU
                from two reused page-locked buffers per reader (bouncedma), against the library (round 6)
 
@@ -115,6 +118,11 @@ def main():
                     ("verify_files O_DIRECT", 16)]
             if os.environ.get("COLD_BOUNCE") == "copy":   # (round 6's first sweep: the host-copy form too)
                 legs += [("ceiling direct 4x4MiB bounce spread", 4), ("ceiling direct 8x4MiB bounce spread", 8)]
+        if os.environ.get("COLD_LIBBOUNCE"):  # the library's bounce path (TV_OPT_FILE_BOUNCE readers per lane)
+            legs = [("ceiling direct 4x4MiB", 4), ("ceiling direct 4x4MiB bouncedma1", 4),
+                    ("verify_files O_DIRECT ring", 16), ("verify_files O_DIRECT bounce2", 16),
+                    ("verify_files O_DIRECT bounce4", 16), ("verify_files O_DIRECT bounce2 1 lane", 16),
+                    ("verify_files O_DIRECT bounce4 1 lane", 16), ("verify_files O_DIRECT bounce8", 16)]
         if os.environ.get("COLD_LANES"):      # also one staging lane (TV_OPT_FILE_CONCURRENT = 0)
             legs = [("ceiling direct 16x4MiB", 16), ("verify_files O_DIRECT", 16),
                     ("verify_files O_DIRECT 1 lane", 16), ("verify_files O_DIRECT 1 lane", 32),
@@ -159,6 +167,10 @@ def main():
                         ctx._reset_file_clock()
                         ctx.set_option(_native.TV_OPT_FILE_CONCURRENT, 0 if "1 lane" in what else 1)
                         ctx.set_option(_native.TV_OPT_NUMA_BIND, 0 if "nobind" in what else 1)
+                        # (bounceR: R bounce readers per lane; ring: the rounds 4-5 ring path; else the default)
+                        nb = (what.split("bounce", 1)[1].split()[0] if "bounce" in what else
+                              "0" if " ring" in what else str(_native.FILE_BOUNCE_DEFAULT))
+                        ctx.set_option(_native.TV_OPT_FILE_BOUNCE, int(nb))
                     t = time.perf_counter()
                     bf = verify_files(info, root, threads=thr)
                     el = time.perf_counter() - t

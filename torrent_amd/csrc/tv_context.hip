@@ -72,6 +72,7 @@ int tv_create(tv_ctx** out, int device) {
     c->device = device;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->win_hs[0], hipStreamNonBlocking);  // (see tv_ctx.h win_hs)
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy_stream2, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
@@ -89,9 +90,8 @@ int tv_create(tv_ctx** out, int device) {
     }
     for (int k = 0; k < tvi::kWinBufsMax; k++)
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->win_ev[k], hipEventDisableTiming);
-    for (int k = 0; k < tvi::kWinHashStreams; k++)
+    for (int k = 0; k < tvi::kWinHashStreams - 1; k++)
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->win_hs_ev[k], hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->win_fill_ev, hipEventDisableTiming);
     if (e != hipSuccess) {
         fail(nullptr, TV_ERR_HIP, "tv_create: %s", hipGetErrorString(e));
         tv_destroy(c);
@@ -127,13 +127,18 @@ void tv_destroy(tv_ctx* c) {
     }
     if (c->h_bits) (void)hipHostFree(c->h_bits);
     if (c->d_clock) (void)hipFree(c->d_clock);
+    for (auto& lane : c->bounce)
+        for (auto& b : lane) {
+            if (b.ev) (void)hipEventSynchronize(b.ev);
+            if (b.ptr) (void)hipHostFree(b.ptr);
+            if (b.ev) (void)hipEventDestroy(b.ev);
+        }
     for (hipEvent_t ev : {c->ev_call0, c->ev_k0, c->ev_k1, c->ev_call1, c->ev_avail, c->col_ev[0], c->col_ev[1],
-                          c->done_ev[0], c->done_ev[1], c->ev_fork, c->ev_join, c->win_cp[0], c->win_cp[1],
-                          c->win_fill_ev})
+                          c->done_ev[0], c->done_ev[1], c->ev_fork, c->ev_join, c->win_cp[0], c->win_cp[1]})
         if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : c->win_ev)
         if (ev) (void)hipEventDestroy(ev);
-    for (int k = 0; k < tvi::kWinHashStreams; k++) {
+    for (int k = 0; k < tvi::kWinHashStreams - 1; k++) {
         if (c->win_hs_ev[k]) (void)hipEventDestroy(c->win_hs_ev[k]);
         if (c->win_hs[k]) (void)hipStreamDestroy(c->win_hs[k]);
     }
@@ -259,6 +264,10 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
         case TV_OPT_FILE_CLOCK_RESET:
             for (auto& v : c->file_ns) v.store(0);
             return TV_OK;
+        case TV_OPT_FILE_BOUNCE:
+            if (value < 0 || value > 16) return fail(c, TV_ERR_ARG, "TV_OPT_FILE_BOUNCE must be 0 (off) .. 16 readers");
+            c->file_bounce = (int)value;
+            return TV_OK;
         case TV_OPT_WIN_BUFS:
             if (value < 0 || value > kWinBufsMax)
                 return fail(c, TV_ERR_ARG, "TV_OPT_WIN_BUFS must be 0 (default) .. %d", kWinBufsMax);
@@ -305,6 +314,7 @@ int tv_get_option(tv_ctx* c, int key, int64_t* value) {
         case TV_OPT_CLOCK_PROBE: *value = c->clock_probe ? 1 : 0; return TV_OK;
         case TV_OPT_LANE_PAIRS: *value = c->lane_pairs; return TV_OK;
         case TV_OPT_WIN_BUFS: *value = c->win_bufs_opt; return TV_OK;
+        case TV_OPT_FILE_BOUNCE: *value = c->file_bounce; return TV_OK;
         case TV_OPT_WIN_STREAMS: *value = c->win_streams_opt; return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);
@@ -433,7 +443,7 @@ int tv_set_layout(tv_ctx* c, uint64_t total_length, uint64_t piece_length, uint6
         c->win_nhs = c->win ? std::max(1, std::min(kWinHashStreams, c->win_streams_opt > 0 ? c->win_streams_opt
                                                                                           : plan.bufs - 1))
                             : 1;
-        for (int k = 0; c->win_nhs > 1 && k < c->win_nhs; k++)
+        for (int k = 0; k + 1 < c->win_nhs; k++)
             if (!c->win_hs[k]) TV_HIP(c, hipStreamCreateWithFlags(&c->win_hs[k], hipStreamNonBlocking));
     } else {
         if (!need_payload || !reuse_fits(need_payload, c->cap_payload)) free_payload(c);

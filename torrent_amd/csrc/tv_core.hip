@@ -491,13 +491,13 @@ uint32_t lane_pairs_for(const tv_ctx* c, uint64_t n) {
 
 // One launch over the resident shard with the chosen kernel (TV_OPT_TWIN_PACK: on the CU-masked pack_stream,
 // forked after everything queued on c->stream and joined back into it).
-int launch_resident(tv_ctx* c, const TvPieces& p_in, int kernel, bool hash, hipStream_t on) {
+int launch_resident(tv_ctx* c, const TvPieces& p_in, int kernel, bool hash, hipStream_t on, bool alone) {
     TvPieces p = p_in;
     p.lane_pairs = lane_pairs_for(c, p.n);
-    if (on && on != c->stream) {
-        // a window's hash on a hash stream of its own: its real grid only (companions would fill every CU and keep
-        // the windows hashing beside it from their CUs)
-        TV_HIP(c, tv_launch_verify(p, kernel, hash, on, c->split_pairs, &c->last_workgroups));
+    if (!alone) {
+        // a window's hash beside others on the hash streams: its real grid only (companions would fill every CU and
+        // keep the windows hashing beside it from their CUs)
+        TV_HIP(c, tv_launch_verify(p, kernel, hash, on ? on : c->stream, c->split_pairs, &c->last_workgroups));
         return TV_OK;
     }
     // A CU running ONE 2-wave twin workgroup spends ~80 more shader cycles per block than one running two
@@ -661,13 +661,17 @@ int win_pass_timing(tv_ctx* c) {
     return TV_OK;
 }
 
-// The stream window w's hash runs on: one of the layout's hash streams, or the compute stream when it has one.
+// The stream window w's hash runs on: the compute stream, then the layout's extra hash streams in turn.  (HIP maps
+// streams onto GPU_MAX_HW_QUEUES hardware queues, 4 by default; a hash queued behind another stream's wait on the
+// same hardware queue waits with it, so the hashes use the compute stream and hash streams created next to it, and
+// nothing else waits on the compute stream during a pass: fills of windows go on the staging lane.)
 hipStream_t win_hash_stream(const tv_ctx* c, uint64_t seq) {
-    return c->win_nhs > 1 ? c->win_hs[seq % (uint64_t)c->win_nhs] : c->stream;
+    const uint64_t k = seq % (uint64_t)std::max(1, c->win_nhs);
+    return k == 0 ? c->stream : c->win_hs[k - 1];
 }
 
-// Hash the open window (no-op when none is open): on its hash stream, after every copy queued into its buffer (on
-// either staging lane) and every fill queued on the compute stream.
+// Hash the open window (no-op when none is open): on its hash stream, after every copy and fill queued into its
+// buffer on either staging lane.
 int win_seal(tv_ctx* c) {
     if (c->win_cur == UINT64_MAX) return TV_OK;
     const uint64_t j0 = c->win_cur * c->win_n, n = std::min(c->win_n, c->count - j0);
@@ -676,14 +680,10 @@ int win_seal(tv_ctx* c) {
         TV_HIP(c, hipEventRecord(c->win_cp[l], lane_stream(c, l)));
         TV_HIP(c, hipStreamWaitEvent(hs, c->win_cp[l], 0));
     }
-    if (hs != c->stream) {
-        TV_HIP(c, hipEventRecord(c->win_fill_ev, c->stream));
-        TV_HIP(c, hipStreamWaitEvent(hs, c->win_fill_ev, 0));
-    }
     if (c->win_launched == 0) TV_HIP(c, hipEventRecord(c->ev_k0, hs));
     const TvPieces p = window_launch(c, j0, n, win_base(c, c->win_buf));
     const int kernel = choose_kernel_n(c, n, p.n_main < p.n);
-    const int rc = launch_resident(c, p, kernel, /*hash=*/true, hs);
+    const int rc = launch_resident(c, p, kernel, /*hash=*/true, hs, /*alone=*/c->win_nhs <= 1);
     if (rc) return rc;
     TV_HIP(c, hipEventRecord(c->win_ev[c->win_buf], hs));
     c->last_kernel = kernel;
@@ -696,8 +696,7 @@ int win_seal(tv_ctx* c) {
 // Everything queued on the hash streams, joined into the compute stream (the compare, digest reads and zeroing
 // after a pass follow every window's hash).
 int win_join(tv_ctx* c) {
-    if (c->win_nhs <= 1) return TV_OK;
-    for (int k = 0; k < c->win_nhs; k++) {
+    for (int k = 0; k + 1 < c->win_nhs; k++) {
         TV_HIP(c, hipEventRecord(c->win_hs_ev[k], c->win_hs[k]));
         TV_HIP(c, hipStreamWaitEvent(c->stream, c->win_hs_ev[k], 0));
     }
@@ -706,7 +705,7 @@ int win_join(tv_ctx* c) {
 
 // Wait for every hash stream (before the payload is freed or re-planned, and at tv_destroy).
 int win_sync_streams(tv_ctx* c) {
-    for (int k = 0; k < kWinHashStreams; k++)
+    for (int k = 0; k < kWinHashStreams - 1; k++)
         if (c->win_hs[k]) TV_HIP(c, hipStreamSynchronize(c->win_hs[k]));
     return TV_OK;
 }
@@ -734,11 +733,9 @@ int win_enter(tv_ctx* c, uint64_t w) {
     if (rc) return rc;
     c->win_valid = w * c->win_n;
     c->win_buf = (c->win_buf + 1) % c->win_bufs;
-    // the buffer is free once the kernel that last read it is done (copies on either lane wait for it, and so do
-    // fills on the compute stream when the hashes run on hash streams of their own)
+    // the buffer is free once the kernel that last read it is done (copies and fills on either lane wait for it)
     TV_HIP(c, hipStreamWaitEvent(c->copy_stream, c->win_ev[c->win_buf], 0));
     TV_HIP(c, hipStreamWaitEvent(c->copy_stream2, c->win_ev[c->win_buf], 0));
-    if (c->win_nhs > 1) TV_HIP(c, hipStreamWaitEvent(c->stream, c->win_ev[c->win_buf], 0));
     c->win_cur = w;
     return TV_OK;
 }

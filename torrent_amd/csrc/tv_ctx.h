@@ -139,6 +139,15 @@ struct StreamState {
     std::vector<uint8_t> av;   // shard-relative availability bits, applied to the bitfield at the end
 };
 
+// A cold-read bounce buffer (TV_OPT_FILE_BOUNCE): kBounceBytes of page-locked memory and the event of the DMA that
+// last read it.
+constexpr uint64_t kBounceBytes = 4ull << 20;
+struct Bounce {
+    uint8_t* ptr = nullptr;
+    hipEvent_t ev = nullptr;
+    bool recorded = false;
+};
+
 }  // namespace tvi
 
 using tvi::kRingSlots;
@@ -170,6 +179,8 @@ struct tv_ctx {
     bool file_direct = false;            // TV_OPT_FILE_DIRECT: long segments DMA'd from registered page-cache pages
     bool file_concurrent = true;         // tv_stage_files: long segments on two staging lanes
     int file_odirect = 1;                // TV_OPT_FILE_ODIRECT: cold chunks read with O_DIRECT (2: its reads fail, tests)
+    int file_bounce = 4;                 // TV_OPT_FILE_BOUNCE: cold O_DIRECT reads into small reused page-locked buffers
+                                         // DMA'd from there (readers per lane), 0 = into the ring's 64 MiB slots
     uint64_t file_direct_min = 32ull << 20;  // tv_stage_files: segments >= this take the tv_stage_file path
     int file_threads = 16;                   // tv_stage_files: reader threads
     bool resident = true;                    // TV_OPT_RESIDENT
@@ -232,6 +243,11 @@ struct tv_ctx {
     bool ring2_lent[kRingSlots] = {false, false, false};
     int ring2_next = 0;
     Pool pool[2];                     // host workers of lane 0 / lane 1
+    // cold-read bounce buffers of lane 0 / lane 1 (TV_OPT_FILE_BOUNCE), handed to the lane's readers from a free list
+    std::vector<tvi::Bounce> bounce[2];
+    std::vector<int> bounce_free[2];
+    std::mutex bounce_mu[2];
+    std::condition_variable bounce_cv[2];
     // the GPU's NUMA node (-1: unknown) and its CPUs the process may use; with numa_bind the library's
     // threads run there and the pinned ring is allocated there (TV_OPT_NUMA_BIND)
     int numa_node = -1;
@@ -274,14 +290,15 @@ struct tv_ctx {
     uint64_t win_passes = 0;           // passes finalized since tv_set_layout
     hipEvent_t win_ev[tvi::kWinBufsMax] = {};   // the last kernel reading buffer k
     hipEvent_t win_cp[2] = {nullptr, nullptr};  // copies into the window queued on lane k (kernel waits on them)
-    // Hash streams: with more than one, window w hashes on win_hs[w mod win_nhs] (companions off), so windows hash
-    // side by side while the next ones stage; with one, on the compute stream (the round-1..5 form).
+    // Hash streams: window w hashes on the compute stream when w mod win_nhs == 0, else on win_hs[w mod win_nhs - 1]
+    // (companions off there), so up to win_nhs windows hash side by side while the next ones stage; win_nhs = 1: every
+    // window on the compute stream (the rounds 4-5 form).  win_hs[0] is created by tv_create right after the compute
+    // stream (its own hardware queue where HIP has one free), the others when a layout needs them.
     int win_bufs_opt = 0;              // TV_OPT_WIN_BUFS (0: tv_plan.h kWinBufsDefault)
     int win_streams_opt = 0;           // TV_OPT_WIN_STREAMS (0: win_bufs - 1, at most kWinHashStreams)
-    int win_nhs = 1;                   // hash streams of the current windowed layout
-    hipStream_t win_hs[tvi::kWinHashStreams] = {};
-    hipEvent_t win_hs_ev[tvi::kWinHashStreams] = {};  // joins a hash stream into the compute stream
-    hipEvent_t win_fill_ev = nullptr;  // compute-stream work (window fills) a window's hash waits for
+    int win_nhs = 1;                   // hash streams of the current windowed layout, the compute stream included
+    hipStream_t win_hs[tvi::kWinHashStreams - 1] = {};
+    hipEvent_t win_hs_ev[tvi::kWinHashStreams - 1] = {};  // joins a hash stream into the compute stream
 
     // Slot pool (TV_OPT_LIST_SLOTS = K): the payload holds K piece slots instead of the shard; a staged piece
     // takes a slot until tv_verify_list lists it (incremental verify).
@@ -446,7 +463,8 @@ int launch_avail(tv_ctx* c, const uint8_t* avail_bits, const uint64_t** out);
 int choose_kernel_n(const tv_ctx* c, uint64_t n, bool short_last);
 int choose_kernel(const tv_ctx* c);
 uint32_t lane_pairs_for(const tv_ctx* c, uint64_t n);
-int launch_resident(tv_ctx* c, const TvPieces& p_in, int kernel, bool hash, hipStream_t on = nullptr);
+int launch_resident(tv_ctx* c, const TvPieces& p_in, int kernel, bool hash, hipStream_t on = nullptr,
+                    bool alone = true);
 int win_sync_streams(tv_ctx* c);
 TvPieces resident_launch(const tv_ctx* c);
 TvPieces window_launch(const tv_ctx* c, uint64_t j0, uint64_t n, const uint8_t* data);

@@ -187,6 +187,94 @@ int unit_open(tv_ctx* c, FileWindows& win, const FileUnit& u) {
     return TV_OK;
 }
 
+// A lane's cold-read bounce buffers: `want` of them, allocated once per context (page-locked, on the GPU's NUMA node
+// when bound) and kept; each starts free.
+int ensure_bounce(tv_ctx* c, int lane, int want) {
+    std::lock_guard<std::mutex> g(c->bounce_mu[lane]);
+    auto& v = c->bounce[lane];
+    while ((int)v.size() < want) {
+        Bounce b;
+        TV_HIP(c, host_malloc_on_node((void**)&b.ptr, kBounceBytes, c->numa_bind ? c->numa_node : -1));
+        const hipError_t e = hipEventCreateWithFlags(&b.ev, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            (void)hipHostFree(b.ptr);
+            return fail(c, TV_ERR_HIP, "hipEventCreateWithFlags: %s", hipGetErrorString(e));
+        }
+        v.push_back(b);
+        c->bounce_free[lane].push_back((int)v.size() - 1);
+    }
+    return TV_OK;
+}
+
+// Cold file bytes [fo, fo + n) (O_DIRECT descriptor dfd) -> LINEAR [p, p + n) through the lane's bounce buffers
+// (TV_OPT_FILE_BOUNCE = `readers`): the readers take 4 MiB parts, 4 KiB-aligned in the file, each into a free buffer
+// (after the DMA that last read it), and queue the part's copies from it on the lane's stream -- the reads land in
+// 2 x readers x 4 MiB of reused memory instead of across the 192 MiB ring (tools/read_ceiling.c RC_BOUNCE=dma1).
+// (fo ^ p) & 3 == 0, so a part's bytes sit at the destination's alignment mod 4.  Returns a TV_ status; *read_err:
+// the errno of a failed O_DIRECT read (0: none; the caller then reads the chunk again buffered).
+int read_cold_bounce(tv_ctx* c, int lane, int readers, int dfd, uint64_t fo, uint64_t n, uint64_t p, int* read_err) {
+    *read_err = 0;
+    const uint64_t al0 = fo / 4096 * 4096, end = fo + n;
+    const uint64_t nparts = (end - al0 + kBounceBytes - 1) / kBounceBytes;
+    int rc = ensure_bounce(c, lane, 2 * readers);
+    if (rc) return rc;
+    hipStream_t cs = lane_stream(c, lane);
+    std::atomic<int> err{0}, hrc{TV_OK};
+    c->pool[lane].run(readers, nparts, [&](uint64_t q) {
+        if (err.load(std::memory_order_relaxed) || hrc.load(std::memory_order_relaxed)) return;
+        int k;
+        {
+            std::unique_lock<std::mutex> lk(c->bounce_mu[lane]);
+            c->bounce_cv[lane].wait(lk, [&] { return !c->bounce_free[lane].empty(); });
+            k = c->bounce_free[lane].back();
+            c->bounce_free[lane].pop_back();
+        }
+        struct Give {   // the buffer goes back to the free list on every exit
+            tv_ctx* c;
+            int lane, k;
+            ~Give() {
+                {
+                    std::lock_guard<std::mutex> g(c->bounce_mu[lane]);
+                    c->bounce_free[lane].push_back(k);
+                }
+                c->bounce_cv[lane].notify_one();
+            }
+        } give{c, lane, k};
+        Bounce& b = c->bounce[lane][k];
+        if (b.recorded && hipEventSynchronize(b.ev) != hipSuccess) {
+            hrc = fail(c, TV_ERR_HIP, "hipEventSynchronize of a bounce buffer failed");
+            return;
+        }
+        const uint64_t s0 = al0 + q * kBounceBytes;                     // the file byte at b.ptr[0]
+        const uint64_t a = std::max(s0, fo), e = std::min(s0 + kBounceBytes, end);
+        const uint64_t want = e - s0, ask = (want + 4095) / 4096 * 4096;   // (the file's end may come back short)
+        uint64_t o = 0;
+        while (o < want) {
+            const ssize_t got = c->file_odirect == 2 ? (errno = EINVAL, -1)   // (fault injection, as the ring path)
+                                                     : pread(dfd, b.ptr + o, ask - o, (off_t)(s0 + o));
+            if (got < 0 && errno == EINTR) continue;
+            if (got <= 0) {
+                int none = 0;
+                err.compare_exchange_strong(none, got < 0 ? errno : EIO);
+                return;
+            }
+            o += (uint64_t)got;
+        }
+        int r = stage_range(c, p + (a - fo), p + (e - fo), b.ptr + (a - s0), p + (a - fo), true, lane,
+                            /*src_in_ring=*/true);
+        if (!r && hipEventRecord(b.ev, cs) != hipSuccess) r = fail(c, TV_ERR_HIP, "hipEventRecord of a bounce buffer");
+        if (r) {
+            hrc = r;
+            return;
+        }
+        b.recorded = true;
+        c->file_ns[TV_FILE_BYTES_ODIRECT].fetch_add(e - a, std::memory_order_relaxed);
+        c->file_ns[TV_FILE_BYTES_READ].fetch_add(e - a, std::memory_order_relaxed);
+    });
+    *read_err = err.load();
+    return hrc.load();
+}
+
 // Stage the units (each lane's in ascending linear order) on staging lane `lane` with `threads` reader threads.
 // Per chunk of the unit: with TV_OPT_FILE_DIRECT a window of TV_OPT_FILE_CHUNK bytes whose pages are mostly in the
 // page cache is mapped, registered read-only and DMA'd to HBM from the page cache; otherwise (and for cold windows)
@@ -273,6 +361,24 @@ int stage_units(tv_ctx* c, const std::vector<FileUnit>& units, int lane, int thr
                 // linear offset's alignment, is used).
                 win.release(k);
                 int dfd = (unit_cold && ((fo ^ p) & 3) == 0) ? win.direct_fd(c->open_rw) : -1;
+                if (dfd >= 0 && c->file_bounce > 0) {
+                    int e = 0;
+                    {
+                        FileClock t(c, TV_FILE_PHASE_READ);
+                        rc = read_cold_bounce(c, lane, std::min(threads, c->file_bounce), dfd, fo, n, p, &e);
+                    }
+                    if (rc) return rc;
+                    if (!e) {
+                        if (c->file_direct) TV_HIP(c, hipEventRecord(drain.ev[k], cs));
+                        continue;
+                    }
+                    // an O_DIRECT read refused: as in the ring path below, this file reads buffered from here on
+                    c->file_ns[TV_FILE_ODIRECT_FALLBACKS].fetch_add(1, std::memory_order_relaxed);
+                    uint64_t none = 0;
+                    c->file_ns[TV_FILE_ODIRECT_ERRNO].compare_exchange_strong(none, (uint64_t)e);
+                    win.no_direct();
+                    dfd = -1;
+                }
                 const uint64_t step = dfd >= 0 ? (uint64_t)kRingSlotBytes - 8192 : (uint64_t)kRingSlotBytes - 4;
                 for (uint64_t q = 0; q < n; q += step) {
                     const uint64_t kq = std::min<uint64_t>(step, n - q);

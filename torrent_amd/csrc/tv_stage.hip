@@ -259,16 +259,17 @@ int tv_fill_synthetic(tv_ctx* c, uint64_t seed) {
     if (c->slots) return fail(c, TV_ERR_STATE, "tv_fill_synthetic: a slot pool (TV_OPT_LIST_SLOTS) holds no shard");
     TV_HIP(c, hipSetDevice(c->device));
     if (c->win) {
-        // every window from the open one (or the next unhashed one; a new pass: the first) is filled in its buffer
-        // and hashed when the next opens, all on the compute stream
+        // every window from the open one (or the next unhashed one; a new pass: the first) is filled in its buffer on
+        // staging lane 0 (after the hash that last read the buffer, as a copy would be) and hashed when the next opens
         uint64_t w = c->win_done ? 0 : (c->win_cur != UINT64_MAX ? c->win_cur : (c->win_valid + c->win_n - 1) / c->win_n);
         for (const uint64_t nwin = (c->count + c->win_n - 1) / c->win_n; w < nwin; w++) {
             rc = win_enter(c, w);
             if (rc) return rc;
             const uint64_t j0 = w * c->win_n;
             TV_HIP(c, tv_launch_fill(win_base(c, c->win_buf), c->stride, c->first + j0,
-                                     (uint32_t)std::min(c->win_n, c->count - j0), c->L, seed, c->stream));
+                                     (uint32_t)std::min(c->win_n, c->count - j0), c->L, seed, c->copy_stream));
         }
+        TV_HIP(c, hipStreamSynchronize(c->copy_stream));
         TV_HIP(c, hipStreamSynchronize(c->stream));
         return TV_OK;
     }
