@@ -53,7 +53,7 @@ int main() {
     CHECK(run(16384, MiB + 256, 2 * GiB, 288 * GiB, &p, &tries, &b, 2) == 0 && p.win && p.bufs == 2);
     CHECK(p.bytes <= 2 * GiB && p.win_n == 1024 - 64);
     // a budget of three one-piece windows asks for four buffers: three (one piece each)
-    CHECK(run(100, MiB + 256, 3 * (MiB + 512), 288 * GiB, &p, &tries, &b) == 0 && p.bufs == 3 && p.win_n == 1);
+    CHECK(run(100, MiB + 256, 3 * (MiB + 512), 288 * GiB, &p, &tries, &b, 4) == 0 && p.bufs == 3 && p.win_n == 1);
     // more buffers than windows are never allocated
     CHECK(run(3, MiB + 256, 3 * MiB, 288 * GiB, &p, &tries, &b, 8) == 0 && p.win && p.win_n * p.bufs <= 3 + 2);
     for (int B = 1; B <= tvi::kWinBufsMax + 2; B++) {

@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round 6 final check of the build: the whole -m gpu suite, smoke(), the default bench line, the TS host's Storage
-# paths and verifyFiles phases on cfg3, the PMC traffic passes of cfg2 and suppl on THIS build (their build id), the
-# default bench under rocprofv3 --kernel-trace --stats, and the driver's torchrun command at N = 2 and 8 rehearsed
-# on the one GPU.  Each GPU step has its own limit; the chain stops at the first failure.
+# Round 6 final check of the build: the whole -m gpu suite, smoke(), the default bench line, the PMC traffic passes
+# of cfg2 and suppl on THIS build (their build id), the default bench under rocprofv3 --kernel-trace --stats, and the
+# driver's torchrun command at N = 2 and 8 rehearsed on the one GPU (the host-path measurements: gpu_r06_paths.sh).
+# Each GPU step has its own limit; the chain stops at the first failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
@@ -11,15 +11,10 @@ mkdir -p $out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $out/pytest_gpu.log 2>&1 && echo TESTS_OK &&
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 && echo SMOKE_OK &&
 timeout -k 10 300 python3 bench.py > $out/bench_n1.json 2> $out/bench_n1.err && echo BENCH_OK &&
-mkdir -p /tmp/tsb && UV_THREADPOOL_SIZE=16 timeout -k 10 300 python3 -u tools/ts_storage_bench.py /tmp/tsb single16 cfg3 \
-    > $out/ts_storage_bench.jsonl 2> $out/ts_storage_bench.err && echo TS_BENCH_OK && rm -rf /tmp/tsb &&
-mkdir -p /tmp/tsp && UV_THREADPOOL_SIZE=16 timeout -k 10 300 python3 -u tools/ts_files_phases.py /tmp/tsp cfg3 8 \
-    > $out/ts_files_phases_cfg3.jsonl 2> $out/ts_files_phases.err && echo TS_PHASES_OK && rm -rf /tmp/tsp &&
 CHECK_OUT=${CHECK_OUT:-r06_final}/pmc bash tools/gpu_r05_pmc.sh > $out/pmc.log 2>&1 && echo PMC_OK &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/prof -o run -- python3 bench.py --steps 10 --warmup 3 \
     > $out/bench_prof.json 2> $out/bench_prof.err && echo PROF_OK &&
 bash tools/rehearse_ranks.sh $out/rehearse ${REHEARSE_N:-2 8} && echo REHEARSE_OK
 rc=$?
-rm -rf /tmp/tsb /tmp/tsp
 tail -3 $out/pytest_gpu.log; head -c 400 $out/bench_n1.json; echo; tail -3 $out/pmc.log
 exit $rc

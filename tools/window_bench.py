@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--budgets", default="0,8,2,0.5")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--variants", default="0:0")
+    ap.add_argument("--files", default=None,
+                    help="also verify_files on a warm single16 layout (one 16 GiB file, 1 MiB pieces) written to this dir")
     a = ap.parse_args()
     L = int(a.piece_mib * MiB)
     total = int(a.gib * GiB) // L * L
@@ -85,6 +87,19 @@ def main():
         ctx.set_option(N.TV_OPT_WIN_STREAMS, 0)
     leg("verify_stream rows", lambda: verify_stream(info, lambda off, n: buf.mv[off:off + n]), None)
     buf.close()
+    if a.files:   # file-backed resume under the same budgets (single16, warm page cache)
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from storage_paths_bench import write_layout
+        from torrent_amd import verify_files
+        root = os.path.join(a.files, "single16")
+        finfo, fexpect, paths = write_layout("single16", root)
+        expect[:] = fexpect
+        verify_files(finfo, root)          # warm the page cache and the context
+        for b in [float(x) for x in a.budgets.split(",")]:
+            budget = int(b * GiB) if b else None
+            leg("verify_files warm", lambda: verify_files(finfo, root, budget=budget), b, "default")
+        for p in paths:
+            os.unlink(p)
 
 
 if __name__ == "__main__":

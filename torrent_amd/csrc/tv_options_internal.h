@@ -33,10 +33,11 @@
                                  part's DMA from it (a compact destination; cold verify_files 22-25 against 19-20
                                  GB/s, profiles/r06/cold_libbounce.jsonl); 0 = parallel preads into the lane's 64 MiB
                                  ring slot, one DMA per slot (rounds 4-5) */
-#define TV_OPT_WIN_BUFS 23    /* windowed layouts: window buffers, 0 (default) = tv_plan.h kWinBufsDefault (4), else 1..8
+#define TV_OPT_WIN_BUFS 23    /* windowed layouts: window buffers, 0 (default) = tv_plan.h kWinBufsDefault (3), else 1..8
                                  (set before tv_set_layout) */
-#define TV_OPT_WIN_STREAMS 24 /* windowed layouts: hash streams, 0 (default) = buffers - 1 (at most 4), else 1..4; 1 =
-                                 every window hashed on the compute stream, one after the other (rounds 1-5) */
+#define TV_OPT_WIN_STREAMS 24 /* windowed layouts: hash streams, the compute stream included, 0 (default) = buffers - 1
+                                 (at most 4), else 1..4; 1 = every window hashed on the compute stream, one after the
+                                 other (rounds 4-5) */
 #define TV_COUNTER_WINDOW_BUFS 122    /* window buffers of the current windowed layout (0: not windowed) */
 #define TV_COUNTER_WINDOW_STREAMS 123 /* its hash streams (1: the compute stream) */
 #define TV_COUNTER_KFD_GPU_ID 121    /* the GPU's KFD gpu_id when the co-tenant check can run (reading it probes for this

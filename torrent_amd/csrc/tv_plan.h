@@ -16,10 +16,12 @@ struct PayloadPlan {
     uint64_t buf_bytes = 0;
 };
 
-// Window buffers of a windowed layout by default (TV_OPT_WIN_BUFS = 0): window w + 1 stages while up to three
-// windows before it hash, each on a hash stream of its own (a window's hash takes one piece's serial SHA-1 whatever
-// its piece count, so under a small budget the windows must hash side by side to keep staging busy).
-constexpr int kWinBufsDefault = 4;
+// Window buffers of a windowed layout by default (TV_OPT_WIN_BUFS = 0): window w + 1 stages while the two windows
+// before it hash side by side, on the compute stream and one hash stream (a window's hash takes one piece's serial
+// SHA-1 whatever its piece count, so under a small budget windows must hash side by side to keep staging busy).
+// Three beat two and four at HIP's default 4 hardware queues: 0.5 GiB 28.3 / 22.2 / 26.5 GB/s, 1 GiB 51.6 / 38.5 /
+// 45.2 (profiles/r06/window_bench_shipped_form.jsonl).
+constexpr int kWinBufsDefault = 3;
 constexpr int kWinBufsMax = 8;
 
 // `count` pieces at `stride` bytes (+ `slack` after the last) under `budget` bytes: the whole shard when it fits,
