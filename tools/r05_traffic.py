@@ -7,7 +7,7 @@ half the bytes actually read (doubled here); TCC_EA0_RDREQ_{32B,64B,128B} count 
 32 x + 64 y + 128 z).  Each counter group ran in its own pass.  The verify dispatches are the bench's resident
 verify launches (the kernel named per workload), the first one (warm-up) dropped.
 
-usage: python tools/r05_traffic.py <gpurun_out dir> <profiles/r05 dir> [workload ...]
+usage: python tools/r05_traffic.py <gpurun_out pmc dir> <profiles/rNN dir> [workload ...]
 """
 import csv
 import glob
@@ -55,7 +55,7 @@ def main():
                          "(tools/gpu_r05_pmc.sh): 2 x FETCH_SIZE x 1024 bytes per verify dispatch (gfx950 reports half "
                          "the bytes of a 16-B/lane streaming read: MI355X_MICROARCH.md HBM section), mean over the "
                          "verify dispatches after the first; TCC_EA0_RDREQ_{32B,64B,128B} by size in a second pass",
-               "source": f"{os.path.relpath(src, ROOT)}/pmc_{w}/p1, p2 -> profiles/r05/"}
+               "source": f"{os.path.relpath(src, ROOT)}/pmc_{w}/p1, p2 -> {os.path.relpath(out, ROOT)}/"}
         json.dump(rec, open(os.path.join(ROOT, "profiles", f"traffic_{w}.json"), "w"), indent=1)
         json.dump(rec, open(os.path.join(out, f"traffic_{w}.json"), "w"), indent=1)
         print(json.dumps({k: v for k, v in rec.items() if not k.startswith("per_")}))
