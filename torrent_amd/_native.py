@@ -55,7 +55,7 @@ TV_OPT_WIN_STREAMS = 24
 TV_COUNTER_WINDOW_BUFS = 122
 TV_COUNTER_WINDOW_STREAMS = 123
 WIN_BUFS_DEFAULT = 3    # tv_plan.h kWinBufsDefault: window buffers of a windowed layout
-FILE_BOUNCE_DEFAULT = 4  # tv_ctx.h file_bounce: cold-read bounce readers per staging lane
+FILE_BOUNCE_DEFAULT = 2  # tv_ctx.h file_bounce: cold-read bounce readers per staging lane
 TV_COUNTER_KFD_GPU_ID = 121
 TV_FILE_PHASES = ("open", "map", "populate", "register", "read", "wait", "queue", "release", "drain", "small", "call",
                   "bytes_direct", "bytes_read", "bytes_odirect", "odirect_fallbacks", "odirect_errno")   # TV_FILE_PHASE_* / TV_FILE_BYTES_* in order

@@ -179,7 +179,7 @@ struct tv_ctx {
     bool file_direct = false;            // TV_OPT_FILE_DIRECT: long segments DMA'd from registered page-cache pages
     bool file_concurrent = true;         // tv_stage_files: long segments on two staging lanes
     int file_odirect = 1;                // TV_OPT_FILE_ODIRECT: cold chunks read with O_DIRECT (2: its reads fail, tests)
-    int file_bounce = 4;                 // TV_OPT_FILE_BOUNCE: cold O_DIRECT reads into small reused page-locked buffers
+    int file_bounce = 2;                 // TV_OPT_FILE_BOUNCE: cold O_DIRECT reads into small reused page-locked buffers
                                          // DMA'd from there (readers per lane), 0 = into the ring's 64 MiB slots
     uint64_t file_direct_min = 32ull << 20;  // tv_stage_files: segments >= this take the tv_stage_file path
     int file_threads = 16;                   // tv_stage_files: reader threads
@@ -430,11 +430,14 @@ struct DrainGuard {
     tv_ctx* c;
     int lane;
     bool compute;
+    bool lane_sync = true;   // false: a staging pass that hands its lane straight to the next window's pass (the copies
+                             // read ring slots and bounce buffers, whose events order their reuse; the call's last
+                             // pass drains)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     explicit DrainGuard(tv_ctx* ctx, int copy_lane = 0, bool sync_compute = true)
         : c(ctx), lane(copy_lane), compute(sync_compute) {}
     ~DrainGuard() {
-        (void)hipStreamSynchronize(lane_stream(c, lane));
+        if (lane_sync) (void)hipStreamSynchronize(lane_stream(c, lane));
         if (compute) (void)hipStreamSynchronize(c->stream);
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);

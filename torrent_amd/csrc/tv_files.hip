@@ -282,7 +282,8 @@ int read_cold_bounce(tv_ctx* c, int lane, int readers, int dfd, uint64_t fo, uin
 // leases order the reads behind the DMAs that last read the slot, so consecutive units stream with no drain between
 // them.  A unit whose file cannot be read sets status[k] = TV_ERR_IO (the caller recovers the segment); a HIP or
 // state error ends the lane with that status.
-int stage_units(tv_ctx* c, const std::vector<FileUnit>& units, int lane, int threads, int32_t* status) {
+int stage_units(tv_ctx* c, const std::vector<FileUnit>& units, int lane, int threads, int32_t* status,
+                bool final_pass = true) {
     if (units.empty()) return TV_OK;
     hipStream_t cs = lane_stream(c, lane);
     FileWindows win(c);  // before `drain`: unmapped after the stream is drained
@@ -434,6 +435,10 @@ int stage_units(tv_ctx* c, const std::vector<FileUnit>& units, int lane, int thr
             if (c->file_direct) TV_HIP(c, hipEventRecord(drain.ev[k], cs));
         }
     }
+    if (!final_pass && !c->file_direct) {   // (mapped page-cache windows, the direct path, must drain before unmapping)
+        drain.lane_sync = false;
+        return TV_OK;
+    }
     FileClock t(c, TV_FILE_PHASE_DRAIN);
     TV_HIP(c, hipStreamSynchronize(cs));
     return TV_OK;
@@ -504,7 +509,7 @@ void read_segments(Pool& pool, const std::vector<SmallSeg>& segs, size_t lo, siz
 // offsets' alignment mod 4, read by the lane's pool (open, pread, close each: read_segments), one DMA per run of
 // readable linear-contiguous segments while the next slot is read.  A failed read sets status[k] = TV_ERR_IO.
 int stage_small(tv_ctx* c, std::vector<SmallSeg>& small, int lane, int threads, const char* const* paths,
-                int32_t* status, std::string* first_err, std::mutex* err_mu) {
+                int32_t* status, std::string* first_err, std::mutex* err_mu, bool final_pass = true) {
     int rc = TV_OK;
     DrainGuard drain(c, lane, /*sync_compute=*/false);
     size_t i = 0;
@@ -544,6 +549,10 @@ int stage_small(tv_ctx* c, std::vector<SmallSeg>& small, int lane, int threads, 
         rc = slot.release();
         if (rc) return rc;
         i = j;
+    }
+    if (!final_pass) {
+        drain.lane_sync = false;
+        return TV_OK;
     }
     FileClock t(c, TV_FILE_PHASE_DRAIN);
     TV_HIP(c, hipStreamSynchronize(lane_stream(c, lane)));
@@ -658,7 +667,8 @@ namespace {
 // (clip_to_shard: the shard, or a windowed layout's open window).  status_out[k] is set to TV_ERR_IO on a
 // failure and left alone otherwise.  check_zero: check the zero-length segments' opens (once per call).
 int stage_files_core(tv_ctx* c, uint64_t n, const char* const* paths, const uint64_t* file_offsets,
-                     const uint64_t* linear_offsets, const uint64_t* lens, int32_t* status_out, bool check_zero) {
+                     const uint64_t* linear_offsets, const uint64_t* lens, int32_t* status_out, bool check_zero,
+                     bool final_pass = true) {
     int rc = TV_OK;
     // Long segments (>= TV_OPT_FILE_DIRECT_MIN bytes) are cut into units of TV_OPT_FILE_CHUNK bytes dealt to two
     // staging lanes (TV_OPT_FILE_CONCURRENT): this thread on lane 0 and a helper thread on lane 1, each walking its
@@ -744,16 +754,17 @@ int stage_files_core(tv_ctx* c, uint64_t n, const char* const* paths, const uint
                 helper_rc = fail(c, TV_ERR_HIP, "tv_stage_files: hipSetDevice(%d) failed", c->device);
                 return;
             }
-            helper_rc = stage_units(c, lane_units[1], 1, threads_per_lane, status_out);
+            helper_rc = stage_units(c, lane_units[1], 1, threads_per_lane, status_out, final_pass);
             if (!helper_rc && !lane_small[1].empty())
-                helper_rc = stage_small(c, lane_small[1], 1, threads_per_lane, paths, status_out, &first_err, &err_mu);
+                helper_rc = stage_small(c, lane_small[1], 1, threads_per_lane, paths, status_out, &first_err, &err_mu,
+                                        final_pass);
         });
     }
-    rc = stage_units(c, lane_units[0], 0, lanes == 2 ? threads_per_lane : c->file_threads, status_out);
+    rc = stage_units(c, lane_units[0], 0, lanes == 2 ? threads_per_lane : c->file_threads, status_out, final_pass);
     if (rc) return rc;
     if (!lane_small[0].empty()) {
         rc = stage_small(c, lane_small[0], 0, lanes == 2 ? threads_per_lane : c->file_threads, paths, status_out,
-                         &first_err, &err_mu);
+                         &first_err, &err_mu, final_pass);
         if (rc) return rc;
     }
     if (helper.joinable()) helper.join();
@@ -879,11 +890,20 @@ int stage_files_locked(tv_ctx* c, uint64_t n, const char* const* paths, const ui
         std::fill(touched.begin() + (ptrdiff_t)w0, touched.begin() + (ptrdiff_t)w1 + 1, (uint8_t)1);
     }
     bool check_zero = true;  // (the zero-length segments' opens are checked in the first pass)
+    uint64_t last_touched = 0;
+    for (uint64_t w = 0; w < nwin; w++)
+        if (touched[w]) last_touched = w;
     for (uint64_t w = 0; w < nwin; w++) {
         if (!touched[w]) continue;
         rc = win_enter(c, w);
-        if (!rc) rc = stage_files_core(c, n, paths, file_offsets, linear_offsets, lens, status_out, check_zero);
-        if (rc) return rc;
+        // (the lanes flow from one window's pass into the next; only the last pass drains them)
+        if (!rc) rc = stage_files_core(c, n, paths, file_offsets, linear_offsets, lens, status_out, check_zero,
+                                       w == last_touched);
+        if (rc) {
+            (void)hipStreamSynchronize(c->copy_stream);
+            (void)hipStreamSynchronize(c->copy_stream2);
+            return rc;
+        }
         check_zero = false;
     }
     return check_zero ? stage_files_core(c, n, paths, file_offsets, linear_offsets, lens, status_out, true) : TV_OK;

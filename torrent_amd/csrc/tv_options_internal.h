@@ -28,11 +28,12 @@
    3 = companions whatever other processes hold on the GPU (the co-tenant check of 1 skipped) */
 #define TV_COUNTER_COTENANT_VRAM 120 /* bytes of this GPU's memory other processes hold (KFD: /sys/class/kfd/kfd/proc/
                                         <pid>/vram_<gpu_id>; 0 when unreadable): >= 1 GiB turns auto companions off */
-#define TV_OPT_FILE_BOUNCE 25 /* cold long-segment chunks (O_DIRECT): R > 0 (default 4) = R readers per lane, each
+#define TV_OPT_FILE_BOUNCE 25 /* cold long-segment chunks (O_DIRECT): R > 0 (default 2) = R readers per lane, each
                                  reading 4 MiB parts into one of 2 R reused 4 MiB page-locked buffers and queueing the
-                                 part's DMA from it (a compact destination; cold verify_files 22-25 against 19-20
-                                 GB/s, profiles/r06/cold_libbounce.jsonl); 0 = parallel preads into the lane's 64 MiB
-                                 ring slot, one DMA per slot (rounds 4-5) */
+                                 part's DMA from it (a compact destination: four reads in flight on two lanes, cold
+                                 verify_files 20.7-24.8 against the ring's 15.9-19.8 GB/s in three interleaved sweeps,
+                                 profiles/r06/cold_*.jsonl); 0 = parallel preads into the lane's 64 MiB ring slot, one
+                                 DMA per slot (rounds 4-5) */
 #define TV_OPT_WIN_BUFS 23    /* windowed layouts: window buffers, 0 (default) = tv_plan.h kWinBufsDefault (3), else 1..8
                                  (set before tv_set_layout) */
 #define TV_OPT_WIN_STREAMS 24 /* windowed layouts: hash streams, the compute stream included, 0 (default) = buffers - 1
