@@ -293,3 +293,66 @@ def test_random_layouts_wrong_length_reads(native, seed):
     for devices in ([0], [0, 0, 0]):
         assert _bits(verify_pieces(info, Longer(), devices=devices), P) == want, (seed, devices)
         assert _bits(verify_stream(info, Longer().get, devices=devices), P) == want, (seed, devices)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", SEEDS)
+def test_random_layouts_file_table(native, tmp_path, monkeypatch, seed):
+    """tv_stage_file_table (the TS host's verifyFiles: the torrent's file table handed over, the library making
+    Storage.get's walk) on the 48 seeded layouts: one shard, three shards and a windowed layout
+    (windows of ~3 pieces), long segments forced on some shards -- bits equal fsStorage.get + hashlib's, the per-file
+    status names exactly the missing / short files that hold shard bytes, and nothing is created."""
+    import shutil
+    from torrent_amd import Storage
+    from torrent_amd.piece import piece_length
+    from torrent_amd.storage import fs_storage
+    from torrent_amd.verify import shard_ranges
+    info, payload, sizes, missing, short, single = _draw(seed)
+    P, L, total = info.n_pieces, info.piece_length, info.length
+    monkeypatch.chdir(tmp_path)
+    disk = _disk(info, payload, sizes, missing, short, single)
+    for root in ("dl", "ref"):
+        for k, data in disk.items():
+            p = tmp_path.joinpath(root, *k)
+            p.parent.mkdir(parents=True, exist_ok=True)
+            p.write_bytes(data)
+    want = _expected(info, Storage(fs_storage, info, str(tmp_path / "ref")))
+    shutil.rmtree(tmp_path / "ref", ignore_errors=True)
+    paths = Storage(fs_storage, info, str(tmp_path / "dl")).file_paths()
+    lengths = [total] if info.files is None else [f.length for f in info.files]
+    before = sorted(str(x) for x in (tmp_path / "dl").rglob("*"))
+    stride = -(-L // 64) * 64 + 256
+    for n, budget, direct_min in ((1, 0, 32 << 20), (3, 0, 1), (1, native.WIN_BUFS_DEFAULT * (3 * stride + 256), 1)):
+        got = []
+        for first, count in shard_ranges(P, n):
+            if not count:
+                continue
+            with native.Context(0) as ctx:
+                ctx.set_option(native.TV_OPT_RESIDENT_BUDGET, budget)
+                ctx.set_option(native.TV_OPT_FILE_DIRECT_MIN, direct_min)
+                ctx.set_option(native.TV_OPT_FILE_THREADS, 3)
+                ctx.set_layout(total, L, P, first, count)
+                ctx.set_digests(info.pieces_raw)
+                status = ctx.stage_file_table(lengths, paths)
+                assert len(status) == len(paths)
+                # pieces whose bytes run past the data (more digests than data): unreadable, as the hosts mark them
+                avail = bytearray(b"\xff" * ((count + 7) // 8))
+                for j in range(count):
+                    i = first + j
+                    if i * L + piece_length(i, info) > total:
+                        avail[j >> 3] &= ~(0x80 >> (j & 7)) & 0xFF
+                bits = ctx.verify(bytes(avail))
+                got += _bits(bits, count)
+                # the per-file status: a failure only for files absent or short that hold bytes of this shard
+                lo, hi = first * L, min(total, (first + count - 1) * L + piece_length(first + count - 1, info))
+                o = 0
+                for k, s in enumerate(sizes):
+                    holds = s > 0 and o < hi and o + s > lo
+                    bad = k in missing or (k in short and short[k] < min(s, hi - o))
+                    if holds:
+                        assert status[k] == (native.TV_ERR_IO if bad else 0), (seed, n, k)
+                    elif s > 0 and (o + s < lo or o >= hi):   # (a file ending at lo has a zero-length segment)
+                        assert status[k] == 0, (seed, n, k)
+                    o += s
+        assert got == want, (seed, n, budget)
+    assert sorted(str(x) for x in (tmp_path / "dl").rglob("*")) == before      # nothing created
