@@ -232,6 +232,21 @@ int tv_verify_list(tv_ctx *ctx, const uint64_t *pieces, uint64_t n, uint8_t *ok_
 int tv_verify_host(tv_ctx *ctx, const uint8_t *src, uint64_t src_len, const uint8_t *avail_bits,
                    uint8_t *bitfield_out);
 
+/*
+ * The resume check from the torrent's FILES through the bounded ring (SURVEY 8f row f2 under a small device
+ * budget): the stream engine of tv_stream_*, with the library's own readers filling each request's rows straight
+ * from the files (the file table as for tv_stage_file_table: n files of lengths[k] bytes, paths NUL-separated in
+ * `paths`).  Each row's linear bytes are walked over the files as Storage.get walks them (storage.ts:98-137) and
+ * read as fsStorage.get reads them; a piece is 0 exactly when fsStorage.get would return null for it (a byte in a
+ * missing, unopenable or short file, a zero-length segment whose open fails, bytes past the files' end) or its
+ * SHA-1 differs.  Device memory: two columns of TV_OPT_STREAM_CHUNK bytes of every shard piece (set it from the
+ * device budget; the layout is set with TV_OPT_RESIDENT = 0), host memory: the 192 MiB ring; every piece's SHA-1
+ * advances with each column, so a shard far larger than the budget verifies at the staging rate.  status_out[k]
+ * (n entries) = TV_ERR_IO when a read or open of file k failed.  Nothing is created.
+ */
+int tv_stream_file_table(tv_ctx *ctx, uint64_t n, const uint64_t *lengths, const char *paths, uint64_t paths_bytes,
+                         const uint8_t *avail_bits, uint8_t *bitfield_out, int32_t *status_out);
+
 /* Creation mode (make_torrent.ts:28-31, :147-173): 20-byte SHA-1 of every resident piece of the
  * shard, written to digests_out (20*shard_count bytes), in piece order. */
 int tv_hash(tv_ctx *ctx, uint8_t *digests_out);

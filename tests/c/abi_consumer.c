@@ -74,6 +74,8 @@ static int run_cpu(void) {
         const uint64_t lens[1] = {7};
         int32_t st[1];
         CHECK(tv_stage_file_table(NULL, 1, lens, "a", 2, st) == TV_ERR_ARG, "NULL ctx file table");
+        uint8_t bf[1];
+        CHECK(tv_stream_file_table(NULL, 1, lens, "a", 2, NULL, bf, st) == TV_ERR_ARG, "NULL ctx streamed file table");
     }
     if (n == 0) {  /* no GPU: creating a context is an error with a message, never a crash */
         tv_ctx *c = NULL;

@@ -356,3 +356,31 @@ def test_random_layouts_file_table(native, tmp_path, monkeypatch, seed):
                     o += s
         assert got == want, (seed, n, budget)
     assert sorted(str(x) for x in (tmp_path / "dl").rglob("*")) == before      # nothing created
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", SEEDS)
+def test_random_layouts_streamed_files(native, tmp_path, monkeypatch, seed):
+    """verify_files through the bounded ring from the files (tv_stream_file_table: the library's readers fill each
+    column's rows, walking the file table per row) on the 48 seeded layouts: one and three shards, the library's
+    column width and columns sized to a budget of a few pieces (64-byte columns at the smallest) -- bits equal
+    fsStorage.get + hashlib's, nothing created."""
+    import shutil
+    from torrent_amd import Storage, verify_files
+    from torrent_amd.storage import fs_storage
+    info, payload, sizes, missing, short, single = _draw(seed)
+    P, L = info.n_pieces, info.piece_length
+    monkeypatch.chdir(tmp_path)
+    disk = _disk(info, payload, sizes, missing, short, single)
+    for root in ("dl", "ref"):
+        for k, data in disk.items():
+            p = tmp_path.joinpath(root, *k)
+            p.parent.mkdir(parents=True, exist_ok=True)
+            p.write_bytes(data)
+    want = _expected(info, Storage(fs_storage, info, str(tmp_path / "ref")))
+    shutil.rmtree(tmp_path / "ref", ignore_errors=True)
+    before = sorted(str(x) for x in (tmp_path / "dl").rglob("*"))
+    for devices, budget in (([0], None), ([0, 0, 0], None), ([0], 2 * (3 * L + 4096)), ([0, 0], 1)):
+        bf = verify_files(info, str(tmp_path / "dl"), devices=devices, threads=3, budget=budget, stream=True)
+        assert _bits(bf, P) == want, (seed, devices, budget)
+    assert sorted(str(x) for x in (tmp_path / "dl").rglob("*")) == before

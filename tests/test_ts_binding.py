@@ -211,6 +211,11 @@ def test_ts_binding_on_the_gpu(native, tmp_path, monkeypatch):
         cases.append({"name": name, "kind": "files", "info": _info_json(L, len(payload), digests, files, "t"),
                       "dir": str(tmp_path / "dl"), "devices": devices})
         expect[name] = bits.hex()
+        # the streamed form (tv_stream_file_table): columns sized to a budget of a few pieces
+        name = f"files_streamed_{len(devices)}"
+        cases.append({"name": name, "kind": "files", "info": _info_json(L, len(payload), digests, files, "t"),
+                      "dir": str(tmp_path / "dl"), "devices": devices, "stream": True, "budget": 3 * (L + 512)})
+        expect[name] = bits.hex()
 
     # verifyPiece and hashPieces
     L = 262144

@@ -6,7 +6,7 @@
 // spec.cases[k].kind:
 //   "pieces"   verifyPieces(info, storage)       storage = the linear payload, minus unreadable pieces
 //   "stream"   verifyStream(info, storage)       (rows of `wrongLength` pieces come back one byte long)
-//   "files"    verifyFiles(info, dir)
+//   "files"    verifyFiles(info, dir) (stream / budget: the streamed-columns form under a device budget)
 //   "piece"    verifyPiece(info, index, bytes)
 //   "hash"     hashPieces(payload, pieceLength)
 //   "verifier" PieceVerifier: onBlock per block, automatic flushes (onVerified), optionally `settleMs` of
@@ -59,7 +59,8 @@ async function main() {
         const o = { ...opts, devices: c.devices };
         r.bitfield = hex(c.kind === "pieces" ? await v.verifyPieces(info, st, o) : await v.verifyStream(info, st, { ...o, chunk: c.chunk || 0 }));
       } else if (c.kind === "files") {
-        r.bitfield = hex(await v.verifyFiles(makeInfo(c.info), c.dir, { ...opts, devices: c.devices }));
+        r.bitfield = hex(await v.verifyFiles(makeInfo(c.info), c.dir,
+                                             { ...opts, devices: c.devices, stream: c.stream, budget: c.budget }));
       } else if (c.kind === "piece") {
         r.ok = await v.verifyPiece(makeInfo(c.info), c.index, b64(c.bytes), opts);
       } else if (c.kind === "hash") {

@@ -97,7 +97,9 @@ def main():
         verify_files(finfo, root)          # warm the page cache and the context
         for b in [float(x) for x in a.budgets.split(",")]:
             budget = int(b * GiB) if b else None
-            leg("verify_files warm", lambda: verify_files(finfo, root, budget=budget), b, "default")
+            leg("verify_files warm", lambda: verify_files(finfo, root, budget=budget, stream=False), b, "windows")
+            leg("verify_files warm streamed", lambda: verify_files(finfo, root, budget=budget, stream=True), b,
+                "columns")
         for p in paths:
             os.unlink(p)
 

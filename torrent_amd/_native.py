@@ -115,6 +115,7 @@ SYMBOLS = [
     ("tv_stage_file", _int, [_p, ctypes.c_char_p, _u64, _u64, _u64]),
     ("tv_stage_files", _int, [_p, _u64, _p, _p, _p, _p, _p]),
     ("tv_stage_file_table", _int, [_p, _u64, _p, _p, _u64, _p]),
+    ("tv_stream_file_table", _int, [_p, _u64, _p, _p, _u64, _p, _p, _p]),
     ("tv_read", _int, [_p, _u64, _p, _u64]),
     ("tv_fill_synthetic", _int, [_p, _u64]),
     ("tv_verify", _int, [_p, _p, _p]),
@@ -387,6 +388,28 @@ class Context:
         st = np.zeros(n, dtype=np.int32)
         self._check(self._L.tv_stage_file_table(self._h, n, ln.ctypes.data, blob, len(blob), st.ctypes.data))
         return st.tolist()
+
+    def stream_file_table(self, lengths, paths, avail: Optional[bytes] = None) -> tuple:
+        """tv_stream_file_table: the resume check from the files through the bounded ring (the library's readers
+        fill each column's rows from the file table).  -> (bitfield, per-file statuses)."""
+        import numpy as np
+
+        n = len(paths)
+        if len(lengths) != n:
+            raise ValueError("stream_file_table: lengths and paths differ in length")
+        if n and all(type(x) is str for x in paths):
+            blob = ("\0".join(paths) + "\0").encode(sys.getfilesystemencoding(), "surrogateescape")
+        else:
+            blob = b"\0".join(os.fsencode(x) for x in paths) + b"\0" if n else b"\0"
+        if n and blob.count(b"\0") != n:
+            raise ValueError("stream_file_table: a path contains a NUL byte")
+        ln = np.ascontiguousarray(lengths if n else [0], dtype=np.uint64)
+        st = np.zeros(max(1, n), dtype=np.int32)
+        out = ctypes.create_string_buffer(max(1, self._nbits()))
+        a, keep = _addr(avail)
+        self._check(self._L.tv_stream_file_table(self._h, n, ln.ctypes.data, blob, len(blob), a, out, st.ctypes.data))
+        del keep
+        return out.raw[: self._nbits()], st[:n].tolist()
 
     def stage_files(self, paths, file_offsets, linear_offsets, lens) -> list:
         """tv_stage_files: stage many file segments in one call.  Returns one status per segment:

@@ -1,5 +1,10 @@
 // tv_stream.hip -- the streamed verify engine (tv_stream_*; tv_verify_host runs on it): a bounded pinned ring
 // between the caller's bytes and two device chunk buffers, one kernel launch per column / window of pieces.
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cerrno>
 #include <cstring>
 
 #include "tv_ctx.h"
@@ -277,6 +282,163 @@ int tv_verify_host(tv_ctx* c, const uint8_t* src, uint64_t src_len, const uint8_
         rc = stream_commit_locked(c, &req, k ? src + base : nullptr, c->L, pinned, k);
         if (rc) break;
     }
+    if (rc) {
+        stream_abort_locked(c);
+        return rc;
+    }
+    return stream_end_locked(c, bitfield_out);
+}
+
+// The resume check from FILES through the bounded ring (tv_stream_file_table): the stream engine with the library's
+// own readers as the producer.  Each request's rows (bytes [offset, offset + width) of consecutive pieces: a column
+// across the shard) are read by the lane-0 pool straight from the files into the request's ring slot, each row's
+// linear range walked over the file table as Storage.get walks it (storage.ts:98-137); the kernels hash one column
+// while the next is read.  Device memory: two columns (TV_OPT_STREAM_CHUNK bytes of every shard piece), so a shard
+// verifies under a small device budget with every piece's SHA-1 advancing at once, where windows of whole pieces
+// pay one piece's serial SHA-1 per window.  A piece is unreadable exactly when fsStorage.get would return null
+// for it: a byte of it in a missing, unopenable or too-short file, a zero-length segment of its walk whose open
+// fails (storage.ts:109-110,158), or bytes past the files' end.  Files are opened as fsStorage.get opens them
+// (TV_OPT_OPEN_RW), kept open for the call, never created.
+int tv_stream_file_table(tv_ctx* c, uint64_t n, const uint64_t* lengths, const char* paths, uint64_t paths_bytes,
+                         const uint8_t* avail_bits, uint8_t* bitfield_out, int32_t* status_out) {
+    if (!c) return fail(nullptr, TV_ERR_ARG, "ctx is NULL");
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = require_layout(c, true);
+    if (rc) return rc;
+    if (!bitfield_out && c->count) return fail(c, TV_ERR_ARG, "bitfield_out is NULL");
+    if (n && (!lengths || !paths || !status_out)) return fail(c, TV_ERR_ARG, "NULL argument");
+    std::vector<const char*> path(n);
+    std::vector<uint64_t> start(n + 1, 0);   // file k's linear bytes: [start[k], start[k + 1])
+    for (uint64_t k = 0, o = 0; k < n; k++) {
+        const void* z = o < paths_bytes ? memchr(paths + o, 0, paths_bytes - o) : nullptr;
+        if (!z)
+            return fail(c, TV_ERR_ARG, "paths holds %llu NUL-terminated paths in %llu bytes, the table %llu files",
+                        (unsigned long long)k, (unsigned long long)paths_bytes, (unsigned long long)n);
+        path[k] = paths + o;
+        o = (uint64_t)((const char*)z - paths) + 1;
+        if (lengths[k] > UINT64_MAX - start[k])
+            return fail(c, TV_ERR_ARG, "file %llu: the lengths overflow 64-bit offsets", (unsigned long long)k);
+        start[k + 1] = start[k] + lengths[k];
+        status_out[k] = TV_OK;
+    }
+    if (!c->count) return TV_OK;
+    TV_HIP(c, hipSetDevice(c->device));
+    // availability before any read: the caller's bits, pieces past the files' end, and the pieces whose walk has a
+    // zero-length segment whose open fails (the same segments tv_stage_file_table checks)
+    const uint64_t last = c->first + c->count - 1;
+    const uint64_t lo = c->first * c->L, hi = std::min(c->total, last * c->L + piece_len(c, last));
+    std::vector<uint8_t> av((c->count + 7) / 8, 0);
+    for (uint64_t j = 0; j < c->count; j++) {
+        const uint64_t i = c->first + j, end = i * c->L + piece_len(c, i);
+        if (end <= std::min(c->total, start[n]) && (!avail_bits || get_bit(avail_bits, j))) set_bit(av.data(), j);
+    }
+    {
+        std::vector<TableSeg> segs;
+        uint64_t bad = 0, reached = 0;
+        if (!walk_file_table(n, lengths, lo, hi, c->L, &segs, &bad, &reached))
+            return fail(c, TV_ERR_ARG, "file %llu: the lengths overflow 64-bit offsets", (unsigned long long)bad);
+        for (const TableSeg& sg : segs) {
+            if (sg.len || sg.linear < lo || sg.linear >= hi) continue;
+            if (fs_openable(path[sg.file], c->open_rw)) {
+                status_out[sg.file] = TV_ERR_IO;
+                const uint64_t j = sg.linear / c->L - c->first;
+                av[j >> 3] &= (uint8_t)~(0x80u >> (j & 7));
+            }
+        }
+    }
+    // the call's open files: the first kCachedFds opened stay open until the end (a one- or few-file torrent opens
+    // each once); past that a reader opens and closes the file around its read (as fsStorage.get does per call), so
+    // a 10,000-file torrent never runs into the descriptor limit.  -2: the open failed.
+    constexpr int kCachedFds = 256;
+    std::vector<int> fds(n, -1);
+    int cached = 0;
+    std::mutex fd_mu;
+    struct Closer {
+        std::vector<int>& f;
+        ~Closer() {
+            for (int d : f)
+                if (d >= 0) close(d);
+        }
+    } closer{fds};
+    // -> a descriptor of file k, and whether the caller closes it after its read
+    auto fd_of = [&](uint64_t k, bool* own) -> int {
+        *own = false;
+        {
+            std::lock_guard<std::mutex> fg(fd_mu);
+            if (fds[k] != -1) return fds[k];
+        }
+        int e = 0;
+        const int d = path[k][0] ? open_file(path[k], c->open_rw, &e) : -1;
+        std::lock_guard<std::mutex> fg(fd_mu);
+        if (fds[k] != -1) {   // another reader opened it meanwhile
+            if (d >= 0) close(d);
+            return fds[k];
+        }
+        if (d < 0) {
+            if (e != EMFILE && e != ENFILE) fds[k] = -2;   // (out of descriptors: not the file's failure, but unread)
+            return -1;
+        }
+        if (cached < kCachedFds) {
+            cached++;
+            fds[k] = d;
+            return d;
+        }
+        *own = true;
+        return d;
+    };
+    DrainGuard drain(c);  // (the ring's copies and the column kernels are done when the call returns)
+    rc = stream_begin_locked(c, av.data());
+    if (rc) {
+        stream_abort_locked(c);
+        return rc;
+    }
+    std::vector<std::atomic<int32_t>> file_err(n);
+    for (auto& e : file_err) e.store(TV_OK);
+    for (;;) {
+        tv_stream_req req;
+        rc = stream_next_locked(c, &req);
+        if (rc || !req.rows) break;
+        uint8_t* slot = c->ring[c->st.slot];
+        std::vector<uint8_t> row_bad(req.rows, 0);
+        c->pool[0].run(c->file_threads, req.rows, [&](uint64_t q) {
+            const uint64_t i = req.piece + q, j = i - c->first;
+            const uint64_t nb = row_bytes(c, i, req.offset, req.width);
+            if (!nb || !get_bit(c->st.av.data(), j)) return;
+            const uint64_t a = i * c->L + req.offset, b = a + nb;   // the row's linear bytes
+            uint8_t* out = slot + q * req.width;
+            // the file holding byte a: the last k with start[k] <= a < start[k + 1] (zero-length files skipped)
+            uint64_t k = (uint64_t)(std::upper_bound(start.begin(), start.end(), a) - start.begin()) - 1;
+            for (uint64_t pos = a; pos < b && k < n; k++) {
+                if (start[k + 1] <= pos) continue;
+                const uint64_t e = std::min(b, start[k + 1]);
+                bool own = false;
+                const int fd = fd_of(k, &own);
+                uint64_t o = 0;
+                while (fd >= 0 && o < e - pos) {
+                    const ssize_t got = pread(fd, out + (pos - a) + o, e - pos - o, (off_t)(pos - start[k] + o));
+                    if (got < 0 && errno == EINTR) continue;
+                    if (got <= 0) break;
+                    o += (uint64_t)got;
+                }
+                if (own) close(fd);
+                if (o < e - pos) {   // missing, unopenable or short: the piece is null, as fsStorage.get's read
+                    row_bad[q] = 1;
+                    file_err[k].store(TV_ERR_IO);
+                    return;
+                }
+                pos = e;
+            }
+        });
+        for (uint64_t q = 0; q < req.rows; q++) {
+            if (!row_bad[q]) continue;
+            const uint64_t j = req.piece + q - c->first;
+            c->st.av[j >> 3] &= (uint8_t)~(0x80u >> (j & 7));
+        }
+        rc = stream_commit_locked(c, &req, nullptr, 0, true, req.rows);
+        if (rc) break;
+    }
+    for (uint64_t k = 0; k < n; k++)
+        if (file_err[k].load() != TV_OK) status_out[k] = TV_ERR_IO;
     if (rc) {
         stream_abort_locked(c);
         return rc;

@@ -464,8 +464,42 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
     return avail
 
 
+def _stream_column(L: int, count: int, budget: Optional[int]) -> int:
+    """Column width of a streamed shard under a device budget: the two chunk buffers of (C + 256) bytes per shard piece
+    fit it (tv_stream_file_table); 0 (the library's default, ~512 MiB columns) without a budget."""
+    if not budget:
+        return 0
+    C = (budget // 2 - 256) // max(1, count) - 256
+    return max(64, min(C // 64 * 64, -(-L // 64) * 64))
+
+
+def _stream_files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: int,
+                        budget: Optional[int]) -> bytes:
+    """A shard's resume check from its files through the bounded ring (tv_stream_file_table): no resident payload,
+    two device columns sized to the budget, the library's readers filling each column from the file table."""
+    L, P = info.piece_length, info.n_pieces
+    ctx.set_option(_native.TV_OPT_RESIDENT, 0)
+    try:
+        ctx.set_option(_native.TV_OPT_RESIDENT_BUDGET, 0)
+        ctx.set_option(_native.TV_OPT_STREAM_CHUNK, _stream_column(L, count, budget))
+        ctx.set_option(_native.TV_OPT_STREAM_ROWS, 0)
+        ctx.set_layout(info.length, L, P, first, count)
+        ctx.set_digests(info.pieces_raw)
+    finally:
+        ctx.set_option(_native.TV_OPT_RESIDENT, 1)
+    if count == 0:
+        return b""
+    ctx.set_option(_native.TV_OPT_FILE_THREADS, max(1, threads))
+    ctx.set_option(_native.TV_OPT_OPEN_RW, 1)
+    lengths = [info.length] if info.files is None else [f.length for f in info.files]
+    paths = [p if "\0" not in p else "" for p in storage.file_paths()]
+    bits, _ = ctx.stream_file_table(lengths, paths)
+    return bits
+
+
 def verify_files(info: InfoDict, dir_path: str, devices=None, threads: Optional[int] = None,
-                 direct_min: Optional[int] = None, budget: Optional[int] = None) -> bytearray:
+                 direct_min: Optional[int] = None, budget: Optional[int] = None,
+                 stream: Optional[bool] = None) -> bytearray:
     """Resume check from disk: the have-bitfield of the files under dir_path,
     laid out as Storage(fs_storage, info, dir_path) maps them (storage.ts:89-137; single-file
     torrents are [dir, name], multi-file [dir, *path] without info.name).
@@ -480,6 +514,8 @@ def verify_files(info: InfoDict, dir_path: str, devices=None, threads: Optional[
     storage = Storage(fs_storage, info, dir_path)
 
     def shard(ctx, first: int, count: int) -> bytes:
+        if stream:
+            return _stream_files_shard(ctx, info, storage, first, count, threads or ctx.thread_budget, budget)
         _layout(ctx, info, L, P, first, count, budget)
         ctx.set_digests(info.pieces_raw)
         if count == 0:

@@ -39,6 +39,11 @@ const SYMBOLS = {
     result: "i32",
     nonblocking: true,
   },
+  tv_stream_file_table: {
+    parameters: ["pointer", "u64", "pointer", "pointer", "u64", "pointer", "pointer", "pointer"],
+    result: "i32",
+    nonblocking: true,
+  },
   tv_read: { parameters: ["pointer", "u64", "pointer", "u64"], result: "i32", nonblocking: true },
   tv_fill_synthetic: { parameters: ["pointer", "u64"], result: "i32" },
   tv_verify: { parameters: ["pointer", "pointer", "pointer"], result: "i32", nonblocking: true },
@@ -82,6 +87,10 @@ export interface VerifyOptions {
   /** verifyPiece only: hash on the CPU with the reference's own crypto.subtle.digest("SHA-1", bytes)
    * (tools/make_torrent.ts:28-31) instead of a ~3 ms GPU launch.  Off by default */
   cpuFallback?: boolean;
+  /** verifyFiles: read the shard's files through the bounded ring in columns sized to `budget`
+   * (tv_stream_file_table) instead of holding windows of whole pieces in device memory -- the faster form under a
+   * small budget, where each window pays one piece's serial SHA-1 */
+  stream?: boolean;
   /** host threads the library may use for one call, over all of its shards (default: the process's CPU share as
    * the library reads it, tv_cpu_share: the cgroup quota, else OMP_NUM_THREADS, else the affinity mask): each
    * shard's context gets its part (TV_OPT_FILE_THREADS), so devices [0..7] do not start 8 x 16 reader threads */
@@ -466,6 +475,14 @@ function fileTable(info: InfoDict, dir: string): FileTable {
   return t;
 }
 
+/** Column width of a streamed shard under a device budget (torrent_amd/verify.py _stream_column): the two device
+ * columns of (C + 256) bytes per shard piece fit it; 0 (the library's ~512 MiB columns) without a budget. */
+export function streamColumn(L: number, count: number, budget?: number): number {
+  if (!budget) return 0;
+  const C = Math.floor((Math.floor(budget / 2) - 256) / Math.max(1, count)) - 256;
+  return Math.max(64, Math.min(Math.floor(C / 64) * 64, Math.ceil(L / 64) * 64));
+}
+
 export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptions = {}): Promise<Uint8Array> {
   const l = load(opts.libPath);
   const P = info.pieces.length;
@@ -481,6 +498,32 @@ export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptio
   await Promise.all(ranges.map(async ([first, count], s) => {
     if (count === 0) return;
     await withContext(l, devices[s], s, async (ctx) => {
+      if (opts.stream) {   // columns through the bounded ring, read by the library from the file table
+        check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_RESIDENT, 0n));
+        check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_RESIDENT_BUDGET, 0n));
+        check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_STREAM_CHUNK, BigInt(streamColumn(L, count, opts.budget))));
+        check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_STREAM_ROWS, 0n));
+        try {
+          check(l, ctx, l.symbols.tv_set_layout(ctx, BigInt(info.length), BigInt(L), BigInt(P), BigInt(first),
+                                                BigInt(count)));
+        } finally {
+          l.symbols.tv_set_option(ctx, TV_OPT_RESIDENT, 1n);
+        }
+        check(l, ctx, l.symbols.tv_set_digests(ctx, ptr(raw), BigInt(raw.length)));
+        check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_OPEN_RW, 1n));
+        check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_FILE_THREADS, BigInt(threads)));
+        const status = new Int32Array(table.n);
+        const out = new Uint8Array(Math.ceil(count / 8));
+        try {
+          check(l, ctx, await l.symbols.tv_stream_file_table(ctx, BigInt(table.n), ptr(u8(table.lengths)),
+                                                             ptr(table.paths), BigInt(table.paths.length), null,
+                                                             ptr(out), ptr(u8(status))));
+        } finally {
+          l.symbols.tv_set_option(ctx, TV_OPT_STREAM_CHUNK, 0n);
+        }
+        bitfield.set(out, first / 8);
+        return;
+      }
       setLayout(l, ctx, info.length, L, P, first, count, opts.budget);
       check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_OPEN_RW, 1n)); // fsStorage.get's read + write open
       check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_FILE_THREADS, BigInt(threads))); // this shard's readers
