@@ -4,7 +4,7 @@
 // libtorrent_verify.so.
 //
 //   open(path) -> handle (BigInt)          sym(handle, name) -> function address (BigInt)
-//   call(fn, args: BigInt[] (<= 7, each the 64-bit register image of an integer / pointer argument),
+//   call(fn, args: BigInt[] (<= 8, each the 64-bit register image of an integer / pointer argument),
 //        result: 0 void | 1 i32) -> number | undefined
 //   callAsync(fn, args, result) -> Promise of the same, the call run on a libuv worker thread
 //   addressOf(typedArray) -> BigInt        arrayBuffer(address: BigInt, length) -> ArrayBuffer over it
@@ -64,7 +64,7 @@ napi_value Sym(napi_env env, napi_callback_info info) {
     return make_u64(env, (uint64_t)(uintptr_t)f);
 }
 
-typedef int64_t (*Fn7)(uint64_t, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t);
+typedef int64_t (*Fn8)(uint64_t, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t);
 
 napi_value Call(napi_env env, napi_callback_info info) {
     size_t argc = 3;
@@ -73,9 +73,9 @@ napi_value Call(napi_env env, napi_callback_info info) {
     uint64_t fn = 0;
     if (argc < 3 || !get_u64(env, argv[0], &fn)) return throw_error(env, "call(fn, args, result)");
     uint32_t nargs = 0;
-    if (napi_get_array_length(env, argv[1], &nargs) != napi_ok || nargs > 7)
-        return throw_error(env, "call: args must be an array of at most 7 BigInts");
-    uint64_t a[7] = {0, 0, 0, 0, 0, 0, 0};
+    if (napi_get_array_length(env, argv[1], &nargs) != napi_ok || nargs > 8)
+        return throw_error(env, "call: args must be an array of at most 8 BigInts");
+    uint64_t a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (uint32_t i = 0; i < nargs; i++) {
         napi_value e;
         napi_get_element(env, argv[1], i, &e);
@@ -83,7 +83,7 @@ napi_value Call(napi_env env, napi_callback_info info) {
     }
     int32_t kind = 0;
     napi_get_value_int32(env, argv[2], &kind);
-    const int64_t r = ((Fn7)(uintptr_t)fn)(a[0], a[1], a[2], a[3], a[4], a[5], a[6]);
+    const int64_t r = ((Fn8)(uintptr_t)fn)(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7]);
     if (kind == 0) {
         napi_value u;
         napi_get_undefined(env, &u);
@@ -99,7 +99,7 @@ napi_value Call(napi_env env, napi_callback_info info) {
 // really overlap, as they do under Deno.
 struct AsyncCall {
     uint64_t fn;
-    uint64_t a[7];
+    uint64_t a[8];
     int32_t kind;
     int64_t r;
     napi_deferred deferred;
@@ -108,7 +108,7 @@ struct AsyncCall {
 
 void AsyncExecute(napi_env, void* data) {
     AsyncCall* c = (AsyncCall*)data;
-    c->r = ((Fn7)(uintptr_t)c->fn)(c->a[0], c->a[1], c->a[2], c->a[3], c->a[4], c->a[5], c->a[6]);
+    c->r = ((Fn8)(uintptr_t)c->fn)(c->a[0], c->a[1], c->a[2], c->a[3], c->a[4], c->a[5], c->a[6], c->a[7]);
 }
 
 void AsyncComplete(napi_env env, napi_status, void* data) {
@@ -128,9 +128,9 @@ napi_value CallAsync(napi_env env, napi_callback_info info) {
     AsyncCall* c = new AsyncCall();
     uint32_t nargs = 0;
     if (argc < 3 || !get_u64(env, argv[0], &c->fn) || napi_get_array_length(env, argv[1], &nargs) != napi_ok ||
-        nargs > 7) {
+        nargs > 8) {
         delete c;
-        return throw_error(env, "callAsync(fn, args: at most 7 BigInts, result)");
+        return throw_error(env, "callAsync(fn, args: at most 8 BigInts, result)");
     }
     for (uint32_t i = 0; i < nargs; i++) {
         napi_value e;
