@@ -134,7 +134,8 @@ def test_random_layouts_cold_long_path(native, tmp_path, monkeypatch, seed):
         with _context(0) as ctx:
             ctx.set_option(native.TV_OPT_FILE_BOUNCE, bounce)
         try:
-            bf = verify_files(info, str(tmp_path / "dl"), devices=devices, threads=4, direct_min=1, budget=budget)
+            bf = verify_files(info, str(tmp_path / "dl"), devices=devices, threads=4, direct_min=1, budget=budget,
+                              stream=False)
         finally:
             with _context(0) as ctx:
                 ctx.set_option(native.TV_OPT_FILE_BOUNCE, native.FILE_BOUNCE_DEFAULT)

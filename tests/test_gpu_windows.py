@@ -98,9 +98,12 @@ def test_golden_layouts_windowed(native, layout, tmp_path, monkeypatch):
         p.write_bytes(data)
     for devices in ([0], [0, 0, 0]):
         budget = _budget(L, rng.choice([2, 5, 16] if info.n_pieces < 1000 else [16, 64]))
-        assert bytes(verify_files(info, str(tmp_path / "dl"), devices=devices, threads=4,
-                                  budget=budget)).hex() == rec["expected_bitfield"], (devices, budget)
+        assert bytes(verify_files(info, str(tmp_path / "dl"), devices=devices, threads=4, budget=budget,
+                                  stream=False)).hex() == rec["expected_bitfield"], (devices, budget)
         _check_windowed(budget, expect_windowed=devices == [0] and info.n_pieces * _stride(L) + 256 > budget)
+        # the same budget as the default chooses it (columns through the ring where windows would lose: _stream_wins)
+        assert bytes(verify_files(info, str(tmp_path / "dl"), devices=devices, threads=4,
+                                  budget=budget)).hex() == rec["expected_bitfield"], (devices, budget, "auto")
     clean = hashlib.sha1(lay["pieces_raw"]).hexdigest()
     assert clean == rec["pieces_sha1"]
     if not lay["corrupted"]:
@@ -142,7 +145,7 @@ def test_random_layouts_windowed(native, tmp_path, monkeypatch, seed):
         assert _bits(verify_pieces(info, st, devices=devices, budget=budget), P) == want, ("pieces", devices, budget)
         assert _bits(verify_payload(info, payload[:info.length], devices=devices, avail=bytes(avail),
                                     budget=budget), P) == want, ("payload", devices, budget)
-        assert _bits(verify_files(info, str(tmp_path / "dl"), devices=devices, threads=3, budget=budget),
+        assert _bits(verify_files(info, str(tmp_path / "dl"), devices=devices, threads=3, budget=budget, stream=False),
                      P) == want_fs, ("files", devices, budget)
         _check_windowed(budget, expect_windowed=False)
 

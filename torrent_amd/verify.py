@@ -473,6 +473,18 @@ def _stream_column(L: int, count: int, budget: Optional[int]) -> int:
     return max(64, min(C // 64 * 64, -(-L // 64) * 64))
 
 
+def _stream_wins(L: int, count: int, budget: Optional[int]) -> bool:
+    """Whether a file-backed shard verifies faster in streamed columns than in windows of whole pieces under this
+    device budget: only when the shard does not fit it, and each window (two of three buffers hashing at once) would
+    cost more than staging -- a window pays one piece's serial SHA-1 (~11.8 ms per MiB of piece), so windows keep up
+    with ~50 GB/s of staging only from ~0.9 GB of budget per MiB of piece length (profiles/r06/window_bench_stream.jsonl:
+    0.5 GiB, 1 MiB pieces: columns 47.5 GB/s against windows 28.3; 1 GiB 50.6 / 50.4; 2 GiB 48.9 / 51.7)."""
+    if not budget:
+        return False
+    stride = -(-L // 64) * 64 + 256
+    return count * stride + 256 > budget and budget < 0.9e9 * L / (1 << 20)
+
+
 def _stream_files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: int,
                         budget: Optional[int]) -> bytes:
     """A shard's resume check from its files through the bounded ring (tv_stream_file_table): no resident payload,
@@ -507,14 +519,17 @@ def verify_files(info: InfoDict, dir_path: str, devices=None, threads: Optional[
     Same bits as verify_pieces(info, Storage(fs_storage, info, dir_path)), without fsStorage.get's
     side effect of creating missing files, and with every file segment of a shard staged by ONE
     tv_stage_files call (see _files_shard) instead of one open/seek/read per piece.  threads: the library's
-    reader threads per shard (default: the shard's part of the process's CPUs, _cpu.shard_threads)."""
+    reader threads per shard (default: the shard's part of the process's CPUs, _cpu.shard_threads).  budget: device
+    bytes the shard's payload may take (default: the GPU's free memory less a margin); a shard above it is held in
+    windows of whole pieces, or -- stream=True, or by default where windows would cost more than staging
+    (_stream_wins) -- read through the bounded ring in columns sized to the budget (tv_stream_file_table)."""
     from .storage import Storage, fs_storage
 
     P, L = info.n_pieces, info.piece_length
     storage = Storage(fs_storage, info, dir_path)
 
     def shard(ctx, first: int, count: int) -> bytes:
-        if stream:
+        if stream or (stream is None and _stream_wins(L, count, budget)):
             return _stream_files_shard(ctx, info, storage, first, count, threads or ctx.thread_budget, budget)
         _layout(ctx, info, L, P, first, count, budget)
         ctx.set_digests(info.pieces_raw)

@@ -89,7 +89,7 @@ export interface VerifyOptions {
   cpuFallback?: boolean;
   /** verifyFiles: read the shard's files through the bounded ring in columns sized to `budget`
    * (tv_stream_file_table) instead of holding windows of whole pieces in device memory -- the faster form under a
-   * small budget, where each window pays one piece's serial SHA-1 */
+   * small budget, where each window pays one piece's serial SHA-1 (default: chosen per shard, streamWins) */
   stream?: boolean;
   /** host threads the library may use for one call, over all of its shards (default: the process's CPU share as
    * the library reads it, tv_cpu_share: the cgroup quota, else OMP_NUM_THREADS, else the affinity mask): each
@@ -483,6 +483,15 @@ export function streamColumn(L: number, count: number, budget?: number): number 
   return Math.max(64, Math.min(Math.floor(C / 64) * 64, Math.ceil(L / 64) * 64));
 }
 
+/** Whether a file-backed shard verifies faster in streamed columns than in windows of whole pieces under the device
+ * budget (torrent_amd/verify.py _stream_wins): the shard does not fit it, and windows would cost more than staging
+ * (each pays one piece's serial SHA-1, ~11.8 ms per MiB of piece: below ~0.9 GB of budget per MiB of piece length). */
+export function streamWins(L: number, count: number, budget?: number): boolean {
+  if (!budget) return false;
+  const stride = Math.ceil(L / 64) * 64 + 256;
+  return count * stride + 256 > budget && budget < 0.9e9 * L / 1048576;
+}
+
 export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptions = {}): Promise<Uint8Array> {
   const l = load(opts.libPath);
   const P = info.pieces.length;
@@ -498,7 +507,8 @@ export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptio
   await Promise.all(ranges.map(async ([first, count], s) => {
     if (count === 0) return;
     await withContext(l, devices[s], s, async (ctx) => {
-      if (opts.stream) {   // columns through the bounded ring, read by the library from the file table
+      if (opts.stream || (opts.stream === undefined && streamWins(L, count, opts.budget))) {
+        // columns through the bounded ring, read by the library from the file table
         check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_RESIDENT, 0n));
         check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_RESIDENT_BUDGET, 0n));
         check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_STREAM_CHUNK, BigInt(streamColumn(L, count, opts.budget))));
