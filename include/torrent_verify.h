@@ -239,9 +239,11 @@ int tv_verify_host(tv_ctx *ctx, const uint8_t *src, uint64_t src_len, const uint
  * `paths`).  Each row's linear bytes are walked over the files as Storage.get walks them (storage.ts:98-137) and
  * read as fsStorage.get reads them; a piece is 0 exactly when fsStorage.get would return null for it (a byte in a
  * missing, unopenable or short file, a zero-length segment whose open fails, bytes past the files' end) or its
- * SHA-1 differs.  Device memory: two columns of TV_OPT_STREAM_CHUNK bytes of every shard piece (set it from the
- * device budget; the layout is set with TV_OPT_RESIDENT = 0), host memory: the 192 MiB ring; every piece's SHA-1
- * advances with each column, so a shard far larger than the budget verifies at the staging rate.  status_out[k]
+ * SHA-1 differs.  The layout is set with TV_OPT_RESIDENT = 0; device memory: two chunk buffers within
+ * TV_OPT_RESIDENT_BUDGET (default 1 GiB), each a column -- a byte range of every piece of a window of >= 2,048 pieces,
+ * as wide as the budget allows -- so each row is one long read and every window's SHA-1s advance with each column;
+ * a shard far larger than the budget verifies at the staging rate (an explicit TV_OPT_STREAM_CHUNK instead gives
+ * columns of that width across the whole shard).  Host memory: the 192 MiB ring.  status_out[k]
  * (n entries) = TV_ERR_IO when a read or open of file k failed.  Nothing is created.
  */
 int tv_stream_file_table(tv_ctx *ctx, uint64_t n, const uint64_t *lengths, const char *paths, uint64_t paths_bytes,

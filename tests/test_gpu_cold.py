@@ -179,3 +179,73 @@ def test_cold_file_end_stays_o_direct(native, oracle, tmp_path, bounce):
     assert _bits(bf, P) == [1] * (P - 1) + [0]
     assert clock["bytes_odirect"] == clock["bytes_read"] == total, clock
     assert clock["odirect_fallbacks"] == 0, clock
+
+
+@pytest.mark.parametrize("odirect", [1, 0, 2])
+def test_cold_files_streamed(native, oracle, tmp_path, odirect):
+    """verify_files through the bounded ring (tv_stream_file_table, stream=True) on files evicted from the page cache:
+    a file whose pages are mostly not cached at its open is read O_DIRECT, rows straight into the ring slot where the
+    file offset, the row and its length are 4 KiB-aligned (file 0) and through a reader's aligned scratch where not
+    (file 1 starts at 40 MiB + 4093), a short file ending mid-row -- every bitfield equal to Storage(fs_storage).get +
+    hashlib's; warm files are never read O_DIRECT, and a refused O_DIRECT read (fault injection) falls back to
+    buffered reads of that file, counted."""
+    import fsutil
+    from torrent_amd import FileInfo, Storage, make_info, verify_files
+    from torrent_amd.storage import fs_storage
+    from torrent_amd.verify import _context
+    MiB = 1 << 20
+    L = MiB
+    sizes = [40 * MiB + 4093, 37 * MiB + 2, 50 * MiB + 12345, 33 * MiB]
+    total = sum(sizes)
+    P = -(-total // L)
+    payload = bytearray(oracle.synth_fill(56, 0, total))
+    digests = bytearray(b"".join(hashlib.sha1(bytes(payload[i * L:min(total, (i + 1) * L)])).digest() for i in range(P)))
+    for i in (0, 41, P - 1):
+        digests[20 * i + 7] ^= 0x04
+    files, paths, o = [], [], 0
+    for k, n in enumerate(sizes):
+        p = tmp_path / f"f{k}.bin"
+        data = payload[o:o + n]
+        if k == 2:
+            data = data[:n - 5 * MiB - 777]     # short: its tail pieces read as null
+        p.write_bytes(bytes(data))
+        files.append(FileInfo(n, [f"f{k}.bin"]))
+        paths.append(str(p))
+        o += n
+    info = make_info(L, bytes(digests), "cold", files=files, length=total)
+    st = Storage(fs_storage, info, str(tmp_path))
+    want = [0] * P
+    for i in range(P):
+        b = st.get(i * L, min(L, total - i * L))
+        want[i] = int(b is not None and hashlib.sha1(b).digest() == bytes(digests[20 * i:20 * i + 20]))
+    budget = 2 * (P * (256 * 1024 + 256) + 256)      # 256 KiB columns: 4 per piece
+    with _context(0) as ctx:
+        ctx.set_option(native.TV_OPT_FILE_ODIRECT, odirect)
+    cwd = os.getcwd()
+    os.chdir(str(tmp_path))
+    try:
+        for cold in (False, True):
+            if cold:
+                assert fsutil.drop_cache(paths) <= 0.01
+            else:
+                assert fsutil.resident(paths) > 0.99
+            with _context(0) as ctx:
+                ctx._reset_file_clock()
+            bf = verify_files(info, str(tmp_path), threads=4, budget=budget, stream=True)
+            with _context(0) as ctx:
+                clock = ctx._file_clock()
+                assert ctx.last_kernel()[1] == 4                 # one window, four columns
+            assert _bits(bf, P) == want, (cold, odirect)
+            if cold and odirect == 1:
+                assert 0 < clock["bytes_odirect"] == clock["bytes_read"], clock
+                assert clock["odirect_fallbacks"] == 0, clock
+            else:
+                assert clock["bytes_odirect"] == 0, clock
+                if cold and odirect == 2:
+                    assert clock["odirect_fallbacks"] > 0 and clock["odirect_errno"] == errno.EINVAL, clock
+                else:
+                    assert clock["odirect_fallbacks"] == 0, clock
+    finally:
+        os.chdir(cwd)
+        with _context(0) as ctx:
+            ctx.set_option(native.TV_OPT_FILE_ODIRECT, 1)

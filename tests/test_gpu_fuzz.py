@@ -39,7 +39,7 @@ def _draw(seed):
         sizes.append(L + 3)
     total = sum(sizes)
     P = -(-total // L)
-    payload = bytearray(rng.getrandbits(8) for _ in range(total))
+    payload = bytearray(rng.randbytes(total))
     digests = bytearray(b"".join(hashlib.sha1(bytes(payload[i * L:(i + 1) * L])).digest() for i in range(P)))
     for i in rng.sample(range(P), max(1, P // 10)):            # corrupted data
         payload[i * L + rng.randrange(min(L, total - i * L))] ^= 1 << rng.randrange(8)
@@ -383,4 +383,68 @@ def test_random_layouts_streamed_files(native, tmp_path, monkeypatch, seed):
     for devices, budget in (([0], None), ([0, 0, 0], None), ([0], 2 * (3 * L + 4096)), ([0, 0], 1)):
         bf = verify_files(info, str(tmp_path / "dl"), devices=devices, threads=3, budget=budget, stream=True)
         assert _bits(bf, P) == want, (seed, devices, budget)
+    assert sorted(str(x) for x in (tmp_path / "dl").rglob("*")) == before
+
+
+@pytest.mark.gpu
+def test_streamed_files_windows_of_columns(native, tmp_path, monkeypatch):
+    """tv_stream_file_table's geometry under a device budget: windows of 2,048 pieces, each hashed in columns as wide
+    as the budget allows (tv_stream.hip), on a 5,000-piece torrent of 4 KiB pieces with a short last piece, a
+    zero-length file, a truncated and a missing file and corrupted pieces -- 1,024-byte columns (3 windows x 4
+    columns), 64-byte columns (3 x 64), whole pieces in one window (no budget), an explicit TV_OPT_STREAM_CHUNK
+    (columns across the shard), on one and two shards: bits equal fsStorage.get + hashlib's."""
+    import shutil
+    from torrent_amd import Storage, verify_files
+    from torrent_amd.metainfo import FileInfo, make_info
+    from torrent_amd.storage import fs_storage
+    from torrent_amd.verify import shard_ranges
+    rng = random.Random(77)
+    L, P = 4096, 5000
+    total = P * L - 1234
+    payload = bytearray(rng.randbytes(total))
+    digests = b"".join(hashlib.sha1(bytes(payload[i * L:(i + 1) * L])).digest() for i in range(P))
+    for i in (0, 63, 64, 2047, 2048, 2049, 4095, 4096, P - 1):     # corrupted around the window and word edges
+        payload[min(total - 1, i * L + rng.randrange(L))] ^= 0x5A
+    sizes = [3 * L + 17, 0, 2000 * L, 1111 * L - 17, 700 * L + 5, 0]
+    sizes.append(total - sum(sizes))
+    names = [f"f{k}.bin" for k in range(len(sizes))]
+    info = make_info(L, digests, "t", files=[FileInfo(n, ["s", nm]) for n, nm in zip(sizes, names)], length=total)
+    monkeypatch.chdir(tmp_path)
+    for root in ("dl", "ref"):
+        (tmp_path / root / "s").mkdir(parents=True)
+        o = 0
+        for n, nm in zip(sizes, names):
+            data = bytes(payload[o:o + n])
+            o += n
+            if nm == "f4.bin":
+                continue                                               # missing
+            if nm == "f3.bin":
+                data = data[:len(data) - 3000]                         # short
+            (tmp_path / root / "s" / nm).write_bytes(data)
+    want = _expected(info, Storage(fs_storage, info, str(tmp_path / "ref")))
+    shutil.rmtree(tmp_path / "ref", ignore_errors=True)
+    assert 0 < sum(want) < P
+    before = sorted(str(x) for x in (tmp_path / "dl").rglob("*"))
+    half = 2048 * (1024 + 256) + 256
+    for devices in ([0], [0, 0]):
+        for budget in (2 * half, 1, None):
+            bf = verify_files(info, str(tmp_path / "dl"), devices=devices, threads=4, budget=budget, stream=True)
+            assert _bits(bf, P) == want, (devices, budget)
+    # the geometry: units = windows x columns (tv_last_kernel's launch count)
+    paths = Storage(fs_storage, info, str(tmp_path / "dl")).file_paths()
+    for budget, chunk, units in ((2 * half, 0, 3 * 4), (1, 0, 3 * 64), (0, 0, 1), (0, 1024, 4)):
+        got = []
+        for first, count in shard_ranges(P, 1):
+            with native.Context(0) as ctx:
+                ctx.set_option(native.TV_OPT_RESIDENT, 0)
+                ctx.set_option(native.TV_OPT_RESIDENT_BUDGET, budget)
+                ctx.set_option(native.TV_OPT_STREAM_CHUNK, chunk)
+                ctx.set_layout(total, L, P, first, count)
+                ctx.set_digests(info.pieces_raw)
+                ctx.set_option(native.TV_OPT_FILE_THREADS, 4)
+                bits, status = ctx.stream_file_table(sizes, paths)
+                assert ctx.last_kernel()[1] == units, (budget, chunk)
+                assert [k for k, s in enumerate(status) if s] == [3, 4], (budget, chunk)
+                got += _bits(bits, count)
+        assert got == want, (budget, chunk)
     assert sorted(str(x) for x in (tmp_path / "dl").rglob("*")) == before

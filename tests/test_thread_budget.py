@@ -130,13 +130,13 @@ def test_storage_paths_honour_an_explicit_thread_count():
 
 def test_stream_rule_is_the_same_in_both_hosts(tmp_path):
     """verify_files / verifyFiles choose streamed columns over windows by the same rule (torrent_amd/verify.py
-    _stream_wins, ts/verify.ts streamWins) and size the columns alike (_stream_column / streamColumn)."""
+    _stream_wins, ts/verify.ts streamWins); both hand the budget to the library, which sizes the columns."""
     import shutil
     cases = [(1 << 20, 16384, None), (1 << 20, 16384, 1 << 29), (1 << 20, 16384, 1 << 30), (1 << 20, 16384, 2 << 30),
              (4 << 20, 51200, 3 << 30), (4 << 20, 51200, 4 << 30), (256 << 10, 100, 1 << 20), (1000, 37, 5000),
              (65536, 1000, 1), (1 << 20, 10, 1 << 29)]
-    want = [[verify._stream_wins(L, n, b), verify._stream_column(L, n, b)] for L, n, b in cases]
-    assert want[1][0] and not want[2][0] and not want[0][0] and want[6][0] and not want[9][0]
+    want = [verify._stream_wins(L, n, b) for L, n, b in cases]
+    assert want[1] and not want[2] and not want[0] and want[6] and not want[9]
     if not shutil.which("node"):
         pytest.skip("needs node")
     from tests.test_ts_binding import erased_module, run_node
@@ -144,8 +144,7 @@ def test_stream_rule_is_the_same_in_both_hosts(tmp_path):
     out = run_node(tmp_path, f"""
 import("{mod}").then((m) => {{
   const cases = {json.dumps([[L, n, b] for L, n, b in cases])};
-  console.log(JSON.stringify(cases.map(([L, n, b]) => [m.streamWins(L, n, b === null ? undefined : b),
-                                                       m.streamColumn(L, n, b === null ? undefined : b)])));
+  console.log(JSON.stringify(cases.map(([L, n, b]) => m.streamWins(L, n, b === null ? undefined : b))));
 }}).catch((e) => {{ console.error(e); process.exit(1); }});
 """)
     assert json.loads(out) == want

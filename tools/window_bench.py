@@ -4,6 +4,7 @@ previous window hashes), beside the streamed path (verify_stream over the same m
 against hashlib's digests of the payload (1 % of them corrupted; tests/synth.py generates it).
 
     python tools/window_bench.py [--gib 16] [--piece-mib 1] [--budgets 0,8,2,0.5] [--reps 3] [--variants 4:0,2:1]
+                                 [--files DIR [--cold [--cold-variants 512:0,2048:16]]]
 
 --variants: window buffers : hash streams (TV_OPT_WIN_BUFS / TV_OPT_WIN_STREAMS; 0 = the library's default) tried
 on every windowed budget (round 6: windows hashed side by side on hash streams of their own).
@@ -37,6 +38,11 @@ def main():
     ap.add_argument("--variants", default="0:0")
     ap.add_argument("--files", default=None,
                     help="also verify_files on a warm single16 layout (one 16 GiB file, 1 MiB pieces) written to this dir")
+    ap.add_argument("--cold", action="store_true",
+                    help="with --files: also cold legs (the file evicted from the page cache before each rep)")
+    ap.add_argument("--cold-variants", default="0:0",
+                    help="cold streamed legs: pieces per window : reader threads [: KiB per request] "
+                         "(TV_OPT_STREAM_COLD_WINDOW / _READERS / _REQ; 0 = the library's default)")
     a = ap.parse_args()
     L = int(a.piece_mib * MiB)
     total = int(a.gib * GiB) // L * L
@@ -57,9 +63,11 @@ def main():
         expect[-1] &= (0xFF << (8 - P % 8)) & 0xFF
     info = make_info(L, bytes(digests), "w", length=total)
 
-    def leg(name, fn, budget_gib, variant=None):
-        walls, ok = [], True
+    def leg(name, fn, budget_gib, variant=None, pre=None):
+        walls, ok, res = [], True, []
         for _ in range(a.reps):
+            if pre:
+                res.append(pre())
             t0 = time.perf_counter()
             bf = fn()
             walls.append(time.perf_counter() - t0)
@@ -72,7 +80,8 @@ def main():
                           "windows": cnt.get("windows"), "window_pieces": cnt.get("window_pieces"),
                           "payload_bytes": cnt.get("payload_bytes"), "best_s": round(min(walls), 4),
                           "median_s": round(statistics.median(walls), 4),
-                          "gbps": round(total / min(walls) / 1e9, 2), "bitfield_exact": ok}), flush=True)
+                          "gbps": round(total / min(walls) / 1e9, 2), "bitfield_exact": ok,
+                          **({"residency": [round(r, 4) for r in res]} if pre else {})}), flush=True)
 
     for b in [float(x) for x in a.budgets.split(",")]:
         budget = int(b * GiB) if b else None
@@ -100,6 +109,24 @@ def main():
             leg("verify_files warm", lambda: verify_files(finfo, root, budget=budget, stream=False), b, "windows")
             leg("verify_files warm streamed", lambda: verify_files(finfo, root, budget=budget, stream=True), b,
                 "columns")
+        if a.cold:
+            import fsutil
+            for b in [float(x) for x in a.budgets.split(",")]:
+                budget = int(b * GiB) if b else None
+                leg("verify_files cold windows", lambda: verify_files(finfo, root, budget=budget, stream=False), b,
+                    "windows", pre=lambda: fsutil.drop_cache(paths))
+                for v in a.cold_variants.split(","):
+                    cw, cr, cq = (int(x) for x in (v + ":0:0").split(":")[:3])
+                    with _context(0) as ctx:
+                        ctx.set_option(N.TV_OPT_STREAM_COLD_WINDOW, cw)
+                        ctx.set_option(N.TV_OPT_STREAM_COLD_READERS, cr)
+                        ctx.set_option(N.TV_OPT_STREAM_COLD_REQ, cq << 10)
+                    leg("verify_files cold streamed", lambda: verify_files(finfo, root, budget=budget, stream=True), b,
+                        f"columns {v}", pre=lambda: fsutil.drop_cache(paths))
+            with _context(0) as ctx:
+                ctx.set_option(N.TV_OPT_STREAM_COLD_WINDOW, 0)
+                ctx.set_option(N.TV_OPT_STREAM_COLD_READERS, 0)
+                ctx.set_option(N.TV_OPT_STREAM_COLD_REQ, 0)
         for p in paths:
             os.unlink(p)
 

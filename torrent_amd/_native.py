@@ -52,6 +52,9 @@ TV_COUNTER_COTENANT_VRAM = 120
 TV_OPT_WIN_BUFS = 23
 TV_OPT_FILE_BOUNCE = 25
 TV_OPT_WIN_STREAMS = 24
+TV_OPT_STREAM_COLD_WINDOW = 26
+TV_OPT_STREAM_COLD_READERS = 27
+TV_OPT_STREAM_COLD_REQ = 28
 TV_COUNTER_WINDOW_BUFS = 122
 TV_COUNTER_WINDOW_STREAMS = 123
 WIN_BUFS_DEFAULT = 3    # tv_plan.h kWinBufsDefault: window buffers of a windowed layout

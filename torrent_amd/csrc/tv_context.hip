@@ -268,6 +268,19 @@ int tv_set_option(tv_ctx* c, int key, int64_t value) {
             if (value < 0 || value > 16) return fail(c, TV_ERR_ARG, "TV_OPT_FILE_BOUNCE must be 0 (off) .. 16 readers");
             c->file_bounce = (int)value;
             return TV_OK;
+        case TV_OPT_STREAM_COLD_WINDOW:
+            if (value < 0 || value % 64 || value > (1ll << 32))
+                return fail(c, TV_ERR_ARG, "TV_OPT_STREAM_COLD_WINDOW must be 0 (default) or a multiple of 64 pieces");
+            c->stream_cold_window = (uint64_t)value;
+            return TV_OK;
+        case TV_OPT_STREAM_COLD_READERS:
+            if (value < 0 || value > 256) return fail(c, TV_ERR_ARG, "TV_OPT_STREAM_COLD_READERS must be 0 .. 256");
+            c->stream_cold_readers = (int)value;
+            return TV_OK;
+        case TV_OPT_STREAM_COLD_REQ:
+            if (value < 0 || (value > 0 && value < 4096)) return fail(c, TV_ERR_ARG, "TV_OPT_STREAM_COLD_REQ must be 0 or >= 4096");
+            c->stream_cold_req = (uint64_t)value;
+            return TV_OK;
         case TV_OPT_WIN_BUFS:
             if (value < 0 || value > kWinBufsMax)
                 return fail(c, TV_ERR_ARG, "TV_OPT_WIN_BUFS must be 0 (default) .. %d", kWinBufsMax);
@@ -315,6 +328,9 @@ int tv_get_option(tv_ctx* c, int key, int64_t* value) {
         case TV_OPT_LANE_PAIRS: *value = c->lane_pairs; return TV_OK;
         case TV_OPT_WIN_BUFS: *value = c->win_bufs_opt; return TV_OK;
         case TV_OPT_FILE_BOUNCE: *value = c->file_bounce; return TV_OK;
+        case TV_OPT_STREAM_COLD_WINDOW: *value = (int64_t)c->stream_cold_window; return TV_OK;
+        case TV_OPT_STREAM_COLD_READERS: *value = c->stream_cold_readers; return TV_OK;
+        case TV_OPT_STREAM_COLD_REQ: *value = (int64_t)c->stream_cold_req; return TV_OK;
         case TV_OPT_WIN_STREAMS: *value = c->win_streams_opt; return TV_OK;
     }
     return fail(c, TV_ERR_ARG, "unknown option %d", key);

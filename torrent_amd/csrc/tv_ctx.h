@@ -180,6 +180,9 @@ struct tv_ctx {
     bool file_concurrent = true;         // tv_stage_files: long segments on two staging lanes
     int file_odirect = 1;                // TV_OPT_FILE_ODIRECT: cold chunks read with O_DIRECT (2: its reads fail, tests)
     int file_bounce = 2;                 // TV_OPT_FILE_BOUNCE: cold O_DIRECT reads into small reused page-locked buffers
+    uint64_t stream_cold_window = 0;     // TV_OPT_STREAM_COLD_WINDOW (0: 512 pieces)
+    int stream_cold_readers = 0;         // TV_OPT_STREAM_COLD_READERS (0: 2 x file_threads)
+    uint64_t stream_cold_req = 0;        // TV_OPT_STREAM_COLD_REQ (0: one ring slot)
                                          // DMA'd from there (readers per lane), 0 = into the ring's 64 MiB slots
     uint64_t file_direct_min = 32ull << 20;  // tv_stage_files: segments >= this take the tv_stage_file path
     int file_threads = 16;                   // tv_stage_files: reader threads
@@ -348,6 +351,7 @@ int require_layout(tv_ctx* c, bool need_digests, bool need_resident = false);
 
 int access_ok(const char* path, bool rw);
 int open_file(const char* path, bool rw, int* err);
+double cached_fraction(int fd, uint64_t fo, uint64_t n);   // page-cache residency of file bytes, sampled (tv_files.hip)
 int fs_openable(const char* path, bool rw);
 
 // ---- NUMA placement and the host worker pools --------------------------------------------------------------------

@@ -69,6 +69,10 @@ int pread_pool(Pool& pool, int threads, int fd, uint8_t* dst, uint64_t fo, uint6
     return err.load();
 }
 
+}  // namespace
+
+namespace tvi {
+
 // Fraction of file bytes [fo, fo + n) in the page cache, sampled: the range is mapped (no page is touched) and
 // mincore asks for 64 pages spread evenly over it; -1 when it cannot be mapped.  (cachestat(2) would be one call,
 // but on an overlay filesystem -- the gpurun boxes' /tmp -- it reports the overlay inode, which caches nothing,
@@ -90,6 +94,10 @@ double cached_fraction(int fd, uint64_t fo, uint64_t n) {
     munmap(m, len);
     return (double)hit / (double)samples;
 }
+
+}  // namespace tvi
+
+namespace {
 
 // The phase clock of file staging (internal counters TV_COUNTER_FILE_NS_*, tv_options_internal.h): nanoseconds a
 // scope spent, added to the ctx's total for its phase (both lanes add; a lane's phases do not overlap each other).

@@ -39,6 +39,13 @@
 #define TV_OPT_WIN_STREAMS 24 /* windowed layouts: hash streams, the compute stream included, 0 (default) = buffers - 1
                                  (at most 4), else 1..4; 1 = every window hashed on the compute stream, one after the
                                  other (rounds 4-5) */
+#define TV_OPT_STREAM_COLD_WINDOW 26 /* tv_stream_file_table on a shard whose files are mostly not in the page cache:
+                                        pieces per window, 0 (default) = 512 (rows four times as long as the warm
+                                        geometry's 2,048-piece windows), else a multiple of 64 */
+#define TV_OPT_STREAM_COLD_READERS 27 /* its reader threads for O_DIRECT rows, 0 (default) = 2 x TV_OPT_FILE_THREADS
+                                         (they wait on the disk, not the CPU), else 1..256 */
+#define TV_OPT_STREAM_COLD_REQ 28 /* its request size: bytes of rows per ring request, 0 (default) = one ring slot
+                                     (64 MiB), else >= 4096 */
 #define TV_COUNTER_WINDOW_BUFS 122    /* window buffers of the current windowed layout (0: not windowed) */
 #define TV_COUNTER_WINDOW_STREAMS 123 /* its hash streams (1: the compute stream) */
 #define TV_COUNTER_KFD_GPU_ID 121    /* the GPU's KFD gpu_id when the co-tenant check can run (reading it probes for this

@@ -6,6 +6,7 @@
 
 #include <cerrno>
 #include <cstring>
+#include <memory>
 
 #include "tv_ctx.h"
 
@@ -68,7 +69,8 @@ uint64_t stream_chunk_need(const tv_ctx* c) {
     return (stream_column(c) + 256) * c->count + kSlack;
 }
 
-int stream_begin_locked(tv_ctx* c, const uint8_t* avail_bits) {
+int stream_begin_locked(tv_ctx* c, const uint8_t* avail_bits, uint64_t col_override = 0, uint64_t win_override = 0,
+                        uint64_t req_bytes = 0) {
     StreamState& st = c->st;
     st = StreamState{};
     st.av.assign((c->count + 7) / 8, 0xFF);
@@ -80,9 +82,9 @@ int stream_begin_locked(tv_ctx* c, const uint8_t* avail_bits) {
     if (stream_rows(c)) {  // whole pieces per row, windows of wn pieces
         st.C = (c->L + 63) / 64 * 64;
         st.wn = stream_row_window(c);
-    } else {               // columns across the whole shard
-        st.C = stream_column(c);
-        st.wn = c->count;
+    } else {               // columns across the whole shard (or across windows of win_override pieces)
+        st.C = col_override ? col_override : stream_column(c);
+        st.wn = win_override ? std::min(win_override, c->count) : c->count;
     }
     st.row_pitch = st.C + 256;  // (tail over-read slack per row)
     const uint64_t need = st.row_pitch * st.wn + kSlack;
@@ -97,7 +99,7 @@ int stream_begin_locked(tv_ctx* c, const uint8_t* avail_bits) {
     st.ncol = (c->L + st.C - 1) / st.C;
     st.nwin = (c->count + st.wn - 1) / st.wn;
     st.nunits = st.nwin * st.ncol;
-    st.rows_per_req = std::max<uint64_t>(1, kRingSlotBytes / st.C);
+    st.rows_per_req = std::max<uint64_t>(1, (req_bytes ? std::min<uint64_t>(req_bytes, kRingSlotBytes) : kRingSlotBytes) / st.C);
     TV_HIP(c, hipEventRecord(c->ev_call0, c->stream));
     TV_HIP(c, hipMemsetAsync(c->d_out, 0, c->bit_words * 8, c->stream));  // fail closed, as tv_verify
     TV_HIP(c, hipEventRecord(c->done_ev[0], c->stream));
@@ -323,10 +325,56 @@ int tv_stream_file_table(tv_ctx* c, uint64_t n, const uint64_t* lengths, const c
     }
     if (!c->count) return TV_OK;
     TV_HIP(c, hipSetDevice(c->device));
-    // availability before any read: the caller's bits, pieces past the files' end, and the pieces whose walk has a
-    // zero-length segment whose open fails (the same segments tv_stage_file_table checks)
     const uint64_t last = c->first + c->count - 1;
     const uint64_t lo = c->first * c->L, hi = std::min(c->total, last * c->L + piece_len(c, last));
+    // Whether the shard's files are mostly not in the page cache (TV_OPT_FILE_ODIRECT): up to 16 of the files holding
+    // >= 1 MiB of its bytes, evenly spread, each sampled as the staging path samples a unit (64 pages), weighted by
+    // bytes.  A cold shard is read in longer rows (fewer pieces per window) by more readers: O_DIRECT reads wait on
+    // the disk, which wants long requests and many in flight (profiles/r06/window_bench_cold_cols*.jsonl).
+    bool cold = false;
+    if (c->file_odirect) {
+        std::vector<uint64_t> big;
+        for (uint64_t k = 0; k < n; k++) {
+            const uint64_t a = std::max(lo, start[k]), b = std::min(hi, start[k + 1]);
+            if (b > a && b - a >= (1u << 20) && path[k][0]) big.push_back(k);
+        }
+        double hit = 0, all = 0;
+        const size_t m = std::min<size_t>(16, big.size());
+        for (size_t q = 0; q < m; q++) {
+            const uint64_t k = big[q * big.size() / m];
+            const uint64_t a = std::max(lo, start[k]), b = std::min(hi, start[k + 1]);
+            const int fd = open(path[k], O_RDONLY | O_CLOEXEC);
+            if (fd < 0) continue;
+            const double f = cached_fraction(fd, a - start[k], b - a);
+            close(fd);
+            if (f < 0) continue;
+            hit += f * (double)(b - a);
+            all += (double)(b - a);
+        }
+        cold = all > 0 && hit < 0.5 * all;
+    }
+    // Geometry: windows of at least kFileStreamWindow pieces, each hashed column by column -- enough pieces that a
+    // column hashes faster than it stages (2,048 pieces x 64 B per ~0.75 us block step: ~175 GB/s; a cold shard's
+    // 512: ~44 GB/s, above what the disk gives) -- and columns as wide as the device budget allows
+    // (TV_OPT_RESIDENT_BUDGET, or 1 GiB; two columns in device memory), so each row is one long read: 124 KiB at a
+    // 0.5 GiB budget and 1 MiB pieces (496 KiB cold) where columns across the whole shard would read 16 KiB.  Where
+    // whole pieces fit, the windows grow to fill the budget.  An explicit TV_OPT_STREAM_CHUNK keeps the engine's
+    // columns across the whole shard.
+    const uint64_t kFileStreamWindow = cold ? (c->stream_cold_window ? c->stream_cold_window : 512) : 2048;
+    uint64_t col = 0, win = 0;
+    if (!c->stream_chunk) {
+        const uint64_t half = (c->budget_opt ? c->budget_opt : (1ull << 30)) / 2;
+        const uint64_t lpad = std::min<uint64_t>((c->L + 63) / 64 * 64, kRingSlotBytes);
+        win = std::min<uint64_t>(c->count, kFileStreamWindow);
+        const uint64_t per = half > kSlack ? (half - kSlack) / win : 0;
+        // (a multiple of 4 KiB from 4 KiB up: a cold file's rows are then read O_DIRECT straight into the slot)
+        const uint64_t w = per > 256 ? per - 256 : 64;
+        col = std::max<uint64_t>(64, std::min<uint64_t>(w >= 4096 ? w / 4096 * 4096 : w / 64 * 64, lpad));
+        if (col == lpad && win < c->count && half > kSlack)
+            win = std::min<uint64_t>(c->count, std::max<uint64_t>(win, (half - kSlack) / (col + 256) / 64 * 64));
+    }
+    // availability before any read: the caller's bits, pieces past the files' end, and the pieces whose walk has a
+    // zero-length segment whose open fails (the same segments tv_stage_file_table checks)
     std::vector<uint8_t> av((c->count + 7) / 8, 0);
     for (uint64_t j = 0; j < c->count; j++) {
         const uint64_t i = c->first + j, end = i * c->L + piece_len(c, i);
@@ -348,30 +396,42 @@ int tv_stream_file_table(tv_ctx* c, uint64_t n, const uint64_t* lengths, const c
     }
     // the call's open files: the first kCachedFds opened stay open until the end (a one- or few-file torrent opens
     // each once); past that a reader opens and closes the file around its read (as fsStorage.get does per call), so
-    // a 10,000-file torrent never runs into the descriptor limit.  -2: the open failed.
+    // a 10,000-file torrent never runs into the descriptor limit.  -2: the open failed.  A cached file whose pages
+    // are mostly not in the page cache at its open (64 sampled pages, TV_OPT_FILE_ODIRECT) is also opened O_DIRECT:
+    // its rows are read past the page cache (dfds; -1 none, and a file whose O_DIRECT read the filesystem refuses
+    // reads buffered from then on: no_direct).
     constexpr int kCachedFds = 256;
-    std::vector<int> fds(n, -1);
+    std::vector<int> fds(n, -1), dfds(n, -1);
+    std::unique_ptr<std::atomic<bool>[]> no_direct(new std::atomic<bool>[n ? n : 1]());
     int cached = 0;
     std::mutex fd_mu;
     struct Closer {
         std::vector<int>& f;
+        std::vector<int>& d;
         ~Closer() {
-            for (int d : f)
-                if (d >= 0) close(d);
+            for (int x : f)
+                if (x >= 0) close(x);
+            for (int x : d)
+                if (x >= 0) close(x);
         }
-    } closer{fds};
-    // -> a descriptor of file k, and whether the caller closes it after its read
-    auto fd_of = [&](uint64_t k, bool* own) -> int {
+    } closer{fds, dfds};
+    // -> a descriptor of file k, and whether the caller closes it after its read; *dfd: its O_DIRECT one or -1
+    auto fd_of = [&](uint64_t k, bool* own, int* dfd) -> int {
         *own = false;
+        *dfd = -1;
         {
             std::lock_guard<std::mutex> fg(fd_mu);
-            if (fds[k] != -1) return fds[k];
+            if (fds[k] != -1) {
+                if (dfds[k] >= 0 && !no_direct[k].load(std::memory_order_relaxed)) *dfd = dfds[k];
+                return fds[k];
+            }
         }
         int e = 0;
         const int d = path[k][0] ? open_file(path[k], c->open_rw, &e) : -1;
         std::lock_guard<std::mutex> fg(fd_mu);
         if (fds[k] != -1) {   // another reader opened it meanwhile
             if (d >= 0) close(d);
+            if (dfds[k] >= 0 && !no_direct[k].load(std::memory_order_relaxed)) *dfd = dfds[k];
             return fds[k];
         }
         if (d < 0) {
@@ -381,13 +441,63 @@ int tv_stream_file_table(tv_ctx* c, uint64_t n, const uint64_t* lengths, const c
         if (cached < kCachedFds) {
             cached++;
             fds[k] = d;
+            if (c->file_odirect && lengths[k] >= (1u << 20)) {
+                const double f = cached_fraction(d, 0, lengths[k]);
+                if (f >= 0 && f < 0.5) dfds[k] = open(path[k], (c->open_rw ? O_RDWR : O_RDONLY) | O_DIRECT | O_CLOEXEC);
+                if (dfds[k] >= 0) *dfd = dfds[k];
+            }
             return d;
         }
         *own = true;
         return d;
     };
+    // file bytes [fo, fo + len) -> dst through the O_DIRECT descriptor: straight into dst when the file offset, dst
+    // and the length are 4 KiB-aligned (whole-row reads of a one-file torrent), else via a 4 KiB-aligned scratch of
+    // the reader thread's in 4 MiB steps.  -> bytes read (short: the file ended), or -errno.
+    auto read_direct = [&](int dfd, uint64_t fo, uint8_t* dst, uint64_t len) -> int64_t {
+        if (c->file_odirect == 2) return -EINVAL;   // (fault injection: the filesystem refusing O_DIRECT reads)
+        uint64_t o = 0;
+        if (fo % 4096 == 0 && (uintptr_t)dst % 4096 == 0 && len % 4096 == 0) {
+            while (o < len) {
+                const ssize_t got = pread(dfd, dst + o, len - o, (off_t)(fo + o));
+                if (got < 0 && errno == EINTR) continue;
+                if (got < 0) return -errno;
+                if (got == 0) break;
+                o += (uint64_t)got;
+            }
+            return (int64_t)o;
+        }
+        constexpr uint64_t kStep = 4ull << 20;
+        struct Scratch {
+            uint8_t* p = nullptr;
+            ~Scratch() { free(p); }
+        };
+        thread_local Scratch scratch;
+        if (!scratch.p && posix_memalign((void**)&scratch.p, 4096, kStep + 8192)) {
+            scratch.p = nullptr;
+            return -ENOMEM;
+        }
+        while (o < len) {
+            const uint64_t at = fo + o, al = at / 4096 * 4096, lead = at - al;
+            const uint64_t m = std::min(kStep, len - o), ask = (lead + m + 4095) / 4096 * 4096;
+            uint64_t got_all = 0;
+            while (got_all < ask) {
+                const ssize_t got = pread(dfd, scratch.p + got_all, ask - got_all, (off_t)(al + got_all));
+                if (got < 0 && errno == EINTR) continue;
+                if (got < 0) return -errno;
+                if (got == 0) break;
+                got_all += (uint64_t)got;
+            }
+            const uint64_t have = got_all > lead ? std::min(m, got_all - lead) : 0;
+            memcpy(dst + o, scratch.p + lead, have);
+            o += have;
+            if (have < m) break;   // the file ended
+        }
+        return (int64_t)o;
+    };
+    const int readers = cold ? (c->stream_cold_readers ? c->stream_cold_readers : 2 * c->file_threads) : c->file_threads;
     DrainGuard drain(c);  // (the ring's copies and the column kernels are done when the call returns)
-    rc = stream_begin_locked(c, av.data());
+    rc = stream_begin_locked(c, av.data(), col, win, cold ? c->stream_cold_req : 0);
     if (rc) {
         stream_abort_locked(c);
         return rc;
@@ -400,7 +510,7 @@ int tv_stream_file_table(tv_ctx* c, uint64_t n, const uint64_t* lengths, const c
         if (rc || !req.rows) break;
         uint8_t* slot = c->ring[c->st.slot];
         std::vector<uint8_t> row_bad(req.rows, 0);
-        c->pool[0].run(c->file_threads, req.rows, [&](uint64_t q) {
+        c->pool[0].run(readers, req.rows, [&](uint64_t q) {
             const uint64_t i = req.piece + q, j = i - c->first;
             const uint64_t nb = row_bytes(c, i, req.offset, req.width);
             if (!nb || !get_bit(c->st.av.data(), j)) return;
@@ -412,8 +522,23 @@ int tv_stream_file_table(tv_ctx* c, uint64_t n, const uint64_t* lengths, const c
                 if (start[k + 1] <= pos) continue;
                 const uint64_t e = std::min(b, start[k + 1]);
                 bool own = false;
-                const int fd = fd_of(k, &own);
+                int dfd = -1;
+                const int fd = fd_of(k, &own, &dfd);
                 uint64_t o = 0;
+                if (dfd >= 0) {
+                    const int64_t got = read_direct(dfd, pos - start[k], out + (pos - a), e - pos);
+                    if (got >= 0) {
+                        o = (uint64_t)got;
+                        c->file_ns[TV_FILE_BYTES_ODIRECT].fetch_add(o, std::memory_order_relaxed);
+                    } else {
+                        // an O_DIRECT read the filesystem refuses is not the file's failure: this file reads buffered
+                        // from here on, this row included (counted, first errno kept, as the staging path's fallback)
+                        no_direct[k].store(true, std::memory_order_relaxed);
+                        c->file_ns[TV_FILE_ODIRECT_FALLBACKS].fetch_add(1, std::memory_order_relaxed);
+                        uint64_t none = 0;
+                        c->file_ns[TV_FILE_ODIRECT_ERRNO].compare_exchange_strong(none, (uint64_t)-got);
+                    }
+                }
                 while (fd >= 0 && o < e - pos) {
                     const ssize_t got = pread(fd, out + (pos - a) + o, e - pos - o, (off_t)(pos - start[k] + o));
                     if (got < 0 && errno == EINTR) continue;
@@ -421,6 +546,7 @@ int tv_stream_file_table(tv_ctx* c, uint64_t n, const uint64_t* lengths, const c
                     o += (uint64_t)got;
                 }
                 if (own) close(fd);
+                c->file_ns[TV_FILE_BYTES_READ].fetch_add(o, std::memory_order_relaxed);
                 if (o < e - pos) {   // missing, unopenable or short: the piece is null, as fsStorage.get's read
                     row_bad[q] = 1;
                     file_err[k].store(TV_ERR_IO);

@@ -464,15 +464,6 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
     return avail
 
 
-def _stream_column(L: int, count: int, budget: Optional[int]) -> int:
-    """Column width of a streamed shard under a device budget: the two chunk buffers of (C + 256) bytes per shard piece
-    fit it (tv_stream_file_table); 0 (the library's default, ~512 MiB columns) without a budget."""
-    if not budget:
-        return 0
-    C = (budget // 2 - 256) // max(1, count) - 256
-    return max(64, min(C // 64 * 64, -(-L // 64) * 64))
-
-
 def _stream_wins(L: int, count: int, budget: Optional[int]) -> bool:
     """Whether a file-backed shard verifies faster in streamed columns than in windows of whole pieces under this
     device budget: only when the shard does not fit it, and each window (two of three buffers hashing at once) would
@@ -488,12 +479,14 @@ def _stream_wins(L: int, count: int, budget: Optional[int]) -> bool:
 def _stream_files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: int,
                         budget: Optional[int]) -> bytes:
     """A shard's resume check from its files through the bounded ring (tv_stream_file_table): no resident payload,
-    two device columns sized to the budget, the library's readers filling each column from the file table."""
+    two device chunk buffers within the budget (columns of windows of >= 2,048 pieces), the library's readers filling
+    each column from the file table."""
     L, P = info.piece_length, info.n_pieces
     ctx.set_option(_native.TV_OPT_RESIDENT, 0)
     try:
-        ctx.set_option(_native.TV_OPT_RESIDENT_BUDGET, 0)
-        ctx.set_option(_native.TV_OPT_STREAM_CHUNK, _stream_column(L, count, budget))
+        # the library sizes windows x columns to the budget (tv_stream_file_table)
+        ctx.set_option(_native.TV_OPT_RESIDENT_BUDGET, int(budget or 0))
+        ctx.set_option(_native.TV_OPT_STREAM_CHUNK, 0)
         ctx.set_option(_native.TV_OPT_STREAM_ROWS, 0)
         ctx.set_layout(info.length, L, P, first, count)
         ctx.set_digests(info.pieces_raw)

@@ -475,14 +475,6 @@ function fileTable(info: InfoDict, dir: string): FileTable {
   return t;
 }
 
-/** Column width of a streamed shard under a device budget (torrent_amd/verify.py _stream_column): the two device
- * columns of (C + 256) bytes per shard piece fit it; 0 (the library's ~512 MiB columns) without a budget. */
-export function streamColumn(L: number, count: number, budget?: number): number {
-  if (!budget) return 0;
-  const C = Math.floor((Math.floor(budget / 2) - 256) / Math.max(1, count)) - 256;
-  return Math.max(64, Math.min(Math.floor(C / 64) * 64, Math.ceil(L / 64) * 64));
-}
-
 /** Whether a file-backed shard verifies faster in streamed columns than in windows of whole pieces under the device
  * budget (torrent_amd/verify.py _stream_wins): the shard does not fit it, and windows would cost more than staging
  * (each pays one piece's serial SHA-1, ~11.8 ms per MiB of piece: below ~0.9 GB of budget per MiB of piece length). */
@@ -510,8 +502,9 @@ export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptio
       if (opts.stream || (opts.stream === undefined && streamWins(L, count, opts.budget))) {
         // columns through the bounded ring, read by the library from the file table
         check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_RESIDENT, 0n));
-        check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_RESIDENT_BUDGET, 0n));
-        check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_STREAM_CHUNK, BigInt(streamColumn(L, count, opts.budget))));
+        // (the library sizes windows x columns to the budget)
+        check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_RESIDENT_BUDGET, BigInt(opts.budget || 0)));
+        check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_STREAM_CHUNK, 0n));
         check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_STREAM_ROWS, 0n));
         try {
           check(l, ctx, l.symbols.tv_set_layout(ctx, BigInt(info.length), BigInt(L), BigInt(P), BigInt(first),
@@ -524,13 +517,9 @@ export async function verifyFiles(info: InfoDict, dir: string, opts: VerifyOptio
         check(l, ctx, l.symbols.tv_set_option(ctx, TV_OPT_FILE_THREADS, BigInt(threads)));
         const status = new Int32Array(table.n);
         const out = new Uint8Array(Math.ceil(count / 8));
-        try {
-          check(l, ctx, await l.symbols.tv_stream_file_table(ctx, BigInt(table.n), ptr(u8(table.lengths)),
-                                                             ptr(table.paths), BigInt(table.paths.length), null,
-                                                             ptr(out), ptr(u8(status))));
-        } finally {
-          l.symbols.tv_set_option(ctx, TV_OPT_STREAM_CHUNK, 0n);
-        }
+        check(l, ctx, await l.symbols.tv_stream_file_table(ctx, BigInt(table.n), ptr(u8(table.lengths)),
+                                                           ptr(table.paths), BigInt(table.paths.length), null,
+                                                           ptr(out), ptr(u8(status))));
         bitfield.set(out, first / 8);
         return;
       }
