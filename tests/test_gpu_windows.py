@@ -53,8 +53,9 @@ def test_reference_fixtures_windowed(native, name):
     payload = bytearray(_ref_payload(name))
     P, L = info.n_pieces, info.piece_length
     budget = 8 << 20
-    assert bytes(verify_payload(info, payload, budget=budget)) == _all_ones(P)
+    assert bytes(verify_payload(info, payload, budget=budget, resident=True)) == _all_ones(P)
     _check_windowed(budget)
+    assert bytes(verify_payload(info, payload, budget=budget)) == _all_ones(P)     # (default: streamed here)
     assert hash_pieces(bytes(payload), L, budget=budget) == info.pieces_raw
     flips = [0, 852, P - 1]
     for i in flips:
@@ -63,7 +64,9 @@ def test_reference_fixtures_windowed(native, name):
     for i in flips:
         want[i >> 3] &= ~(0x80 >> (i & 7)) & 0xFF
     for devices in ([0], [0, 0, 0]):
-        assert bytes(verify_payload(info, payload, devices=devices, budget=budget)) == bytes(want), devices
+        assert bytes(verify_payload(info, payload, devices=devices, budget=budget,
+                                    resident=True)) == bytes(want), devices
+        assert bytes(verify_payload(info, payload, devices=devices, budget=budget)) == bytes(want), (devices, "auto")
     if name == "multifile":
         n0 = info.files[0].length
         mem = MemoryStorage({tuple(info.files[0].path): bytes(payload[:n0]),
@@ -88,9 +91,12 @@ def test_golden_layouts_windowed(native, layout, tmp_path, monkeypatch):
     sizes = [1, 3, 16] if info.n_pieces < 1000 else [16, 64]    # (a window kernel costs one piece's SHA-1)
     for devices in ([0], [0, 0, 0]):
         budget = _budget(L, rng.choice(sizes))
-        assert bytes(verify_payload(info, lay["payload"], avail=lay["avail"], devices=devices,
-                                    budget=budget)).hex() == rec["expected_bitfield"], (devices, budget)
+        assert bytes(verify_payload(info, lay["payload"], avail=lay["avail"], devices=devices, budget=budget,
+                                    resident=True)).hex() == rec["expected_bitfield"], (devices, budget)
         _check_windowed(budget, expect_windowed=devices == [0] and info.n_pieces * _stride(L) + 256 > budget)
+        # the default: streamed windows x columns within the budget (tv_verify_host) when the shard exceeds it
+        assert bytes(verify_payload(info, lay["payload"], avail=lay["avail"], devices=devices,
+                                    budget=budget)).hex() == rec["expected_bitfield"], (devices, budget, "auto")
     monkeypatch.chdir(tmp_path)
     for path, data in lay["disk_files"]().items():
         p = tmp_path.joinpath("dl", *path)
@@ -144,7 +150,9 @@ def test_random_layouts_windowed(native, tmp_path, monkeypatch, seed):
         budget = _budget(L, rng.choice([1, 2, 3, 5]))
         assert _bits(verify_pieces(info, st, devices=devices, budget=budget), P) == want, ("pieces", devices, budget)
         assert _bits(verify_payload(info, payload[:info.length], devices=devices, avail=bytes(avail),
-                                    budget=budget), P) == want, ("payload", devices, budget)
+                                    budget=budget, resident=True), P) == want, ("payload", devices, budget)
+        assert _bits(verify_payload(info, payload[:info.length], devices=devices, avail=bytes(avail),
+                                    budget=budget), P) == want, ("payload auto", devices, budget)
         assert _bits(verify_files(info, str(tmp_path / "dl"), devices=devices, threads=3, budget=budget, stream=False),
                      P) == want_fs, ("files", devices, budget)
         _check_windowed(budget, expect_windowed=False)

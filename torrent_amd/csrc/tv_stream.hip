@@ -69,6 +69,29 @@ uint64_t stream_chunk_need(const tv_ctx* c) {
     return (stream_column(c) + 256) * c->count + kSlack;
 }
 
+// Geometry of a stream under a device budget (tv_stream_file_table; tv_verify_host when TV_OPT_RESIDENT_BUDGET is
+// set): windows of at least `min_win` pieces (a multiple of 64), each hashed column by column -- enough pieces that a
+// column hashes faster than it stages (2,048 pieces x 64 B per ~0.75 us block step: ~175 GB/s) -- and columns as
+// wide as two chunk buffers within the budget allow, so each row is one long read or DMA row: 124 KiB at a 0.5 GiB
+// budget and 1 MiB pieces where columns across all 16,384 pieces would be 16 KiB.  A multiple of 4 KiB from 4 KiB up
+// (a cold file's rows are read O_DIRECT straight into the slot); where whole pieces fit, the windows grow to fill
+// the budget.  Each chunk buffer is at most kStreamChunkMax: wider columns gained nothing and larger units overlap
+// less (the first unit's copy and the last unit's kernel run alone): budgets of 2 GiB (1 GiB units) ran 44-49 GB/s
+// against 52-55 at 0.5 GiB (profiles/r06/window_bench_payload_cols*.jsonl).
+constexpr uint64_t kStreamChunkMax = 256ull << 20;
+void budget_geometry(const tv_ctx* c, uint64_t budget, uint64_t min_win, uint64_t* col, uint64_t* win) {
+    const uint64_t half = std::min<uint64_t>(budget / 2, kStreamChunkMax);
+    const uint64_t lpad = std::min<uint64_t>((c->L + 63) / 64 * 64, kRingSlotBytes);
+    uint64_t w = std::min<uint64_t>(c->count, min_win);
+    const uint64_t per = half > kSlack ? (half - kSlack) / w : 0;
+    const uint64_t wid = per > 256 ? per - 256 : 64;
+    uint64_t C = std::max<uint64_t>(64, std::min<uint64_t>(wid >= 4096 ? wid / 4096 * 4096 : wid / 64 * 64, lpad));
+    if (C == lpad && w < c->count && half > kSlack)
+        w = std::min<uint64_t>(c->count, std::max<uint64_t>(w, (half - kSlack) / (C + 256) / 64 * 64));
+    *col = C;
+    *win = w;
+}
+
 int stream_begin_locked(tv_ctx* c, const uint8_t* avail_bits, uint64_t col_override = 0, uint64_t win_override = 0,
                         uint64_t req_bytes = 0) {
     StreamState& st = c->st;
@@ -267,8 +290,10 @@ int tv_verify_host(tv_ctx* c, const uint8_t* src, uint64_t src_len, const uint8_
         if (end <= src_len && (!avail_bits || get_bit(avail_bits, j))) set_bit(av.data(), j);
     }
     const bool pinned = is_pinned(src);
+    uint64_t col = 0, win = 0;   // (under a device budget: windows x columns within it)
+    if (c->budget_opt && !c->stream_chunk && !stream_rows(c)) budget_geometry(c, c->budget_opt, 2048, &col, &win);
     DrainGuard drain(c);  // no DMA reads the caller's buffer after the call returns, also on error paths
-    rc = stream_begin_locked(c, av.data());
+    rc = stream_begin_locked(c, av.data(), col, win);
     if (rc) {
         stream_abort_locked(c);
         return rc;
@@ -353,25 +378,13 @@ int tv_stream_file_table(tv_ctx* c, uint64_t n, const uint64_t* lengths, const c
         }
         cold = all > 0 && hit < 0.5 * all;
     }
-    // Geometry: windows of at least kFileStreamWindow pieces, each hashed column by column -- enough pieces that a
-    // column hashes faster than it stages (2,048 pieces x 64 B per ~0.75 us block step: ~175 GB/s; a cold shard's
-    // 512: ~44 GB/s, above what the disk gives) -- and columns as wide as the device budget allows
-    // (TV_OPT_RESIDENT_BUDGET, or 1 GiB; two columns in device memory), so each row is one long read: 124 KiB at a
-    // 0.5 GiB budget and 1 MiB pieces (496 KiB cold) where columns across the whole shard would read 16 KiB.  Where
-    // whole pieces fit, the windows grow to fill the budget.  An explicit TV_OPT_STREAM_CHUNK keeps the engine's
-    // columns across the whole shard.
-    const uint64_t kFileStreamWindow = cold ? (c->stream_cold_window ? c->stream_cold_window : 512) : 2048;
+    // Geometry: windows x columns within the budget (TV_OPT_RESIDENT_BUDGET, or 1 GiB); a cold shard's windows are
+    // 512 pieces (rows 4 x longer; ~44 GB/s of hashing, above what the disk gives).  An explicit TV_OPT_STREAM_CHUNK
+    // keeps the engine's columns across the whole shard.
     uint64_t col = 0, win = 0;
     if (!c->stream_chunk) {
-        const uint64_t half = (c->budget_opt ? c->budget_opt : (1ull << 30)) / 2;
-        const uint64_t lpad = std::min<uint64_t>((c->L + 63) / 64 * 64, kRingSlotBytes);
-        win = std::min<uint64_t>(c->count, kFileStreamWindow);
-        const uint64_t per = half > kSlack ? (half - kSlack) / win : 0;
-        // (a multiple of 4 KiB from 4 KiB up: a cold file's rows are then read O_DIRECT straight into the slot)
-        const uint64_t w = per > 256 ? per - 256 : 64;
-        col = std::max<uint64_t>(64, std::min<uint64_t>(w >= 4096 ? w / 4096 * 4096 : w / 64 * 64, lpad));
-        if (col == lpad && win < c->count && half > kSlack)
-            win = std::min<uint64_t>(c->count, std::max<uint64_t>(win, (half - kSlack) / (col + 256) / 64 * 64));
+        const uint64_t min_win = cold ? (c->stream_cold_window ? c->stream_cold_window : 512) : 2048;
+        budget_geometry(c, c->budget_opt ? c->budget_opt : (1ull << 30), min_win, &col, &win);
     }
     // availability before any read: the caller's bits, pieces past the files' end, and the pieces whose walk has a
     // zero-length segment whose open fails (the same segments tv_stage_file_table checks)

@@ -16,12 +16,14 @@ library or a GPU these functions raise.
 
 Device memory.  The bulk calls take `budget` (bytes of HBM the payload may use per device; None = the
 GPU's free memory less a margin).  A shard larger than it is verified in windows of pieces that fit, each
-hashed while the next one stages (tv_set_layout's windowed layout): no torrent is too large for a GPU.
+hashed while the next one stages (tv_set_layout's windowed layout): no torrent is too large for a GPU.  Where such
+windows would lose (a window pays one piece's serial SHA-1), verify_files (_stream_wins) and verify_payload stream
+the shard instead, windows x columns within the budget through the bounded ring.
 
 Public API (names follow the reference's camelCase surface, snake_cased):
     verify_pieces(info, storage, devices=None) -> bytearray         (verifyPieces)
     verify_piece(info, index, data) -> bool                         (verifyPiece)
-    verify_payload(info, payload, devices=None, resident=True) -> bytearray
+    verify_payload(info, payload, devices=None, resident=None) -> bytearray
     verify_stream(info, read, devices=None) -> bytearray             (bounded-ring resume check)
     hash_pieces(payload, piece_length, devices=None) -> bytes       (creation mode, make_torrent.ts)
 and asyncio wrappers verify_pieces_async / verify_piece_async (the reference API is Promise-based).
@@ -278,17 +280,21 @@ def verify_pieces(info: InfoDict, storage, devices=None, threads: Optional[int] 
     return _concat(slices, ranges, P)
 
 
-def verify_payload(info: InfoDict, payload, devices=None, resident: bool = True,
+def verify_payload(info: InfoDict, payload, devices=None, resident: Optional[bool] = None,
                    avail: Optional[bytes] = None, budget: Optional[int] = None) -> bytearray:
     """Verify a linear payload already in host memory (the concatenation of info.files in
-    order).  resident=True stages it into HBM and verifies there (in windows when the shard exceeds
+    order).  resident=True stages it into HBM and verifies there (in windows of whole pieces when the shard exceeds
     `budget`); resident=False streams it column by column over PCIe (tv_verify_host, the end-to-end
-    resume-check path)."""
+    resume-check path; under a `budget`, windows x columns within it).  None (default): resident when the shard fits
+    the budget, else streamed -- from host memory the stream beats windows of whole pieces at every budget (54.9-55.5
+    GB/s at 0.25-2 GiB against 14.4 / 28.3 / 51.6 / 53.8, profiles/r06/window_bench_payload_cols3.jsonl)."""
     P, L = info.n_pieces, info.piece_length
     mv = memoryview(payload).cast("B")
 
     def shard(ctx, first: int, count: int) -> bytes:
-        if not resident:        # the streamed path needs no resident payload (tv_verify_host)
+        streamed = resident is False or (resident is None and bool(budget) and
+                                         count * (-(-L // 64) * 64 + 256) + 256 > budget)
+        if streamed:            # the streamed path needs no resident payload (tv_verify_host)
             ctx.set_option(_native.TV_OPT_RESIDENT, 0)
         try:
             _layout(ctx, info, L, P, first, count, budget)
@@ -298,7 +304,7 @@ def verify_payload(info: InfoDict, payload, devices=None, resident: bool = True,
         av = _shard_avail(avail, first, count)
         lo = min(first * L, len(mv))
         hi = min((first + count) * L, len(mv))
-        if resident:
+        if not streamed:
             if hi > lo:
                 ctx.stage(lo, mv[lo:hi])
             # pieces whose bytes are not all present are unreadable
