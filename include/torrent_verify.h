@@ -227,7 +227,9 @@ int tv_verify_list(tv_ctx *ctx, const uint64_t *pieces, uint64_t n, uint8_t *ok_
  * Verify the shard from a HOST buffer (end-to-end resume check): `src` holds the
  * shard's linear bytes [shard_first*piece_length, ...) (src_len bytes; pieces extending past
  * src_len are unreadable).  Data streams host -> pinned ring -> HBM over PCIe with copy/compute
- * overlap; no resident payload is needed.
+ * overlap; no resident payload is needed (set the layout with TV_OPT_RESIDENT = 0).  Device memory: two chunk
+ * buffers within TV_OPT_RESIDENT_BUDGET (default 1 GiB), each a column of a window of >= 2,048 pieces, at most
+ * 256 MiB; TV_OPT_STREAM_CHUNK instead gives columns of that width across the whole shard.
  */
 int tv_verify_host(tv_ctx *ctx, const uint8_t *src, uint64_t src_len, const uint8_t *avail_bits,
                    uint8_t *bitfield_out);
@@ -315,8 +317,10 @@ int tv_host_unregister(void *ptr);
 /* Options (tv_set_option keys): what a host integrating the library sets.  (Measurement and test knobs -- kernel
  * forcing, stride padding, file-staging A/B modes, NUMA binding, probes, fault injection -- are keys of the
  * library's internal header torrent_amd/csrc/tv_options_internal.h, which only the tests and tools use.) */
-#define TV_OPT_STREAM_CHUNK 3 /* tv_verify_host / tv_stream_*: bytes of each piece per streamed column (0, default:
-                                 automatic, the widest power of two <= L whose column over the shard is <= 512 MiB) */
+#define TV_OPT_STREAM_CHUNK 3 /* tv_verify_host / tv_stream_*: bytes of each piece per streamed column across the
+                                 whole shard (0, default: tv_stream_*: the widest power of two <= L whose column over
+                                 the shard is <= 512 MiB; tv_verify_host / tv_stream_file_table: windows x columns
+                                 within TV_OPT_RESIDENT_BUDGET, or 1 GiB) */
 #define TV_OPT_FILE_DIRECT_MIN 7 /* tv_stage_files: segment length that takes the long-segment path (default 32 MiB) */
 #define TV_OPT_FILE_THREADS 8    /* host threads of the context (default 16): tv_stage_file(s)' readers (shared by the
                                     two staging lanes), and the copies of pageable tv_stage sources into the pinned

@@ -91,9 +91,8 @@ def main():
                 ctx.set_option(N.TV_OPT_WIN_BUFS, nb)
                 ctx.set_option(N.TV_OPT_WIN_STREAMS, ns)
             leg("verify_payload resident", lambda: verify_payload(info, buf.mv, budget=budget, resident=True), b, v)
-        if b:   # the same budget streamed: windows x columns within it (tv_verify_host)
-            leg("verify_payload streamed", lambda: verify_payload(info, buf.mv, budget=budget, resident=False), b,
-                "columns")
+        # streamed: windows x columns within the budget (or 1 GiB), tv_verify_host
+        leg("verify_payload streamed", lambda: verify_payload(info, buf.mv, budget=budget, resident=False), b, "columns")
     with _context(0) as ctx:
         ctx.set_option(N.TV_OPT_WIN_BUFS, 0)
         ctx.set_option(N.TV_OPT_WIN_STREAMS, 0)

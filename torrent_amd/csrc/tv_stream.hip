@@ -69,8 +69,8 @@ uint64_t stream_chunk_need(const tv_ctx* c) {
     return (stream_column(c) + 256) * c->count + kSlack;
 }
 
-// Geometry of a stream under a device budget (tv_stream_file_table; tv_verify_host when TV_OPT_RESIDENT_BUDGET is
-// set): windows of at least `min_win` pieces (a multiple of 64), each hashed column by column -- enough pieces that a
+// Geometry of a stream under a device budget (tv_stream_file_table, tv_verify_host; without TV_OPT_RESIDENT_BUDGET
+// 1 GiB): windows of at least `min_win` pieces (a multiple of 64), each hashed column by column -- enough pieces that a
 // column hashes faster than it stages (2,048 pieces x 64 B per ~0.75 us block step: ~175 GB/s) -- and columns as
 // wide as two chunk buffers within the budget allow, so each row is one long read or DMA row: 124 KiB at a 0.5 GiB
 // budget and 1 MiB pieces where columns across all 16,384 pieces would be 16 KiB.  A multiple of 4 KiB from 4 KiB up
@@ -290,8 +290,9 @@ int tv_verify_host(tv_ctx* c, const uint8_t* src, uint64_t src_len, const uint8_
         if (end <= src_len && (!avail_bits || get_bit(avail_bits, j))) set_bit(av.data(), j);
     }
     const bool pinned = is_pinned(src);
-    uint64_t col = 0, win = 0;   // (under a device budget: windows x columns within it)
-    if (c->budget_opt && !c->stream_chunk && !stream_rows(c)) budget_geometry(c, c->budget_opt, 2048, &col, &win);
+    uint64_t col = 0, win = 0;   // windows x columns within the device budget (or 1 GiB), unless a width is set
+    if (!c->stream_chunk && !stream_rows(c))
+        budget_geometry(c, c->budget_opt ? c->budget_opt : (1ull << 30), 2048, &col, &win);
     DrainGuard drain(c);  // no DMA reads the caller's buffer after the call returns, also on error paths
     rc = stream_begin_locked(c, av.data(), col, win);
     if (rc) {
