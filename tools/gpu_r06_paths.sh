@@ -18,5 +18,5 @@ COLD_LIBBOUNCE=1 COLD_ROUNDS=${COLD_ROUNDS:-2} timeout -k 10 500 python3 -u tool
     > $out/cold_sweep.jsonl 2> $out/cold_sweep.err && echo COLD_OK
 rc=$?
 rm -rf /tmp/tsb /tmp/tsp /tmp/wf /tmp/cs
-tail -2 $out/*.err
+tail -n 2 $out/*.err
 exit $rc

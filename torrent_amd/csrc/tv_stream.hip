@@ -482,14 +482,21 @@ int tv_stream_file_table(tv_ctx* c, uint64_t n, const uint64_t* lengths, const c
             return (int64_t)o;
         }
         constexpr uint64_t kStep = 4ull << 20;
-        struct Scratch {
+        struct Scratch {   // (sized to the longest read the thread has needed: a row, at most kStep + 8 KiB)
             uint8_t* p = nullptr;
+            uint64_t cap = 0;
             ~Scratch() { free(p); }
         };
         thread_local Scratch scratch;
-        if (!scratch.p && posix_memalign((void**)&scratch.p, 4096, kStep + 8192)) {
-            scratch.p = nullptr;
-            return -ENOMEM;
+        const uint64_t need = std::min(kStep, len) + 8192;
+        if (scratch.cap < need) {
+            free(scratch.p);
+            scratch.cap = 0;
+            if (posix_memalign((void**)&scratch.p, 4096, need)) {
+                scratch.p = nullptr;
+                return -ENOMEM;
+            }
+            scratch.cap = need;
         }
         while (o < len) {
             const uint64_t at = fo + o, al = at / 4096 * 4096, lead = at - al;
