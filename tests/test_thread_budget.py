@@ -148,3 +148,17 @@ import("{mod}").then((m) => {{
 }}).catch((e) => {{ console.error(e); process.exit(1); }});
 """)
     assert json.loads(out) == want
+
+
+def test_payload_streams_exactly_when_the_shard_exceeds_the_budget():
+    """verify_payload streams (tv_verify_host, windows x columns) by default exactly when the shard's padded payload
+    -- tv_set_layout's count x (L rounded up to 64 + 256) + 256 bytes -- exceeds the budget; without a budget the
+    library's own (free HBM) decides and the shard is held resident.  _stream_wins (verify_files) is a subset."""
+    L, n = 1 << 20, 16384
+    need = n * (L + 256) + 256
+    assert not verify._exceeds(L, n, None) and not verify._exceeds(L, n, 0)
+    assert not verify._exceeds(L, n, need) and verify._exceeds(L, n, need - 1)
+    assert verify._exceeds(1000, 37, 37 * (1024 + 256))               # (1000 rounds up to 1024)
+    assert not verify._exceeds(1000, 37, 37 * (1024 + 256) + 256)
+    for b in (1 << 28, 1 << 29, 1 << 30, 2 << 30, need - 1, need):
+        assert not verify._stream_wins(L, n, b) or verify._exceeds(L, n, b)

@@ -292,8 +292,7 @@ def verify_payload(info: InfoDict, payload, devices=None, resident: Optional[boo
     mv = memoryview(payload).cast("B")
 
     def shard(ctx, first: int, count: int) -> bytes:
-        streamed = resident is False or (resident is None and bool(budget) and
-                                         count * (-(-L // 64) * 64 + 256) + 256 > budget)
+        streamed = resident is False or (resident is None and _exceeds(L, count, budget))
         if streamed:            # the streamed path needs no resident payload (tv_verify_host)
             ctx.set_option(_native.TV_OPT_RESIDENT, 0)
         try:
@@ -470,16 +469,19 @@ def _files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: 
     return avail
 
 
+def _exceeds(L: int, count: int, budget: Optional[int]) -> bool:
+    """Whether a shard's padded payload (tv_set_layout: count x (L rounded up to 64 + 256) + 256 bytes) exceeds a
+    device budget (None: the library's automatic one, never exceeded here)."""
+    return bool(budget) and count * (-(-L // 64) * 64 + 256) + 256 > budget
+
+
 def _stream_wins(L: int, count: int, budget: Optional[int]) -> bool:
     """Whether a file-backed shard verifies faster in streamed columns than in windows of whole pieces under this
     device budget: only when the shard does not fit it, and each window (two of three buffers hashing at once) would
     cost more than staging -- a window pays one piece's serial SHA-1 (~11.8 ms per MiB of piece), so windows keep up
     with ~50 GB/s of staging only from ~0.9 GB of budget per MiB of piece length (profiles/r06/window_bench_stream.jsonl:
     0.5 GiB, 1 MiB pieces: columns 47.5 GB/s against windows 28.3; 1 GiB 50.6 / 50.4; 2 GiB 48.9 / 51.7)."""
-    if not budget:
-        return False
-    stride = -(-L // 64) * 64 + 256
-    return count * stride + 256 > budget and budget < 0.9e9 * L / (1 << 20)
+    return _exceeds(L, count, budget) and budget < 0.9e9 * L / (1 << 20)
 
 
 def _stream_files_shard(ctx, info: InfoDict, storage, first: int, count: int, threads: int,
