@@ -217,6 +217,33 @@ def test_ts_binding_on_the_gpu(native, tmp_path, monkeypatch):
                       "dir": str(tmp_path / "dl"), "devices": devices, "stream": True, "budget": 3 * (L + 512)})
         expect[name] = bits.hex()
 
+    # the streamed form on 5,000 pieces: windows of 2,048 pieces x two 512-byte columns within the budget (the
+    # library's geometry), a short last piece, files ending mid-piece, two corrupted pieces at window edges
+    L, P = 1024, 5000
+    total = L * (P - 1) + 333
+    payload = bytearray(rng.randbytes(total))
+    digests = b"".join(hashlib.sha1(bytes(payload[i * L:(i + 1) * L])).digest() for i in range(P))
+    for i in (2047, 4096):
+        payload[i * L + 5] ^= 0x01
+    sizes = [1500 * L + 77, 2600 * L - 77, total - 4100 * L]
+    files = [(n, (f"w{k}.bin",)) for k, n in enumerate(sizes)]
+    off = 0
+    for n, p in files:
+        q = tmp_path.joinpath("dl2", *p)
+        q.parent.mkdir(parents=True, exist_ok=True)
+        q.write_bytes(bytes(payload[off:off + n]))
+        off += n
+    bits = bytearray((P + 7) // 8)
+    for i in range(P):
+        if i not in (2047, 4096):
+            bits[i >> 3] |= 0x80 >> (i & 7)
+    for devices in ([0], [0, 0]):
+        name = f"files_streamed_windows_{len(devices)}"
+        cases.append({"name": name, "kind": "files", "info": _info_json(L, total, digests, files, "t"),
+                      "dir": str(tmp_path / "dl2"), "devices": devices, "stream": True,
+                      "budget": 2 * (2048 * (512 + 256) + 256)})
+        expect[name] = bits.hex()
+
     # verifyPiece and hashPieces
     L = 262144
     blob = bytes(rng.getrandbits(8) for _ in range(3 * L + 12345))
