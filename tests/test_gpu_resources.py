@@ -408,3 +408,26 @@ def test_verify_files_name_with_a_nul_reads_as_null(native, tmp_path, monkeypatc
     (tmp_path / "c.bin").write_bytes(payload[L + 100:])
     monkeypatch.chdir(tmp_path)
     assert _bits(verify_files(info, str(tmp_path)), 3) == [1, 0, 1]
+
+
+@pytest.mark.gpu
+def test_verify_files_fifo_in_the_table_reads_as_null(native, tmp_path, monkeypatch):
+    """A named pipe where the table has a 2 MiB file: fsStorage.get opens it (read + write: no block) and its seek
+    fails, so the reference's pieces over it are null.  Every file path -- staged in windows or whole, streamed in
+    columns (whose residency sample opens files nonblocking and samples only regular files) -- reports them 0 without
+    blocking, and the other pieces as their bytes say."""
+    from torrent_amd import make_info, verify_files
+    from torrent_amd.metainfo import FileInfo
+    MiB = 1 << 20
+    L = MiB
+    payload = bytes((j * 13 + 5) & 0xFF for j in range(5 * L))
+    sizes, names = [2 * L, 2 * L, L], [["a.bin"], ["p.fifo"], ["c.bin"]]
+    digests = b"".join(hashlib.sha1(payload[i * L:(i + 1) * L]).digest() for i in range(5))
+    info = make_info(L, digests, "t", files=[FileInfo(n, p) for n, p in zip(sizes, names)])
+    (tmp_path / "a.bin").write_bytes(payload[:2 * L])
+    os.mkfifo(tmp_path / "p.fifo")
+    (tmp_path / "c.bin").write_bytes(payload[4 * L:])
+    monkeypatch.chdir(tmp_path)
+    for kw in ({}, {"stream": False, "budget": 2 * (L + 256) * 3}, {"stream": True, "budget": 1 << 24},
+               {"stream": True}):
+        assert _bits(verify_files(info, str(tmp_path), threads=2, **kw), 5) == [1, 1, 0, 0, 1], kw

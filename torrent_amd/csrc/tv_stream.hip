@@ -369,9 +369,11 @@ int tv_stream_file_table(tv_ctx* c, uint64_t n, const uint64_t* lengths, const c
         for (size_t q = 0; q < m; q++) {
             const uint64_t k = big[q * big.size() / m];
             const uint64_t a = std::max(lo, start[k]), b = std::min(hi, start[k + 1]);
-            const int fd = open(path[k], O_RDONLY | O_CLOEXEC);
+            // (nonblocking: a FIFO in the table must not hang the sample; only regular files are sampled)
+            const int fd = open(path[k], O_RDONLY | O_NONBLOCK | O_CLOEXEC);
             if (fd < 0) continue;
-            const double f = cached_fraction(fd, a - start[k], b - a);
+            struct stat sb;
+            const double f = fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode) ? cached_fraction(fd, a - start[k], b - a) : -1;
             close(fd);
             if (f < 0) continue;
             hit += f * (double)(b - a);
