@@ -14,6 +14,7 @@ question the round-5 records under profiles/r05/cold_sweep_*.jsonl answer:
   COLD_SPREAD  the C reader's destination spread over 192 MiB (RC_SPREAD), as the library fills its ring
   COLD_FOOT    that destination at 16 / 32 / 48 / 64 MiB
   COLD_DMA     the C reader with a page-locked H2D DMA stream running beside it
+  COLD_LANEAB  the default bounce path (two lanes x 2 readers) against one lane x 4 readers, with the C reader
   COLD_LIBBOUNCE  the library's own bounce path (TV_OPT_FILE_BOUNCE = R readers per lane) against the ring path
                (a "verify_files" leg runs the library's default, since round 6 the bounce path with 4 readers per lane;
                "ring" names the rounds 4-5 ring path)
@@ -123,6 +124,9 @@ def main():
                     ("verify_files O_DIRECT ring", 16), ("verify_files O_DIRECT bounce2", 16),
                     ("verify_files O_DIRECT bounce4", 16), ("verify_files O_DIRECT bounce2 1 lane", 16),
                     ("verify_files O_DIRECT bounce4 1 lane", 16), ("verify_files O_DIRECT bounce8", 16)]
+        if os.environ.get("COLD_LANEAB"):     # the default (two lanes x 2 readers) against one lane x 4 readers
+            legs = [("ceiling direct 4x4MiB", 4), ("verify_files O_DIRECT bounce2", 16),
+                    ("verify_files O_DIRECT bounce4 1 lane", 16)]
         if os.environ.get("COLD_LANES"):      # also one staging lane (TV_OPT_FILE_CONCURRENT = 0)
             legs = [("ceiling direct 16x4MiB", 16), ("verify_files O_DIRECT", 16),
                     ("verify_files O_DIRECT 1 lane", 16), ("verify_files O_DIRECT 1 lane", 32),
