@@ -14,6 +14,8 @@ question the round-5 records under profiles/r05/cold_sweep_*.jsonl answer:
   COLD_SPREAD  the C reader's destination spread over 192 MiB (RC_SPREAD), as the library fills its ring
   COLD_FOOT    that destination at 16 / 32 / 48 / 64 MiB
   COLD_DMA     the C reader with a page-locked H2D DMA stream running beside it
+  COLD_STRIDE  the C reader in the streamed columns' pattern (RC_STRIDE: part c of every 1 MiB piece, then c + 1)
+               against sequential parts, beside verify_files windowed and streamed (0.5 GiB budget)
   COLD_LANEAB  the default bounce path (two lanes x 2 readers) against one lane x 4 readers, with the C reader
   COLD_LIBBOUNCE  the library's own bounce path (TV_OPT_FILE_BOUNCE = R readers per lane) against the ring path
                (a "verify_files" leg runs the library's default, since round 6 the bounce path with 4 readers per lane;
@@ -36,7 +38,7 @@ from storage_paths_bench import read_ceiling, write_layout  # noqa: E402
 from torrent_amd import _native, verify_files  # noqa: E402
 from torrent_amd.verify import _context  # noqa: E402
 
-MiB = 1 << 20
+MiB, GiB = 1 << 20, 1 << 30
 
 
 class _DmaLoad:
@@ -124,6 +126,15 @@ def main():
                     ("verify_files O_DIRECT ring", 16), ("verify_files O_DIRECT bounce2", 16),
                     ("verify_files O_DIRECT bounce4", 16), ("verify_files O_DIRECT bounce2 1 lane", 16),
                     ("verify_files O_DIRECT bounce4 1 lane", 16), ("verify_files O_DIRECT bounce8", 16)]
+        if os.environ.get("COLD_STRIDE"):     # the streamed columns' read pattern (RC_STRIDE) against sequential parts
+            legs = [("ceiling direct 4x4MiB", 4), ("ceiling direct 16x512KiB", 16),
+                    ("ceiling direct 16x512KiB stride", 16), ("ceiling direct 32x512KiB stride", 32),
+                    ("ceiling direct 32x128KiB stride", 32), ("verify_files O_DIRECT bounce2", 16),
+                    ("verify_files streamed 0.5GiB", 16)]
+            if os.environ.get("COLD_STRIDE") == "spread":   # the same reads landing across the ring's footprint
+                legs = [("ceiling direct 32x512KiB stride", 32), ("ceiling direct 32x512KiB stride spread", 32),
+                        ("ceiling direct 32x512KiB stride spread48", 32), ("ceiling direct 32x512KiB stride pinned", 32),
+                        ("ceiling direct 32x512KiB stride spread pinned", 32), ("verify_files streamed 0.5GiB", 16)]
         if os.environ.get("COLD_LANEAB"):     # the default (two lanes x 2 readers) against one lane x 4 readers
             legs = [("ceiling direct 4x4MiB", 4), ("verify_files O_DIRECT bounce2", 16),
                     ("verify_files O_DIRECT bounce4 1 lane", 16)]
@@ -155,12 +166,17 @@ def main():
                             nd = ctx.counter(_native.TV_COUNTER_NUMA_NODE)
                         env["RC_CPU_NODE"] = str(nd if nd < (1 << 63) else 0)
                         rec["node"] = env["RC_CPU_NODE"]
+                    part = 4 * MiB
+                    if "KiB" in what.split("x", 1)[-1].split()[0]:   # ("ceiling direct 16x512KiB ...": 512 KiB parts)
+                        part = int(what.split("x", 1)[1].split("KiB")[0]) << 10
+                    if "stride" in what:   # column-major parts of 1 MiB pieces, as the streamed columns read
+                        env["RC_STRIDE"] = str(MiB)
                     dma = None
                     if what.endswith(" dma"):   # (not the bouncedma legs: their DMA is the reader's own)
                         dma = _DmaLoad()
                     t = time.perf_counter()
                     try:
-                        got = read_ceiling(paths, threads=thr, part=4 * MiB, direct=True, env=env)
+                        got = read_ceiling(paths, threads=thr, part=part, direct=True, env=env)
                     finally:
                         if dma:
                             rec["dma_gbps"] = dma.stop()
@@ -176,7 +192,8 @@ def main():
                               "0" if " ring" in what else str(_native.FILE_BOUNCE_DEFAULT))
                         ctx.set_option(_native.TV_OPT_FILE_BOUNCE, int(nb))
                     t = time.perf_counter()
-                    bf = verify_files(info, root, threads=thr)
+                    bf = (verify_files(info, root, threads=thr, budget=GiB // 2, stream=True) if "streamed" in what
+                          else verify_files(info, root, threads=thr))
                     el = time.perf_counter() - t
                     with _context(0) as ctx:
                         clock = ctx._file_clock()

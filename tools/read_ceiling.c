@@ -15,6 +15,9 @@
  * buffer (hipMemcpyAsync at (t mod 256) * part), the next read into a buffer waiting for the DMA that last read it
  * (compact destination, no host copy: the library's cold path without its 192 MiB ring); RC_BOUNCE=dma1 the same with
  * ONE stream shared by every reader (the library's form: the bounce DMAs queued on the staging lane's copy stream).
+ * RC_STRIDE=<bytes> (a multiple of the part) orders the requests column-major, as the library's streamed columns read
+ * a file: part c of every stride-long piece before part c + 1 of any (is the disk's rate for such reads the bound of
+ * a cold streamed verify?).
  * build: gcc -O2 -pthread tools/read_ceiling.c -o read_ceiling -ldl;  usage: read_ceiling THREADS PART_BYTES [direct] < paths */
 #define _GNU_SOURCE
 #include <dlfcn.h>
@@ -33,6 +36,7 @@
 typedef struct { char* path; uint64_t size; int fd; } file_t;
 static file_t* files;
 static uint64_t nfiles, part, ntasks;
+static uint64_t stride;   /* RC_STRIDE: column-major tasks (see the header comment); 0 = sequential parts */
 static uint64_t* task_file;   /* task -> file; offset = (task - first task of the file) * part */
 static uint64_t* first_task;
 static atomic_uint_fast64_t next_task, total_bytes;
@@ -96,7 +100,13 @@ static void* worker(void* arg) {
         const uint64_t t = atomic_fetch_add(&next_task, 1);
         if (t >= ntasks) break;
         file_t* f = &files[task_file[t]];
-        uint64_t off = (t - first_task[task_file[t]]) * part, n = f->size - off < part ? f->size - off : part;
+        uint64_t off = (t - first_task[task_file[t]]) * part;
+        if (stride) {   /* column-major: every piece's part `col` before any piece's part col + 1 */
+            const uint64_t i = t - first_task[task_file[t]], np = (f->size + stride - 1) / stride;
+            off = (i % np) * stride + (i / np) * part;
+            if (off >= f->size) continue;
+        }
+        uint64_t n = f->size - off < part ? f->size - off : part;
         char* into = buf;
         if (bounce == 2) {   /* the buffer's last DMA must be done before it is read into again */
             if (recorded[k] && hip_event_sync(dev[k])) atomic_fetch_add(&hip_errors, 1);
@@ -135,6 +145,10 @@ int main(int argc, char** argv) {
     const int threads = atoi(argv[1]);
     part = strtoull(argv[2], NULL, 10);
     direct = argc > 3 && strcmp(argv[3], "direct") == 0;
+    if (getenv("RC_STRIDE")) {
+        stride = strtoull(getenv("RC_STRIDE"), NULL, 10);
+        if (stride && (stride % part || stride < part)) return 2;   /* a whole number of parts per stride */
+    }
     const char* lib = getenv("RC_HOST_ALLOC_LIB");
     if (lib && lib[0]) {
         void* h = dlopen(lib, RTLD_NOW);
@@ -218,11 +232,12 @@ int main(int argc, char** argv) {
         files[k].fd = open(files[k].path, O_RDONLY | (direct ? O_DIRECT : 0));
         files[k].size = (files[k].fd >= 0 && fstat(files[k].fd, &st) == 0) ? (uint64_t)st.st_size : 0;
         first_task[k] = ntasks;
-        ntasks += (files[k].size + part - 1) / part;
+        ntasks += stride ? (files[k].size + stride - 1) / stride * (stride / part) : (files[k].size + part - 1) / part;
     }
+    first_task[nfiles] = ntasks;
     task_file = malloc((ntasks + 1) * sizeof(uint64_t));
     for (uint64_t k = 0; k < nfiles; k++)
-        for (uint64_t t = first_task[k]; t < first_task[k] + (files[k].size + part - 1) / part; t++) task_file[t] = k;
+        for (uint64_t t = first_task[k]; t < first_task[k + 1]; t++) task_file[t] = k;
     pthread_t* th = malloc(threads * sizeof(pthread_t));
     for (int i = 0; i < threads; i++) pthread_create(&th[i], NULL, worker, NULL);
     for (int i = 0; i < threads; i++) pthread_join(th[i], NULL);
