@@ -87,9 +87,10 @@ export interface VerifyOptions {
   /** verifyPiece only: hash on the CPU with the reference's own crypto.subtle.digest("SHA-1", bytes)
    * (tools/make_torrent.ts:28-31) instead of a ~3 ms GPU launch.  Off by default */
   cpuFallback?: boolean;
-  /** verifyFiles: read the shard's files through the bounded ring in columns sized to `budget`
-   * (tv_stream_file_table) instead of holding windows of whole pieces in device memory -- the faster form under a
-   * small budget, where each window pays one piece's serial SHA-1 (default: chosen per shard, streamWins) */
+  /** verifyFiles: read the shard's files through the bounded ring in columns within `budget` (tv_stream_file_table:
+   * the library picks windows of >= 2,048 pieces and columns as wide as the budget allows) instead of holding
+   * windows of whole pieces in device memory -- the faster form under a small budget, where each window pays one
+   * piece's serial SHA-1 (default: chosen per shard, streamWins) */
   stream?: boolean;
   /** host threads the library may use for one call, over all of its shards (default: the process's CPU share as
    * the library reads it, tv_cpu_share: the cgroup quota, else OMP_NUM_THREADS, else the affinity mask): each
