@@ -86,6 +86,46 @@ int main() {
     int calls = 0;
     CHECK(tvi::allocate_payload(100, MiB, 256, GiB, [&](const PayloadPlan&, uint64_t) { calls++; return 2; }, &p, &b,
                                 &failed) == 2 && calls == 1);
+    // a stream's geometry under a device budget (stream_geometry: tv_stream_file_table, tv_verify_host)
+    {
+        const uint64_t slot = 64 * MiB, slack = 256, KiB = 1024;
+        uint64_t col = 0, win = 0;
+        auto geo = [&](uint64_t L, uint64_t count, uint64_t budget, uint64_t min_win) {
+            tvi::stream_geometry(L, count, budget, min_win, slot, slack, &col, &win);
+        };
+        geo(MiB, 16384, GiB / 2, 2048);   // cfg2 at 0.5 GiB: 124 KiB rows, 9 columns
+        CHECK(col == 124 * KiB && win == 2048);
+        geo(MiB, 16384, 2 * GiB, 2048);   // each chunk buffer at most 256 MiB: the same geometry
+        CHECK(col == 124 * KiB && win == 2048);
+        geo(MiB, 16384, GiB / 4, 2048);   // 0.25 GiB: 60 KiB
+        CHECK(col == 60 * KiB && win == 2048);
+        geo(MiB, 16384, GiB, 512);        // a cold shard's 512-piece windows: 4 x longer rows
+        CHECK(col == 508 * KiB && win == 512);
+        geo(4096, 5000, GiB, 2048);       // whole pieces fit: one window of the shard
+        CHECK(col == 4096 && win == 5000);
+        geo(4096, 5000, 2 * (2048 * (1024 + 256) + 256), 2048);   // tests/test_gpu_fuzz.py: 3 windows x 4 columns
+        CHECK(col == 1024 && win == 2048);
+        geo(4096, 5000, 1, 2048);         // no room: 64-byte columns
+        CHECK(col == 64 && win == 2048);
+        geo(MiB, 160, 2 * (160 * (256 * KiB + 256) + 256), 64);   // tests/test_gpu_cold.py: 640 KiB, 2 columns
+        CHECK(col == 640 * KiB && win == 64);
+        geo(1 << 30, 3, GiB, 2048);       // a piece larger than a ring slot: rows of one slot
+        CHECK(col == slot && win == 3);
+        // invariants over a sweep: columns a multiple of 64 (of 4 KiB from 4 KiB up) within a slot and the piece,
+        // windows a multiple of 64 or the whole shard, both chunk buffers within the budget whenever it has room
+        uint64_t seed = 1;
+        for (int t = 0; t < 20000; t++) {
+            seed = seed * 6364136223846793005ull + 1442695040888963407ull;
+            const uint64_t L = 1 + (seed >> 33) % (96 * MiB), count = 1 + (seed >> 13) % 70000;
+            const uint64_t budget = (seed >> 7) % (8 * GiB), mw = (t & 1) ? 2048 : 512;
+            geo(L, count, budget, mw);
+            const uint64_t lpad = std::min<uint64_t>((L + 63) / 64 * 64, slot);
+            CHECK(col >= 64 && col % 64 == 0 && col <= lpad && (col < 4096 || col % 4096 == 0 || col == lpad));
+            CHECK(win >= 1 && win <= count && (win == count || win % 64 == 0));
+            if (col > 64)
+                CHECK((col + 256) * win + slack <= std::min<uint64_t>(budget / 2, tvi::kStreamChunkMax));
+        }
+    }
     if (failures) return 1;
     std::printf("ok\n");
     return 0;

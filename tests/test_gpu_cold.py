@@ -245,7 +245,7 @@ def test_cold_files_streamed(native, oracle, tmp_path, odirect):
                     assert clock["odirect_fallbacks"] > 0 and clock["odirect_errno"] == errno.EINVAL, clock
                 else:
                     assert clock["odirect_fallbacks"] == 0, clock
-        if odirect:   # a cold shard in windows of 64 pieces: 3 windows (64 + 64 + 32) x 2 columns of 636 KiB
+        if odirect:   # a cold shard in windows of 64 pieces: 3 windows (64 + 64 + 32) x 2 columns of 640 KiB
             with _context(0) as ctx:
                 ctx.set_option(native.TV_OPT_STREAM_COLD_WINDOW, 64)
             assert fsutil.drop_cache(paths) <= 0.01

@@ -1,5 +1,7 @@
-"""CPU unit test of the resident payload planner (torrent_amd/csrc/tv_plan.h): tv_set_layout's out-of-memory
-retry loop ends for every shape, including pieces larger than the memory left (it looped forever)."""
+"""CPU unit tests of torrent_amd/csrc/tv_plan.h: the resident payload planner (tv_set_layout's out-of-memory retry loop
+ends for every shape, including pieces larger than the memory left; ADVICE r04: it looped forever), a stream's
+windows x columns under a device budget (stream_geometry: the documented shapes, and its invariants over a sweep),
+and the file table's walk."""
 import os
 import shutil
 import subprocess

@@ -1,5 +1,6 @@
-// tv_plan.h -- the resident payload's shape under a device budget (tv_set_layout), as plain host code with no HIP
-// in it, so its retry loop is unit-tested on the CPU (tests/c/plan_test.cpp, tests/test_plan.py).
+// tv_plan.h -- the resident payload's shape under a device budget (tv_set_layout), a stream's windows x columns under
+// one (stream_geometry) and the file table's walk (walk_file_table), as plain host code with no HIP in it, so they are
+// unit-tested on the CPU (tests/c/plan_test.cpp, tests/c/walk_main.cpp, tests/test_plan.py).
 #pragma once
 #include <stdint.h>
 
@@ -105,6 +106,32 @@ inline bool walk_file_table(uint64_t n, const uint64_t* lengths, uint64_t lo, ui
     }
     *reached = start;
     return true;
+}
+
+// ---- a stream's geometry under a device budget (tv_stream.hip: tv_stream_file_table, tv_verify_host) ----------------
+//
+// Windows of at least `min_win` pieces (a multiple of 64 unless the shard is smaller), each hashed column by column --
+// enough pieces that a column hashes faster than it stages (2,048 pieces x 64 B per ~0.75 us block step: ~175 GB/s)
+// -- and columns as wide as two chunk buffers within the budget allow, so each row is one long read or DMA row: 124 KiB
+// at a 0.5 GiB budget and 1 MiB pieces where columns across all 16,384 pieces would be 16 KiB.  A multiple of 4 KiB
+// from 4 KiB up (a cold file's rows are read O_DIRECT straight into the ring slot); where whole pieces fit, the
+// windows grow to fill the budget.  Each chunk buffer is at most kStreamChunkMax: wider columns gained nothing and
+// larger units overlap less (the first unit's copy and the last unit's kernel run alone): budgets of 2 GiB (1 GiB
+// units) ran 44-49 GB/s against 52-55 at 0.5 GiB (profiles/r06/window_bench_payload_cols*.jsonl).  `slot` bounds a
+// row (one ring slot), `slack` is the bytes after the last row.
+constexpr uint64_t kStreamChunkMax = 256ull << 20;
+inline void stream_geometry(uint64_t L, uint64_t count, uint64_t budget, uint64_t min_win, uint64_t slot,
+                            uint64_t slack, uint64_t* col, uint64_t* win) {
+    const uint64_t half = std::min<uint64_t>(budget / 2, kStreamChunkMax);
+    const uint64_t lpad = std::min<uint64_t>((L + 63) / 64 * 64, slot);
+    uint64_t w = std::min<uint64_t>(count, min_win);
+    const uint64_t per = half > slack && w ? (half - slack) / w : 0;
+    const uint64_t wid = per > 256 ? per - 256 : 64;
+    uint64_t C = std::max<uint64_t>(64, std::min<uint64_t>(wid >= 4096 ? wid / 4096 * 4096 : wid / 64 * 64, lpad));
+    if (C == lpad && w < count && half > slack)
+        w = std::min<uint64_t>(count, std::max<uint64_t>(w, (half - slack) / (C + 256) / 64 * 64));
+    *col = C;
+    *win = w;
 }
 
 }  // namespace tvi

@@ -69,27 +69,9 @@ uint64_t stream_chunk_need(const tv_ctx* c) {
     return (stream_column(c) + 256) * c->count + kSlack;
 }
 
-// Geometry of a stream under a device budget (tv_stream_file_table, tv_verify_host; without TV_OPT_RESIDENT_BUDGET
-// 1 GiB): windows of at least `min_win` pieces (a multiple of 64), each hashed column by column -- enough pieces that a
-// column hashes faster than it stages (2,048 pieces x 64 B per ~0.75 us block step: ~175 GB/s) -- and columns as
-// wide as two chunk buffers within the budget allow, so each row is one long read or DMA row: 124 KiB at a 0.5 GiB
-// budget and 1 MiB pieces where columns across all 16,384 pieces would be 16 KiB.  A multiple of 4 KiB from 4 KiB up
-// (a cold file's rows are read O_DIRECT straight into the slot); where whole pieces fit, the windows grow to fill
-// the budget.  Each chunk buffer is at most kStreamChunkMax: wider columns gained nothing and larger units overlap
-// less (the first unit's copy and the last unit's kernel run alone): budgets of 2 GiB (1 GiB units) ran 44-49 GB/s
-// against 52-55 at 0.5 GiB (profiles/r06/window_bench_payload_cols*.jsonl).
-constexpr uint64_t kStreamChunkMax = 256ull << 20;
+// The geometry of a stream under a device budget: tv_plan.h stream_geometry (its rationale there).
 void budget_geometry(const tv_ctx* c, uint64_t budget, uint64_t min_win, uint64_t* col, uint64_t* win) {
-    const uint64_t half = std::min<uint64_t>(budget / 2, kStreamChunkMax);
-    const uint64_t lpad = std::min<uint64_t>((c->L + 63) / 64 * 64, kRingSlotBytes);
-    uint64_t w = std::min<uint64_t>(c->count, min_win);
-    const uint64_t per = half > kSlack ? (half - kSlack) / w : 0;
-    const uint64_t wid = per > 256 ? per - 256 : 64;
-    uint64_t C = std::max<uint64_t>(64, std::min<uint64_t>(wid >= 4096 ? wid / 4096 * 4096 : wid / 64 * 64, lpad));
-    if (C == lpad && w < c->count && half > kSlack)
-        w = std::min<uint64_t>(c->count, std::max<uint64_t>(w, (half - kSlack) / (C + 256) / 64 * 64));
-    *col = C;
-    *win = w;
+    stream_geometry(c->L, c->count, budget, min_win, kRingSlotBytes, kSlack, col, win);
 }
 
 int stream_begin_locked(tv_ctx* c, const uint8_t* avail_bits, uint64_t col_override = 0, uint64_t win_override = 0,
